@@ -1,0 +1,1934 @@
+// mpcc_oracle.cpp — CPU restatement of the reference MPCC per-control-step solve.
+//
+// TEST INFRASTRUCTURE ONLY (parity checker + CPU baseline).  See oracle_api.h for the rules and
+// for how this restatement is pinned.  Every function cites the reference file:line it restates
+// (paths relative to the reference's cpp/ directory).  Written in plain C++17 with fixed-size
+// arrays; no Eigen/RBDL/OSQP.  Deliberately scalar and layout-faithful: it mirrors the reference's
+// data flow (AoS State/Input, dense QP layout) rather than the GPU engine's SoA/stage layout.
+#include "oracle_api.h"
+
+#include <algorithm>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <fstream>
+#include <limits>
+#include <map>
+#include <sstream>
+#include <string>
+#include <vector>
+#ifdef _OPENMP
+#include <omp.h>
+#endif
+
+namespace orc {
+
+constexpr int NX = 9, NU = 8, NPC = 11, DOF = 7, NLINK = 9;
+constexpr double INF = 1e30;                 // config.h:37
+constexpr int N_SPLINE = 100;                // config.h:38
+constexpr int REC = 143;                     // robot record size (see rec_* offsets)
+// RobotData layout (robot_data.h:13-31)
+constexpr int R_POS = 0, R_ROT = 3, R_J = 12, R_MU = 54, R_DMU = 55, R_SEL = 62, R_DSEL = 63,
+              R_OBSR = 70, R_ENV = 71, R_DENV = 80;
+
+enum Status {  // solver_interface.h:28-42
+    SOLVED, MAX_ITER_EXCEEDED, QP_DualInfeasibleInaccurate, QP_PrimalInfeasibleInaccurate,
+    QP_SolvedInaccurate, QP_MaxIterReached, QP_PrimalInfeasible, QP_DualInfeasible, Sigint,
+    INVALID_SETTINGS, NAN_HESSIAN, NON_PD_HESSIAN
+};
+
+// ------------------------------------------------------------------------------------------------
+// small dense helpers (row-major)
+// ------------------------------------------------------------------------------------------------
+static inline void mat3_mul(const double* A, const double* B, double* C) {
+    double T[9];
+    for (int i = 0; i < 3; i++)
+        for (int j = 0; j < 3; j++) {
+            double s = 0;
+            for (int k = 0; k < 3; k++) s += A[3 * i + k] * B[3 * k + j];
+            T[3 * i + j] = s;
+        }
+    std::memcpy(C, T, sizeof T);
+}
+static inline void mat3_mul_tn(const double* A, const double* B, double* C) {  // A^T B
+    double T[9];
+    for (int i = 0; i < 3; i++)
+        for (int j = 0; j < 3; j++) {
+            double s = 0;
+            for (int k = 0; k < 3; k++) s += A[3 * k + i] * B[3 * k + j];
+            T[3 * i + j] = s;
+        }
+    std::memcpy(C, T, sizeof T);
+}
+static inline void mat3_vec(const double* A, const double* v, double* o) {
+    double t[3];
+    for (int i = 0; i < 3; i++) t[i] = A[3 * i] * v[0] + A[3 * i + 1] * v[1] + A[3 * i + 2] * v[2];
+    o[0] = t[0]; o[1] = t[1]; o[2] = t[2];
+}
+static inline void skew(const double* v, double* S) {  // cubic_spline_rot.cpp:25-35
+    S[0] = 0; S[1] = -v[2]; S[2] = v[1];
+    S[3] = v[2]; S[4] = 0; S[5] = -v[0];
+    S[6] = -v[1]; S[7] = v[0]; S[8] = 0;
+}
+static inline void invskew(const double* S, double* v) {  // cubic_spline_rot.cpp:37-42
+    v[0] = S[7]; v[1] = S[2]; v[2] = S[3];
+}
+
+// 3x3 symmetric eigen-decomposition (cyclic Jacobi) on the LOWER triangle, as Eigen's
+// SelfAdjointEigenSolver reads it.  Eigenvalues ascending.  Used only by LogMatrix's theta=pi
+// branch; eigenvector signs follow this routine (parity unpinned in that branch).
+static void sym_eig3(const double* Rin, double* w, double* V) {
+    double A[9];
+    for (int i = 0; i < 3; i++)
+        for (int j = 0; j < 3; j++) A[3 * i + j] = (i >= j) ? Rin[3 * i + j] : Rin[3 * j + i];
+    for (int i = 0; i < 9; i++) V[i] = (i % 4 == 0) ? 1.0 : 0.0;
+    for (int sweep = 0; sweep < 50; sweep++) {
+        double off = std::fabs(A[1]) + std::fabs(A[2]) + std::fabs(A[5]);
+        if (off < 1e-300) break;
+        for (int p = 0; p < 2; p++)
+            for (int q = p + 1; q < 3; q++) {
+                double apq = A[3 * p + q];
+                if (std::fabs(apq) < 1e-300) continue;
+                double theta = (A[3 * q + q] - A[3 * p + p]) / (2 * apq);
+                double t = (theta >= 0 ? 1.0 : -1.0) / (std::fabs(theta) + std::sqrt(theta * theta + 1));
+                double c = 1 / std::sqrt(t * t + 1), s = t * c;
+                for (int k = 0; k < 3; k++) {
+                    double akp = A[3 * k + p], akq = A[3 * k + q];
+                    A[3 * k + p] = c * akp - s * akq;
+                    A[3 * k + q] = s * akp + c * akq;
+                }
+                for (int k = 0; k < 3; k++) {
+                    double apk = A[3 * p + k], aqk = A[3 * q + k];
+                    A[3 * p + k] = c * apk - s * aqk;
+                    A[3 * q + k] = s * apk + c * aqk;
+                }
+                for (int k = 0; k < 3; k++) {
+                    double vkp = V[3 * k + p], vkq = V[3 * k + q];
+                    V[3 * k + p] = c * vkp - s * vkq;
+                    V[3 * k + q] = s * vkp + c * vkq;
+                }
+            }
+    }
+    int idx[3] = {0, 1, 2};
+    std::sort(idx, idx + 3, [&](int a, int b) { return A[4 * a] < A[4 * b]; });
+    double Vs[9];
+    for (int j = 0; j < 3; j++) {
+        w[j] = A[4 * idx[j]];
+        for (int i = 0; i < 3; i++) Vs[3 * i + j] = V[3 * i + idx[j]];
+    }
+    std::memcpy(V, Vs, sizeof Vs);
+}
+
+// LogMatrix — cubic_spline_rot.cpp:44-79 (quirk Q10)
+static void log_matrix(const double* R, double* out) {
+    double tr = R[0] + R[4] + R[8];
+    for (int i = 0; i < 9; i++) out[i] = 0;
+    if (std::fabs(tr + 1.0) < 1e-6) {
+        double w[3], V[9];
+        sym_eig3(R, w, V);
+        for (int i = 0; i < 3; i++) {
+            if (std::fabs(w[i] - 1.0) < 1e-4) {
+                double v[3] = {V[i], V[3 + i], V[6 + i]};
+                double n = std::sqrt(v[0] * v[0] + v[1] * v[1] + v[2] * v[2]);
+                for (int k = 0; k < 3; k++) v[k] /= n;
+                double S[9];
+                skew(v, S);
+                for (int k = 0; k < 9; k++) out[k] = -S[k] * M_PI;
+            }
+        }
+    } else if (std::fabs(tr - 3.0) < 1e-6) {
+        // zero
+    } else {
+        double th = std::acos((tr - 1.0) / 2.0);
+        double f = 1.0 / 2.0 * th / std::sin(th);
+        for (int i = 0; i < 3; i++)
+            for (int j = 0; j < 3; j++) out[3 * i + j] = f * (R[3 * i + j] - R[3 * j + i]);
+    }
+}
+
+// ExpMatrix — cubic_spline_rot.cpp:81-95 (quirk Q11: integer 1/2 == 0)
+static void exp_matrix(const double* sk, double* out) {
+    double sym = 0, dg = 0;
+    for (int i = 0; i < 3; i++)
+        for (int j = 0; j < 3; j++) {
+            double t = sk[3 * j + i] + sk[3 * i + j];
+            sym += t * t;
+        }
+    for (int i = 0; i < 3; i++) dg += sk[4 * i] * sk[4 * i];
+    if (std::sqrt(sym) >= 1e-8 || std::sqrt(dg) >= 1e-8) {
+        for (int i = 0; i < 9; i++) out[i] = 0;
+        return;
+    }
+    double v[3];
+    invskew(sk, v);
+    double vn = std::sqrt(v[0] * v[0] + v[1] * v[1] + v[2] * v[2]);
+    double sk2[9];
+    mat3_mul(sk, sk, sk2);
+    if (vn <= 1e-8) {
+        for (int i = 0; i < 9; i++) out[i] = (i % 4 == 0 ? 1.0 : 0.0) + std::cos(vn) * sk[i] + 0 * sk2[i];
+        return;
+    }
+    double a = std::sin(vn) / vn, b = (1 - std::cos(vn)) / (vn * vn);
+    for (int i = 0; i < 9; i++) out[i] = (i % 4 == 0 ? 1.0 : 0.0) + a * sk[i] + b * sk2[i];
+}
+
+// ------------------------------------------------------------------------------------------------
+// Splines — cubic_spline.cpp:25-246, cubic_spline_rot.cpp:97-259, arc_length_spline.cpp:33-379
+// ------------------------------------------------------------------------------------------------
+struct CubicSpline {
+    std::vector<double> x, y, a, b, c, d;
+    bool regular = false;
+    double dx = 0;
+    std::map<double, int> xmap;
+
+    void gen(const std::vector<double>& xin, const std::vector<double>& yin, bool is_regular) {  // :162-183
+        x = xin; y = yin; regular = is_regular;
+        int n = (int)x.size();
+        if (is_regular) dx = x[1] - x[0];
+        else { dx = 0; xmap.clear(); for (int i = 0; i < n; i++) xmap[x[i]] = i; }
+        // compSplineParams :65-124
+        a = y; b.assign(n - 1, 0); c.assign(n, 0); d.assign(n - 1, 0);
+        std::vector<double> mu(n - 1, 0), h(n - 1, 0), alpha(n - 1, 0), l(n, 0), z(n, 0);
+        for (int i = 0; i < n - 1; i++) h[i] = x[i + 1] - x[i];
+        for (int i = 1; i < n - 1; i++)
+            alpha[i] = 3.0 / h[i] * (a[i + 1] - a[i]) - 3.0 / h[i - 1] * (a[i] - a[i - 1]);
+        l[0] = 1.0; mu[0] = 0.0; z[0] = 0.0;
+        for (int i = 1; i < n - 1; i++) {
+            l[i] = 2.0 * (x[i + 1] - x[i - 1]) - h[i - 1] * mu[i - 1];
+            mu[i] = h[i] / l[i];
+            z[i] = (alpha[i] - h[i - 1] * z[i - 1]) / l[i];
+        }
+        l[n - 1] = 1.0; z[n - 1] = 0.0;
+        c[n - 1] = 0.0;
+        for (int i = n - 2; i >= 0; i--) {
+            c[i] = z[i] - mu[i] * c[i + 1];
+            b[i] = (a[i + 1] - a[i]) / h[i] - (h[i] * (c[i + 1] + 2.0 * c[i])) / 3.0;
+            d[i] = (c[i + 1] - c[i]) / (3.0 * h[i]);
+        }
+    }
+    int index(double xx) const {  // :126-153
+        int n = (int)x.size();
+        if (xx == x[n - 1]) return n - 1;
+        if (regular) return int(std::floor(xx / dx));
+        auto it = xmap.upper_bound(xx);
+        if (it == xmap.end()) return -1;
+        return it->second - 1;
+    }
+    double unwrap(double xx) const { return std::max(0., std::min(xx, x.back())); }
+    double point(double xx) const {  // :185-207
+        xx = unwrap(xx);
+        int i = index(xx);
+        double d1 = xx - x[i], d2 = d1 * d1, d3 = d1 * d2;
+        if (i == (int)x.size() - 1) return y.back();
+        return a[i] + b[i] * d1 + c[i] * d2 + d[i] * d3;
+    }
+    double deriv(double xx) const {  // :209-227
+        xx = unwrap(xx);
+        int i = index(xx);
+        double d1 = xx - x[i], d2 = d1 * d1;
+        if (i == (int)x.size() - 1) return 0.;
+        return b[i] + 2.0 * c[i] * d1 + 3.0 * d[i] * d2;
+    }
+    double deriv2(double xx) const {  // :229-246
+        xx = unwrap(xx);
+        int i = index(xx);
+        double d1 = xx - x[i];
+        if (i == (int)x.size() - 1) return 2.0 * c[i];
+        return 2.0 * c[i] + 6.0 * d[i] * d1;
+    }
+};
+
+struct CubicSplineRot {
+    std::vector<double> x, c, d;
+    std::vector<std::array<double, 9>> R;
+    bool regular = false;
+    double dx = 0;
+    std::map<double, int> xmap;
+    void gen(const std::vector<double>& xin, const std::vector<std::array<double, 9>>& Rin, bool is_regular) {
+        x = xin; R = Rin; regular = is_regular;
+        int n = (int)x.size();
+        if (is_regular) dx = x[1] - x[0];
+        else { dx = 0; xmap.clear(); for (int i = 0; i < n; i++) xmap[x[i]] = i; }
+        c.assign(n - 1, 0); d.assign(n - 1, 0);  // compSplineRotParams :137-155
+        for (int i = 0; i < n - 1; i++) {
+            c[i] = 3.0 / std::pow(x[i + 1] - x[i], 2);
+            d[i] = -2.0 / std::pow(x[i + 1] - x[i], 3);
+        }
+    }
+    int index(double xx) const {
+        int n = (int)x.size();
+        if (xx == x[n - 1]) return n - 1;
+        if (regular) return int(std::floor(xx / dx));
+        auto it = xmap.upper_bound(xx);
+        if (it == xmap.end()) return -1;
+        return it->second - 1;
+    }
+    double unwrap(double xx) const { return std::max(0., std::min(xx, x.back())); }
+    void point(double xx, double* out) const {  // :216-238
+        xx = unwrap(xx);
+        int i = index(xx);
+        if (i == (int)x.size() - 1) { std::memcpy(out, R.back().data(), 72); return; }
+        double d1 = xx - x[i], d2 = d1 * d1, d3 = d1 * d2;
+        double RtR[9], L[9], E[9];
+        mat3_mul_tn(R[i].data(), R[i + 1].data(), RtR);
+        log_matrix(RtR, L);
+        double f = c[i] * d2 + d[i] * d3;
+        for (int k = 0; k < 9; k++) L[k] *= f;
+        exp_matrix(L, E);
+        mat3_mul(R[i].data(), E, out);
+    }
+    void deriv(double xx, double* out) const {  // :240-259
+        xx = unwrap(xx);
+        int i = index(xx);
+        if (i == (int)x.size() - 1) { out[0] = out[1] = out[2] = 0; return; }
+        double d1 = xx - x[i], d2 = d1 * d1;
+        double RtR[9], L[9], v[3];
+        mat3_mul_tn(R[i].data(), R[i + 1].data(), RtR);
+        log_matrix(RtR, L);
+        invskew(L, v);
+        double f = 2.0 * c[i] * d1 + 3.0 * d[i] * d2;
+        for (int k = 0; k < 3; k++) out[k] = v[k] * f;
+    }
+};
+
+struct ArcLengthSpline {
+    std::vector<double> s, X, Y, Z;
+    std::vector<std::array<double, 9>> R;
+    CubicSpline sx, sy, sz;
+    CubicSplineRot sr;
+    double proj_max_dist = 0.03;
+    bool set = false;
+
+    static std::vector<double> arc_length(const std::vector<double>& X, const std::vector<double>& Y,
+                                          const std::vector<double>& Z) {  // :66-87
+        int n = (int)X.size();
+        std::vector<double> s(n, 0.0);
+        for (int i = 0; i < n - 1; i++) {
+            double dx = X[i + 1] - X[i], dy = Y[i + 1] - Y[i], dz = Z[i + 1] - Z[i];
+            s[i + 1] = s[i] + std::sqrt(dx * dx + dy * dy + dz * dz);
+        }
+        return s;
+    }
+    static std::vector<double> linspaced(int n, double lo, double hi) {  // Eigen LinSpaced (no flip for lo=0)
+        std::vector<double> v(n);
+        double step = (hi - lo) / double(n - 1);
+        bool flip = std::fabs(hi) < std::fabs(lo);
+        for (int i = 0; i < n; i++) {
+            if (flip) v[i] = (i == 0) ? lo : hi - double(n - 1 - i) * step;
+            else v[i] = (i == n - 1) ? hi : lo + double(i) * step;
+        }
+        return v;
+    }
+    void resample(const CubicSpline& fx, const CubicSpline& fy, const CubicSpline& fz, const CubicSplineRot& fr,
+                  double total, std::vector<double>& rs, std::vector<double>& rx, std::vector<double>& ry,
+                  std::vector<double>& rz, std::vector<std::array<double, 9>>& rR) const {  // :89-119
+        rs = linspaced(N_SPLINE, 0, total);
+        rx.assign(N_SPLINE, 0); ry.assign(N_SPLINE, 0); rz.assign(N_SPLINE, 0); rR.assign(N_SPLINE, {});
+        for (int i = 0; i < N_SPLINE; i++) {
+            rx[i] = fx.point(rs[i]);
+            ry[i] = fy.point(rs[i]);
+            rz[i] = fz.point(rs[i]);
+            fr.point(rs[i], rR[i].data());
+        }
+    }
+    void fit(const std::vector<double>& X0, const std::vector<double>& Y0, const std::vector<double>& Z0,
+             const std::vector<std::array<double, 9>>& R0) {  // fitSpline :213-253
+        std::vector<double> sa = arc_length(X0, Y0, Z0);
+        double total = sa.back();
+        CubicSpline f1x, f1y, f1z; CubicSplineRot f1r;
+        f1x.gen(sa, X0, false); f1y.gen(sa, Y0, false); f1z.gen(sa, Z0, false); f1r.gen(sa, R0, false);
+        std::vector<double> s1, x1, y1, z1; std::vector<std::array<double, 9>> R1;
+        resample(f1x, f1y, f1z, f1r, total, s1, x1, y1, z1, R1);
+        sa = arc_length(x1, y1, z1);
+        total = sa.back();
+        CubicSpline f2x, f2y, f2z; CubicSplineRot f2r;
+        f2x.gen(sa, x1, false); f2y.gen(sa, y1, false); f2z.gen(sa, z1, false); f2r.gen(sa, R1, false);
+        std::vector<double> s2, x2, y2, z2; std::vector<std::array<double, 9>> R2;
+        resample(f2x, f2y, f2z, f2r, total, s2, x2, y2, z2, R2);
+        s = s2; X = x2; Y = y2; Z = z2; R = R2;  // setRegularData
+        sx.gen(s, X, true); sy.gen(s, Y, true); sz.gen(s, Z, true); sr.gen(s, R, true);
+        set = true;
+    }
+    double length() const { return s.back(); }
+    double unwrap(double x) const { return std::max(0., std::min(x, length())); }
+    void pos(double t, double* o) const { o[0] = sx.point(t); o[1] = sy.point(t); o[2] = sz.point(t); }
+    void dpos(double t, double* o) const { o[0] = sx.deriv(t); o[1] = sy.deriv(t); o[2] = sz.deriv(t); }
+    void ddpos(double t, double* o) const { o[0] = sx.deriv2(t); o[1] = sy.deriv2(t); o[2] = sz.deriv2(t); }
+    void rot(double t, double* o) const { sr.point(t, o); }
+    void drot(double t, double* o) const { sr.deriv(t, o); }
+
+    // projectOnSpline — arc_length_spline.cpp:318-379 (quirk Q12 in the far branch)
+    double project(double s_guess, const double* ee) const {
+        double pp[3];
+        pos(s_guess, pp);
+        double s_opt = s_guess;
+        double dist = std::sqrt((ee[0] - pp[0]) * (ee[0] - pp[0]) + (ee[1] - pp[1]) * (ee[1] - pp[1]) +
+                                (ee[2] - pp[2]) * (ee[2] - pp[2]));
+        if (dist >= proj_max_dist) {
+            int n = (int)s.size();
+            std::vector<double> d2(n), filt(n);
+            bool any = false;
+            for (int i = 0; i < n; i++) {
+                double dx = X[i] - ee[0], dy = Y[i] - ee[1], dz = Z[i] - ee[2];
+                d2[i] = dx * dx + dy * dy + dz * dz;
+                bool valid = std::fabs(s[i] - s_guess) <= proj_max_dist;
+                any |= valid;
+                double m = valid ? 1.0 : 0.0;
+                filt[i] = d2[i] * m + (1.0 - m) * std::numeric_limits<double>::infinity();  // NaN for valid
+            }
+            // Eigen minCoeff, scalar semantics: first index, replaced only by strictly smaller.
+            int mi = 0;
+            double mv = filt[0];
+            for (int i = 1; i < n; i++)
+                if (filt[i] < mv) { mv = filt[i]; mi = i; }
+            if (!any) {
+                int mj = (int)(std::min_element(d2.begin(), d2.end()) - d2.begin());
+                s_opt = s[mj];
+            } else {
+                s_opt = s[mi];
+            }
+        }
+        if (s_opt >= s.back()) return s.back();
+        double s_old = s_opt;
+        for (int i = 0; i < 20; i++) {
+            double p[3], dp[3], ddp[3];
+            pos(s_opt, p); dpos(s_opt, dp); ddpos(s_opt, ddp);
+            double df[3] = {p[0] - ee[0], p[1] - ee[1], p[2] - ee[2]};
+            double jac = 2.0 * df[0] * dp[0] + 2.0 * df[1] * dp[1] + 2.0 * df[2] * dp[2];
+            double hes = 2.0 * dp[0] * dp[0] + 2.0 * df[0] * ddp[0] + 2.0 * dp[1] * dp[1] + 2.0 * df[1] * ddp[1] +
+                         2.0 * dp[2] * dp[2] + 2.0 * df[2] * ddp[2];
+            s_opt -= jac / hes;
+            s_opt = unwrap(s_opt);
+            if (std::fabs(s_old - s_opt) <= 1e-5) return s_opt;
+            s_old = s_opt;
+        }
+        return s_guess;
+    }
+};
+
+// ------------------------------------------------------------------------------------------------
+// Robot kinematics — RBDL restatement of robot_model.cpp:68-319 (Panda chain) and :366-450
+// RBDL SpatialTransform(E, r): E maps parent to child coordinates, so the child frame's rotation
+// in the parent is E^T; a revolute-z joint contributes Rz(q).
+// ------------------------------------------------------------------------------------------------
+static const double JOINT_E[9][9] = {
+    {1, 0, 0, 0, 1, 0, 0, 0, 1},                 // [0] world->link0 (base rotation = I)
+    {1, 0, 0, 0, 1, 0, 0, 0, 1},                 // [1] link0->link1   :189-193
+    {1, 0, 0, 0, 0, -1, 0, 1, 0},                // [2] link1->link2   :196-200
+    {1, 0, 0, 0, 0, 1, 0, -1, 0},                // [3]                :203-207
+    {1, 0, 0, 0, 0, 1, 0, -1, 0},                // [4]                :210-214
+    {1, 0, 0, 0, 0, -1, 0, 1, 0},                // [5]                :217-221
+    {1, 0, 0, 0, 0, 1, 0, -1, 0},                // [6]                :224-228
+    {1, 0, 0, 0, 0, 1, 0, -1, 0},                // [7]                :231-235
+    {0.707107, -0.707107, 0., 0.707107, 0.707107, 0., 0., 0., 1.},  // [8] link7->hand :238-242 (Q19)
+};
+static const double JOINT_R[9][3] = {
+    {0, 0, 0}, {0, 0, 0.333}, {0, 0, 0}, {0, -0.316, 0}, {0.0825, 0, 0},
+    {-0.0825, 0.384, 0}, {0, 0, 0}, {0.088, 0, 0}, {0, 0, 0.107}};  // :171-179
+static const double TCP_R[3] = {0, 0, 0.1034};                      // :182
+
+// FK + geometric Jacobian of panda_hand_tcp.  J rows 0-2 = Jv, 3-5 = Jw (robot_model.cpp:372-375)
+static void fk(const double* q, double* pos, double* Rout, double* J) {
+    double Rc[9] = {1, 0, 0, 0, 1, 0, 0, 0, 1}, pc[3] = {0, 0, 0};
+    double z[7][3], o[7][3];
+    for (int i = 1; i <= 7; i++) {
+        double t[3];
+        mat3_vec(Rc, JOINT_R[i], t);
+        pc[0] += t[0]; pc[1] += t[1]; pc[2] += t[2];
+        double Et[9], Rt[9];
+        for (int a = 0; a < 3; a++)
+            for (int b = 0; b < 3; b++) Et[3 * a + b] = JOINT_E[i][3 * b + a];
+        mat3_mul(Rc, Et, Rt);
+        z[i - 1][0] = Rt[2]; z[i - 1][1] = Rt[5]; z[i - 1][2] = Rt[8];
+        o[i - 1][0] = pc[0]; o[i - 1][1] = pc[1]; o[i - 1][2] = pc[2];
+        double c = std::cos(q[i - 1]), s = std::sin(q[i - 1]);
+        double Rz[9] = {c, -s, 0, s, c, 0, 0, 0, 1};
+        mat3_mul(Rt, Rz, Rc);
+    }
+    {   // hand (fixed)
+        double t[3];
+        mat3_vec(Rc, JOINT_R[8], t);
+        pc[0] += t[0]; pc[1] += t[1]; pc[2] += t[2];
+        double Et[9], Rt[9];
+        for (int a = 0; a < 3; a++)
+            for (int b = 0; b < 3; b++) Et[3 * a + b] = JOINT_E[8][3 * b + a];
+        mat3_mul(Rc, Et, Rt);
+        std::memcpy(Rc, Rt, sizeof Rt);
+        mat3_vec(Rc, TCP_R, t);  // tcp (fixed, identity rotation)
+        pc[0] += t[0]; pc[1] += t[1]; pc[2] += t[2];
+    }
+    if (pos) { pos[0] = pc[0]; pos[1] = pc[1]; pos[2] = pc[2]; }
+    if (Rout) std::memcpy(Rout, Rc, 72);
+    if (J) {
+        for (int i = 0; i < 7; i++) {
+            double r[3] = {pc[0] - o[i][0], pc[1] - o[i][1], pc[2] - o[i][2]};
+            J[0 * 7 + i] = z[i][1] * r[2] - z[i][2] * r[1];
+            J[1 * 7 + i] = z[i][2] * r[0] - z[i][0] * r[2];
+            J[2 * 7 + i] = z[i][0] * r[1] - z[i][1] * r[0];
+            J[3 * 7 + i] = z[i][0];
+            J[4 * 7 + i] = z[i][1];
+            J[5 * 7 + i] = z[i][2];
+        }
+    }
+}
+
+// det via partial-pivot LU (Eigen MatrixXd::determinant for n>4 -> PartialPivLU)
+static double det_lu(double* A, int n) {
+    double det = 1.0;
+    for (int k = 0; k < n; k++) {
+        int p = k;
+        double mx = std::fabs(A[k * n + k]);
+        for (int i = k + 1; i < n; i++)
+            if (std::fabs(A[i * n + k]) > mx) { mx = std::fabs(A[i * n + k]); p = i; }
+        if (p != k) {
+            for (int j = 0; j < n; j++) std::swap(A[k * n + j], A[p * n + j]);
+            det = -det;
+        }
+        double piv = A[k * n + k];
+        det *= piv;
+        if (piv == 0.0) continue;
+        for (int i = k + 1; i < n; i++) {
+            double f = A[i * n + k] / piv;
+            for (int j = k + 1; j < n; j++) A[i * n + j] -= f * A[k * n + j];
+        }
+    }
+    return det;
+}
+
+// Manipulability — robot_model.cpp:431-435
+static double manipulability(const double* q) {
+    double J[42], JJ[36];
+    fk(q, nullptr, nullptr, J);
+    for (int i = 0; i < 6; i++)
+        for (int j = 0; j < 6; j++) {
+            double s = 0;
+            for (int k = 0; k < 7; k++) s += J[7 * i + k] * J[7 * j + k];
+            JJ[6 * i + j] = s;
+        }
+    return std::sqrt(det_lu(JJ, 6));
+}
+// dManipulability — robot_model.cpp:437-450 (central FD, delta = 1e-4)
+static void dmanipulability(const double* q, double* d) {
+    const double delta = 1e-4;
+    for (int i = 0; i < 7; i++) {
+        double qp[7], qm[7];
+        for (int k = 0; k < 7; k++) { qp[k] = q[k] + (k == i ? delta : 0.0); qm[k] = q[k] - (k == i ? delta : 0.0); }
+        double m1 = manipulability(qp), m2 = manipulability(qm);
+        d[i] = (m1 - m2) / (2 * delta);
+    }
+}
+
+// ------------------------------------------------------------------------------------------------
+// NeRF MLP with forward-mode input Jacobian — SelfCollisionModel.cpp:140-250 (Env identical)
+// ------------------------------------------------------------------------------------------------
+struct MLP {
+    int n_in = 0, n_out = 0;
+    std::vector<int> dims;                 // [3*n_in, hidden..., n_out]
+    std::vector<std::vector<double>> W, b; // W[l] rows=dims[l+1], cols=dims[l]
+    bool ok = false;
+
+    bool load(const std::string& dir, int nin, int nout, const std::vector<int>& hidden) {
+        n_in = nin; n_out = nout;
+        dims.clear(); dims.push_back(3 * nin);
+        for (int h : hidden) dims.push_back(h);
+        dims.push_back(nout);
+        W.assign(dims.size() - 1, {}); b.assign(dims.size() - 1, {});
+        for (size_t l = 0; l + 1 < dims.size(); l++) {
+            size_t nw = (size_t)dims[l + 1] * dims[l], nb = dims[l + 1];
+            W[l].resize(nw); b[l].resize(nb);
+            std::ifstream fw(dir + "/weight_" + std::to_string(l) + ".f64", std::ios::binary);
+            std::ifstream fb(dir + "/bias_" + std::to_string(l) + ".f64", std::ios::binary);
+            if (!fw || !fb) return false;
+            fw.read((char*)W[l].data(), nw * 8);
+            fb.read((char*)b[l].data(), nb * 8);
+            if (!fw || !fb) return false;
+        }
+        ok = true;
+        return true;
+    }
+    // out [n_out], jac [n_out * n_in] row-major
+    void eval(const double* in, double* out, double* jac) const {
+        int L = (int)dims.size() - 1;
+        int n0 = dims[0];
+        std::vector<double> nerf(n0);
+        for (int i = 0; i < n_in; i++) {
+            nerf[i] = in[i];
+            nerf[n_in + i] = std::sin(in[i]);
+            nerf[2 * n_in + i] = std::cos(in[i]);
+        }
+        std::vector<double> hid, hprev;
+        std::vector<double> temp;  // current derivative (rows = layer width, cols = n_in)
+        for (int l = 0; l < L; l++) {
+            int r = dims[l + 1], c = dims[l];
+            const std::vector<double>& x = (l == 0) ? nerf : hprev;
+            hid.assign(r, 0.0);
+            for (int i = 0; i < r; i++) {
+                double s = 0;
+                for (int k = 0; k < c; k++) s += W[l][(size_t)i * c + k] * x[k];
+                hid[i] = s + b[l][i];
+            }
+            if (l == L - 1) {  // output layer :194-203
+                for (int i = 0; i < r; i++) out[i] = hid[i];
+                for (int i = 0; i < r; i++)
+                    for (int j = 0; j < n_in; j++) {
+                        double s = 0;
+                        for (int k = 0; k < c; k++) s += W[l][(size_t)i * c + k] * temp[(size_t)k * n_in + j];
+                        jac[i * n_in + j] = s;
+                    }
+                break;
+            }
+            // hidden_derivative.row(h) = ReLU'(h) * W.row(h); then chain
+            std::vector<double> nt((size_t)r * n_in, 0.0);
+            if (l == 0) {
+                // temp = hd0 * nerf_jac, nerf_jac = [I; diag(cos x); diag(-sin x)]  :177-188
+                for (int i = 0; i < r; i++) {
+                    double g = hid[i] > 0 ? 1.0 : 0.0;
+                    for (int j = 0; j < n_in; j++) {
+                        double h0 = g * W[0][(size_t)i * c + j];
+                        double h1 = g * W[0][(size_t)i * c + n_in + j];
+                        double h2 = g * W[0][(size_t)i * c + 2 * n_in + j];
+                        nt[(size_t)i * n_in + j] = h0 * 1.0 + h1 * std::cos(in[j]) + h2 * (-std::sin(in[j]));
+                    }
+                }
+            } else {
+                for (int i = 0; i < r; i++) {
+                    double g = hid[i] > 0 ? 1.0 : 0.0;
+                    for (int j = 0; j < n_in; j++) {
+                        double s = 0;
+                        for (int k = 0; k < c; k++) s += (g * W[l][(size_t)i * c + k]) * temp[(size_t)k * n_in + j];
+                        nt[(size_t)i * n_in + j] = s;
+                    }
+                }
+            }
+            for (int i = 0; i < r; i++) hid[i] = std::max(0.0, hid[i]);
+            temp.swap(nt);
+            hprev = hid;
+        }
+    }
+};
+
+// ------------------------------------------------------------------------------------------------
+// Oracle state
+// ------------------------------------------------------------------------------------------------
+struct Oracle {
+    OracleParams p;
+    OracleOptions opt;
+    MLP self_nn, env_nn;
+    ArcLengthSpline track;
+    // discretized LTI model (model.cpp:47-91): A = I + Ts e_s e_vs^T, B closed form of expm
+    double A[NX * NX], B[NX * NU];
+
+    void set_params(const OracleParams* pp) {
+        p = *pp;
+        track.proj_max_dist = p.proj_max_dist;
+        for (int i = 0; i < NX * NX; i++) A[i] = (i % (NX + 1) == 0) ? 1.0 : 0.0;
+        for (int i = 0; i < NX * NU; i++) B[i] = 0.0;
+        A[7 * NX + 8] = p.Ts;                          // s <- vs
+        for (int j = 0; j < DOF; j++) B[j * NU + j] = p.Ts;  // q <- dq
+        B[7 * NU + 7] = p.Ts * p.Ts / 2.0;             // s <- dVs
+        B[8 * NU + 7] = p.Ts;                          // vs <- dVs
+    }
+    int N() const { return p.N; }
+    int nvar() const { return (N() + 1) * NX + N() * NU; }
+    int nconstr() const { return (N() + 1) * NX + ((N() + 1) * NX + N() * NU + N() * NU) + (N() + 1) * NPC; }
+};
+
+static void robot_record(const Oracle& o, const double* q, const double* obs, double obs_r, double* rec) {
+    // RobotData::update (robot_data.h:55-71)
+    for (int i = 0; i < REC; i++) rec[i] = 0;
+    fk(q, rec + R_POS, rec + R_ROT, rec + R_J);
+    rec[R_MU] = manipulability(q);
+    dmanipulability(q, rec + R_DMU);
+    if ((o.p.constraint_mask & 1) && o.self_nn.ok) {
+        o.self_nn.eval(q, rec + R_SEL, rec + R_DSEL);
+    } else {
+        rec[R_SEL] = std::numeric_limits<double>::infinity();  // masked: no self-collision data
+    }
+    // RobotData::updateEnv (robot_data.h:74-88)
+    rec[R_OBSR] = obs_r;
+    if ((o.p.constraint_mask & 4) && o.env_nn.ok) {
+        double in[10] = {q[0], q[1], q[2], q[3], q[4], q[5], q[6], obs[0], obs[1], obs[2]};
+        double out[9], jac[90];
+        o.env_nn.eval(in, out, jac);
+        for (int i = 0; i < 9; i++) {
+            rec[R_ENV + i] = out[i];
+            for (int j = 0; j < 7; j++) rec[R_DENV + 7 * i + j] = jac[10 * i + j];  // 9x7 block (Q17)
+        }
+    } else {
+        for (int i = 0; i < 9; i++) rec[R_ENV + i] = std::numeric_limits<double>::infinity();
+    }
+}
+
+// ------------------------------------------------------------------------------------------------
+// Cost — cost.cpp:36-357
+// ------------------------------------------------------------------------------------------------
+static double cubic_blend(double x, double x0, double xf, double y0, double yf) {  // :36-43
+    double t = (x - x0) / (xf - x0);
+    double t2 = std::pow(t, 2), t3 = std::pow(t, 3);
+    return y0 + (yf - y0) * (3 * t2 - 2 * t3);
+}
+
+struct CostOut {
+    double obj;
+    double fx[NX], fu[NU], fxx[NX * NX], fuu[NU * NU], fxu[NX * NU];
+};
+
+static void stage_cost(const Oracle& o, const double* x, const double* u, const double* rec, int k, bool want_grad,
+                       CostOut& out) {
+    const OracleParams& p = o.p;
+    const int N = p.N;
+    // weight schedule :293-308
+    double ratio = std::min(rec[R_SEL] / (p.cost_tol_selcol * 2.0), rec[R_MU] / (p.cost_tol_sing * 2.0));
+    double qc, ql, qo;
+    if (ratio <= 1.0) {
+        qc = p.q_c * cubic_blend(ratio, 0.5, 1.0, p.q_c_red_ratio, 1.0);
+        ql = p.q_l * cubic_blend(ratio, 0.5, 1.0, p.q_l_inc_ratio, 1.0);
+        qo = p.q_ori * cubic_blend(ratio, 0.5, 1.0, p.q_ori_red_ratio, 1.0);
+    } else {
+        qc = p.q_c; ql = p.q_l; qo = p.q_ori;
+    }
+    const double s = x[7], vs = x[8];
+    // getRefPoint :46-68 (Q2: ddz_ref = ddpos(1))
+    double pr[3], dpr[3], ddp[3];
+    o.track.pos(s, pr);
+    o.track.dpos(s, dpr);
+    o.track.ddpos(s, ddp);
+    double ddr[3] = {ddp[0], ddp[1], ddp[1]};
+
+    // ---- contouring + lag + vs (getContouringCost :119-162, getErrorInfo :82-117)
+    const double* pos = rec + R_POS;
+    double et[3] = {pos[0] - pr[0], pos[1] - pr[1], pos[2] - pr[2]};
+    const double* T = dpr;
+    double Te = T[0] * et[0] + T[1] * et[1] + T[2] * et[2];
+    double el[3] = {Te * T[0], Te * T[1], Te * T[2]};
+    double ec[3] = {et[0] - el[0], et[1] - el[1], et[2] - el[2]};
+    // d_total (3x9): q cols = Jv, s col = -T
+    double dt[3][NX] = {};
+    for (int i = 0; i < 3; i++) {
+        for (int j = 0; j < DOF; j++) dt[i][j] = rec[R_J + 7 * i + j];
+        dt[i][7] = -T[i];
+    }
+    double nel = std::sqrt(el[0] * el[0] + el[1] * el[1] + el[2] * el[2]);
+    // d_lag = (T T^T) d_total + (T e^T + |e_l| I) d_T, d_T only in s col = ddr  (Q3)
+    double dl[3][NX], dc[3][NX];
+    for (int i = 0; i < 3; i++)
+        for (int j = 0; j < NX; j++) {
+            double a = T[i] * T[0] * dt[0][j] + T[i] * T[1] * dt[1][j] + T[i] * T[2] * dt[2][j];
+            double b = 0;
+            if (j == 7) {
+                for (int m = 0; m < 3; m++) b += (T[i] * et[m] + (i == m ? nel : 0.0)) * ddr[m];
+            }
+            dl[i][j] = a + b;
+            dc[i][j] = dt[i][j] - dl[i][j];
+        }
+    double CC0 = (k < N) ? qc : p.q_c_N_mult * qc;
+    double CC1 = ql;
+    double s_max = o.track.length();
+    double des = (s < s_max * p.deacc_ratio) ? p.desired_ee_velocity
+                                             : -p.desired_ee_velocity / (s_max * p.deacc_ratio) * (s - s_max);
+    double obj_c = CC0 * (ec[0] * ec[0] + ec[1] * ec[1] + ec[2] * ec[2]) +
+                   CC1 * (el[0] * el[0] + el[1] * el[1] + el[2] * el[2]) + p.q_vs * std::pow(vs - des, 2);
+
+    // ---- heading (getHeadingCost :164-207)
+    double Rref[9], dRref[3];
+    o.track.rot(s, Rref);
+    o.track.drot(s, dRref);
+    const double* Rcur = rec + R_ROT;
+    double Rbar[9], Lm[9], w[3];
+    mat3_mul_tn(Rref, Rcur, Rbar);
+    log_matrix(Rbar, Lm);
+    invskew(Lm, w);
+    double wn2 = w[0] * w[0] + w[1] * w[1] + w[2] * w[2];
+    double obj_h = qo * wn2;
+
+    // ---- input (getInputCost :209-270)
+    double obj_i = 0;
+    if (k != N) {
+        double dq2 = 0;
+        for (int j = 0; j < DOF; j++) dq2 += u[j] * u[j];
+        obj_i = p.r_dq * dq2 + p.r_dVs * std::pow(u[7], 2);
+    }
+    // ---- singularity (:272-288)
+    double obj_s = -p.q_sing * rec[R_MU];
+    out.obj = obj_c + obj_h + obj_i + obj_s;
+    if (!want_grad) return;
+
+    // gradients / Hessians
+    double gxc[NX] = {}, hxc[NX * NX] = {};
+    for (int j = 0; j < NX; j++) {
+        double s1 = 0, s2 = 0;
+        for (int i = 0; i < 3; i++) { s1 += dc[i][j] * ec[i]; s2 += dl[i][j] * el[i]; }
+        gxc[j] = 2.0 * CC0 * s1 + 2.0 * CC1 * s2;
+    }
+    gxc[8] += 2.0 * p.q_vs * (vs - des);
+    for (int a = 0; a < NX; a++)
+        for (int b = 0; b < NX; b++) {
+            double s1 = 0, s2 = 0;
+            for (int i = 0; i < 3; i++) { s1 += dc[i][a] * dc[i][b]; s2 += dl[i][a] * dl[i][b]; }
+            hxc[a * NX + b] = 2.0 * CC0 * s1 + 2.0 * CC1 * s2;
+        }
+    hxc[8 * NX + 8] += 2.0 * p.q_vs;
+
+    // heading linearization :183-205 (Q23: '+' sign in the J_r^{-1} coefficient, as written)
+    double Jri[9];
+    double wn = std::sqrt(wn2);
+    if (wn < 1e-8) {
+        for (int i = 0; i < 9; i++) Jri[i] = (i % 4 == 0) ? 1.0 : 0.0;
+    } else {
+        double S[9], S2[9];
+        skew(w, S);
+        mat3_mul(S, S, S2);
+        double coef = 1. / wn2 + (1. + std::cos(wn)) / (2. * wn * std::sin(wn));
+        for (int i = 0; i < 9; i++) Jri[i] = ((i % 4 == 0) ? 1.0 : 0.0) + 1. / 2. * S[i] + coef * S2[i];
+    }
+    double JRt[9];  // J_r_inv * cur_R^T
+    for (int i = 0; i < 3; i++)
+        for (int j = 0; j < 3; j++) {
+            double sacc = 0;
+            for (int m = 0; m < 3; m++) sacc += Jri[3 * i + m] * Rcur[3 * j + m];
+            JRt[3 * i + j] = sacc;
+        }
+    double dL[3][NX] = {};
+    for (int i = 0; i < 3; i++) {
+        for (int j = 0; j < DOF; j++) {
+            double sacc = 0;
+            for (int m = 0; m < 3; m++) sacc += JRt[3 * i + m] * rec[R_J + 7 * (3 + m) + j];
+            dL[i][j] = sacc;
+        }
+        double sacc = 0;
+        for (int m = 0; m < 3; m++) sacc += JRt[3 * i + m] * dRref[m];
+        dL[i][7] = -sacc;
+    }
+    double gxh[NX], hxh[NX * NX];
+    for (int j = 0; j < NX; j++) {
+        double sacc = 0;
+        for (int i = 0; i < 3; i++) sacc += dL[i][j] * w[i];
+        gxh[j] = 2.0 * qo * sacc;
+    }
+    for (int a = 0; a < NX; a++)
+        for (int b = 0; b < NX; b++) {
+            double sacc = 0;
+            for (int i = 0; i < 3; i++) sacc += dL[i][a] * dL[i][b];
+            hxh[a * NX + b] = 2.0 * qo * sacc;
+        }
+    // input grads
+    double gui[NU] = {}, huu[NU * NU] = {};
+    if (k != N) {
+        for (int j = 0; j < DOF; j++) gui[j] = 2.0 * p.r_dq * u[j];
+        gui[7] = 2.0 * p.r_dVs * u[7];
+        for (int j = 0; j < DOF; j++) huu[j * NU + j] = 2.0 * p.r_dq;
+        huu[7 * NU + 7] = 2.0 * p.r_dVs;
+    }
+    double gxs[NX] = {};
+    for (int j = 0; j < DOF; j++) gxs[j] = -p.q_sing * rec[R_DMU + j];
+
+    for (int j = 0; j < NX; j++) out.fx[j] = gxc[j] + gxh[j] + 0.0 + gxs[j];
+    for (int j = 0; j < NU; j++) out.fu[j] = 0.0 + 0.0 + gui[j] + 0.0;
+    for (int i = 0; i < NX * NX; i++) out.fxx[i] = hxc[i] + hxh[i] + 0.0 + 0.0;
+    for (int i = 0; i < NU * NU; i++) out.fuu[i] = 0.0 + 0.0 + huu[i] + 0.0;
+    for (int i = 0; i < NX * NU; i++) out.fxu[i] = 0.0;
+    for (int i = 0; i < NX; i++) out.fxx[i * NX + i] += 1e-6;  // :353-354
+    for (int i = 0; i < NU; i++) out.fuu[i * NU + i] += 1e-6;
+}
+
+// ------------------------------------------------------------------------------------------------
+// Constraints — constraints.cpp:34-243
+// ------------------------------------------------------------------------------------------------
+static double rbf(double delta, double h) {  // :34-43
+    if (h >= delta) return -std::log(h + 1);
+    return -std::log(delta + 1) - 1 / (delta + 1) * (h - delta) + 1 / (2 * std::pow(delta + 1, 2)) * std::pow(h - delta, 2);
+}
+static double drbf(double delta, double h) {  // :52-61
+    if (h >= delta) return -1 / (h + 1);
+    return -1 / (delta + 1) + 1 / (std::pow(delta + 1, 2)) * (h - delta);
+}
+
+struct ConOut {
+    double c[NPC], l[NPC], u[NPC];
+    double cx[NPC * NX], cu[NPC * NU];
+};
+
+static void stage_constraints(const Oracle& o, const double* x, const double* u, const double* rec, int k, bool want_jac,
+                              ConOut& out) {
+    const OracleParams& p = o.p;
+    const int N = p.N;
+    std::memset(&out, 0, sizeof out);
+    const double delta = -0.5;
+    auto masked = [&](int r) { out.c[r] = 0; out.l[r] = -INF; out.u[r] = INF; };
+    // self collision :70-108
+    if (p.constraint_mask & 1) {
+        double md = 0.01 * rec[R_SEL];
+        double dmd[DOF];
+        for (int j = 0; j < DOF; j++) dmd[j] = 0.01 * rec[R_DSEL + j];
+        double r = p.con_tol_selcol * 0.01;
+        double R = rbf(delta, md - r);
+        if (k != N) {
+            double dot = 0;
+            for (int j = 0; j < DOF; j++) dot += dmd[j] * u[j];
+            out.l[0] = -INF; out.u[0] = 0.0; out.c[0] = -dot + R;
+            if (want_jac) {
+                double dR = drbf(delta, md - r);
+                for (int j = 0; j < DOF; j++) { out.cx[0 * NX + j] = dR * dmd[j]; out.cu[0 * NU + j] = -dmd[j]; }
+            }
+        }
+    } else if (k != N) masked(0);
+    // singularity :110-147
+    if (p.constraint_mask & 2) {
+        double mu = rec[R_MU];
+        double eps = p.con_tol_sing;
+        double R = rbf(delta, mu - eps);
+        if (k != N) {
+            double dot = 0;
+            for (int j = 0; j < DOF; j++) dot += rec[R_DMU + j] * u[j];
+            out.l[1] = -INF; out.u[1] = 0.0; out.c[1] = -dot + R;
+            if (want_jac) {
+                double dR = drbf(delta, mu - eps);
+                for (int j = 0; j < DOF; j++) { out.cx[1 * NX + j] = dR * rec[R_DMU + j]; out.cu[1 * NU + j] = -rec[R_DMU + j]; }
+            }
+        }
+    } else if (k != N) masked(1);
+    // env collision :149-190
+    if (p.constraint_mask & 4) {
+        double r = 0.01 * p.con_tol_envcol;
+        for (int m = 0; m < NLINK; m++) {
+            double md = 0.01 * (rec[R_ENV + m] - rec[R_OBSR] * 1.2);
+            double R = rbf(delta, md - r);
+            if (k != N) {
+                double dot = 0;
+                for (int j = 0; j < DOF; j++) dot += (0.01 * rec[R_DENV + 7 * m + j]) * u[j];
+                out.l[2 + m] = -INF; out.u[2 + m] = 0.0; out.c[2 + m] = -dot + R;
+                if (want_jac) {
+                    double dR = drbf(delta, md - r);
+                    for (int j = 0; j < DOF; j++) {
+                        double g = 0.01 * rec[R_DENV + 7 * m + j];
+                        out.cx[(2 + m) * NX + j] = dR * g;
+                        out.cu[(2 + m) * NU + j] = -g;
+                    }
+                }
+            }
+        }
+    } else if (k != N) for (int m = 0; m < NLINK; m++) masked(2 + m);
+}
+
+// ------------------------------------------------------------------------------------------------
+// Dense QP assembly in the reference layout — osqp_interface.cpp:129-396
+// guess layout here: (N+1) x [x(9), u(8)]  (u of stage N is zero/unused)
+// ------------------------------------------------------------------------------------------------
+struct DenseQP {
+    int nv, nc;
+    double obj;
+    std::vector<double> P, g, A, c, l, u;
+};
+
+static inline const double* gx(const double* guess, int i) { return guess + 17 * i; }
+static inline const double* gu(const double* guess, int i) { return guess + 17 * i + 9; }
+
+// setCost (:129-219) + setConstraints (:221-389).  want: 0 = obj/constr/l/u only, 1 = full.
+static void set_qp(const Oracle& o, const double* guess, const double* recs, const double* ucur, bool full, DenseQP& q) {
+    const OracleParams& p = o.p;
+    const int N = p.N;
+    const double* Tx = p.Tx; const double* Tu = p.Tu;
+    q.nv = o.nvar(); q.nc = o.nconstr();
+    const int nv = q.nv, nc = q.nc;
+    const int Neq = (N + 1) * NX, Nib = nv + N * NU;
+    q.obj = 0;
+    if (full) { q.P.assign((size_t)nv * nv, 0.0); q.g.assign(nv, 0.0); q.A.assign((size_t)nc * nv, 0.0); }
+    q.c.assign(nc, 0.0); q.l.assign(nc, 0.0); q.u.assign(nc, 0.0);
+    auto P = [&](int i, int j) -> double& { return q.P[(size_t)i * nv + j]; };
+    auto A = [&](int i, int j) -> double& { return q.A[(size_t)i * nv + j]; };
+    const double rddq = p.qp_r_ddq;
+    // ---- cost
+    for (int i = 0; i <= N; i++) {
+        CostOut co;
+        stage_cost(o, gx(guess, i), gu(guess, i), recs + (size_t)REC * i, i, full, co);
+        q.obj += co.obj;
+        if (full) {
+            for (int a = 0; a < NX; a++) q.g[NX * i + a] = Tx[a] * co.fx[a];
+            for (int a = 0; a < NX; a++)
+                for (int b = 0; b < NX; b++) P(NX * i + a, NX * i + b) = Tx[a] * co.fxx[a * NX + b] * Tx[b];
+            if (i != N) {
+                int u0 = NX * (N + 1) + NU * i;
+                for (int a = 0; a < NU; a++) q.g[u0 + a] = Tu[a] * co.fu[a];
+                for (int a = 0; a < NU; a++)
+                    for (int b = 0; b < NU; b++) P(u0 + a, u0 + b) = Tu[a] * co.fuu[a * NU + b] * Tu[b];
+                for (int a = 0; a < NX; a++)
+                    for (int b = 0; b < NU; b++) {
+                        double v = Tx[a] * co.fxu[a * NU + b] * Tu[b];
+                        P(NX * i + a, u0 + b) = v;
+                        P(u0 + b, NX * i + a) = v;
+                    }
+            }
+        }
+        if (i != N) {  // ddq cost :166-217
+            const double* ui = gu(guess, i);
+            if (i != N - 1) {
+                const double* un = gu(guess, i + 1);
+                double sq = 0;
+                for (int j = 0; j < DOF; j++) sq += (un[j] - ui[j]) * (un[j] - ui[j]);
+                q.obj += rddq * sq;
+            }
+            if (full) {
+                int u0 = NX * (N + 1) + NU * i;
+                for (int j = 0; j < DOF; j++) {
+                    double gg;
+                    if (i == 0) gg = 2. * rddq * (ui[j] - gu(guess, i + 1)[j]);
+                    else if (i == N - 1) gg = 2. * rddq * (ui[j] - gu(guess, i - 1)[j]);
+                    else gg = 2. * rddq * (2. * ui[j] - gu(guess, i + 1)[j] - gu(guess, i - 1)[j]);
+                    q.g[u0 + j] += Tu[j] * gg;
+                }
+                double cii, cij;
+                if (i == 0) { cii = 2. * rddq; cij = -2. * rddq; }
+                else if (i == N - 1) { cii = 2. * rddq; cij = 0; }
+                else { cii = 4. * rddq; cij = -2. * rddq; }
+                for (int j = 0; j < DOF; j++) {
+                    P(u0 + j, u0 + j) += Tu[j] * cii * Tu[j];
+                    if (i != N - 1) {
+                        P(u0 + j, u0 + NU + j) += Tu[j] * cij * Tu[j];
+                        P(u0 + NU + j, u0 + j) += Tu[j] * cij * Tu[j];
+                    }
+                }
+            }
+        }
+    }
+    // ---- dynamics (setDynamics :221-252)
+    for (int i = 0; i <= N; i++) {
+        if (i == 0) {
+            if (full) for (int a = 0; a < NX; a++) A(a, a) = 1.0;
+            continue;
+        }
+        const double* xp = gx(guess, i - 1); const double* up = gu(guess, i - 1); const double* xi = gx(guess, i);
+        double pred[NX];
+        for (int a = 0; a < NX; a++) {
+            double s1 = 0, s2 = 0;
+            for (int b = 0; b < NX; b++) s1 += o.A[a * NX + b] * xp[b];
+            for (int b = 0; b < NU; b++) s2 += o.B[a * NU + b] * up[b];
+            pred[a] = s1 + s2 + 0.0;
+        }
+        for (int a = 0; a < NX; a++) q.c[NX * i + a] = (1.0 / Tx[a]) * (xi[a] - pred[a]);
+        if (full) {
+            for (int a = 0; a < NX; a++) {
+                for (int b = 0; b < NX; b++) A(NX * i + a, NX * (i - 1) + b) = -(1.0 / Tx[a]) * o.A[a * NX + b] * Tx[b];
+                A(NX * i + a, NX * i + a) = 1.0;
+                for (int b = 0; b < NU; b++)
+                    A(NX * i + a, NX * (N + 1) + NU * (i - 1) + b) = -(1.0 / Tx[a]) * o.B[a * NU + b] * Tu[b];
+            }
+        }
+    }
+    // ---- bounds (setBounds :254-300, Bounds::getBounds* bounds.cpp:85-128)
+    const double L = o.track.length();
+    for (int i = 0; i <= N; i++) {
+        const double* xi = gx(guess, i);
+        int r0 = Neq + NX * i;
+        for (int a = 0; a < NX; a++) {
+            if (full) A(r0 + a, NX * i + a) = Tx[a];
+            q.c[r0 + a] = xi[a];
+            q.l[r0 + a] = p.lx[a];
+            q.u[r0 + a] = p.ux[a];
+        }
+        q.l[r0 + 7] = std::max(xi[7] - p.s_trust_region, 0.);
+        q.u[r0 + 7] = std::min(xi[7] + p.s_trust_region, L);
+        if (i != N) {
+            const double* ui = gu(guess, i);
+            int r1 = Neq + NX * (N + 1) + NU * i;  // input bounds, Q1: columns NU*i (state columns)
+            for (int a = 0; a < NU; a++) {
+                if (full) A(r1 + a, NU * i + a) = Tu[a];
+                q.c[r1 + a] = ui[a];
+                q.l[r1 + a] = p.lu[a];
+                q.u[r1 + a] = p.uu[a];
+            }
+            int r2 = Neq + NX * (N + 1) + NU * N + NU * i;  // ddq rows (8th row zero: Q15)
+            for (int j = 0; j < DOF; j++) {
+                if (i == 0) {
+                    if (full) A(r2 + j, NX * (N + 1) + NU * i + j) = 1. / p.Ts * Tu[j];
+                    q.c[r2 + j] = 1. / p.Ts * ui[j];
+                    q.l[r2 + j] = p.lddq[j] + 1. / p.Ts * ucur[j];
+                    q.u[r2 + j] = p.uddq[j] + 1. / p.Ts * ucur[j];
+                } else {
+                    if (full) {
+                        A(r2 + j, NX * (N + 1) + NU * i + j) = 1. / p.Ts * Tu[j];
+                        A(r2 + j, NX * (N + 1) + NU * (i - 1) + j) = -1. / p.Ts * Tu[j];
+                    }
+                    q.c[r2 + j] = 1. / p.Ts * (ui[j] - gu(guess, i - 1)[j]);
+                    q.l[r2 + j] = p.lddq[j];
+                    q.u[r2 + j] = p.uddq[j];
+                }
+            }
+        }
+    }
+    // ---- polytopic (setPolytopicConstraints :302-344)
+    for (int i = 0; i <= N; i++) {
+        ConOut co;
+        stage_constraints(o, gx(guess, i), gu(guess, i), recs + (size_t)REC * i, i, full, co);
+        int r0 = Neq + Nib + NPC * i;
+        for (int r = 0; r < NPC; r++) {
+            q.c[r0 + r] = co.c[r]; q.l[r0 + r] = co.l[r]; q.u[r0 + r] = co.u[r];
+            if (full) {
+                for (int a = 0; a < NX; a++) A(r0 + r, NX * i + a) = co.cx[r * NX + a] * Tx[a];
+                if (i != N)
+                    for (int b = 0; b < NU; b++) A(r0 + r, NX * (N + 1) + NU * i + b) = co.cu[r * NU + b] * Tu[b];
+            }
+        }
+    }
+}
+
+// constraint_norm — osqp_interface.cpp:824-833
+static double constraint_norm(const DenseQP& q) {
+    double a = 0, b = 0;
+    for (int i = 0; i < q.nc; i++) a += std::max(q.l[i] - q.c[i], 0.0);
+    for (int i = 0; i < q.nc; i++) b += std::max(q.c[i] - q.u[i], 0.0);
+    return a + b;
+}
+
+// ------------------------------------------------------------------------------------------------
+// QP solvers (replacing OSQP, osqp_interface.cpp:592-656)
+// ------------------------------------------------------------------------------------------------
+constexpr double BIG = 1e20;  // |bound| >= BIG is treated as infinite (OSQP_INFTY semantics)
+constexpr int IPM_MAX_IT = 60;
+constexpr double IPM_TOL_MU = 1e-13, IPM_TOL_P = 1e-11, IPM_TOL_STEP = 1e-11;
+constexpr double FEAS_TOL = 1e-9;
+
+// ---------------- stage-structured primal-dual IPM with a Riccati factorization ----------------
+// Stage vector z_k = [y(9) | w(7) | v(8)] (normalized step of x_k; w_k = previous joint-input step
+// v_{k-1}[0:7]; v_k = normalized step of u_k).  Dynamics: y_{k+1} = M y_k + G v_k, w_{k+1} = E v_k
+// with M = Tx^-1 A Tx, G = Tx^-1 B Tu.  y_0 = 0, w_0 = 0 (dynamics row block 0, osqp_interface.cpp:231-237).
+constexpr int NZ = 24, NXA = 16;
+
+struct SRow { double c[NZ]; double lb, ub; };
+struct SStage {
+    double H[NZ * NZ];
+    double h[NZ];
+    double b[NX];            // y_{k+1} = M y_k + G v_k + b_k  (b_k = -c_{k+1})
+    std::vector<SRow> rows;
+};
+
+struct StructQP {
+    int N;
+    double M[NX * NX], G[NX * NU];
+    std::vector<SStage> st;  // N+1 stages (stage N has no v)
+    bool infeasible = false;
+};
+
+// Build the stage-structured QP equivalent to the dense layout (same primal solution).
+static void build_struct_qp(const Oracle& o, const double* guess, const double* recs, const double* ucur, StructQP& S) {
+    const OracleParams& p = o.p;
+    const int N = p.N;
+    const double* Tx = p.Tx; const double* Tu = p.Tu;
+    S.N = N;
+    S.st.assign(N + 1, SStage());
+    S.infeasible = false;
+    for (int a = 0; a < NX; a++) {
+        for (int b = 0; b < NX; b++) S.M[a * NX + b] = (1.0 / Tx[a]) * o.A[a * NX + b] * Tx[b];
+        for (int b = 0; b < NU; b++) S.G[a * NU + b] = (1.0 / Tx[a]) * o.B[a * NU + b] * Tu[b];
+    }
+    const double rddq = p.qp_r_ddq;
+    const double L = o.track.length();
+    // Box bounds on y (state bounds + Q1 rows), accumulated as intersections in y-units.
+    std::vector<double> ylb((N + 1) * NX, -INF), yub((N + 1) * NX, INF);
+    auto add_box = [&](int k, int m, double lo, double hi) {
+        if (lo > -BIG) ylb[k * NX + m] = std::max(ylb[k * NX + m], lo);
+        if (hi < BIG) yub[k * NX + m] = std::min(yub[k * NX + m], hi);
+    };
+    for (int k = 0; k <= N; k++) {
+        SStage& s = S.st[k];
+        std::memset(s.H, 0, sizeof s.H); std::memset(s.h, 0, sizeof s.h); std::memset(s.b, 0, sizeof s.b);
+        const double* xk = gx(guess, k); const double* uk = gu(guess, k);
+        CostOut co;
+        stage_cost(o, xk, uk, recs + (size_t)REC * k, k, true, co);
+        for (int a = 0; a < NX; a++) {
+            s.h[a] = Tx[a] * co.fx[a];
+            for (int b = 0; b < NX; b++) s.H[a * NZ + b] = Tx[a] * co.fxx[a * NX + b] * Tx[b];
+        }
+        if (k != N) {
+            for (int a = 0; a < NU; a++) {
+                s.h[16 + a] = Tu[a] * co.fu[a];
+                for (int b = 0; b < NU; b++) s.H[(16 + a) * NZ + 16 + b] = Tu[a] * co.fuu[a * NU + b] * Tu[b];
+                for (int b = 0; b < NX; b++) {
+                    double v = Tx[b] * co.fxu[b * NU + a] * Tu[a];
+                    s.H[(16 + a) * NZ + b] = v; s.H[b * NZ + 16 + a] = v;
+                }
+            }
+            // ddq cost gradient + diagonal, coupling to v_{k-1} via w_k
+            for (int j = 0; j < DOF; j++) {
+                double gg;
+                if (k == 0) gg = 2. * rddq * (uk[j] - gu(guess, k + 1)[j]);
+                else if (k == N - 1) gg = 2. * rddq * (uk[j] - gu(guess, k - 1)[j]);
+                else gg = 2. * rddq * (2. * uk[j] - gu(guess, k + 1)[j] - gu(guess, k - 1)[j]);
+                s.h[16 + j] += Tu[j] * gg;
+                double cii = (k == 0 || k == N - 1) ? 2. * rddq : 4. * rddq;
+                s.H[(16 + j) * NZ + 16 + j] += Tu[j] * cii * Tu[j];
+                if (k >= 1) {  // coupling between v_{k-1} (= w_k) and v_k, present when k-1 != N-1
+                    double cij = -2. * rddq;
+                    double v = Tu[j] * cij * Tu[j];
+                    s.H[(16 + j) * NZ + 9 + j] += v;
+                    s.H[(9 + j) * NZ + 16 + j] += v;
+                }
+            }
+        }
+        // dynamics offset b_k = -c_{k+1}
+        if (k < N) {
+            const double* xn = gx(guess, k + 1);
+            for (int a = 0; a < NX; a++) {
+                double s1 = 0, s2 = 0;
+                for (int b = 0; b < NX; b++) s1 += o.A[a * NX + b] * xk[b];
+                for (int b = 0; b < NU; b++) s2 += o.B[a * NU + b] * uk[b];
+                double pred = s1 + s2 + 0.0;
+                s.b[a] = -((1.0 / Tx[a]) * (xn[a] - pred));
+            }
+        }
+        // state bounds
+        for (int a = 0; a < NX; a++) {
+            double lo = p.lx[a], hi = p.ux[a];
+            if (a == 7) { lo = std::max(xk[7] - p.s_trust_region, 0.); hi = std::min(xk[7] + p.s_trust_region, L); }
+            add_box(k, a, (lo - xk[a]) / Tx[a], (hi - xk[a]) / Tx[a]);
+        }
+        if (k != N) {
+            // Q1 input-bound rows: variable index NU*k + a of the stacked state-step vector
+            for (int a = 0; a < NU; a++) {
+                int idx = NU * k + a;
+                int kk = idx / NX, m = idx % NX;
+                add_box(kk, m, (p.lu[a] - uk[a]) / Tu[a], (p.uu[a] - uk[a]) / Tu[a]);
+            }
+            // ddq rows
+            for (int j = 0; j < DOF; j++) {
+                double coef = 1. / p.Ts * Tu[j];
+                SRow r; std::memset(r.c, 0, sizeof r.c);
+                double c, lo, hi;
+                if (k == 0) {
+                    c = 1. / p.Ts * uk[j];
+                    lo = p.lddq[j] + 1. / p.Ts * ucur[j];
+                    hi = p.uddq[j] + 1. / p.Ts * ucur[j];
+                    r.c[16 + j] = 1.0;
+                } else {
+                    c = 1. / p.Ts * (uk[j] - gu(guess, k - 1)[j]);
+                    lo = p.lddq[j]; hi = p.uddq[j];
+                    r.c[16 + j] = 1.0; r.c[9 + j] = -1.0;
+                }
+                r.lb = (lo - c) / coef; r.ub = (hi - c) / coef;
+                s.rows.push_back(r);
+            }
+            // polytopic rows
+            ConOut cn;
+            stage_constraints(o, xk, uk, recs + (size_t)REC * k, k, true, cn);
+            for (int r = 0; r < NPC; r++) {
+                double lo = cn.l[r] - cn.c[r], hi = cn.u[r] - cn.c[r];
+                bool lo_inf = cn.l[r] <= -BIG, hi_inf = cn.u[r] >= BIG;
+                if (lo_inf && hi_inf) continue;
+                SRow row; std::memset(row.c, 0, sizeof row.c);
+                for (int a = 0; a < NX; a++) row.c[a] = cn.cx[r * NX + a] * Tx[a];
+                for (int b = 0; b < NU; b++) row.c[16 + b] = cn.cu[r * NU + b] * Tu[b];
+                row.lb = lo_inf ? -INF : lo;
+                row.ub = hi_inf ? INF : hi;
+                s.rows.push_back(row);
+            }
+        }
+    }
+    // stage-0 y rows are constants (y_0 = 0): feasibility check only
+    for (int m = 0; m < NX; m++) {
+        if (ylb[m] > FEAS_TOL || yub[m] < -FEAS_TOL) S.infeasible = true;
+    }
+    for (int k = 1; k <= N; k++)
+        for (int m = 0; m < NX; m++) {
+            double lo = ylb[k * NX + m], hi = yub[k * NX + m];
+            if (lo > hi) { S.infeasible = true; continue; }
+            if (lo <= -BIG && hi >= BIG) continue;
+            SRow r; std::memset(r.c, 0, sizeof r.c);
+            r.c[m] = 1.0; r.lb = lo; r.ub = hi;
+            S.st[k].rows.push_back(r);
+        }
+}
+
+// Cholesky in place (lower), returns false if not PD
+static bool chol(double* F, int n) {
+    for (int j = 0; j < n; j++) {
+        double d = F[j * n + j];
+        for (int k = 0; k < j; k++) d -= F[j * n + k] * F[j * n + k];
+        if (!(d > 0)) return false;
+        d = std::sqrt(d);
+        F[j * n + j] = d;
+        for (int i = j + 1; i < n; i++) {
+            double s = F[i * n + j];
+            for (int k = 0; k < j; k++) s -= F[i * n + k] * F[j * n + k];
+            F[i * n + j] = s / d;
+        }
+        for (int i = 0; i < j; i++) F[i * n + j] = 0;
+    }
+    return true;
+}
+static void chol_solve(const double* L, int n, double* x) {
+    for (int i = 0; i < n; i++) {
+        double s = x[i];
+        for (int k = 0; k < i; k++) s -= L[i * n + k] * x[k];
+        x[i] = s / L[i * n + i];
+    }
+    for (int i = n - 1; i >= 0; i--) {
+        double s = x[i];
+        for (int k = i + 1; k < n; k++) s -= L[k * n + i] * x[k];
+        x[i] = s / L[i * n + i];
+    }
+}
+
+struct Ineq { int k; int row; double sgn; double bnd; };  // sgn*(c^T z_k) <= sgn*bnd
+
+// Riccati factorization of the step system with stage Hessians Hk (NZ x NZ) and the solve for gk.
+struct Riccati {
+    int N;
+    std::vector<double> K, kff, LF, Gm;   // per stage: K 8x16, kff 8, LF 8x8, Gm 8x16
+    bool factor(const StructQP& S, const std::vector<double>& Hs) {
+        N = S.N;
+        K.assign((size_t)N * NU * NXA, 0); kff.assign((size_t)N * NU, 0);
+        LF.assign((size_t)N * NU * NU, 0); Gm.assign((size_t)N * NU * NXA, 0);
+        // A~ = [[M,0],[0,0]], B~ = [[G],[E]]
+        double At[NXA * NXA] = {}, Bt[NXA * NU] = {};
+        for (int a = 0; a < NX; a++) {
+            for (int b = 0; b < NX; b++) At[a * NXA + b] = S.M[a * NX + b];
+            for (int b = 0; b < NU; b++) Bt[a * NU + b] = S.G[a * NU + b];
+        }
+        for (int j = 0; j < DOF; j++) Bt[(9 + j) * NU + j] = 1.0;
+        double P[NXA * NXA];
+        const double* HN = &Hs[(size_t)N * NZ * NZ];
+        for (int a = 0; a < NXA; a++)
+            for (int b = 0; b < NXA; b++) P[a * NXA + b] = HN[a * NZ + b];
+        for (int k = N - 1; k >= 0; k--) {
+            const double* H = &Hs[(size_t)k * NZ * NZ];
+            double PB[NXA * NU], PA[NXA * NXA];
+            for (int a = 0; a < NXA; a++) {
+                for (int j = 0; j < NU; j++) { double s = 0; for (int m = 0; m < NXA; m++) s += P[a * NXA + m] * Bt[m * NU + j]; PB[a * NU + j] = s; }
+                for (int j = 0; j < NXA; j++) { double s = 0; for (int m = 0; m < NXA; m++) s += P[a * NXA + m] * At[m * NXA + j]; PA[a * NXA + j] = s; }
+            }
+            double F[NU * NU], Gk[NU * NXA], Hb[NXA * NXA];
+            for (int i = 0; i < NU; i++)
+                for (int j = 0; j < NU; j++) {
+                    double s = 0; for (int m = 0; m < NXA; m++) s += Bt[m * NU + i] * PB[m * NU + j];
+                    F[i * NU + j] = H[(16 + i) * NZ + 16 + j] + s;
+                }
+            for (int i = 0; i < NU; i++)
+                for (int j = 0; j < NXA; j++) {
+                    double s = 0; for (int m = 0; m < NXA; m++) s += Bt[m * NU + i] * PA[m * NXA + j];
+                    Gk[i * NXA + j] = H[(16 + i) * NZ + j] + s;
+                }
+            for (int i = 0; i < NXA; i++)
+                for (int j = 0; j < NXA; j++) {
+                    double s = 0; for (int m = 0; m < NXA; m++) s += At[m * NXA + i] * PA[m * NXA + j];
+                    Hb[i * NXA + j] = H[i * NZ + j] + s;
+                }
+            if (!chol(F, NU)) return false;
+            double* Kk = &K[(size_t)k * NU * NXA];
+            for (int j = 0; j < NXA; j++) {
+                double col[NU];
+                for (int i = 0; i < NU; i++) col[i] = Gk[i * NXA + j];
+                chol_solve(F, NU, col);
+                for (int i = 0; i < NU; i++) Kk[i * NXA + j] = -col[i];
+            }
+            std::memcpy(&LF[(size_t)k * NU * NU], F, sizeof F);
+            std::memcpy(&Gm[(size_t)k * NU * NXA], Gk, sizeof Gk);
+            for (int i = 0; i < NXA; i++)
+                for (int j = 0; j < NXA; j++) {
+                    double s = 0; for (int m = 0; m < NU; m++) s += Gk[m * NXA + i] * Kk[m * NXA + j];
+                    P[i * NXA + j] = Hb[i * NXA + j] + s;
+                }
+            for (int i = 0; i < NXA; i++)  // symmetrize
+                for (int j = i + 1; j < NXA; j++) { double v = 0.5 * (P[i * NXA + j] + P[j * NXA + i]); P[i * NXA + j] = P[j * NXA + i] = v; }
+        }
+        return true;
+    }
+    // solve for gradient gs (per stage NZ) -> dz (per stage NZ); dynamics homogeneous, z~_0 = 0
+    void solve(const StructQP& S, const std::vector<double>& gs, std::vector<double>& dz) const {
+        double At[NXA * NXA] = {}, Bt[NXA * NU] = {};
+        for (int a = 0; a < NX; a++) {
+            for (int b = 0; b < NX; b++) At[a * NXA + b] = S.M[a * NX + b];
+            for (int b = 0; b < NU; b++) Bt[a * NU + b] = S.G[a * NU + b];
+        }
+        for (int j = 0; j < DOF; j++) Bt[(9 + j) * NU + j] = 1.0;
+        std::vector<double> kf((size_t)N * NU);
+        double pv[NXA];
+        for (int a = 0; a < NXA; a++) pv[a] = gs[(size_t)N * NZ + a];
+        for (int k = N - 1; k >= 0; k--) {
+            const double* g = &gs[(size_t)k * NZ];
+            double f[NU];
+            for (int i = 0; i < NU; i++) { double s = 0; for (int m = 0; m < NXA; m++) s += Bt[m * NU + i] * pv[m]; f[i] = g[16 + i] + s; }
+            chol_solve(&LF[(size_t)k * NU * NU], NU, f);
+            for (int i = 0; i < NU; i++) kf[(size_t)k * NU + i] = -f[i];
+            const double* Gk = &Gm[(size_t)k * NU * NXA];
+            double np[NXA];
+            for (int i = 0; i < NXA; i++) {
+                double s = 0; for (int m = 0; m < NXA; m++) s += At[m * NXA + i] * pv[m];
+                double t = 0; for (int m = 0; m < NU; m++) t += Gk[m * NXA + i] * kf[(size_t)k * NU + m];
+                np[i] = g[i] + s + t;
+            }
+            std::memcpy(pv, np, sizeof np);
+        }
+        dz.assign((size_t)(N + 1) * NZ, 0.0);
+        double x[NXA] = {};
+        for (int k = 0; k < N; k++) {
+            double* z = &dz[(size_t)k * NZ];
+            for (int a = 0; a < NXA; a++) z[a] = x[a];
+            const double* Kk = &K[(size_t)k * NU * NXA];
+            for (int i = 0; i < NU; i++) { double s = 0; for (int m = 0; m < NXA; m++) s += Kk[i * NXA + m] * x[m]; z[16 + i] = s + kf[(size_t)k * NU + i]; }
+            double xn[NXA];
+            for (int a = 0; a < NXA; a++) {
+                double s = 0; for (int m = 0; m < NXA; m++) s += At[a * NXA + m] * x[m];
+                for (int m = 0; m < NU; m++) s += Bt[a * NU + m] * z[16 + m];
+                xn[a] = s;
+            }
+            std::memcpy(x, xn, sizeof xn);
+        }
+        for (int a = 0; a < NXA; a++) dz[(size_t)N * NZ + a] = x[a];
+    }
+};
+
+// Returns 0 on success (step filled in reference layout: [y_0..y_N | v_0..v_{N-1}]), else Status.
+static int solve_struct_ipm(const StructQP& S, std::vector<double>& step, int* iters_out) {
+    const int N = S.N;
+    if (S.infeasible) return QP_PrimalInfeasible;
+    std::vector<Ineq> I;
+    for (int k = 0; k <= N; k++)
+        for (int r = 0; r < (int)S.st[k].rows.size(); r++) {
+            const SRow& row = S.st[k].rows[r];
+            if (row.lb > -BIG) I.push_back({k, r, -1.0, row.lb});
+            if (row.ub < BIG) I.push_back({k, r, 1.0, row.ub});
+        }
+    const int m = (int)I.size();
+    // initial primal: dynamics rollout with v = 0
+    std::vector<double> z((size_t)(N + 1) * NZ, 0.0);
+    for (int k = 0; k < N; k++) {
+        const double* zk = &z[(size_t)k * NZ];
+        double* zn = &z[(size_t)(k + 1) * NZ];
+        for (int a = 0; a < NX; a++) {
+            double s = 0; for (int b = 0; b < NX; b++) s += S.M[a * NX + b] * zk[b];
+            zn[a] = s + S.st[k].b[a];
+        }
+    }
+    auto rowdot = [&](const Ineq& q, const std::vector<double>& zz) {
+        const SRow& row = S.st[q.k].rows[q.row];
+        const double* zk = &zz[(size_t)q.k * NZ];
+        double s = 0; for (int a = 0; a < NZ; a++) s += row.c[a] * zk[a];
+        return s;
+    };
+    std::vector<double> sl(m), lam(m, 1.0), rp(m), W(m), dsa(m), dla(m), ds(m), dl(m), rc(m);
+    for (int i = 0; i < m; i++) {
+        double g = I[i].sgn * rowdot(I[i], z) - I[i].sgn * I[i].bnd;
+        sl[i] = std::max(-g, 1.0);
+    }
+    std::vector<double> Hs((size_t)(N + 1) * NZ * NZ), gs((size_t)(N + 1) * NZ), dz, dza;
+    Riccati R;
+    int it;
+    bool conv = false;
+    double last_dz = 1e30;
+    for (it = 0; it < IPM_MAX_IT; it++) {
+        double mu = 0, rpmax = 0;
+        for (int i = 0; i < m; i++) {
+            rp[i] = I[i].sgn * rowdot(I[i], z) - I[i].sgn * I[i].bnd + sl[i];
+            mu += sl[i] * lam[i];
+            rpmax = std::max(rpmax, std::fabs(rp[i]));
+        }
+        mu = (m > 0) ? mu / m : 0.0;
+        if (it > 0 && mu < IPM_TOL_MU && rpmax < IPM_TOL_P && last_dz < IPM_TOL_STEP) {
+            conv = true;
+            break;
+        }
+        for (int i = 0; i < m; i++) W[i] = lam[i] / sl[i];
+        // H~ = H + sum W c c^T ; base gradient Hz + h
+        for (int k = 0; k <= N; k++) {
+            std::memcpy(&Hs[(size_t)k * NZ * NZ], S.st[k].H, sizeof(double) * NZ * NZ);
+            const double* zk = &z[(size_t)k * NZ];
+            for (int a = 0; a < NZ; a++) {
+                double s = 0; for (int b = 0; b < NZ; b++) s += S.st[k].H[a * NZ + b] * zk[b];
+                gs[(size_t)k * NZ + a] = s + S.st[k].h[a];
+            }
+        }
+        for (int i = 0; i < m; i++) {
+            const SRow& row = S.st[I[i].k].rows[I[i].row];
+            double* H = &Hs[(size_t)I[i].k * NZ * NZ];
+            for (int a = 0; a < NZ; a++) {
+                if (row.c[a] == 0) continue;
+                for (int b = 0; b < NZ; b++) H[a * NZ + b] += W[i] * row.c[a] * row.c[b];
+            }
+        }
+        if (!R.factor(S, Hs)) break;
+        std::vector<double> g0 = gs;
+        auto add_rows = [&](std::vector<double>& g, const std::vector<double>& coef) {
+            for (int i = 0; i < m; i++) {
+                const SRow& row = S.st[I[i].k].rows[I[i].row];
+                double* gk = &g[(size_t)I[i].k * NZ];
+                double cf = I[i].sgn * coef[i];
+                for (int a = 0; a < NZ; a++) gk[a] += cf * row.c[a];
+            }
+        };
+        auto recover = [&](const std::vector<double>& d, std::vector<double>& dS, std::vector<double>& dL) {
+            for (int i = 0; i < m; i++) {
+                double cd = I[i].sgn * rowdot(I[i], d);
+                dS[i] = -rp[i] - cd;
+                dL[i] = W[i] * (cd + rp[i]) - rc[i] / sl[i];
+            }
+        };
+        auto max_step = [&](const std::vector<double>& dS, const std::vector<double>& dL, double cap) {
+            double a = cap;
+            for (int i = 0; i < m; i++) {
+                if (dS[i] < 0) a = std::min(a, -sl[i] / dS[i]);
+                if (dL[i] < 0) a = std::min(a, -lam[i] / dL[i]);
+            }
+            return a;
+        };
+        // predictor
+        std::vector<double> coef(m);
+        for (int i = 0; i < m; i++) { rc[i] = sl[i] * lam[i]; coef[i] = lam[i] + W[i] * rp[i] - rc[i] / sl[i]; }
+        gs = g0; add_rows(gs, coef);
+        R.solve(S, gs, dza);
+        recover(dza, dsa, dla);
+        double aa = max_step(dsa, dla, 1.0);
+        double mua = 0;
+        for (int i = 0; i < m; i++) mua += (sl[i] + aa * dsa[i]) * (lam[i] + aa * dla[i]);
+        mua = (m > 0) ? mua / m : 0.0;
+        double sigma = (mu > 0) ? std::pow(mua / mu, 3) : 0.0;
+        // corrector
+        for (int i = 0; i < m; i++) { rc[i] = sl[i] * lam[i] + dsa[i] * dla[i] - sigma * mu; coef[i] = lam[i] + W[i] * rp[i] - rc[i] / sl[i]; }
+        gs = g0; add_rows(gs, coef);
+        R.solve(S, gs, dz);
+        recover(dz, ds, dl);
+        double a = std::min(1.0, 0.995 * max_step(ds, dl, 1e30));
+        double dzmax = 0;
+        for (size_t i = 0; i < z.size(); i++) { z[i] += a * dz[i]; dzmax = std::max(dzmax, std::fabs(dz[i])); }
+        for (int i = 0; i < m; i++) { sl[i] += a * ds[i]; lam[i] += a * dl[i]; }
+        last_dz = dzmax;
+    }
+    if (iters_out) *iters_out = it;
+    if (!conv) return QP_MaxIterReached;
+    // export in reference layout
+    step.assign((size_t)(N + 1) * NX + N * NU, 0.0);
+    for (int k = 0; k <= N; k++) {
+        for (int a = 0; a < NX; a++) step[(size_t)NX * k + a] = z[(size_t)k * NZ + a];
+        if (k < N)
+            for (int b = 0; b < NU; b++) step[(size_t)NX * (N + 1) + NU * k + b] = z[(size_t)k * NZ + 16 + b];
+    }
+    return 0;
+}
+
+// ---------------- dense-layout primal-dual IPM (validation; solves the reference QP verbatim) ---
+static bool lu_solve_dense(std::vector<double>& M, int n, std::vector<double>& rhs) {
+    std::vector<int> piv(n);
+    for (int k = 0; k < n; k++) {
+        int p = k;
+        double mx = std::fabs(M[(size_t)k * n + k]);
+        for (int i = k + 1; i < n; i++) if (std::fabs(M[(size_t)i * n + k]) > mx) { mx = std::fabs(M[(size_t)i * n + k]); p = i; }
+        if (mx == 0) return false;
+        piv[k] = p;
+        if (p != k) { for (int j = 0; j < n; j++) std::swap(M[(size_t)k * n + j], M[(size_t)p * n + j]); std::swap(rhs[k], rhs[p]); }
+        double d = M[(size_t)k * n + k];
+        for (int i = k + 1; i < n; i++) {
+            double f = M[(size_t)i * n + k] / d;
+            if (f == 0) continue;
+            M[(size_t)i * n + k] = f;
+            for (int j = k + 1; j < n; j++) M[(size_t)i * n + j] -= f * M[(size_t)k * n + j];
+            rhs[i] -= f * rhs[k];
+        }
+    }
+    for (int i = n - 1; i >= 0; i--) {
+        double s = rhs[i];
+        for (int j = i + 1; j < n; j++) s -= M[(size_t)i * n + j] * rhs[j];
+        rhs[i] = s / M[(size_t)i * n + i];
+    }
+    return true;
+}
+
+static int solve_dense_ipm(const DenseQP& q, std::vector<double>& step, int* iters_out) {
+    const int nv = q.nv, nc = q.nc;
+    // classify rows
+    std::vector<int> eq, in;
+    std::vector<double> beq;
+    struct DI { int row; double sgn, bnd; };
+    std::vector<DI> I;
+    // variables fixed to zero by the stage-0 dynamics rows (identity on y_0, rhs 0)
+    auto fixed0 = [&](int col) { return col < NX; };
+    for (int r = 0; r < nc; r++) {
+        const double* a = &q.A[(size_t)r * nv];
+        bool nz = false, only_fixed = true;
+        for (int j = 0; j < nv; j++) if (a[j] != 0) { nz = true; if (!fixed0(j)) only_fixed = false; }
+        double lo = q.l[r] - q.c[r], hi = q.u[r] - q.c[r];
+        if (!nz) { if (lo > FEAS_TOL || hi < -FEAS_TOL) return QP_PrimalInfeasible; continue; }
+        if (r < NX) { eq.push_back(r); beq.push_back(lo); continue; }  // y_0 = 0 (dynamics block 0)
+        if (only_fixed) { if (lo > FEAS_TOL || hi < -FEAS_TOL) return QP_PrimalInfeasible; continue; }
+        if (q.l[r] == q.u[r]) { eq.push_back(r); beq.push_back(lo); continue; }
+        if (q.l[r] > -BIG) I.push_back({r, -1.0, lo});
+        if (q.u[r] < BIG) I.push_back({r, 1.0, hi});
+    }
+    const int ne = (int)eq.size(), m = (int)I.size();
+    std::vector<double> x(nv, 0.0), nu(ne, 0.0), s(m), lam(m, 1.0), rp(m), W(m), rc(m);
+    auto Arow = [&](int r) { return &q.A[(size_t)r * nv]; };
+    auto rowdot = [&](int r, const std::vector<double>& v) { const double* a = Arow(r); double t = 0; for (int j = 0; j < nv; j++) t += a[j] * v[j]; return t; };
+    for (int i = 0; i < m; i++) s[i] = std::max(-(I[i].sgn * rowdot(I[i].row, x) - I[i].sgn * I[i].bnd), 1.0);
+    int n = nv + ne;
+    int it; bool conv = false;
+    double last_dx = 1e30;
+    for (it = 0; it < IPM_MAX_IT; it++) {
+        double mu = 0, rpmax = 0;
+        for (int i = 0; i < m; i++) { rp[i] = I[i].sgn * rowdot(I[i].row, x) - I[i].sgn * I[i].bnd + s[i]; mu += s[i] * lam[i]; rpmax = std::max(rpmax, std::fabs(rp[i])); }
+        mu = m ? mu / m : 0;
+        std::vector<double> re(ne);
+        double remax = 0;
+        for (int e = 0; e < ne; e++) { re[e] = rowdot(eq[e], x) - beq[e]; remax = std::max(remax, std::fabs(re[e])); }
+        if (it > 0 && mu < IPM_TOL_MU && rpmax < IPM_TOL_P && remax < IPM_TOL_P && last_dx < IPM_TOL_STEP) { conv = true; break; }
+        for (int i = 0; i < m; i++) W[i] = lam[i] / s[i];
+        std::vector<double> K((size_t)n * n, 0.0);
+        for (int i = 0; i < nv; i++) for (int j = 0; j < nv; j++) K[(size_t)i * n + j] = q.P[(size_t)i * nv + j];
+        for (int i = 0; i < m; i++) {
+            const double* a = Arow(I[i].row);
+            for (int u = 0; u < nv; u++) { if (a[u] == 0) continue; for (int v = 0; v < nv; v++) if (a[v] != 0) K[(size_t)u * n + v] += W[i] * a[u] * a[v]; }
+        }
+        for (int e = 0; e < ne; e++) { const double* a = Arow(eq[e]); for (int j = 0; j < nv; j++) { K[(size_t)(nv + e) * n + j] = a[j]; K[(size_t)j * n + nv + e] = a[j]; } }
+        // rd0 = P x + g + A_e^T nu  (inequality part added per solve)
+        std::vector<double> rd0(nv);
+        for (int i = 0; i < nv; i++) { double t = q.g[i]; for (int j = 0; j < nv; j++) t += q.P[(size_t)i * nv + j] * x[j]; rd0[i] = t; }
+        for (int e = 0; e < ne; e++) { const double* a = Arow(eq[e]); for (int j = 0; j < nv; j++) rd0[j] += a[j] * nu[e]; }
+        auto do_solve = [&](const std::vector<double>& rcv, std::vector<double>& dx, std::vector<double>& dnu, std::vector<double>& dS, std::vector<double>& dL) {
+            std::vector<double> rhs(n, 0.0);
+            for (int i = 0; i < nv; i++) rhs[i] = -rd0[i];
+            for (int i = 0; i < m; i++) {
+                const double* a = Arow(I[i].row);
+                double cf = I[i].sgn * (lam[i] + W[i] * rp[i] - rcv[i] / s[i]);
+                for (int j = 0; j < nv; j++) rhs[j] -= cf * a[j];
+            }
+            for (int e = 0; e < ne; e++) rhs[nv + e] = -re[e];
+            std::vector<double> Kc = K;
+            if (!lu_solve_dense(Kc, n, rhs)) return false;
+            dx.assign(rhs.begin(), rhs.begin() + nv);
+            dnu.assign(rhs.begin() + nv, rhs.end());
+            dS.resize(m); dL.resize(m);
+            for (int i = 0; i < m; i++) { double cd = I[i].sgn * rowdot(I[i].row, dx); dS[i] = -rp[i] - cd; dL[i] = W[i] * (cd + rp[i]) - rcv[i] / s[i]; }
+            return true;
+        };
+        auto max_step = [&](const std::vector<double>& dS, const std::vector<double>& dL, double cap) {
+            double a = cap;
+            for (int i = 0; i < m; i++) { if (dS[i] < 0) a = std::min(a, -s[i] / dS[i]); if (dL[i] < 0) a = std::min(a, -lam[i] / dL[i]); }
+            return a;
+        };
+        for (int i = 0; i < m; i++) rc[i] = s[i] * lam[i];
+        std::vector<double> dxa, dnua, dsa, dla;
+        if (!do_solve(rc, dxa, dnua, dsa, dla)) break;
+        double aa = max_step(dsa, dla, 1.0);
+        double mua = 0; for (int i = 0; i < m; i++) mua += (s[i] + aa * dsa[i]) * (lam[i] + aa * dla[i]);
+        mua = m ? mua / m : 0;
+        double sigma = mu > 0 ? std::pow(mua / mu, 3) : 0;
+        for (int i = 0; i < m; i++) rc[i] = s[i] * lam[i] + dsa[i] * dla[i] - sigma * mu;
+        std::vector<double> dx, dnu, dS, dL;
+        if (!do_solve(rc, dx, dnu, dS, dL)) break;
+        double a = std::min(1.0, 0.995 * max_step(dS, dL, 1e30));
+        double dxmax = 0;
+        for (int j = 0; j < nv; j++) { x[j] += a * dx[j]; dxmax = std::max(dxmax, std::fabs(dx[j])); }
+        last_dx = dxmax;
+        for (int e = 0; e < ne; e++) nu[e] += dnu[e];  // equality multipliers: full step
+        for (int i = 0; i < m; i++) { s[i] += a * dS[i]; lam[i] += a * dL[i]; }
+    }
+    if (iters_out) *iters_out = it;
+    if (!conv) return QP_MaxIterReached;
+    step = x;
+    return 0;
+}
+
+// ------------------------------------------------------------------------------------------------
+// SQP — OsqpInterface::solveOCP (osqp_interface.cpp:398-590) with filterLineSearch (:759-808)
+// ------------------------------------------------------------------------------------------------
+struct Filter { double obj, vio; };
+
+static void denorm_add(const Oracle& o, const double* base, const std::vector<double>& step, double alpha, double* out) {
+    // out = base + alpha * deNormalizeStep(step)  (:859-869), base/out in (N+1)x17 layout
+    const int N = o.p.N;
+    for (int i = 0; i <= N; i++) {
+        for (int a = 0; a < NX; a++) out[17 * i + a] = base[17 * i + a] + alpha * (o.p.Tx[a] * step[(size_t)NX * i + a]);
+        for (int b = 0; b < NU; b++)
+            out[17 * i + 9 + b] = (i != N) ? base[17 * i + 9 + b] + alpha * (o.p.Tu[b] * step[(size_t)NX * (N + 1) + NU * i + b]) : base[17 * i + 9 + b];
+    }
+}
+
+static int solve_ocp(const Oracle& o, double* guess, const double* recs, const double* ucur, double* opt_sol, int* iters_out) {
+    const OracleParams& p = o.p;
+    const int N = p.N;
+    const int nv = o.nvar();
+    std::vector<double> step(nv, 0.0);
+    std::vector<Filter> filter;
+    std::vector<double> zero((size_t)(N + 1) * 17, 0.0);
+    for (int i = 0; i <= N; i++) for (int a = 0; a < NX; a++) zero[17 * i + a] = guess[a];
+    int status = MAX_ITER_EXCEEDED;
+    bool status_set = false;
+    int it;
+    std::vector<double> trial((size_t)(N + 1) * 17);
+    for (it = 0; it < p.max_iter; it++) {
+        // setQP + PD / NaN checks of the normalized Hessian (:445-473)
+        bool nan = false, pd = true;
+        if (o.opt.qp_mode == 1) {
+            DenseQP q;
+            set_qp(o, guess, recs, ucur, true, q);
+            for (double v : q.P) if (std::isnan(v)) nan = true;
+            std::vector<double> Pc = q.P;
+            // Eigen LLT semantics: fails only on pivot <= 0 (NaN pivots pass)
+            for (int j = 0; j < nv && pd; j++) {
+                double d = Pc[(size_t)j * nv + j];
+                for (int k = 0; k < j; k++) d -= Pc[(size_t)j * nv + k] * Pc[(size_t)j * nv + k];
+                if (d <= 0) { pd = false; break; }
+                d = std::sqrt(d);
+                Pc[(size_t)j * nv + j] = d;
+                for (int i = j + 1; i < nv; i++) {
+                    double s = Pc[(size_t)i * nv + j];
+                    for (int k = 0; k < j; k++) s -= Pc[(size_t)i * nv + k] * Pc[(size_t)j * nv + k];
+                    Pc[(size_t)i * nv + j] = s / d;
+                }
+            }
+            if (!pd) { status = NON_PD_HESSIAN; status_set = true; break; }
+            if (nan) { status = NAN_HESSIAN; status_set = true; break; }
+            std::vector<double> st;
+            int qs = solve_dense_ipm(q, st, nullptr);
+            if (qs == 0) step = st; else { status = qs; status_set = true; }  // Q6: keep old step
+        } else {
+            StructQP S;
+            build_struct_qp(o, guess, recs, ucur, S);
+            // PD check on the block structure: state blocks and the per-component tridiagonal input blocks
+            for (int k = 0; k <= N && pd; k++) {
+                double Q[NX * NX];
+                for (int a = 0; a < NX; a++) for (int b = 0; b < NX; b++) { Q[a * NX + b] = S.st[k].H[a * NZ + b]; if (std::isnan(Q[a * NX + b])) nan = true; }
+                bool ok = true;
+                for (int j = 0; j < NX && ok; j++) {  // LLT pivots (NaN passes, as Eigen)
+                    double d = Q[j * NX + j];
+                    for (int kk = 0; kk < j; kk++) d -= Q[j * NX + kk] * Q[j * NX + kk];
+                    if (d <= 0) { ok = false; break; }
+                    d = std::sqrt(d); Q[j * NX + j] = d;
+                    for (int i = j + 1; i < NX; i++) { double s = Q[i * NX + j]; for (int kk = 0; kk < j; kk++) s -= Q[i * NX + kk] * Q[j * NX + kk]; Q[i * NX + j] = s / d; }
+                }
+                if (!ok) pd = false;
+            }
+            for (int b = 0; b < NU && pd; b++) {
+                double prev_l = 0;  // L_{k,k-1}
+                double prev_d = 0;
+                for (int k = 0; k < N; k++) {
+                    double dk = S.st[k].H[(16 + b) * NZ + 16 + b];
+                    if (std::isnan(dk)) nan = true;
+                    double off = (k >= 1 && b < DOF) ? S.st[k].H[(16 + b) * NZ + 9 + b] : 0.0;
+                    double l = (k >= 1) ? off / prev_d : 0.0;
+                    double d = dk - l * l;
+                    if (d <= 0) { pd = false; break; }
+                    prev_d = std::sqrt(d);
+                    prev_l = l;
+                }
+                (void)prev_l;
+            }
+            if (!pd) { status = NON_PD_HESSIAN; status_set = true; break; }
+            if (nan) { status = NAN_HESSIAN; status_set = true; break; }
+            std::vector<double> st;
+            int qs = solve_struct_ipm(S, st, nullptr);
+            if (qs == 0) step = st; else { status = qs; status_set = true; }
+        }
+        // filterLineSearch :759-808
+        bool accepted = true;
+        double alpha = 1.0;
+        for (int ls = 0; ls < p.line_search_max_iter; ls++) {
+            if (!accepted) { alpha *= p.line_search_tau; continue; }  // later trials cannot be accepted (Q5)
+            denorm_add(o, guess, step, alpha, trial.data());
+            DenseQP q;
+            set_qp(o, trial.data(), recs, ucur, false, q);
+            Filter f{q.obj, constraint_norm(q)};
+            for (size_t j = 0; j < filter.size(); j++)
+                if (f.obj >= filter[j].obj && f.vio >= filter[j].vio) { accepted = false; break; }
+            if (accepted) {
+                std::vector<Filter> nf;
+                for (size_t j = 0; j < filter.size(); j++)
+                    if (f.obj > filter[j].obj || f.vio > filter[j].vio) nf.push_back(filter[j]);
+                nf.push_back(f);
+                filter = nf;
+                break;
+            } else {
+                alpha *= p.line_search_tau;
+            }
+        }
+        // take step :549-551
+        denorm_add(o, guess, step, alpha, trial.data());
+        std::memcpy(guess, trial.data(), sizeof(double) * (N + 1) * 17);
+        double nrm = 0;
+        for (int i = 0; i < nv; i++) nrm = std::max(nrm, std::fabs(step[i]));
+        double pn = alpha * nrm;
+        if (pn < p.eps_prim) { status = SOLVED; status_set = true; break; }
+    }
+    if (it == p.max_iter) status = MAX_ITER_EXCEEDED;
+    (void)status_set;
+    if (iters_out) *iters_out = it;
+    if (status == SOLVED) std::memcpy(opt_sol, guess, sizeof(double) * (N + 1) * 17);
+    else std::memcpy(opt_sol, zero.data(), sizeof(double) * (N + 1) * 17);
+    return status;
+}
+
+// integrator.cpp:29-43
+static void rk4(const double* x, const double* u, double ts, double* out) {
+    auto f = [&](const double* xx, double* o) {
+        for (int j = 0; j < DOF; j++) o[j] = u[j];
+        o[7] = xx[8]; o[8] = u[7];
+    };
+    double k1[9], k2[9], k3[9], k4[9], t[9];
+    f(x, k1);
+    for (int i = 0; i < 9; i++) t[i] = x[i] + ts / 2. * k1[i];
+    f(t, k2);
+    for (int i = 0; i < 9; i++) t[i] = x[i] + ts / 2. * k2[i];
+    f(t, k3);
+    for (int i = 0; i < 9; i++) t[i] = x[i] + ts * k3[i];
+    f(t, k4);
+    for (int i = 0; i < 9; i++) out[i] = x[i] + ts * (k1[i] / 6. + k2[i] / 3. + k3[i] / 3. + k4[i] / 6.);
+}
+
+// MPC::runMPC_ — mpc.cpp:104-190 for one instance
+static int run_mpc_one(const Oracle& o, double* x0, const double* u0, const double* obs, double* guess, int* valid,
+                       int* fails, double* u0_out, double* horizon, int* ok, int* iters) {
+    const OracleParams& p = o.p;
+    const int N = p.N;
+    double last_s = x0[7];
+    double ee[3], J[42];
+    fk(x0, ee, nullptr, nullptr);
+    x0[7] = o.track.project(last_s, ee);
+    fk(x0, nullptr, nullptr, J);
+    double ev[3] = {0, 0, 0};
+    for (int i = 0; i < 3; i++) { double s = 0; for (int j = 0; j < DOF; j++) s += J[7 * i + j] * u0[j]; ev[i] = s; }
+    double dir[3];
+    o.track.dpos(x0[7], dir);
+    x0[8] = ev[0] * dir[0] + ev[1] * dir[1] + ev[2] * dir[2];
+    if (std::fabs(last_s - x0[7]) > p.guess_max_dist) { *valid = 0; (*fails)++; }
+    const double L = o.track.length();
+    if (*valid) {  // updateInitialGuess :54-68
+        for (int i = 1; i < N; i++) std::memcpy(guess + 17 * (i - 1), guess + 17 * i, sizeof(double) * 17);
+        std::memcpy(guess, x0, sizeof(double) * 9);
+        std::memcpy(guess + 17 * (N - 1), guess + 17 * (N - 2), sizeof(double) * 17);
+        rk4(guess + 17 * (N - 1), guess + 17 * (N - 1) + 9, p.Ts, guess + 17 * N);
+        for (int b = 0; b < NU; b++) guess[17 * N + 9 + b] = 0.0;
+    } else {  // generateNewInitialGuess :79-89
+        for (int i = 0; i <= N; i++) {
+            std::memcpy(guess + 17 * i, x0, sizeof(double) * 9);
+            for (int b = 0; b < NU; b++) guess[17 * i + 9 + b] = 0.0;
+        }
+        *valid = 1;
+    }
+    for (int i = 1; i <= N; i++) guess[17 * i + 7] = std::min(guess[17 * i + 7], L);  // unwrapInitialGuess
+    // setInitialGuess + setEnvData: robot records at the warm start (Q4)
+    std::vector<double> recs((size_t)REC * (N + 1));
+    for (int i = 0; i <= N; i++) robot_record(o, guess + 17 * i, obs, obs[3], &recs[(size_t)REC * i]);
+    std::vector<double> sol((size_t)(N + 1) * 17);
+    int status = solve_ocp(o, guess, recs.data(), u0, sol.data(), iters);
+    std::memcpy(guess, sol.data(), sizeof(double) * 17 * (N + 1));  // initial_guess_ = opt_sol
+    if (status == SOLVED) { *valid = 1; *fails = 0; }
+    else { *valid = 0; (*fails)++; }
+    std::memcpy(u0_out, guess + 9, sizeof(double) * 8);
+    std::memcpy(horizon, guess, sizeof(double) * 17 * (N + 1));
+    *ok = (status == SOLVED || (status == MAX_ITER_EXCEEDED && *fails < 5)) ? 1 : 0;
+    return status;
+}
+
+}  // namespace orc
+
+using namespace orc;
+
+extern "C" {
+
+void* oracle_create(const OracleParams* p, const char* nn_dir, OracleOptions opt) {
+    Oracle* o = new Oracle();
+    o->opt = opt;
+    o->set_params(p);
+    if (nn_dir) {
+        std::string d(nn_dir);
+        o->self_nn.load(d + "/self", 7, 1, {256, 64});
+        o->env_nn.load(d + "/env", 10, 9, {256, 256, 256, 256});
+    }
+    return o;
+}
+void oracle_destroy(void* h) { delete (Oracle*)h; }
+void oracle_set_params(void* h, const OracleParams* p) { ((Oracle*)h)->set_params(p); }
+void oracle_set_track(void* h, int n, const double* X, const double* Y, const double* Z, const double* R9) {
+    Oracle* o = (Oracle*)h;
+    std::vector<double> x(X, X + n), y(Y, Y + n), z(Z, Z + n);
+    std::vector<std::array<double, 9>> R(n);
+    for (int i = 0; i < n; i++) std::memcpy(R[i].data(), R9 + 9 * i, 72);
+    o->track.fit(x, y, z, R);
+}
+double oracle_track_length(void* h) { return ((Oracle*)h)->track.length(); }
+void oracle_track_path(void* h, double* s, double* X, double* Y, double* Z, double* R9) {
+    Oracle* o = (Oracle*)h;
+    for (int i = 0; i < N_SPLINE; i++) {
+        s[i] = o->track.s[i]; X[i] = o->track.X[i]; Y[i] = o->track.Y[i]; Z[i] = o->track.Z[i];
+        std::memcpy(R9 + 9 * i, o->track.R[i].data(), 72);
+    }
+}
+void oracle_fk(const double* q, double* pos3, double* R9, double* J42) { fk(q, pos3, R9, J42); }
+double oracle_manipulability(const double* q) { return manipulability(q); }
+void oracle_dmanipulability(const double* q, double* d7) { dmanipulability(q, d7); }
+void oracle_self_mlp(void* h, const double* q7, double* d, double* grad7) { ((Oracle*)h)->self_nn.eval(q7, d, grad7); }
+void oracle_env_mlp(void* h, const double* in10, double* d9, double* jac90) { ((Oracle*)h)->env_nn.eval(in10, d9, jac90); }
+void oracle_spline_eval(void* h, double s, double* pos, double* d, double* dd, double* R9, double* dR) {
+    Oracle* o = (Oracle*)h;
+    o->track.pos(s, pos); o->track.dpos(s, d); o->track.ddpos(s, dd); o->track.rot(s, R9); o->track.drot(s, dR);
+}
+double oracle_project(void* h, double s, const double* ee3) { return ((Oracle*)h)->track.project(s, ee3); }
+void oracle_robot_record(void* h, const double* q7, const double* obs3, double obs_r, double* rec) {
+    robot_record(*(Oracle*)h, q7, obs3, obs_r, rec);
+}
+void oracle_stage_cost(void* h, const double* x9, const double* u8, const double* rec, int k, double* obj, double* fx,
+                       double* fu, double* fxx, double* fuu, double* fxu) {
+    CostOut c;
+    stage_cost(*(Oracle*)h, x9, u8, rec, k, true, c);
+    *obj = c.obj;
+    std::memcpy(fx, c.fx, sizeof c.fx); std::memcpy(fu, c.fu, sizeof c.fu);
+    std::memcpy(fxx, c.fxx, sizeof c.fxx); std::memcpy(fuu, c.fuu, sizeof c.fuu); std::memcpy(fxu, c.fxu, sizeof c.fxu);
+}
+void oracle_stage_constraints(void* h, const double* x9, const double* u8, const double* rec, int k, double* c, double* l,
+                              double* u, double* cx, double* cu) {
+    ConOut co;
+    stage_constraints(*(Oracle*)h, x9, u8, rec, k, true, co);
+    std::memcpy(c, co.c, sizeof co.c); std::memcpy(l, co.l, sizeof co.l); std::memcpy(u, co.u, sizeof co.u);
+    std::memcpy(cx, co.cx, sizeof co.cx); std::memcpy(cu, co.cu, sizeof co.cu);
+}
+double oracle_dense_qp(void* h, const double* guess, const double* recs, const double* u_current, double* P, double* g,
+                       double* A, double* c, double* l, double* u) {
+    Oracle* o = (Oracle*)h;
+    DenseQP q;
+    set_qp(*o, guess, recs, u_current, true, q);
+    std::memcpy(P, q.P.data(), q.P.size() * 8); std::memcpy(g, q.g.data(), q.g.size() * 8);
+    std::memcpy(A, q.A.data(), q.A.size() * 8); std::memcpy(c, q.c.data(), q.c.size() * 8);
+    std::memcpy(l, q.l.data(), q.l.size() * 8); std::memcpy(u, q.u.data(), q.u.size() * 8);
+    return q.obj;
+}
+int oracle_solve_qp(void* h, int mode, const double* guess, const double* recs, const double* u_current, double* step,
+                    int* iters) {
+    Oracle* o = (Oracle*)h;
+    std::vector<double> st;
+    int rc;
+    if (mode == 1) {
+        DenseQP q;
+        set_qp(*o, guess, recs, u_current, true, q);
+        rc = solve_dense_ipm(q, st, iters);
+    } else {
+        StructQP S;
+        build_struct_qp(*o, guess, recs, u_current, S);
+        rc = solve_struct_ipm(S, st, iters);
+    }
+    if (rc == 0) std::memcpy(step, st.data(), st.size() * 8);
+    return rc;
+}
+void oracle_rk4(const double* x9, const double* u8, double ts, double* out9) { rk4(x9, u8, ts, out9); }
+void oracle_sim_time_step(const double* x9, const double* u8, double ts, double* out9) {  // integrator.cpp:55-68
+    const double fine = 0.001;
+    int steps = (int)(ts / fine);
+    double x[9];
+    std::memcpy(x, x9, 72);
+    for (int i = 0; i < steps; i++) { double t[9]; rk4(x, u8, fine, t); std::memcpy(x, t, 72); }
+    std::memcpy(out9, x, 72);
+}
+int oracle_run_mpc(void* h, int B, double* x0, const double* u0, const double* obs, double* guess, int* valid, int* fails,
+                   double* u0_out, double* horizon, int* status, int* ok, int* sqp_iters) {
+    Oracle* o = (Oracle*)h;
+    const int N = o->p.N;
+#ifdef _OPENMP
+    int nt = o->opt.nthreads > 0 ? o->opt.nthreads : 1;
+#pragma omp parallel for num_threads(nt) schedule(dynamic, 4)
+#endif
+    for (int b = 0; b < B; b++) {
+        int it = 0;
+        status[b] = run_mpc_one(*o, x0 + 9 * b, u0 + 8 * b, obs + 4 * b, guess + (size_t)17 * (N + 1) * b, valid + b,
+                                fails + b, u0_out + 8 * b, horizon + (size_t)17 * (N + 1) * b, ok + b, &it);
+        if (sqp_iters) sqp_iters[b] = it;
+    }
+    return 0;
+}
+int oracle_rec_size(void) { return REC; }
+
+}  // extern "C"
