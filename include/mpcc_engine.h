@@ -1,0 +1,183 @@
+/*
+ * mpcc_engine.h — C ABI of the MI355X batched MPCC solve engine (libmpcc_engine.so).
+ *
+ * Drop-in boundary for the reference's per-control-step solve (JunHeonYoon/MPCC_manipulator):
+ *   - the solver plugin interface  SolverInterface            cpp/include/Interfaces/solver_interface.h:44-54
+ *       setTrack(ArcLengthSpline)           -> mpcc_set_track
+ *       setParam(const ParamValue&)         -> mpcc_set_params (+ mpcc_params_load_json)
+ *       setEnvData(obs_position, radius)    -> per-instance obs[] argument of mpcc_solve
+ *       setInitialGuess(vector<OptVariables>) + setCurrentInput(Input)
+ *                                           -> device-resident warm start (mpcc_set_warmstart) and u0[]
+ *       solveOCP(opt_sol, Status*, ComputeTime*) -> mpcc_solve (status[], horizon[], mpcc_timing)
+ *   - the controller entry point MPC::runMPC_                cpp/src/MPC/mpc.cpp:104-190
+ *       (projection, vs estimate, warm-start shift/regeneration, solve, status bookkeeping)
+ *       -> mpcc_solve / mpcc_solve_device for B independent controllers at once.
+ *   - MPC::setTrack(X, Y, Z, R)                              cpp/src/MPC/mpc.cpp:192-197
+ *   - Params JSON loaders + ParamValue overrides           cpp/src/Params/params.cpp:24-448
+ *
+ * Conventions: plain pointers and sizes, row-major doubles, no C++ types and no exceptions across
+ * the ABI.  Every entry point returns 0 on success or a negative MPCC_E_* code; the message of
+ * the last error of the calling thread is available from mpcc_last_error().  Calls on one engine
+ * handle must be serialized by the caller (as the reference's RobotModel is not reentrant);
+ * engines on different devices are independent.
+ *
+ * Layouts (per instance b):
+ *   x0     [9]            q1..q7, s, vs         (types.h:33-57)       in/out: s, vs are overwritten
+ *   u0     [8]            dq1..dq7, dVs         (types.h:59-76)       current input (setCurrentInput)
+ *   obs    [4]            obstacle x, y, z [m], radius [cm]  (runMPC_ obs_position, obs_radius)
+ *   guess  [(N+1)*17]     per stage [x_k(9), u_k(8)] (OptVariables, osqp_interface.h:48-62)
+ *   status                Status enum values (solver_interface.h:28-42)
+ *   ok                    runMPC_ return value (mpc.cpp:188-189)
+ */
+#ifndef MPCC_ENGINE_H
+#define MPCC_ENGINE_H
+#include <stdint.h>
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define MPCC_ABI_VERSION 1
+
+enum {
+    MPCC_OK = 0,
+    MPCC_E_INVALID = -1,     /* bad argument / size / state */
+    MPCC_E_HIP = -2,         /* HIP runtime error */
+    MPCC_E_OOM = -3,         /* device allocation failed */
+    MPCC_E_IO = -4,          /* file / JSON error */
+    MPCC_E_NOTRACK = -5      /* solve before set_track */
+};
+
+/* Status — solver_interface.h:28-42 (same numeric values) */
+enum {
+    MPCC_SOLVED = 0, MPCC_MAX_ITER_EXCEEDED, MPCC_QP_DualInfeasibleInaccurate,
+    MPCC_QP_PrimalInfeasibleInaccurate, MPCC_QP_SolvedInaccurate, MPCC_QP_MaxIterReached,
+    MPCC_QP_PrimalInfeasible, MPCC_QP_DualInfeasible, MPCC_Sigint, MPCC_INVALID_SETTINGS,
+    MPCC_NAN_HESSIAN, MPCC_NON_PD_HESSIAN
+};
+
+/* constraint_mask bits (polytopic rows, constraints.cpp:192-243) */
+#define MPCC_CON_SELFCOL 1
+#define MPCC_CON_SING 2
+#define MPCC_CON_ENVCOL 4
+
+/* Effective parameter values per consumer.  The reference keeps one copy per class and applies
+ * ParamValue overrides inconsistently; mpcc_params_load_json resolves them exactly
+ * as the reference's constructors and setParam do. */
+typedef struct {
+    int32_t N;                 /* horizon length (runtime; reference: compile-time, config.h:36) */
+    double  Ts;                /* sample time (config.json) */
+    int32_t constraint_mask;   /* MPCC_CON_* bits; reference behaviour = 7 */
+
+    double proj_max_dist;      /* ArcLengthSpline::param_.max_dist_proj (projection)   */
+    double guess_max_dist;     /* MPC::param_.max_dist_proj (warm-start invalidation)  */
+    double desired_ee_velocity, deacc_ratio, cost_tol_selcol, cost_tol_sing;   /* Cost::param_ */
+    double q_c, q_c_N_mult, q_l, q_vs, q_ori, q_sing, r_dq, r_dVs;              /* Cost::cost_param_ */
+    double q_c_red_ratio, q_l_inc_ratio, q_ori_red_ratio;
+    double qp_r_ddq;           /* OsqpInterface::cost_param_.r_ddq (file value only, Q8) */
+    double con_tol_selcol, con_tol_sing, con_tol_envcol;                        /* Constraints::param_ */
+    double s_trust_region;                                                      /* Bounds::param_ */
+    double lx[9], ux[9], lu[8], uu[8], lddq[7], uddq[7];                        /* BoundsParam (file) */
+    double Tx[9], Tu[8];                                                        /* NormalizationParam */
+    double eps_prim, eps_dual, line_search_tau, line_search_eta, line_search_rho; /* SQPParam */
+    int32_t max_iter, line_search_max_iter, do_SOC, use_BFGS;
+} mpcc_params;
+
+/* PathToJson (types.h:63-70).  Any of the six may be NULL when 'merged' is given: a single JSON
+ * object with sections "model","cost","bounds","normalization","sqp","config". */
+typedef struct {
+    const char* param_path;
+    const char* cost_path;
+    const char* bounds_path;
+    const char* normalization_path;
+    const char* sqp_path;
+    const char* merged_path;
+} mpcc_json_paths;
+
+/* One ParamValue entry (types.h:72-79): section in {"param","cost","bounds","normalization","sqp"} */
+typedef struct {
+    const char* section;
+    const char* key;
+    double value;
+} mpcc_override;
+
+typedef struct {
+    int32_t N;                 /* horizon */
+    double  Ts;
+    int32_t max_batch;         /* instances the engine can hold (warm-start state is allocated for this many) */
+    int32_t device;            /* HIP device ordinal */
+    int32_t constraint_mask;   /* overrides params.constraint_mask when >= 0 */
+    int32_t faithful_dead_trials; /* 1: also evaluate the line-search trials whose result the reference discards */
+} mpcc_config;
+
+/* ComputeTime (osqp_interface.h:71-79) for one batch call, seconds of device time (HIP events) */
+typedef struct {
+    double set_env;     /* stage linearization: kinematics, manipulability, NN distances */
+    double set_qp;      /* QP assembly (cost/constraint/bound records) */
+    double solve_qp;    /* interior-point QP solves */
+    double get_alpha;   /* line search / step */
+    double total;       /* whole runMPC_ batch incl. projection and warm start */
+} mpcc_timing;
+
+typedef struct mpcc_engine mpcc_engine;
+
+int         mpcc_abi_version(void);
+const char* mpcc_last_error(void);
+
+/* Params JSON files + ParamValue -> effective values.  ctor_semantics=1 resolves as the
+ * MPC(Ts, path, param_value) constructor (normalization/sqp overrides applied); 0 as
+ * MPC::setParam (normalization/sqp keep their file values, osqp_interface.cpp:95-100). */
+int mpcc_params_load_json(const mpcc_json_paths* paths, const mpcc_override* overrides, int n_overrides,
+                          int ctor_semantics, int N, mpcc_params* out);
+
+int  mpcc_create(const mpcc_config* cfg, const mpcc_params* params, const char* nn_dir, mpcc_engine** out);
+void mpcc_destroy(mpcc_engine* e);
+int  mpcc_set_params(mpcc_engine* e, const mpcc_params* params);
+int  mpcc_get_params(mpcc_engine* e, mpcc_params* out);
+
+/* MPC::setTrack(X, Y, Z, R): n way-points, R9 = n row-major 3x3.  Builds the arc-length spline on
+ * the host (gen6DSpline, arc_length_spline.cpp:213-265) and uploads its tables.  Invalidates
+ * every instance's warm start (mpc.cpp:196). */
+int    mpcc_set_track(mpcc_engine* e, int n, const double* X, const double* Y, const double* Z, const double* R9);
+double mpcc_track_length(mpcc_engine* e);
+/* final regular path data (getPathData): s, X, Y, Z [100], R9 [100*9] */
+/* host-only: build the arc-length spline from way-points without an engine (no GPU needed) and
+ * return its path data and total length (ArcLengthSpline::gen6DSpline + getPathData). */
+int    mpcc_track_build_host(int n, const double* X, const double* Y, const double* Z, const double* R9,
+                             double* s, double* Xo, double* Yo, double* Zo, double* Ro9, double* length);
+int    mpcc_get_track_path(mpcc_engine* e, double* s, double* X, double* Y, double* Z, double* R9);
+
+/* Per-instance controller state (mpc.h:119-127), device resident.  guess [B*(N+1)*17]. */
+int mpcc_set_warmstart(mpcc_engine* e, int B, const double* guess, const int32_t* valid, const int32_t* fails);
+int mpcc_get_warmstart(mpcc_engine* e, int B, double* guess, int32_t* valid, int32_t* fails);
+int mpcc_reset_warmstart(mpcc_engine* e, int B, const uint8_t* mask /* NULL = all */);
+
+/* Batched MPC::runMPC_ on host arrays (H2D, solve, D2H).  Any output pointer may be NULL. */
+int mpcc_solve(mpcc_engine* e, int B, double* x0, const double* u0, const double* obs,
+               double* u0_out, double* horizon_out, int32_t* status, int32_t* ok, mpcc_timing* timing);
+
+/* Same on device-resident arrays; asynchronous on 'stream' (hipStream_t, NULL = engine stream).
+ * Instances [0, B) of the engine's warm-start state are used. */
+int mpcc_solve_device(mpcc_engine* e, int B, double* d_x0, const double* d_u0, const double* d_obs,
+                      double* d_u0_out, double* d_horizon, int32_t* d_status, int32_t* d_ok, void* stream);
+
+/* Integrator::simTimeStep (integrator.cpp:55-68) for B states, host arrays (closed-loop driver). */
+int mpcc_sim_time_step(mpcc_engine* e, int B, const double* x, const double* u, double ts, double* x_next);
+
+/* ---- stage-level entry points for parity tests (host arrays) ---- */
+#define MPCC_REC_SIZE 143
+/* RobotData::update + updateEnv (robot_data.h:55-88) for M joint vectors q[M*7], obs[M*4] */
+int mpcc_debug_robot_records(mpcc_engine* e, int M, const double* q, const double* obs, double* rec);
+/* ArcLengthSpline evals at M arc lengths: pos,d,dd [M*3], R [M*9], dR [M*3] */
+int mpcc_debug_spline(mpcc_engine* e, int M, const double* s, double* pos, double* d, double* dd, double* R, double* dR);
+/* Cost::getCost for M (x,u,rec,k) tuples: obj [M], fx [M*9], fu [M*8], fxx [M*81], fuu [M*64] */
+int mpcc_debug_stage_cost(mpcc_engine* e, int M, const double* x, const double* u, const double* rec, const int32_t* k,
+                          double* obj, double* fx, double* fu, double* fxx, double* fuu);
+/* one QP of the SQP for B instances: guess [B*(N+1)*17], rec [B*(N+1)*143], u_cur [B*8]
+ * -> step [B*(17N+9)] in the reference's stacked layout, qp_status [B], ipm_iters [B] */
+int mpcc_debug_solve_qp(mpcc_engine* e, int B, const double* guess, const double* rec, const double* u_cur,
+                        double* step, int32_t* qp_status, int32_t* ipm_iters);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* MPCC_ENGINE_H */

@@ -1,0 +1,52 @@
+"""In-tree build of libmpcc_engine.so (hipcc, gfx950).  Used by __graft_entry__.build() and tests.
+
+The shared library is written to mpcc_manipulator_amd/_build/ (git-ignored; travels to the GPU box
+with the repository snapshot)."""
+import concurrent.futures as cf
+import os
+import subprocess
+
+PKG = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(PKG)
+CSRC = os.path.join(PKG, "csrc")
+BUILD = os.path.join(PKG, "_build")
+LIB = os.path.join(BUILD, "libmpcc_engine.so")
+SOURCES = ["kernels.hip", "engine.cpp", "host_params.cpp", "host_spline.cpp", "mpc.cpp"]
+ARCH = os.environ.get("MPCC_OFFLOAD_ARCH", "gfx950")
+HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+CFLAGS = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-I", os.path.join(ROOT, "include"),
+          "-I", CSRC, "-Wno-unused-result"]
+
+
+def _compile(src):
+    path = os.path.join(CSRC, src)
+    obj = os.path.join(BUILD, os.path.splitext(src)[0] + ".o")
+    deps = [path] + [os.path.join(CSRC, h) for h in os.listdir(CSRC) if h.endswith(".h")]
+    deps.append(os.path.join(ROOT, "include", "mpcc_engine.h"))
+    if os.path.exists(obj) and os.path.getmtime(obj) >= max(os.path.getmtime(d) for d in deps):
+        return obj
+    lang = ["-x", "hip"] if src.endswith(".cpp") else []
+    cmd = [HIPCC] + CFLAGS + lang + ["-c", path, "-o", obj]
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if r.returncode != 0:
+        raise RuntimeError(f"compile failed: {' '.join(cmd)}\n{r.stdout}\n{r.stderr}")
+    return obj
+
+
+def build(verbose=False):
+    os.makedirs(BUILD, exist_ok=True)
+    with cf.ThreadPoolExecutor(max_workers=min(8, len(SOURCES))) as ex:
+        objs = list(ex.map(_compile, SOURCES))
+    if os.path.exists(LIB) and os.path.getmtime(LIB) >= max(os.path.getmtime(o) for o in objs):
+        return LIB
+    cmd = [HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", LIB] + objs
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if r.returncode != 0:
+        raise RuntimeError(f"link failed: {' '.join(cmd)}\n{r.stdout}\n{r.stderr}")
+    if verbose:
+        print("built", LIB)
+    return LIB
+
+
+if __name__ == "__main__":
+    build(verbose=True)

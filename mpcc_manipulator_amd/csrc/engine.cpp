@@ -1,0 +1,665 @@
+// engine.cpp — C-ABI implementation (include/mpcc_engine.h): engine object, device memory,
+// track upload and the batched runMPC_ launch sequence.
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <fstream>
+#include <memory>
+#include <sstream>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+#include "host_json.h"
+#include "host_spline.h"
+#include "kernels.h"
+#include "mpcc_engine.h"
+
+namespace mpcc {
+
+static thread_local std::string g_last_error;
+void set_last_error(const std::string& m) { g_last_error = m; }
+
+struct HipError : std::runtime_error {
+    using std::runtime_error::runtime_error;
+};
+#define HIPCHK(x)                                                                                          \
+    do {                                                                                                   \
+        hipError_t e_ = (x);                                                                               \
+        if (e_ != hipSuccess) throw HipError(std::string(#x) + ": " + hipGetErrorString(e_));              \
+    } while (0)
+
+template <class T>
+static T* dmalloc(size_t n) {
+    void* p = nullptr;
+    if (n == 0) n = 1;
+    hipError_t e = hipMalloc(&p, n * sizeof(T));
+    if (e != hipSuccess) throw std::bad_alloc();
+    return (T*)p;
+}
+
+struct NNWeights {
+    double* d = nullptr;
+    NNDesc desc{};
+    bool loaded = false;
+};
+
+}  // namespace mpcc
+
+using namespace mpcc;
+
+struct mpcc_engine {
+    mpcc_config cfg{};
+    mpcc_params params{};
+    int N = 0, maxB = 0;
+    hipStream_t stream = nullptr;
+    SplineTables track;
+    bool has_track = false;
+    double* d_spl = nullptr;
+    SplineDev spl{};
+    DevBuffers d{};
+    // host-API staging
+    double *s_x0 = nullptr, *s_u0 = nullptr, *s_obs = nullptr, *s_u0out = nullptr, *s_hor = nullptr;
+    int32_t *s_status = nullptr, *s_ok = nullptr;
+    NNWeights nn_self, nn_env;
+    double A[81], B[72], M[81], G[72];
+    std::vector<hipEvent_t> events;
+
+    ~mpcc_engine() {
+        auto f = [](void* p) { if (p) (void)hipFree(p); };
+        f(d_spl);
+        f(d.guess); f(d.valid); f(d.fails); f(d.rec); f(d.qs); f(d.is); f(d.step); f(d.trial); f(d.sqi); f(d.sqd);
+        f(s_x0); f(s_u0); f(s_obs); f(s_u0out); f(s_hor); f(s_status); f(s_ok);
+        f(nn_self.d); f(nn_env.d);
+        for (auto ev : events) (void)hipEventDestroy(ev);
+        if (stream) (void)hipStreamDestroy(stream);
+    }
+
+    void set_model() {
+        const mpcc_params& p = params;
+        // ZOH of the kinematic model (model.cpp:47-91); the 18x18 expm is exact in closed form because
+        // the continuous A is nilpotent: A = I + Ts e_s e_vs^T, B = Ts [I7 0; 0 Ts/2; 0 1] (dVs column).
+        for (int i = 0; i < 81; i++) A[i] = (i % 10 == 0) ? 1.0 : 0.0;
+        for (int i = 0; i < 72; i++) B[i] = 0.0;
+        A[7 * 9 + 8] = p.Ts;
+        for (int j = 0; j < 7; j++) B[j * 8 + j] = p.Ts;
+        B[7 * 8 + 7] = p.Ts * p.Ts / 2.0;
+        B[8 * 8 + 7] = p.Ts;
+        for (int a = 0; a < 9; a++) {
+            for (int b = 0; b < 9; b++) M[a * 9 + b] = (1.0 / p.Tx[a]) * A[a * 9 + b] * p.Tx[b];
+            for (int b = 0; b < 8; b++) G[a * 8 + b] = (1.0 / p.Tx[a]) * B[a * 8 + b] * p.Tu[b];
+        }
+    }
+
+    DevConst make_const(int Bn) const {
+        DevConst c;
+        std::memset(&c, 0, sizeof c);
+        c.p = params;
+        std::memcpy(c.A, A, sizeof A);
+        std::memcpy(c.B, B, sizeof B);
+        std::memcpy(c.M, M, sizeof M);
+        std::memcpy(c.G, G, sizeof G);
+        c.spl = spl;
+        c.N = N;
+        c.Bn = Bn;
+        c.S = Bn * (N + 1);
+        c.faithful_dead_trials = cfg.faithful_dead_trials;
+        return c;
+    }
+
+    hipEvent_t ev(size_t i) {
+        while (events.size() <= i) {
+            hipEvent_t e;
+            HIPCHK(hipEventCreate(&e));
+            events.push_back(e);
+        }
+        return events[i];
+    }
+};
+
+namespace {
+
+// ---- NN weights: binary (manifest.json + *.f64, this repo's data/nn) or the reference's text files
+bool read_doubles_bin(const std::string& path, std::vector<double>& out, size_t n) {
+    std::ifstream f(path, std::ios::binary);
+    if (!f) return false;
+    out.resize(n);
+    f.read((char*)out.data(), (std::streamsize)(n * sizeof(double)));
+    return (bool)f;
+}
+bool read_doubles_txt(const std::string& path, std::vector<double>& out, size_t n) {
+    std::ifstream f(path);
+    if (!f) return false;
+    out.resize(n);
+    for (size_t i = 0; i < n; i++)
+        if (!(f >> out[i])) return false;  // operator>> as SelfCollisionModel.cpp:29
+    return true;
+}
+
+void load_nn(mpcc_engine* e, const std::string& dir, int nin, int nout, std::vector<int> hidden, NNWeights& w) {
+    std::vector<int> dims;
+    dims.push_back(3 * nin);
+    for (int h : hidden) dims.push_back(h);
+    dims.push_back(nout);
+    const int L = (int)dims.size() - 1;
+    NNDesc nd{};
+    nd.L = L;
+    nd.nin = nin;
+    for (int i = 0; i <= L; i++) nd.dims[i] = dims[i];
+    std::vector<double> packed;
+    for (int l = 0; l < L; l++) {
+        const int R = dims[l + 1], C = dims[l];
+        std::vector<double> W, b;
+        std::string base = dir + "/";
+        bool ok = read_doubles_bin(base + "weight_" + std::to_string(l) + ".f64", W, (size_t)R * C) &&
+                  read_doubles_bin(base + "bias_" + std::to_string(l) + ".f64", b, R);
+        if (!ok) {  // reference layout: <dir>/parameter/weight_l.txt or <dir>/weight_l.txt
+            std::string tb = base + "parameter/";
+            ok = read_doubles_txt(tb + "weight_" + std::to_string(l) + ".txt", W, (size_t)R * C) &&
+                 read_doubles_txt(tb + "bias_" + std::to_string(l) + ".txt", b, R);
+            if (!ok)
+                ok = read_doubles_txt(base + "weight_" + std::to_string(l) + ".txt", W, (size_t)R * C) &&
+                     read_doubles_txt(base + "bias_" + std::to_string(l) + ".txt", b, R);
+        }
+        if (!ok) throw std::runtime_error("cannot read MLP layer " + std::to_string(l) + " under " + dir);
+        nd.offW[l] = (long)packed.size();
+        for (int k = 0; k < C; k++)  // transpose: W^T[k][r]
+            for (int r = 0; r < R; r++) packed.push_back(W[(size_t)r * C + k]);
+        nd.offb[l] = (long)packed.size();
+        packed.insert(packed.end(), b.begin(), b.end());
+    }
+    w.d = dmalloc<double>(packed.size());
+    HIPCHK(hipMemcpy(w.d, packed.data(), packed.size() * sizeof(double), hipMemcpyHostToDevice));
+    w.desc = nd;
+    w.loaded = true;
+    (void)e;
+}
+
+int fail(int code, const std::string& m) {
+    set_last_error(m);
+    return code;
+}
+
+void validate_params(const mpcc_params& p) {
+    if (p.N < 1 || p.N > NMAX) throw std::invalid_argument("N out of range [1, 64]");
+    if (!(p.Ts > 0)) throw std::invalid_argument("Ts must be > 0");
+    for (int i = 0; i < 9; i++) if (!(p.Tx[i] > 0)) throw std::invalid_argument("T_x must be > 0");
+    for (int i = 0; i < 8; i++) if (!(p.Tu[i] > 0)) throw std::invalid_argument("T_u must be > 0");
+    if (p.max_iter < 0 || p.line_search_max_iter < 0) throw std::invalid_argument("negative iteration limit");
+}
+
+void upload_track(mpcc_engine* e) {
+    const SplineTables& t = e->track;
+    const int n = t.n;
+    // layout: s | a0 b0 c0 d0 | a1 .. | a2 .. | R (9n) | cr | dr | logv (3n)
+    std::vector<double> buf;
+    buf.reserve((size_t)n * 27);
+    auto push = [&](const std::vector<double>& v) { buf.insert(buf.end(), v.begin(), v.end()); };
+    push(t.s);
+    for (int a = 0; a < 3; a++) { push(t.a[a]); push(t.b[a]); push(t.c[a]); push(t.d[a]); }
+    push(t.R); push(t.cr); push(t.dr); push(t.logv);
+    if (e->d_spl) HIPCHK(hipFree(e->d_spl));
+    e->d_spl = dmalloc<double>(buf.size());
+    HIPCHK(hipMemcpy(e->d_spl, buf.data(), buf.size() * sizeof(double), hipMemcpyHostToDevice));
+    SplineDev& s = e->spl;
+    const double* p = e->d_spl;
+    s.s = p; p += n;
+    for (int a = 0; a < 3; a++) { s.a[a] = p; p += n; s.b[a] = p; p += n; s.c[a] = p; p += n; s.d[a] = p; p += n; }
+    s.R = p; p += 9 * n;
+    s.cr = p; p += n;
+    s.dr = p; p += n;
+    s.logv = p;
+    s.n = n;
+    s.delta = t.delta;
+    s.L = t.length();
+}
+
+void run_batch(mpcc_engine* e, int B, hipStream_t st, mpcc_timing* timing) {
+    DevConst c = e->make_const(B);
+    DevBuffers& d = e->d;
+    const bool tm = timing != nullptr;
+    int ei = 0;
+    auto mark = [&]() { hipEvent_t ev = e->ev(ei++); HIPCHK(hipEventRecord(ev, st)); return ev; };
+    std::vector<std::pair<int, int>> set_qp, solve_qp, get_alpha;
+    int t0 = 0, t_env0 = 0, t_env1 = 0, t_end = 0;
+    if (tm) { t0 = ei; mark(); }
+    launch_prepare(c, d, st);
+    if (tm) { t_env0 = ei; mark(); }
+    launch_stage_records(c, d, st);
+    if (c.p.constraint_mask & MPCC_CON_SELFCOL)
+        launch_nn(c, d, e->nn_self.desc, e->nn_self.d, 0, c.S, nullptr, nullptr, d.rec, c.S, st);
+    if (c.p.constraint_mask & MPCC_CON_ENVCOL)
+        launch_nn(c, d, e->nn_env.desc, e->nn_env.d, 1, c.S, nullptr, nullptr, d.rec, c.S, st);
+    if (tm) { t_env1 = ei; mark(); }
+    const double* ucur = d.u0;
+    for (int it = 0; it < c.p.max_iter; it++) {
+        int a0 = 0, a1 = 0, b1 = 0, c1 = 0;
+        if (tm) { a0 = ei; mark(); }
+        launch_setqp(c, d, ucur, st);
+        if (tm) { a1 = ei; mark(); }
+        launch_ipm(c, d, st);
+        if (tm) { b1 = ei; mark(); }
+        launch_trial(c, d, ucur, 1.0, 0, st);
+        launch_accept(c, d, st);
+        if (c.faithful_dead_trials) {
+            double alpha = 1.0;
+            for (int l = 1; l < c.p.line_search_max_iter; l++) {
+                alpha *= c.p.line_search_tau;
+                launch_trial(c, d, ucur, alpha, 1, st);
+            }
+        }
+        launch_apply(c, d, st);
+        if (tm) {
+            c1 = ei; mark();
+            set_qp.push_back({a0, a1});
+            solve_qp.push_back({a1, b1});
+            get_alpha.push_back({b1, c1});
+        }
+    }
+    launch_finalize(c, d, st);
+    HIPCHK(hipGetLastError());
+    if (tm) {
+        t_end = ei; mark();
+        HIPCHK(hipEventSynchronize(e->ev(t_end)));
+        auto el = [&](int a, int b) { float ms = 0; (void)hipEventElapsedTime(&ms, e->ev(a), e->ev(b)); return ms * 1e-3; };
+        timing->set_env = el(t_env0, t_env1);
+        timing->set_qp = 0; timing->solve_qp = 0; timing->get_alpha = 0;
+        for (auto& pr : set_qp) timing->set_qp += el(pr.first, pr.second);
+        for (auto& pr : solve_qp) timing->solve_qp += el(pr.first, pr.second);
+        for (auto& pr : get_alpha) timing->get_alpha += el(pr.first, pr.second);
+        timing->total = el(t0, t_end);
+    }
+}
+
+}  // namespace
+
+extern "C" {
+
+int mpcc_abi_version(void) { return MPCC_ABI_VERSION; }
+const char* mpcc_last_error(void) { return g_last_error.c_str(); }
+
+int mpcc_create(const mpcc_config* cfg, const mpcc_params* params, const char* nn_dir, mpcc_engine** out) {
+    if (!cfg || !params || !out) return fail(MPCC_E_INVALID, "mpcc_create: null argument");
+    std::unique_ptr<mpcc_engine> e(new mpcc_engine());
+    try {
+        e->cfg = *cfg;
+        e->params = *params;
+        e->params.N = cfg->N;
+        e->params.Ts = cfg->Ts;
+        if (cfg->constraint_mask >= 0) e->params.constraint_mask = cfg->constraint_mask;
+        validate_params(e->params);
+        if (cfg->max_batch < 1) throw std::invalid_argument("max_batch must be >= 1");
+        e->N = cfg->N;
+        e->maxB = cfg->max_batch;
+        HIPCHK(hipSetDevice(cfg->device));
+        HIPCHK(hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking));
+        const size_t B = (size_t)e->maxB, NS = (size_t)e->N + 1;
+        DevBuffers& d = e->d;
+        d.guess = dmalloc<double>(B * NS * 17);
+        d.valid = dmalloc<int32_t>(B);
+        d.fails = dmalloc<int32_t>(B);
+        d.rec = dmalloc<double>((size_t)REC * B * NS);
+        d.qs = dmalloc<double>(B * NS * QS);
+        d.is = dmalloc<double>(B * NS * IS);
+        d.step = dmalloc<double>(B * NS * 17);
+        d.trial = dmalloc<double>(B * NS * 4);
+        d.sqi = dmalloc<int32_t>(B * SQI);
+        d.sqd = dmalloc<double>(B * SQ);
+        HIPCHK(hipMemset(d.guess, 0, B * NS * 17 * sizeof(double)));
+        HIPCHK(hipMemset(d.valid, 0, B * sizeof(int32_t)));
+        HIPCHK(hipMemset(d.fails, 0, B * sizeof(int32_t)));
+        HIPCHK(hipMemset(d.sqi, 0, B * SQI * sizeof(int32_t)));
+        e->s_x0 = dmalloc<double>(B * 9);
+        e->s_u0 = dmalloc<double>(B * 8);
+        e->s_obs = dmalloc<double>(B * 4);
+        e->s_u0out = dmalloc<double>(B * 8);
+        e->s_hor = dmalloc<double>(B * NS * 17);
+        e->s_status = dmalloc<int32_t>(B);
+        e->s_ok = dmalloc<int32_t>(B);
+        e->set_model();
+        const int mask = e->params.constraint_mask;
+        if (mask & (MPCC_CON_SELFCOL | MPCC_CON_ENVCOL)) {
+            if (!nn_dir) throw std::invalid_argument("nn_dir required when collision rows are enabled");
+            std::string dir(nn_dir);
+            load_nn(e.get(), dir + "/self", 7, 1, {256, 64}, e->nn_self);      // osqp_interface.cpp:35-38
+            load_nn(e.get(), dir + "/env", 10, 9, {256, 256, 256, 256}, e->nn_env);  // :40-43
+        }
+    } catch (const std::bad_alloc&) {
+        return fail(MPCC_E_OOM, "mpcc_create: device allocation failed");
+    } catch (const HipError& x) {
+        return fail(MPCC_E_HIP, std::string("mpcc_create: ") + x.what());
+    } catch (const std::invalid_argument& x) {
+        return fail(MPCC_E_INVALID, std::string("mpcc_create: ") + x.what());
+    } catch (const std::exception& x) {
+        return fail(MPCC_E_IO, std::string("mpcc_create: ") + x.what());
+    }
+    *out = e.release();
+    return MPCC_OK;
+}
+
+void mpcc_destroy(mpcc_engine* e) { delete e; }
+
+int mpcc_set_params(mpcc_engine* e, const mpcc_params* p) {
+    if (!e || !p) return fail(MPCC_E_INVALID, "mpcc_set_params: null argument");
+    mpcc_params np = *p;
+    np.N = e->N;  // horizon and Ts are fixed at creation (device buffers, model)
+    np.Ts = e->params.Ts;
+    if ((np.constraint_mask & (MPCC_CON_SELFCOL | MPCC_CON_ENVCOL)) && !(e->nn_self.loaded && e->nn_env.loaded))
+        return fail(MPCC_E_INVALID, "mpcc_set_params: collision rows need NN weights loaded at create");
+    try {
+        validate_params(np);
+    } catch (const std::exception& x) {
+        return fail(MPCC_E_INVALID, std::string("mpcc_set_params: ") + x.what());
+    }
+    e->params = np;
+    e->set_model();
+    return MPCC_OK;
+}
+
+int mpcc_get_params(mpcc_engine* e, mpcc_params* out) {
+    if (!e || !out) return fail(MPCC_E_INVALID, "mpcc_get_params: null argument");
+    *out = e->params;
+    return MPCC_OK;
+}
+
+int mpcc_set_track(mpcc_engine* e, int n, const double* X, const double* Y, const double* Z, const double* R9) {
+    if (!e || n < 3 || !X || !Y || !Z || !R9) return fail(MPCC_E_INVALID, "mpcc_set_track: invalid argument");
+    try {
+        e->track = build_track_spline(n, X, Y, Z, R9);
+        upload_track(e);
+        e->has_track = true;
+        HIPCHK(hipMemset(e->d.valid, 0, (size_t)e->maxB * sizeof(int32_t)));  // valid_initial_guess_ = false
+    } catch (const HipError& x) {
+        return fail(MPCC_E_HIP, std::string("mpcc_set_track: ") + x.what());
+    } catch (const std::exception& x) {
+        return fail(MPCC_E_INVALID, std::string("mpcc_set_track: ") + x.what());
+    }
+    return MPCC_OK;
+}
+
+int mpcc_track_build_host(int n, const double* X, const double* Y, const double* Z, const double* R9, double* s,
+                          double* Xo, double* Yo, double* Zo, double* Ro9, double* length) {
+    if (n < 3 || !X || !Y || !Z || !R9) return fail(MPCC_E_INVALID, "mpcc_track_build_host: invalid argument");
+    try {
+        SplineTables t = build_track_spline(n, X, Y, Z, R9);
+        if (s) std::memcpy(s, t.s.data(), t.n * sizeof(double));
+        if (Xo) std::memcpy(Xo, t.X.data(), t.n * sizeof(double));
+        if (Yo) std::memcpy(Yo, t.Y.data(), t.n * sizeof(double));
+        if (Zo) std::memcpy(Zo, t.Z.data(), t.n * sizeof(double));
+        if (Ro9) std::memcpy(Ro9, t.R.data(), (size_t)t.n * 9 * sizeof(double));
+        if (length) *length = t.length();
+    } catch (const std::exception& x) {
+        return fail(MPCC_E_INVALID, std::string("mpcc_track_build_host: ") + x.what());
+    }
+    return MPCC_OK;
+}
+
+double mpcc_track_length(mpcc_engine* e) { return (e && e->has_track) ? e->track.length() : 0.0; }
+
+int mpcc_get_track_path(mpcc_engine* e, double* s, double* X, double* Y, double* Z, double* R9) {
+    if (!e || !e->has_track) return fail(MPCC_E_NOTRACK, "mpcc_get_track_path: no track");
+    const SplineTables& t = e->track;
+    if (s) std::memcpy(s, t.s.data(), t.n * sizeof(double));
+    if (X) std::memcpy(X, t.X.data(), t.n * sizeof(double));
+    if (Y) std::memcpy(Y, t.Y.data(), t.n * sizeof(double));
+    if (Z) std::memcpy(Z, t.Z.data(), t.n * sizeof(double));
+    if (R9) std::memcpy(R9, t.R.data(), (size_t)t.n * 9 * sizeof(double));
+    return MPCC_OK;
+}
+
+int mpcc_set_warmstart(mpcc_engine* e, int B, const double* guess, const int32_t* valid, const int32_t* fails) {
+    if (!e || B < 0 || B > e->maxB) return fail(MPCC_E_INVALID, "mpcc_set_warmstart: invalid argument");
+    try {
+        const size_t NS = e->N + 1;
+        if (guess) HIPCHK(hipMemcpy(e->d.guess, guess, (size_t)B * NS * 17 * sizeof(double), hipMemcpyHostToDevice));
+        if (valid) HIPCHK(hipMemcpy(e->d.valid, valid, (size_t)B * sizeof(int32_t), hipMemcpyHostToDevice));
+        if (fails) HIPCHK(hipMemcpy(e->d.fails, fails, (size_t)B * sizeof(int32_t), hipMemcpyHostToDevice));
+    } catch (const HipError& x) {
+        return fail(MPCC_E_HIP, x.what());
+    }
+    return MPCC_OK;
+}
+
+int mpcc_get_warmstart(mpcc_engine* e, int B, double* guess, int32_t* valid, int32_t* fails) {
+    if (!e || B < 0 || B > e->maxB) return fail(MPCC_E_INVALID, "mpcc_get_warmstart: invalid argument");
+    try {
+        const size_t NS = e->N + 1;
+        HIPCHK(hipStreamSynchronize(e->stream));
+        if (guess) HIPCHK(hipMemcpy(guess, e->d.guess, (size_t)B * NS * 17 * sizeof(double), hipMemcpyDeviceToHost));
+        if (valid) HIPCHK(hipMemcpy(valid, e->d.valid, (size_t)B * sizeof(int32_t), hipMemcpyDeviceToHost));
+        if (fails) HIPCHK(hipMemcpy(fails, e->d.fails, (size_t)B * sizeof(int32_t), hipMemcpyDeviceToHost));
+    } catch (const HipError& x) {
+        return fail(MPCC_E_HIP, x.what());
+    }
+    return MPCC_OK;
+}
+
+int mpcc_reset_warmstart(mpcc_engine* e, int B, const uint8_t* mask) {
+    if (!e || B < 0 || B > e->maxB) return fail(MPCC_E_INVALID, "mpcc_reset_warmstart: invalid argument");
+    try {
+        HIPCHK(hipStreamSynchronize(e->stream));
+        if (!mask) {
+            HIPCHK(hipMemset(e->d.valid, 0, (size_t)B * sizeof(int32_t)));
+            HIPCHK(hipMemset(e->d.fails, 0, (size_t)B * sizeof(int32_t)));
+            return MPCC_OK;
+        }
+        std::vector<int32_t> v(B), f(B);
+        HIPCHK(hipMemcpy(v.data(), e->d.valid, B * sizeof(int32_t), hipMemcpyDeviceToHost));
+        HIPCHK(hipMemcpy(f.data(), e->d.fails, B * sizeof(int32_t), hipMemcpyDeviceToHost));
+        for (int i = 0; i < B; i++) if (mask[i]) { v[i] = 0; f[i] = 0; }
+        HIPCHK(hipMemcpy(e->d.valid, v.data(), B * sizeof(int32_t), hipMemcpyHostToDevice));
+        HIPCHK(hipMemcpy(e->d.fails, f.data(), B * sizeof(int32_t), hipMemcpyHostToDevice));
+    } catch (const HipError& x) {
+        return fail(MPCC_E_HIP, x.what());
+    }
+    return MPCC_OK;
+}
+
+int mpcc_solve_device(mpcc_engine* e, int B, double* d_x0, const double* d_u0, const double* d_obs, double* d_u0_out,
+                      double* d_horizon, int32_t* d_status, int32_t* d_ok, void* stream) {
+    if (!e || B < 1 || B > e->maxB || !d_x0 || !d_u0 || !d_obs)
+        return fail(MPCC_E_INVALID, "mpcc_solve_device: invalid argument");
+    if (!e->has_track) return fail(MPCC_E_NOTRACK, "mpcc_solve_device: set_track first");
+    try {
+        hipStream_t st = stream ? (hipStream_t)stream : e->stream;
+        e->d.x0 = d_x0; e->d.u0 = d_u0; e->d.obs = d_obs;
+        e->d.u0_out = d_u0_out; e->d.horizon = d_horizon; e->d.status = d_status; e->d.ok = d_ok;
+        run_batch(e, B, st, nullptr);
+    } catch (const HipError& x) {
+        return fail(MPCC_E_HIP, std::string("mpcc_solve_device: ") + x.what());
+    }
+    return MPCC_OK;
+}
+
+int mpcc_solve(mpcc_engine* e, int B, double* x0, const double* u0, const double* obs, double* u0_out, double* horizon_out,
+               int32_t* status, int32_t* ok, mpcc_timing* timing) {
+    if (!e || B < 1 || B > e->maxB || !x0 || !u0 || !obs) return fail(MPCC_E_INVALID, "mpcc_solve: invalid argument");
+    if (!e->has_track) return fail(MPCC_E_NOTRACK, "mpcc_solve: set_track first");
+    try {
+        hipStream_t st = e->stream;
+        const size_t NS = e->N + 1;
+        HIPCHK(hipMemcpyAsync(e->s_x0, x0, B * 9 * sizeof(double), hipMemcpyHostToDevice, st));
+        HIPCHK(hipMemcpyAsync(e->s_u0, u0, B * 8 * sizeof(double), hipMemcpyHostToDevice, st));
+        HIPCHK(hipMemcpyAsync(e->s_obs, obs, B * 4 * sizeof(double), hipMemcpyHostToDevice, st));
+        e->d.x0 = e->s_x0; e->d.u0 = e->s_u0; e->d.obs = e->s_obs;
+        e->d.u0_out = e->s_u0out; e->d.horizon = e->s_hor; e->d.status = e->s_status; e->d.ok = e->s_ok;
+        run_batch(e, B, st, timing);
+        HIPCHK(hipMemcpyAsync(x0, e->s_x0, B * 9 * sizeof(double), hipMemcpyDeviceToHost, st));
+        if (u0_out) HIPCHK(hipMemcpyAsync(u0_out, e->s_u0out, B * 8 * sizeof(double), hipMemcpyDeviceToHost, st));
+        if (horizon_out)
+            HIPCHK(hipMemcpyAsync(horizon_out, e->s_hor, B * NS * 17 * sizeof(double), hipMemcpyDeviceToHost, st));
+        if (status) HIPCHK(hipMemcpyAsync(status, e->s_status, B * sizeof(int32_t), hipMemcpyDeviceToHost, st));
+        if (ok) HIPCHK(hipMemcpyAsync(ok, e->s_ok, B * sizeof(int32_t), hipMemcpyDeviceToHost, st));
+        HIPCHK(hipStreamSynchronize(st));
+    } catch (const HipError& x) {
+        return fail(MPCC_E_HIP, std::string("mpcc_solve: ") + x.what());
+    }
+    return MPCC_OK;
+}
+
+int mpcc_sim_time_step(mpcc_engine* e, int B, const double* x, const double* u, double ts, double* x_next) {
+    if (!e || B < 1 || !x || !u || !x_next) return fail(MPCC_E_INVALID, "mpcc_sim_time_step: invalid argument");
+    try {
+        double* dx = dmalloc<double>((size_t)B * 9);
+        double* du = dmalloc<double>((size_t)B * 8);
+        double* dn = dmalloc<double>((size_t)B * 9);
+        HIPCHK(hipMemcpy(dx, x, B * 9 * sizeof(double), hipMemcpyHostToDevice));
+        HIPCHK(hipMemcpy(du, u, B * 8 * sizeof(double), hipMemcpyHostToDevice));
+        launch_sim_step(B, dx, du, ts, dn, e->stream);
+        HIPCHK(hipStreamSynchronize(e->stream));
+        HIPCHK(hipMemcpy(x_next, dn, B * 9 * sizeof(double), hipMemcpyDeviceToHost));
+        (void)hipFree(dx); (void)hipFree(du); (void)hipFree(dn);
+    } catch (const std::bad_alloc&) {
+        return fail(MPCC_E_OOM, "mpcc_sim_time_step: allocation failed");
+    } catch (const HipError& x) {
+        return fail(MPCC_E_HIP, x.what());
+    }
+    return MPCC_OK;
+}
+
+int mpcc_debug_robot_records(mpcc_engine* e, int M, const double* q, const double* obs, double* rec) {
+    if (!e || M < 1 || !q || !obs || !rec) return fail(MPCC_E_INVALID, "mpcc_debug_robot_records: invalid argument");
+    try {
+        double* dq = dmalloc<double>((size_t)M * 7);
+        double* dob = dmalloc<double>((size_t)M * 4);
+        double* drec = dmalloc<double>((size_t)M * REC);
+        HIPCHK(hipMemcpy(dq, q, M * 7 * sizeof(double), hipMemcpyHostToDevice));
+        HIPCHK(hipMemcpy(dob, obs, M * 4 * sizeof(double), hipMemcpyHostToDevice));
+        DevConst c = e->make_const(1);
+        launch_debug_records(c, M, dq, dob, drec, e->stream);
+        if (c.p.constraint_mask & MPCC_CON_SELFCOL)
+            launch_nn(c, e->d, e->nn_self.desc, e->nn_self.d, 0, M, dq, dob, drec, M, e->stream);
+        if (c.p.constraint_mask & MPCC_CON_ENVCOL)
+            launch_nn(c, e->d, e->nn_env.desc, e->nn_env.d, 1, M, dq, dob, drec, M, e->stream);
+        HIPCHK(hipStreamSynchronize(e->stream));
+        std::vector<double> soa((size_t)M * REC);
+        HIPCHK(hipMemcpy(soa.data(), drec, soa.size() * sizeof(double), hipMemcpyDeviceToHost));
+        for (int t = 0; t < M; t++)
+            for (int f = 0; f < REC; f++) rec[(size_t)t * REC + f] = soa[(size_t)f * M + t];
+        (void)hipFree(dq); (void)hipFree(dob); (void)hipFree(drec);
+    } catch (const std::bad_alloc&) {
+        return fail(MPCC_E_OOM, "allocation failed");
+    } catch (const HipError& x) {
+        return fail(MPCC_E_HIP, x.what());
+    }
+    return MPCC_OK;
+}
+
+int mpcc_debug_spline(mpcc_engine* e, int M, const double* s, double* pos, double* dd1, double* dd2, double* R, double* dR) {
+    if (!e || M < 1 || !s) return fail(MPCC_E_INVALID, "mpcc_debug_spline: invalid argument");
+    if (!e->has_track) return fail(MPCC_E_NOTRACK, "mpcc_debug_spline: no track");
+    try {
+        double* ds = dmalloc<double>(M);
+        double* dout = dmalloc<double>((size_t)M * 21);
+        HIPCHK(hipMemcpy(ds, s, M * sizeof(double), hipMemcpyHostToDevice));
+        DevConst c = e->make_const(1);
+        launch_debug_spline(c, M, ds, dout, e->stream);
+        HIPCHK(hipStreamSynchronize(e->stream));
+        std::vector<double> o((size_t)M * 21);
+        HIPCHK(hipMemcpy(o.data(), dout, o.size() * sizeof(double), hipMemcpyDeviceToHost));
+        for (int t = 0; t < M; t++) {
+            const double* r = &o[(size_t)t * 21];
+            for (int a = 0; a < 3; a++) {
+                if (pos) pos[3 * t + a] = r[a];
+                if (dd1) dd1[3 * t + a] = r[3 + a];
+                if (dd2) dd2[3 * t + a] = r[6 + a];
+                if (dR) dR[3 * t + a] = r[18 + a];
+            }
+            if (R) for (int a = 0; a < 9; a++) R[9 * t + a] = r[9 + a];
+        }
+        (void)hipFree(ds); (void)hipFree(dout);
+    } catch (const std::bad_alloc&) {
+        return fail(MPCC_E_OOM, "allocation failed");
+    } catch (const HipError& x) {
+        return fail(MPCC_E_HIP, x.what());
+    }
+    return MPCC_OK;
+}
+
+int mpcc_debug_stage_cost(mpcc_engine* e, int M, const double* x, const double* u, const double* rec, const int32_t* k,
+                          double* obj, double* fx, double* fu, double* fxx, double* fuu) {
+    if (!e || M < 1 || !x || !u || !rec || !k) return fail(MPCC_E_INVALID, "mpcc_debug_stage_cost: invalid argument");
+    if (!e->has_track) return fail(MPCC_E_NOTRACK, "mpcc_debug_stage_cost: no track");
+    try {
+        const int W = 1 + 9 + 8 + 81 + 64;
+        double* dx = dmalloc<double>((size_t)M * 9);
+        double* du = dmalloc<double>((size_t)M * 8);
+        double* dr = dmalloc<double>((size_t)M * REC);
+        int32_t* dk = dmalloc<int32_t>(M);
+        double* dout = dmalloc<double>((size_t)M * W);
+        std::vector<double> soa((size_t)M * REC);
+        for (int t = 0; t < M; t++)
+            for (int f = 0; f < REC; f++) soa[(size_t)f * M + t] = rec[(size_t)t * REC + f];
+        HIPCHK(hipMemcpy(dx, x, M * 9 * sizeof(double), hipMemcpyHostToDevice));
+        HIPCHK(hipMemcpy(du, u, M * 8 * sizeof(double), hipMemcpyHostToDevice));
+        HIPCHK(hipMemcpy(dr, soa.data(), soa.size() * sizeof(double), hipMemcpyHostToDevice));
+        HIPCHK(hipMemcpy(dk, k, M * sizeof(int32_t), hipMemcpyHostToDevice));
+        DevConst c = e->make_const(1);
+        launch_debug_cost(c, M, dx, du, dr, dk, dout, e->stream);
+        HIPCHK(hipStreamSynchronize(e->stream));
+        std::vector<double> o((size_t)M * W);
+        HIPCHK(hipMemcpy(o.data(), dout, o.size() * sizeof(double), hipMemcpyDeviceToHost));
+        for (int t = 0; t < M; t++) {
+            const double* r = &o[(size_t)t * W];
+            if (obj) obj[t] = r[0];
+            if (fx) std::memcpy(fx + 9 * t, r + 1, 9 * sizeof(double));
+            if (fu) std::memcpy(fu + 8 * t, r + 10, 8 * sizeof(double));
+            if (fxx) std::memcpy(fxx + 81 * t, r + 18, 81 * sizeof(double));
+            if (fuu) std::memcpy(fuu + 64 * t, r + 99, 64 * sizeof(double));
+        }
+        (void)hipFree(dx); (void)hipFree(du); (void)hipFree(dr); (void)hipFree(dk); (void)hipFree(dout);
+    } catch (const std::bad_alloc&) {
+        return fail(MPCC_E_OOM, "allocation failed");
+    } catch (const HipError& x) {
+        return fail(MPCC_E_HIP, x.what());
+    }
+    return MPCC_OK;
+}
+
+int mpcc_debug_solve_qp(mpcc_engine* e, int B, const double* guess, const double* rec, const double* u_cur, double* step,
+                        int32_t* qp_status, int32_t* ipm_iters) {
+    if (!e || B < 1 || B > e->maxB || !guess || !rec || !u_cur)
+        return fail(MPCC_E_INVALID, "mpcc_debug_solve_qp: invalid argument");
+    if (!e->has_track) return fail(MPCC_E_NOTRACK, "mpcc_debug_solve_qp: no track");
+    try {
+        hipStream_t st = e->stream;
+        const int N = e->N;
+        const size_t NS = N + 1, S = (size_t)B * NS;
+        DevConst c = e->make_const(B);
+        std::vector<double> soa((size_t)REC * S);
+        for (size_t t = 0; t < S; t++)
+            for (int f = 0; f < REC; f++) soa[(size_t)f * S + t] = rec[t * REC + f];
+        HIPCHK(hipMemcpy(e->d.guess, guess, S * 17 * sizeof(double), hipMemcpyHostToDevice));
+        HIPCHK(hipMemcpy(e->d.rec, soa.data(), soa.size() * sizeof(double), hipMemcpyHostToDevice));
+        HIPCHK(hipMemcpy(e->s_u0, u_cur, B * 8 * sizeof(double), hipMemcpyHostToDevice));
+        std::vector<int32_t> sqi((size_t)B * SQI, 0);
+        for (int b = 0; b < B; b++) sqi[(size_t)b * SQI + SQ_ACTIVE] = 1;
+        HIPCHK(hipMemcpy(e->d.sqi, sqi.data(), sqi.size() * sizeof(int32_t), hipMemcpyHostToDevice));
+        HIPCHK(hipMemset(e->d.step, 0, S * 17 * sizeof(double)));
+        launch_setqp(c, e->d, e->s_u0, st);
+        launch_ipm(c, e->d, st);
+        HIPCHK(hipStreamSynchronize(st));
+        std::vector<double> stp(S * 17);
+        HIPCHK(hipMemcpy(stp.data(), e->d.step, stp.size() * sizeof(double), hipMemcpyDeviceToHost));
+        HIPCHK(hipMemcpy(sqi.data(), e->d.sqi, sqi.size() * sizeof(int32_t), hipMemcpyDeviceToHost));
+        const size_t nv = NS * 9 + (size_t)N * 8;
+        for (int b = 0; b < B; b++) {
+            for (size_t k = 0; k < NS; k++) {
+                for (int a = 0; a < 9; a++) step[b * nv + 9 * k + a] = stp[(b * NS + k) * 17 + a];
+                if ((int)k < N)
+                    for (int a = 0; a < 8; a++) step[b * nv + 9 * NS + 8 * k + a] = stp[(b * NS + k) * 17 + 9 + a];
+            }
+            int active = sqi[(size_t)b * SQI + SQ_ACTIVE];
+            int qs = sqi[(size_t)b * SQI + SQ_QPSTAT];
+            if (qp_status) qp_status[b] = active ? qs : sqi[(size_t)b * SQI + SQ_STATUS];
+            if (ipm_iters) ipm_iters[b] = sqi[(size_t)b * SQI + SQ_IPMIT];
+        }
+    } catch (const HipError& x) {
+        return fail(MPCC_E_HIP, x.what());
+    }
+    return MPCC_OK;
+}
+
+}  // extern "C"

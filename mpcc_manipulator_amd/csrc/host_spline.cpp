@@ -1,0 +1,278 @@
+// host_spline.cpp — see host_spline.h.
+#include "host_spline.h"
+
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+#include <map>
+
+namespace mpcc {
+
+namespace {
+
+constexpr int NSPLINE = 100;  // N_SPLINE, config.h:38
+using Mat3 = std::array<double, 9>;
+
+Mat3 mul(const Mat3& A, const Mat3& B) {
+    Mat3 C{};
+    for (int i = 0; i < 3; i++)
+        for (int j = 0; j < 3; j++) C[3 * i + j] = A[3 * i] * B[j] + A[3 * i + 1] * B[3 + j] + A[3 * i + 2] * B[6 + j];
+    return C;
+}
+Mat3 mul_tn(const Mat3& A, const Mat3& B) {
+    Mat3 C{};
+    for (int i = 0; i < 3; i++)
+        for (int j = 0; j < 3; j++) C[3 * i + j] = A[i] * B[j] + A[3 + i] * B[3 + j] + A[6 + i] * B[6 + j];
+    return C;
+}
+
+// symmetric eigen decomposition of the lower triangle (Jacobi), ascending eigenvalues
+void sym_eig3(const double* Rin, double* w, double* V) {
+    double A[9];
+    for (int i = 0; i < 3; i++)
+        for (int j = 0; j < 3; j++) A[3 * i + j] = (i >= j) ? Rin[3 * i + j] : Rin[3 * j + i];
+    for (int i = 0; i < 9; i++) V[i] = (i % 4 == 0) ? 1.0 : 0.0;
+    for (int sweep = 0; sweep < 50; sweep++) {
+        if (std::fabs(A[1]) + std::fabs(A[2]) + std::fabs(A[5]) < 1e-300) break;
+        for (int pq = 0; pq < 3; pq++) {
+            int p = (pq == 2) ? 1 : 0, q = (pq == 0) ? 1 : 2;
+            double apq = A[3 * p + q];
+            if (std::fabs(apq) < 1e-300) continue;
+            double theta = (A[3 * q + q] - A[3 * p + p]) / (2 * apq);
+            double t = (theta >= 0 ? 1.0 : -1.0) / (std::fabs(theta) + std::sqrt(theta * theta + 1));
+            double c = 1 / std::sqrt(t * t + 1), s = t * c;
+            for (int k = 0; k < 3; k++) {
+                double akp = A[3 * k + p], akq = A[3 * k + q];
+                A[3 * k + p] = c * akp - s * akq;
+                A[3 * k + q] = s * akp + c * akq;
+            }
+            for (int k = 0; k < 3; k++) {
+                double apk = A[3 * p + k], aqk = A[3 * q + k];
+                A[3 * p + k] = c * apk - s * aqk;
+                A[3 * q + k] = s * apk + c * aqk;
+            }
+            for (int k = 0; k < 3; k++) {
+                double vkp = V[3 * k + p], vkq = V[3 * k + q];
+                V[3 * k + p] = c * vkp - s * vkq;
+                V[3 * k + q] = s * vkp + c * vkq;
+            }
+        }
+    }
+    int idx[3] = {0, 1, 2};
+    std::sort(idx, idx + 3, [&](int a, int b) { return A[4 * a] < A[4 * b]; });
+    double Vs[9];
+    for (int j = 0; j < 3; j++) {
+        w[j] = A[4 * idx[j]];
+        for (int i = 0; i < 3; i++) Vs[3 * i + j] = V[3 * i + idx[j]];
+    }
+    std::memcpy(V, Vs, sizeof Vs);
+}
+
+void exp_skew(const double* v, double* E) {  // ExpMatrix(skew(v)), Q11
+    double sk[9] = {0, -v[2], v[1], v[2], 0, -v[0], -v[1], v[0], 0};
+    double sk2[9];
+    for (int i = 0; i < 3; i++)
+        for (int j = 0; j < 3; j++) sk2[3 * i + j] = sk[3 * i] * sk[j] + sk[3 * i + 1] * sk[3 + j] + sk[3 * i + 2] * sk[6 + j];
+    double vn = std::sqrt(v[0] * v[0] + v[1] * v[1] + v[2] * v[2]);
+    if (vn <= 1e-8) {
+        for (int i = 0; i < 9; i++) E[i] = ((i % 4 == 0) ? 1.0 : 0.0) + std::cos(vn) * sk[i];
+        return;
+    }
+    double a = std::sin(vn) / vn, b = (1 - std::cos(vn)) / (vn * vn);
+    for (int i = 0; i < 9; i++) E[i] = ((i % 4 == 0) ? 1.0 : 0.0) + a * sk[i] + b * sk2[i];
+}
+
+struct Cubic {  // CubicSpline (cubic_spline.cpp)
+    std::vector<double> x, y, a, b, c, d;
+    bool regular = false;
+    double dx = 0;
+    std::map<double, int> xmap;
+    void gen(const std::vector<double>& xin, const std::vector<double>& yin, bool reg) {
+        x = xin; y = yin; regular = reg;
+        const int n = (int)x.size();
+        if (reg) dx = x[1] - x[0];
+        else { xmap.clear(); for (int i = 0; i < n; i++) xmap[x[i]] = i; }
+        a = y; b.assign(n, 0.0); c.assign(n, 0.0); d.assign(n, 0.0);
+        std::vector<double> mu(n, 0.0), h(n, 0.0), alpha(n, 0.0), l(n, 0.0), z(n, 0.0);
+        for (int i = 0; i < n - 1; i++) h[i] = x[i + 1] - x[i];
+        for (int i = 1; i < n - 1; i++) alpha[i] = 3.0 / h[i] * (a[i + 1] - a[i]) - 3.0 / h[i - 1] * (a[i] - a[i - 1]);
+        l[0] = 1.0;
+        for (int i = 1; i < n - 1; i++) {
+            l[i] = 2.0 * (x[i + 1] - x[i - 1]) - h[i - 1] * mu[i - 1];
+            mu[i] = h[i] / l[i];
+            z[i] = (alpha[i] - h[i - 1] * z[i - 1]) / l[i];
+        }
+        for (int i = n - 2; i >= 0; i--) {
+            c[i] = z[i] - mu[i] * c[i + 1];
+            b[i] = (a[i + 1] - a[i]) / h[i] - (h[i] * (c[i + 1] + 2.0 * c[i])) / 3.0;
+            d[i] = (c[i + 1] - c[i]) / (3.0 * h[i]);
+        }
+    }
+    int index(double xx) const {
+        if (xx == x.back()) return (int)x.size() - 1;
+        if (regular) return (int)std::floor(xx / dx);
+        auto it = xmap.upper_bound(xx);
+        return (it == xmap.end()) ? -1 : it->second - 1;
+    }
+    double point(double xx) const {
+        xx = std::max(0., std::min(xx, x.back()));
+        int i = index(xx);
+        double d1 = xx - x[i], d2 = d1 * d1, d3 = d1 * d2;
+        if (i == (int)x.size() - 1) return y.back();
+        return a[i] + b[i] * d1 + c[i] * d2 + d[i] * d3;
+    }
+};
+
+struct CubicRot {  // CubicSplineRot (cubic_spline_rot.cpp)
+    std::vector<double> x, c, d;
+    std::vector<Mat3> R;
+    std::vector<std::array<double, 3>> lv;
+    bool regular = false;
+    double dx = 0;
+    std::map<double, int> xmap;
+    void gen(const std::vector<double>& xin, const std::vector<Mat3>& Rin, bool reg) {
+        x = xin; R = Rin; regular = reg;
+        const int n = (int)x.size();
+        if (reg) dx = x[1] - x[0];
+        else { xmap.clear(); for (int i = 0; i < n; i++) xmap[x[i]] = i; }
+        c.assign(n, 0.0); d.assign(n, 0.0); lv.assign(n, {0, 0, 0});
+        for (int i = 0; i < n - 1; i++) {
+            c[i] = 3.0 / std::pow(x[i + 1] - x[i], 2);
+            d[i] = -2.0 / std::pow(x[i + 1] - x[i], 3);
+            Mat3 RtR = mul_tn(R[i], R[i + 1]);
+            host_log_vec(RtR.data(), lv[i].data());
+        }
+    }
+    int index(double xx) const {
+        if (xx == x.back()) return (int)x.size() - 1;
+        if (regular) return (int)std::floor(xx / dx);
+        auto it = xmap.upper_bound(xx);
+        return (it == xmap.end()) ? -1 : it->second - 1;
+    }
+    Mat3 point(double xx) const {
+        xx = std::max(0., std::min(xx, x.back()));
+        int i = index(xx);
+        if (i == (int)x.size() - 1) return R.back();
+        double d1 = xx - x[i], d2 = d1 * d1, d3 = d1 * d2;
+        double f = c[i] * d2 + d[i] * d3;
+        double v[3] = {lv[i][0] * f, lv[i][1] * f, lv[i][2] * f};
+        Mat3 E;
+        exp_skew(v, E.data());
+        return mul(R[i], E);
+    }
+};
+
+std::vector<double> arc_length(const std::vector<double>& X, const std::vector<double>& Y, const std::vector<double>& Z) {
+    const int n = (int)X.size();
+    std::vector<double> s(n, 0.0);
+    for (int i = 0; i < n - 1; i++) {
+        double dx = X[i + 1] - X[i], dy = Y[i + 1] - Y[i], dz = Z[i + 1] - Z[i];
+        s[i + 1] = s[i] + std::sqrt(dx * dx + dy * dy + dz * dz);
+    }
+    return s;
+}
+
+std::vector<double> lin_spaced(int n, double lo, double hi) {  // Eigen::VectorXd::LinSpaced
+    std::vector<double> v(n);
+    const double step = (hi - lo) / double(n - 1);
+    const bool flip = std::fabs(hi) < std::fabs(lo);
+    for (int i = 0; i < n; i++) {
+        if (flip) v[i] = (i == 0) ? lo : hi - double(n - 1 - i) * step;
+        else v[i] = (i == n - 1) ? hi : lo + double(i) * step;
+    }
+    return v;
+}
+
+struct Path {
+    std::vector<double> s, X, Y, Z;
+    std::vector<Mat3> R;
+};
+
+Path resample(const Cubic& fx, const Cubic& fy, const Cubic& fz, const CubicRot& fr, double total) {  // :89-119
+    Path p;
+    p.s = lin_spaced(NSPLINE, 0, total);
+    p.X.resize(NSPLINE); p.Y.resize(NSPLINE); p.Z.resize(NSPLINE); p.R.resize(NSPLINE);
+    for (int i = 0; i < NSPLINE; i++) {
+        p.X[i] = fx.point(p.s[i]);
+        p.Y[i] = fy.point(p.s[i]);
+        p.Z[i] = fz.point(p.s[i]);
+        p.R[i] = fr.point(p.s[i]);
+    }
+    return p;
+}
+
+}  // namespace
+
+void host_log_vec(const double* R, double* v) {  // invskew(LogMatrix(R)), Q10
+    const double tr = R[0] + R[4] + R[8];
+    v[0] = v[1] = v[2] = 0.0;
+    if (std::fabs(tr + 1.0) < 1e-6) {
+        double w[3], V[9];
+        sym_eig3(R, w, V);
+        for (int i = 0; i < 3; i++) {
+            if (std::fabs(w[i] - 1.0) < 1e-4) {
+                double e0 = V[i], e1 = V[3 + i], e2 = V[6 + i];
+                double n = std::sqrt(e0 * e0 + e1 * e1 + e2 * e2);
+                v[0] = -(e0 / n) * M_PI; v[1] = -(e1 / n) * M_PI; v[2] = -(e2 / n) * M_PI;
+            }
+        }
+    } else if (std::fabs(tr - 3.0) < 1e-6) {
+        // zero
+    } else {
+        const double th = std::acos((tr - 1.0) / 2.0);
+        const double f = 1.0 / 2.0 * th / std::sin(th);
+        v[0] = f * (R[7] - R[5]);
+        v[1] = f * (R[2] - R[6]);
+        v[2] = f * (R[3] - R[1]);
+    }
+}
+
+void quat_to_rot(double qx, double qy, double qz, double qw, double* R) {
+    const double n = std::sqrt(qx * qx + qy * qy + qz * qz + qw * qw);
+    const double x = qx / n, y = qy / n, z = qz / n, w = qw / n;
+    const double tx = 2 * x, ty = 2 * y, tz = 2 * z;
+    const double twx = tx * w, twy = ty * w, twz = tz * w;
+    const double txx = tx * x, txy = ty * x, txz = tz * x;
+    const double tyy = ty * y, tyz = tz * y, tzz = tz * z;
+    R[0] = 1 - (tyy + tzz); R[1] = txy - twz; R[2] = txz + twy;
+    R[3] = txy + twz; R[4] = 1 - (txx + tzz); R[5] = tyz - twx;
+    R[6] = txz - twy; R[7] = tyz + twx; R[8] = 1 - (txx + tyy);
+}
+
+SplineTables build_track_spline(int n, const double* X, const double* Y, const double* Z, const double* R9) {
+    std::vector<double> x0(X, X + n), y0(Y, Y + n), z0(Z, Z + n);
+    std::vector<Mat3> r0(n);
+    for (int i = 0; i < n; i++) std::memcpy(r0[i].data(), R9 + 9 * i, sizeof(double) * 9);
+    // fitSpline (arc_length_spline.cpp:213-253): two irregular fit/resample passes, final regular fit
+    std::vector<double> sa = arc_length(x0, y0, z0);
+    double total = sa.back();
+    Cubic f1x, f1y, f1z;
+    CubicRot f1r;
+    f1x.gen(sa, x0, false); f1y.gen(sa, y0, false); f1z.gen(sa, z0, false); f1r.gen(sa, r0, false);
+    Path p1 = resample(f1x, f1y, f1z, f1r, total);
+    sa = arc_length(p1.X, p1.Y, p1.Z);
+    total = sa.back();
+    Cubic f2x, f2y, f2z;
+    CubicRot f2r;
+    f2x.gen(sa, p1.X, false); f2y.gen(sa, p1.Y, false); f2z.gen(sa, p1.Z, false); f2r.gen(sa, p1.R, false);
+    Path p2 = resample(f2x, f2y, f2z, f2r, total);
+    Cubic fx, fy, fz;
+    CubicRot fr;
+    fx.gen(p2.s, p2.X, true); fy.gen(p2.s, p2.Y, true); fz.gen(p2.s, p2.Z, true); fr.gen(p2.s, p2.R, true);
+
+    SplineTables t;
+    t.n = NSPLINE;
+    t.delta = p2.s[1] - p2.s[0];
+    t.s = p2.s; t.X = p2.X; t.Y = p2.Y; t.Z = p2.Z;
+    const Cubic* ax[3] = {&fx, &fy, &fz};
+    for (int a = 0; a < 3; a++) { t.a[a] = ax[a]->a; t.b[a] = ax[a]->b; t.c[a] = ax[a]->c; t.d[a] = ax[a]->d; }
+    t.R.resize((size_t)NSPLINE * 9);
+    for (int i = 0; i < NSPLINE; i++) std::memcpy(&t.R[(size_t)9 * i], p2.R[i].data(), sizeof(double) * 9);
+    t.cr = fr.c; t.dr = fr.d;
+    t.logv.resize((size_t)NSPLINE * 3);
+    for (int i = 0; i < NSPLINE; i++)
+        for (int a = 0; a < 3; a++) t.logv[(size_t)3 * i + a] = fr.lv[i][a];
+    return t;
+}
+
+}  // namespace mpcc

@@ -1,0 +1,61 @@
+// kernels.h — host-side launch wrappers of the engine's HIP kernels (kernels.hip).
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include "dev_common.h"
+
+namespace mpcc {
+
+struct DevBuffers {
+    // per-call I/O (device)
+    double* x0;        // [B*9]  in/out
+    const double* u0;  // [B*8]
+    const double* obs; // [B*4]
+    double* u0_out;    // [B*8]
+    double* horizon;   // [B*(N+1)*17]
+    int32_t* status;   // [B]
+    int32_t* ok;       // [B]
+    // persistent controller state
+    double* guess;     // [maxB*(N+1)*17]
+    int32_t* valid;    // [maxB]
+    int32_t* fails;    // [maxB]
+    // workspaces
+    double* rec;       // [REC * maxB*(N+1)]  SoA
+    double* qs;        // [maxB*(N+1)*QS]
+    double* is;        // [maxB*(N+1)*IS]
+    double* step;      // [maxB*(N+1)*17]
+    double* trial;     // [maxB*(N+1)*4]  per stage: obj, vio_lo, vio_up, spare
+    int32_t* sqi;      // [maxB*SQI]
+    double* sqd;       // [maxB*SQ]
+    // NN weights (device)
+    const double* nn_self;  // packed W0,b0,W1,b1,W2,b2
+    const double* nn_env;   // packed W0,b0,...,W4,b4
+};
+
+constexpr int SQI = 8;  // int bookkeeping per instance: status, active, iter, nfilt, qp_status, ipm_iters, reject
+constexpr int SQ_REJECT = 6;
+
+struct NNDesc {
+    int L;              // number of layers
+    int nin;            // raw input size (7 self, 10 env)
+    int dims[6];        // dims[0] = 3*nin ... dims[L] = nout
+    long offW[5], offb[5];
+};
+
+void launch_prepare(const DevConst& c, const DevBuffers& d, hipStream_t s);
+void launch_stage_records(const DevConst& c, const DevBuffers& d, hipStream_t s);
+void launch_nn(const DevConst& c, const DevBuffers& d, const NNDesc& nd, const double* W, int which, int M,
+               const double* q, const double* obs, double* rec, int rec_stride, hipStream_t s);
+void launch_setqp(const DevConst& c, const DevBuffers& d, const double* u_cur, hipStream_t s);
+void launch_ipm(const DevConst& c, const DevBuffers& d, hipStream_t s);
+void launch_trial(const DevConst& c, const DevBuffers& d, const double* u_cur, double alpha_scale, int dead, hipStream_t s);
+void launch_accept(const DevConst& c, const DevBuffers& d, hipStream_t s);
+void launch_apply(const DevConst& c, const DevBuffers& d, hipStream_t s);
+void launch_finalize(const DevConst& c, const DevBuffers& d, hipStream_t s);
+void launch_sim_step(int B, const double* x, const double* u, double ts, double* xn, hipStream_t s);
+void launch_debug_records(const DevConst& c, int M, const double* q, const double* obs, double* rec, hipStream_t s);
+void launch_debug_spline(const DevConst& c, int M, const double* sv, double* out, hipStream_t s);
+void launch_debug_cost(const DevConst& c, int M, const double* x, const double* u, const double* rec, const int32_t* k,
+                       double* out, hipStream_t s);
+
+}  // namespace mpcc
