@@ -80,6 +80,11 @@ typedef struct {
     double Tx[9], Tu[8];                                                        /* NormalizationParam */
     double eps_prim, eps_dual, line_search_tau, line_search_eta, line_search_rho; /* SQPParam */
     int32_t max_iter, line_search_max_iter, do_SOC, use_BFGS;
+    /* Parity policy P1: per-row constraint violations <= vio_floor count as zero in
+     * the filter line search's constraint_norm (osqp_interface.cpp:824-833).  An exactly solved QP step
+     * leaves violations at rounding-noise level (~1e-16..1e-12) where the reference's OSQP steps carry
+     * ~eps_abs = 1e-4; without the floor the filter decision compares noise.  Default 1e-9. */
+    double vio_floor;
 } mpcc_params;
 
 /* PathToJson (types.h:63-70).  Any of the six may be NULL when 'merged' is given: a single JSON

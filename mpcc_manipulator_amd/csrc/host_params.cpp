@@ -136,6 +136,7 @@ extern "C" int mpcc_params_load_json(const mpcc_json_paths* paths, const mpcc_ov
         p.line_search_max_iter = (int32_t)on.get(q, "sqp", "line_search_max_iter");
         p.do_SOC = on.get(q, "sqp", "do_SOC") != 0.0;
         p.use_BFGS = on.get(q, "sqp", "use_BFGS") != 0.0;
+        p.vio_floor = 1e-9;
         *out = p;
         return MPCC_OK;
     } catch (const std::exception& e) {

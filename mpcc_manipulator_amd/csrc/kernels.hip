@@ -953,7 +953,9 @@ __global__ void __launch_bounds__(64) k_trial(DevConst c, DevBuffers d, const do
         for (int j = 0; j < DOF; j++) { double dlt = tu(k + 1, j) - u[j]; sq += dlt * dlt; }
         objd = p.qp_r_ddq * sq;
     }
-    double lo = 0, up = 0;  // sum (l - c)^+ and sum (c - u)^+
+    double lo = 0, up = 0;  // sum (l - c)^+ and sum (c - u)^+ (parity policy P1: noise floor per row)
+    const double vf = p.vio_floor;
+    auto vfloor = [](double v, double f) { return (v > f) ? v : 0.0; };
     if (k >= 1) {  // dynamics rows, l = u = 0
         double xp[9], up_[8];
         for (int a = 0; a < 9; a++) xp[a] = tx(k - 1, a);
@@ -963,20 +965,20 @@ __global__ void __launch_bounds__(64) k_trial(DevConst c, DevBuffers d, const do
             for (int m = 0; m < 9; m++) s1 += c.A[a * 9 + m] * xp[m];
             for (int m = 0; m < 8; m++) s2 += c.B[a * 8 + m] * up_[m];
             double cv = (1.0 / p.Tx[a]) * (x[a] - (s1 + s2 + 0.0));
-            lo += fmax(0.0 - cv, 0.0);
-            up += fmax(cv - 0.0, 0.0);
+            lo += vfloor(fmax(0.0 - cv, 0.0), vf);
+            up += vfloor(fmax(cv - 0.0, 0.0), vf);
         }
     }
     for (int a = 0; a < 9; a++) {  // state bounds
         double l = p.lx[a], h = p.ux[a];
         if (a == 7) { l = fmax(x[7] - p.s_trust_region, 0.); h = fmin(x[7] + p.s_trust_region, c.spl.L); }
-        lo += fmax(l - x[a], 0.0);
-        up += fmax(x[a] - h, 0.0);
+        lo += vfloor(fmax(l - x[a], 0.0), vf);
+        up += vfloor(fmax(x[a] - h, 0.0), vf);
     }
     if (k < N) {
         for (int a = 0; a < 8; a++) {  // input bounds (constr = u, :274)
-            lo += fmax(p.lu[a] - u[a], 0.0);
-            up += fmax(u[a] - p.uu[a], 0.0);
+            lo += vfloor(fmax(p.lu[a] - u[a], 0.0), vf);
+            up += vfloor(fmax(u[a] - p.uu[a], 0.0), vf);
         }
         for (int j = 0; j < DOF; j++) {  // ddq rows
             double cv, l, h;
@@ -989,14 +991,14 @@ __global__ void __launch_bounds__(64) k_trial(DevConst c, DevBuffers d, const do
                 l = p.lddq[j];
                 h = p.uddq[j];
             }
-            lo += fmax(l - cv, 0.0);
-            up += fmax(cv - h, 0.0);
+            lo += vfloor(fmax(l - cv, 0.0), vf);
+            up += vfloor(fmax(cv - h, 0.0), vf);
         }
         for (int r = 0; r < NPC; r++) {  // polytopic: l = -INF, u = 0
             double val;
             if (!poly_row(c, u, rv, r, &val, false, nullptr, nullptr)) continue;
-            lo += fmax(-INF - val, 0.0);
-            up += fmax(val - 0.0, 0.0);
+            lo += vfloor(fmax(-INF - val, 0.0), vf);
+            up += vfloor(fmax(val - 0.0, 0.0), vf);
         }
     }
     if (dead) return;  // faithful evaluation of a discarded trial: results are not used

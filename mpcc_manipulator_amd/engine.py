@@ -43,6 +43,7 @@ class MpccParams(C.Structure):
         ("Tx", D * 9), ("Tu", D * 8),
         ("eps_prim", D), ("eps_dual", D), ("line_search_tau", D), ("line_search_eta", D), ("line_search_rho", D),
         ("max_iter", I32), ("line_search_max_iter", I32), ("do_SOC", I32), ("use_BFGS", I32),
+        ("vio_floor", D),
     ]
 
     def as_dict(self):

@@ -1071,11 +1071,12 @@ static void set_qp(const Oracle& o, const double* guess, const double* recs, con
     }
 }
 
-// constraint_norm — osqp_interface.cpp:824-833
-static double constraint_norm(const DenseQP& q) {
+// constraint_norm — osqp_interface.cpp:824-833, with parity policy P1: per-row violations at or below
+// vio_floor (rounding noise of an exactly solved QP step) count as zero.
+static double constraint_norm(const DenseQP& q, double floor_) {
     double a = 0, b = 0;
-    for (int i = 0; i < q.nc; i++) a += std::max(q.l[i] - q.c[i], 0.0);
-    for (int i = 0; i < q.nc; i++) b += std::max(q.c[i] - q.u[i], 0.0);
+    for (int i = 0; i < q.nc; i++) { double v = std::max(q.l[i] - q.c[i], 0.0); a += (v > floor_) ? v : 0.0; }
+    for (int i = 0; i < q.nc; i++) { double v = std::max(q.c[i] - q.u[i], 0.0); b += (v > floor_) ? v : 0.0; }
     return a + b;
 }
 
@@ -1723,7 +1724,7 @@ static int solve_ocp(const Oracle& o, double* guess, const double* recs, const d
             denorm_add(o, guess, step, alpha, trial.data());
             DenseQP q;
             set_qp(o, trial.data(), recs, ucur, false, q);
-            Filter f{q.obj, constraint_norm(q)};
+            Filter f{q.obj, constraint_norm(q, p.vio_floor)};
             for (size_t j = 0; j < filter.size(); j++)
                 if (f.obj >= filter[j].obj && f.vio >= filter[j].vio) { accepted = false; break; }
             if (accepted) {

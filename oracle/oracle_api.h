@@ -45,6 +45,9 @@ typedef struct {
     /* SQPParam */
     double eps_prim, eps_dual, line_search_tau, line_search_eta, line_search_rho;
     int    max_iter, line_search_max_iter, do_SOC, use_BFGS;
+    /* Parity policy P1: per-row constraint violations <= vio_floor count as zero in the
+     * filter line search (constraint_norm), removing the rounding noise an exact QP leaves behind. */
+    double vio_floor;
 } OracleParams;
 
 typedef struct {

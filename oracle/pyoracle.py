@@ -33,6 +33,7 @@ class OracleParams(C.Structure):
         ("eps_prim", D), ("eps_dual", D), ("line_search_tau", D), ("line_search_eta", D),
         ("line_search_rho", D),
         ("max_iter", C.c_int), ("line_search_max_iter", C.c_int), ("do_SOC", C.c_int), ("use_BFGS", C.c_int),
+        ("vio_floor", D),
     ]
 
 

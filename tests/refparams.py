@@ -94,4 +94,5 @@ def resolve(sections=None, overrides=None, N=20, Ts=None, constraint_mask=7, cto
         line_search_eta=q_o["line_search_eta"], line_search_rho=q_o["line_search_rho"],
         max_iter=int(q_o["max_iter"]), line_search_max_iter=int(q_o["line_search_max_iter"]),
         do_SOC=int(bool(q_o["do_SOC"])), use_BFGS=int(bool(q_o["use_BFGS"])),
+        vio_floor=1e-9,
     )
