@@ -1,0 +1,216 @@
+"""Benchmark: MPCC solves/sec (7-DOF Panda, N=20, 2 SQP iterations) — BASELINE.json configs[1].
+
+One step = one batched MPC::runMPC_ (cpp/src/MPC/mpc.cpp:104-190) over B independent controllers per
+GPU (default B = 4096, bounds + singularity rows: constraint_mask = 2), inputs resident in HBM; for
+N > 1 GPUs every rank solves its own B instances (weak scaling) and the optimal inputs u0 are gathered
+over RCCL each step.  Prints one JSON line (rank 0).
+
+    python bench.py [--gpus N --steps K --warmup W --batch B]
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+FP64_PEAK_TFLOPS = 78.6  # MI355X FP64 dense peak (matrix = vector, spec) — the roof of the FP64 solve kernels
+SEED = 0x4D504343
+Q0 = np.array([0, 0, 0, -np.pi / 2, 0, np.pi / 2, np.pi / 4])
+
+
+def algorithmic_qp_flops(N):
+    """SURVEY.md §8(d) F_qp per SQP iteration (condensing + Cholesky + solves; inequality handling is
+    solver overhead and not credited): 2(96N^3 + 324N^2) + 616N^2 + n^3/3 + 4n^2, n = 8N."""
+    n = 8 * N
+    return 2 * (96 * N ** 3 + 324 * N ** 2) + 616 * N ** 2 + n ** 3 / 3 + 4 * n ** 2
+
+
+def make_pool(m, params, mask, steps, device):
+    """B = 1 closed loop on the GPU (main.cpp:100-114) -> per-step controller inputs."""
+    from mpcc_manipulator_amd.integrator import sim_time_step
+    eng = m.Engine(params, max_batch=1, device=device, constraint_mask=mask)
+    ee = eng.robot_records(Q0, np.array([[3.0, 3.0, 3.0, 0.0]]))[0, :3]
+    X, Y, Z, q = m.load_default_track()
+    track = m.track_from_points(X, Y, Z, q, ee)
+    eng.set_track(*track)
+    N = params.N
+    x = np.zeros((1, 9)); x[0, :7] = Q0
+    u = np.zeros((1, 8))
+    obs = np.array([[3.0, 3.0, 3.0, 0.0]])
+    pool = {k: [] for k in ["x0", "u0", "guess", "valid", "fails", "status"]}
+    for _ in range(steps):
+        g, v, f = eng.get_warmstart(1)
+        pool["x0"].append(x[0].copy()); pool["u0"].append(u[0].copy())
+        pool["guess"].append(g[0]); pool["valid"].append(v[0]); pool["fails"].append(f[0])
+        xin = x.copy()
+        out = eng.solve(xin, u, obs)
+        pool["status"].append(out["status"][0])
+        u = out["u0"].copy()
+        x = sim_time_step(x, u, params.Ts)
+    eng.close()
+    return {k: np.array(v) for k, v in pool.items()}, track
+
+
+def cpu_baseline(params_dict, track, x0, u0, obs, guess, valid, fails, threads, sample):
+    """The oracle (CPU restatement of the reference algorithm, oracle/) on a bounded sample of the same
+    workload, OpenMP over instances.  Test infrastructure used only as the reported baseline."""
+    from oracle.pyoracle import Oracle
+    o = Oracle(params_dict, os.path.join(ROOT, "mpcc_manipulator_amd", "data", "nn"), qp_mode=0, nthreads=threads)
+    o.set_track(*track)
+    n = min(sample, x0.shape[0])
+    xs, gs, vs, fs = x0[:n].copy(), guess[:n].copy(), valid[:n].copy(), fails[:n].copy()
+    o.run_mpc(xs[:2].copy(), u0[:2], obs[:2], gs[:2].copy(), vs[:2].copy(), fs[:2].copy())  # warm caches
+    t0 = time.perf_counter()
+    o.run_mpc(xs, u0[:n], obs[:n], gs, vs, fs)
+    dt = time.perf_counter() - t0
+    o.close()
+    return n / dt, n, dt
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--batch", type=int, default=4096, help="instances per GPU")
+    ap.add_argument("--N", type=int, default=20)
+    ap.add_argument("--mask", type=int, default=2, help="polytopic rows: 1 self, 2 singularity, 4 env (configs[1] = 2)")
+    ap.add_argument("--max-iter", type=int, default=2)
+    ap.add_argument("--pool-steps", type=int, default=400)
+    ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--cpu-sample", type=int, default=256)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "pmc_traffic_k_ipm.json"))
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    import torch
+    torch.cuda.set_device(local)
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+
+    import mpcc_manipulator_amd as m
+
+    N, B = args.N, args.batch
+    params = m.load_params(N, overrides={"sqp": {"max_iter": args.max_iter}})
+    params.constraint_mask = args.mask
+    pool, track = make_pool(m, params, args.mask, args.pool_steps, local)
+    eng = m.Engine(params, max_batch=B, device=local, constraint_mask=args.mask)
+    eng.set_track(*track)
+
+    # instances: pool step t = (global index) mod T, q += N(0, 0.005)
+    rng = np.random.default_rng(SEED + rank)
+    T = len(pool["x0"])
+    idx = (np.arange(B) + rank * B) % T
+    x0 = pool["x0"][idx].copy()
+    x0[:, :7] += rng.normal(0.0, 0.005, size=(B, 7))
+    u0 = pool["u0"][idx].copy()
+    guess = pool["guess"][idx].copy()
+    valid = pool["valid"][idx].astype(np.int32)
+    fails = pool["fails"][idx].astype(np.int32)
+    obs = np.tile(np.array([3.0, 3.0, 3.0, 0.0]), (B, 1))
+
+    dev = torch.device("cuda", local)
+    t = lambda a, dt=torch.float64: torch.from_numpy(np.ascontiguousarray(a)).to(dev, dt)
+    x0_p, u0_d, obs_d = t(x0), t(u0), t(obs)
+    g_p, v_p, f_p = t(guess), t(valid, torch.int32), t(fails, torch.int32)
+    x0_d = x0_p.clone()
+    u_out = torch.empty((B, 8), dtype=torch.float64, device=dev)
+    hor = torch.empty((B, N + 1, 17), dtype=torch.float64, device=dev)
+    status = torch.empty(B, dtype=torch.int32, device=dev)
+    ok = torch.empty(B, dtype=torch.int32, device=dev)
+    u_all = torch.empty((world * B, 8), dtype=torch.float64, device=dev) if world > 1 else None
+    stream = torch.cuda.current_stream(dev)
+
+    def step():
+        x0_d.copy_(x0_p)
+        eng.set_warmstart_device(B, g_p, v_p, f_p, stream=stream)
+        eng.solve_device(B, x0_d, u0_d, obs_d, u_out, hor, status, ok, stream=stream)
+        if world > 1:
+            dist.all_gather_into_tensor(u_all, u_out)  # RCCL gather of u0 over xGMI
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    eng.timing_begin()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    tm, ncalls, nipm = eng.timing_end()
+    if world > 1:
+        te = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(te, op=dist.ReduceOp.MAX)
+        elapsed = float(te.item())
+
+    st = status.cpu().numpy()
+    stats = eng.solve_stats(B)
+    solved = float(np.mean(st == 0))
+    value = B * world * args.steps / elapsed
+    ms = elapsed / args.steps * 1e3
+
+    # roofline of the dominant kernel (k_ipm: interior-point QP solve, one wave per instance)
+    t_ipm = tm["solve_qp"] / max(1, nipm)
+    flops = B * algorithmic_qp_flops(N)
+    achieved = flops / t_ipm / 1e12
+    traffic = None
+    if os.path.exists(args.traffic):
+        with open(args.traffic) as f:
+            tr = json.load(f)
+        if tr.get("batch") == B and tr.get("N") == N:
+            traffic = tr.get("hbm_bytes_per_launch")
+    roof = {"kernel": "k_ipm", "bound": "mfma", "achieved": achieved, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
+            "frac": achieved / FP64_PEAK_TFLOPS, "traffic": traffic,
+            "avg_launch_ms": t_ipm * 1e3, "launches_timed": nipm, "algorithmic_flops_per_launch": flops}
+
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        try:
+            pd = params.as_dict()
+            v, n, dt = cpu_baseline(pd, track, x0, u0, obs, guess, valid, fails, args.cpu_threads, args.cpu_sample)
+            cpu = {"value": v, "unit": "solves/s", "cores": args.cpu_threads, "kind": "port",
+                   "sample": f"{n} instances of the same workload (CPU restatement of the reference algorithm, "
+                             f"OSQP -> exact IPM), {dt:.2f} s"}
+        except Exception as e:  # baseline is reported, never the target
+            print(f"cpu baseline failed: {e}", file=sys.stderr)
+
+    if rank == 0:
+        phases = {k: round(v / max(1, ncalls) * 1e3, 4) for k, v in tm.items()}
+        print(json.dumps({"phase_ms_per_step": phases, "solved_frac": solved,
+                          "sqp_iter_hist": np.bincount(stats["sqp_iter"], minlength=3).tolist(),
+                          "ipm_iters_mean": float(stats["ipm_iters"].mean())}), file=sys.stderr)
+        line = {
+            "metric": "MPCC solves/sec (whole node), 7-DOF Panda N=20, 2 SQP iters",
+            "value": value, "unit": "solves/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+            "ms_per_step": ms, "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f64",
+            "data": "synthetic (closed-loop state pool on the default track, q + N(0, 0.005 rad))",
+            "config": {"workload": f"configs[1]: batch={B}/GPU Panda MPCC instances, N={N}, bounds+singularity "
+                                   f"constraints (mask={args.mask}), {args.max_iter} SQP iters",
+                       "batch_per_gpu": B, "global_batch": B * world, "horizon": N, "sqp_iters": args.max_iter,
+                       "parallelism": f"instance-sharded x{world}" + (", RCCL all_gather(u0)" if world > 1 else "")},
+            "roofline": roof,
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(line))
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -156,6 +156,20 @@ int mpcc_set_warmstart(mpcc_engine* e, int B, const double* guess, const int32_t
 int mpcc_get_warmstart(mpcc_engine* e, int B, double* guess, int32_t* valid, int32_t* fails);
 int mpcc_reset_warmstart(mpcc_engine* e, int B, const uint8_t* mask /* NULL = all */);
 
+/* Device-to-device variant of mpcc_set_warmstart (asynchronous on 'stream', NULL = engine stream). */
+int mpcc_set_warmstart_device(mpcc_engine* e, int B, const double* d_guess, const int32_t* d_valid,
+                              const int32_t* d_fails, void* stream);
+
+/* Live per-phase device timing of mpcc_solve_device calls: between begin and end every call records
+ * HIP events on its stream (no synchronization); end synchronizes and returns the summed phase times
+ * and the number of calls and of IPM (k_ipm) launches timed. */
+int mpcc_timing_begin(mpcc_engine* e);
+int mpcc_timing_end(mpcc_engine* e, mpcc_timing* sum, int32_t* n_calls, int32_t* n_ipm_launches);
+
+/* Per-instance iteration counts of the last solve: SQP iteration index at exit and IPM iterations of
+ * the last QP (host arrays, may be NULL). */
+int mpcc_get_solve_stats(mpcc_engine* e, int B, int32_t* sqp_iter, int32_t* ipm_iters, int32_t* qp_status);
+
 /* Batched MPC::runMPC_ on host arrays (H2D, solve, D2H).  Any output pointer may be NULL. */
 int mpcc_solve(mpcc_engine* e, int B, double* x0, const double* u0, const double* obs,
                double* u0_out, double* horizon_out, int32_t* status, int32_t* ok, mpcc_timing* timing);

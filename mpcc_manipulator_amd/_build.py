@@ -11,7 +11,7 @@ ROOT = os.path.dirname(PKG)
 CSRC = os.path.join(PKG, "csrc")
 BUILD = os.path.join(PKG, "_build")
 LIB = os.path.join(BUILD, "libmpcc_engine.so")
-SOURCES = ["kernels.hip", "engine.cpp", "host_params.cpp", "host_spline.cpp", "mpc.cpp"]
+SOURCES = ["kernels.hip", "ipm.hip", "engine.cpp", "host_params.cpp", "host_spline.cpp", "mpc.cpp"]
 ARCH = os.environ.get("MPCC_OFFLOAD_ARCH", "gfx950")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 CFLAGS = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-I", os.path.join(ROOT, "include"),

@@ -66,6 +66,20 @@ struct mpcc_engine {
     NNWeights nn_self, nn_env;
     double A[81], B[72], M[81], G[72];
     std::vector<hipEvent_t> events;
+    // live timing (mpcc_timing_begin/end): event pairs per phase over many calls
+    bool live = false;
+    std::vector<hipEvent_t> live_pool;
+    size_t live_used = 0;
+    std::vector<std::pair<hipEvent_t, hipEvent_t>> lv_env, lv_setqp, lv_ipm, lv_alpha, lv_total;
+    int live_calls = 0;
+    hipEvent_t live_ev() {
+        if (live_used == live_pool.size()) {
+            hipEvent_t e;
+            HIPCHK(hipEventCreate(&e));
+            live_pool.push_back(e);
+        }
+        return live_pool[live_used++];
+    }
 
     ~mpcc_engine() {
         auto f = [](void* p) { if (p) (void)hipFree(p); };
@@ -74,6 +88,7 @@ struct mpcc_engine {
         f(s_x0); f(s_u0); f(s_obs); f(s_u0out); f(s_hor); f(s_status); f(s_ok);
         f(nn_self.d); f(nn_env.d);
         for (auto ev : events) (void)hipEventDestroy(ev);
+        for (auto ev : live_pool) (void)hipEventDestroy(ev);
         if (stream) (void)hipStreamDestroy(stream);
     }
 
@@ -184,6 +199,8 @@ int fail(int code, const std::string& m) {
 
 void validate_params(const mpcc_params& p) {
     if (p.N < 1 || p.N > NMAX) throw std::invalid_argument("N out of range [1, 64]");
+    if (ipm_lds_bytes(p.N, poly_rows_max(p.constraint_mask)) > 160 * 1024)
+        throw std::invalid_argument("horizon too long for the LDS-resident interior point (N x constraint rows)");
     if (!(p.Ts > 0)) throw std::invalid_argument("Ts must be > 0");
     for (int i = 0; i < 9; i++) if (!(p.Tx[i] > 0)) throw std::invalid_argument("T_x must be > 0");
     for (int i = 0; i < 8; i++) if (!(p.Tu[i] > 0)) throw std::invalid_argument("T_u must be > 0");
@@ -219,28 +236,36 @@ void upload_track(mpcc_engine* e) {
 void run_batch(mpcc_engine* e, int B, hipStream_t st, mpcc_timing* timing) {
     DevConst c = e->make_const(B);
     DevBuffers& d = e->d;
-    const bool tm = timing != nullptr;
+    // Event recording: 'timing' (one synchronous call) or live mode (pairs kept until timing_end).
+    const bool tm = timing != nullptr || e->live;
+    std::vector<hipEvent_t> evs;
     int ei = 0;
-    auto mark = [&]() { hipEvent_t ev = e->ev(ei++); HIPCHK(hipEventRecord(ev, st)); return ev; };
+    auto mark = [&]() -> int {
+        hipEvent_t ev = e->live ? e->live_ev() : e->ev(ei);
+        ei++;
+        HIPCHK(hipEventRecord(ev, st));
+        evs.push_back(ev);
+        return (int)evs.size() - 1;
+    };
     std::vector<std::pair<int, int>> set_qp, solve_qp, get_alpha;
-    int t0 = 0, t_env0 = 0, t_env1 = 0, t_end = 0;
-    if (tm) { t0 = ei; mark(); }
+    int t0 = -1, t_env0 = -1, t_env1 = -1, t_end = -1;
+    if (tm) t0 = mark();
     launch_prepare(c, d, st);
-    if (tm) { t_env0 = ei; mark(); }
+    if (tm) t_env0 = mark();
     launch_stage_records(c, d, st);
     if (c.p.constraint_mask & MPCC_CON_SELFCOL)
         launch_nn(c, d, e->nn_self.desc, e->nn_self.d, 0, c.S, nullptr, nullptr, d.rec, c.S, st);
     if (c.p.constraint_mask & MPCC_CON_ENVCOL)
         launch_nn(c, d, e->nn_env.desc, e->nn_env.d, 1, c.S, nullptr, nullptr, d.rec, c.S, st);
-    if (tm) { t_env1 = ei; mark(); }
+    if (tm) t_env1 = mark();
     const double* ucur = d.u0;
     for (int it = 0; it < c.p.max_iter; it++) {
-        int a0 = 0, a1 = 0, b1 = 0, c1 = 0;
-        if (tm) { a0 = ei; mark(); }
+        int a0 = -1, a1 = -1, b1 = -1, c1 = -1;
+        if (tm) a0 = mark();
         launch_setqp(c, d, ucur, st);
-        if (tm) { a1 = ei; mark(); }
-        launch_ipm(c, d, st);
-        if (tm) { b1 = ei; mark(); }
+        if (tm) a1 = mark();
+        launch_ipm(c, d, poly_rows_max(c.p.constraint_mask), st);
+        if (tm) b1 = mark();
         launch_trial(c, d, ucur, 1.0, 0, st);
         launch_accept(c, d, st);
         if (c.faithful_dead_trials) {
@@ -252,7 +277,7 @@ void run_batch(mpcc_engine* e, int B, hipStream_t st, mpcc_timing* timing) {
         }
         launch_apply(c, d, st);
         if (tm) {
-            c1 = ei; mark();
+            c1 = mark();
             set_qp.push_back({a0, a1});
             solve_qp.push_back({a1, b1});
             get_alpha.push_back({b1, c1});
@@ -260,10 +285,19 @@ void run_batch(mpcc_engine* e, int B, hipStream_t st, mpcc_timing* timing) {
     }
     launch_finalize(c, d, st);
     HIPCHK(hipGetLastError());
-    if (tm) {
-        t_end = ei; mark();
-        HIPCHK(hipEventSynchronize(e->ev(t_end)));
-        auto el = [&](int a, int b) { float ms = 0; (void)hipEventElapsedTime(&ms, e->ev(a), e->ev(b)); return ms * 1e-3; };
+    if (!tm) return;
+    t_end = mark();
+    if (e->live) {
+        e->lv_total.push_back({evs[t0], evs[t_end]});
+        e->lv_env.push_back({evs[t_env0], evs[t_env1]});
+        for (auto& pr : set_qp) e->lv_setqp.push_back({evs[pr.first], evs[pr.second]});
+        for (auto& pr : solve_qp) e->lv_ipm.push_back({evs[pr.first], evs[pr.second]});
+        for (auto& pr : get_alpha) e->lv_alpha.push_back({evs[pr.first], evs[pr.second]});
+        e->live_calls++;
+    }
+    if (timing) {
+        HIPCHK(hipEventSynchronize(evs[t_end]));
+        auto el = [&](int a, int b) { float ms = 0; (void)hipEventElapsedTime(&ms, evs[a], evs[b]); return ms * 1e-3; };
         timing->set_env = el(t_env0, t_env1);
         timing->set_qp = 0; timing->solve_qp = 0; timing->get_alpha = 0;
         for (auto& pr : set_qp) timing->set_qp += el(pr.first, pr.second);
@@ -473,6 +507,79 @@ int mpcc_solve_device(mpcc_engine* e, int B, double* d_x0, const double* d_u0, c
     return MPCC_OK;
 }
 
+int mpcc_set_warmstart_device(mpcc_engine* e, int B, const double* d_guess, const int32_t* d_valid,
+                              const int32_t* d_fails, void* stream) {
+    if (!e || B < 0 || B > e->maxB) return fail(MPCC_E_INVALID, "mpcc_set_warmstart_device: invalid argument");
+    try {
+        hipStream_t st = stream ? (hipStream_t)stream : e->stream;
+        const size_t NS = e->N + 1;
+        if (d_guess)
+            HIPCHK(hipMemcpyAsync(e->d.guess, d_guess, (size_t)B * NS * 17 * sizeof(double), hipMemcpyDeviceToDevice, st));
+        if (d_valid) HIPCHK(hipMemcpyAsync(e->d.valid, d_valid, (size_t)B * sizeof(int32_t), hipMemcpyDeviceToDevice, st));
+        if (d_fails) HIPCHK(hipMemcpyAsync(e->d.fails, d_fails, (size_t)B * sizeof(int32_t), hipMemcpyDeviceToDevice, st));
+    } catch (const HipError& x) {
+        return fail(MPCC_E_HIP, x.what());
+    }
+    return MPCC_OK;
+}
+
+int mpcc_timing_begin(mpcc_engine* e) {
+    if (!e) return fail(MPCC_E_INVALID, "mpcc_timing_begin: null engine");
+    e->live = true;
+    e->live_used = 0;
+    e->live_calls = 0;
+    e->lv_env.clear(); e->lv_setqp.clear(); e->lv_ipm.clear(); e->lv_alpha.clear(); e->lv_total.clear();
+    return MPCC_OK;
+}
+
+int mpcc_timing_end(mpcc_engine* e, mpcc_timing* sum, int32_t* n_calls, int32_t* n_ipm) {
+    if (!e || !e->live) return fail(MPCC_E_INVALID, "mpcc_timing_end: timing not active");
+    try {
+        mpcc_timing t{};
+        auto acc = [&](const std::vector<std::pair<hipEvent_t, hipEvent_t>>& v) {
+            double s = 0;
+            for (auto& pr : v) {
+                HIPCHK(hipEventSynchronize(pr.second));
+                float ms = 0;
+                HIPCHK(hipEventElapsedTime(&ms, pr.first, pr.second));
+                s += ms * 1e-3;
+            }
+            return s;
+        };
+        t.total = acc(e->lv_total);
+        t.set_env = acc(e->lv_env);
+        t.set_qp = acc(e->lv_setqp);
+        t.solve_qp = acc(e->lv_ipm);
+        t.get_alpha = acc(e->lv_alpha);
+        if (sum) *sum = t;
+        if (n_calls) *n_calls = e->live_calls;
+        if (n_ipm) *n_ipm = (int32_t)e->lv_ipm.size();
+    } catch (const HipError& x) {
+        e->live = false;
+        return fail(MPCC_E_HIP, x.what());
+    }
+    e->live = false;
+    return MPCC_OK;
+}
+
+int mpcc_get_solve_stats(mpcc_engine* e, int B, int32_t* sqp_iter, int32_t* ipm_iters, int32_t* qp_status) {
+    if (!e || B < 1 || B > e->maxB) return fail(MPCC_E_INVALID, "mpcc_get_solve_stats: invalid argument");
+    try {
+        HIPCHK(hipStreamSynchronize(e->stream));
+        HIPCHK(hipDeviceSynchronize());
+        std::vector<int32_t> sqi((size_t)B * SQI);
+        HIPCHK(hipMemcpy(sqi.data(), e->d.sqi, sqi.size() * sizeof(int32_t), hipMemcpyDeviceToHost));
+        for (int b = 0; b < B; b++) {
+            if (sqp_iter) sqp_iter[b] = sqi[(size_t)b * SQI + SQ_ITER];
+            if (ipm_iters) ipm_iters[b] = sqi[(size_t)b * SQI + SQ_IPMIT];
+            if (qp_status) qp_status[b] = sqi[(size_t)b * SQI + SQ_QPSTAT];
+        }
+    } catch (const HipError& x) {
+        return fail(MPCC_E_HIP, x.what());
+    }
+    return MPCC_OK;
+}
+
 int mpcc_solve(mpcc_engine* e, int B, double* x0, const double* u0, const double* obs, double* u0_out, double* horizon_out,
                int32_t* status, int32_t* ok, mpcc_timing* timing) {
     if (!e || B < 1 || B > e->maxB || !x0 || !u0 || !obs) return fail(MPCC_E_INVALID, "mpcc_solve: invalid argument");
@@ -639,7 +746,7 @@ int mpcc_debug_solve_qp(mpcc_engine* e, int B, const double* guess, const double
         HIPCHK(hipMemcpy(e->d.sqi, sqi.data(), sqi.size() * sizeof(int32_t), hipMemcpyHostToDevice));
         HIPCHK(hipMemset(e->d.step, 0, S * 17 * sizeof(double)));
         launch_setqp(c, e->d, e->s_u0, st);
-        launch_ipm(c, e->d, st);
+        launch_ipm(c, e->d, poly_rows_max(c.p.constraint_mask), st);
         HIPCHK(hipStreamSynchronize(st));
         std::vector<double> stp(S * 17);
         HIPCHK(hipMemcpy(stp.data(), e->d.step, stp.size() * sizeof(double), hipMemcpyDeviceToHost));

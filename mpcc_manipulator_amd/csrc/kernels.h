@@ -47,7 +47,11 @@ void launch_stage_records(const DevConst& c, const DevBuffers& d, hipStream_t s)
 void launch_nn(const DevConst& c, const DevBuffers& d, const NNDesc& nd, const double* W, int which, int M,
                const double* q, const double* obs, double* rec, int rec_stride, hipStream_t s);
 void launch_setqp(const DevConst& c, const DevBuffers& d, const double* u_cur, hipStream_t s);
-void launch_ipm(const DevConst& c, const DevBuffers& d, hipStream_t s);
+void launch_ipm(const DevConst& c, const DevBuffers& d, int npmax, hipStream_t s);
+size_t ipm_lds_bytes(int N, int npmax);
+inline int poly_rows_max(int mask) {
+    return ((mask & MPCC_CON_SELFCOL) ? 1 : 0) + ((mask & MPCC_CON_SING) ? 1 : 0) + ((mask & MPCC_CON_ENVCOL) ? 9 : 0);
+}
 void launch_trial(const DevConst& c, const DevBuffers& d, const double* u_cur, double alpha_scale, int dead, hipStream_t s);
 void launch_accept(const DevConst& c, const DevBuffers& d, hipStream_t s);
 void launch_apply(const DevConst& c, const DevBuffers& d, hipStream_t s);

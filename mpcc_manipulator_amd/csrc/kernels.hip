@@ -377,551 +377,6 @@ __global__ void __launch_bounds__(64) k_setqp(DevConst c, DevBuffers d, const do
 }
 
 // ------------------------------------------------------------------------------------------------
-// k_ipm: Mehrotra predictor-corrector interior point for the stage-structured QP of one instance,
-// one wavefront per instance.  Step systems are solved by a Riccati recursion over the augmented
-// stage state z~ = [y(9), w(7)] (w_k = v_{k-1}[0:7] carries the ddq coupling) with input v(8).
-// Matches oracle/mpcc_oracle.cpp solve_struct_ipm (same algorithm, tolerances and iteration rule).
-// ------------------------------------------------------------------------------------------------
-constexpr int IPM_MAX_IT = 60;
-constexpr double IPM_TOL_MU = 1e-13, IPM_TOL_P = 1e-11, IPM_TOL_STEP = 1e-11;
-
-struct IpmShared {
-    double M[81], G[72];
-    double P[256], PB[128], PM[81], F[64], Gm[128], Hb[81], U[128];
-    double st[QS];                 // staged stage record
-    double W[NSLOT];
-    double pv[2][16];              // backward vector recursion
-    double fv[8];
-    double xv[2][16];              // forward rollout
-    double hv[8];
-    double red[4];
-};
-
-// c_i^T z_k for slot i (unsigned) — z points at the stage's 24-vector [y, w, v]
-__device__ __forceinline__ double slot_cz(int i, int k, const double* z, const double* qsk) {
-    if (i < 9) return z[i];
-    if (i < 18) return z[i - 9];
-    if (i < 32) {
-        int j = (i < 25) ? i - 18 : i - 25;
-        return (k == 0) ? z[16 + j] : z[16 + j] - z[9 + j];
-    }
-    const double* row = qsk + QS_POLY + POLY_W * (i - 32);
-    double s = 0;
-#pragma unroll
-    for (int j = 0; j < 7; j++) s += row[j] * z[j] + row[7 + j] * z[16 + j];
-    return s;
-}
-__device__ __forceinline__ double slot_sgn(int i) { return (i < 9 || (i >= 18 && i < 25)) ? -1.0 : 1.0; }
-
-__global__ void __launch_bounds__(64) k_ipm(DevConst c, DevBuffers d) {
-    const int b = blockIdx.x;
-    const int lane = threadIdx.x;
-    int32_t* si = d.sqi + (size_t)b * SQI;
-    if (!si[SQ_ACTIVE]) return;
-    __shared__ IpmShared sh;
-    const int N = c.N, NS = N + 1;
-    const double* QSb = d.qs + (size_t)b * NS * QS;
-    double* ISb = d.is + (size_t)b * NS * IS;
-    for (int e = lane; e < 81; e += 64) sh.M[e] = c.M[e];
-    for (int e = lane; e < 72; e += 64) sh.G[e] = c.G[e];
-    const double* Tu = c.p.Tu;
-    const double rddq = c.p.qp_r_ddq;
-
-    // ---- Hessian checks (osqp_interface.cpp:454-473): state blocks (flags from k_setqp) and the
-    // per-component tridiagonal input blocks.
-    int fl = 0;
-    for (int k = lane; k < NS; k += 64) fl |= (int)QSb[(size_t)k * QS + QS_FLAG];
-    if (lane < 8) {
-        const int j = lane;
-        double prev_d = 0;
-        for (int k = 0; k < N; k++) {
-            double dk = QSb[(size_t)k * QS + QS_R + j];
-            double off = (k >= 1 && j < DOF) ? (Tu[j] * (-2. * rddq) * Tu[j]) : 0.0;
-            double l = (k >= 1) ? off / prev_d : 0.0;
-            double dd = dk - l * l;
-            if (dd <= 0) { fl |= 2; break; }
-            prev_d = sqrt(dd);
-        }
-    }
-    fl = wave_or(fl);
-    if (fl & 2) {
-        if (lane == 0) { si[SQ_STATUS] = MPCC_NON_PD_HESSIAN; si[SQ_ACTIVE] = 0; }
-        return;
-    }
-    if (fl & 1) {
-        if (lane == 0) { si[SQ_STATUS] = MPCC_NAN_HESSIAN; si[SQ_ACTIVE] = 0; }
-        return;
-    }
-    if (fl & 4) {  // constant rows violated / empty box: OSQP reports primal infeasibility; keep step (Q6)
-        if (lane == 0) si[SQ_QPSTAT] = MPCC_QP_PrimalInfeasible;
-        return;
-    }
-
-    // ---- slot setup: bounds, active flags; z = dynamics rollout with v = 0; s, lambda
-    const int nslots = NS * NSLOT;
-    double mcount = 0;
-    for (int e = lane; e < nslots; e += 64) {
-        const int k = e / NSLOT, i = e - k * NSLOT;
-        const double* q = QSb + (size_t)k * QS;
-        double bnd;
-        bool act;
-        if (i < 18) {
-            bnd = (i < 9) ? q[QS_YLB + i] : q[QS_YUB + i - 9];
-            act = (k >= 1) && fabs(bnd) < BIG;
-        } else if (i < 32) {
-            bnd = (i < 25) ? q[QS_DLB + i - 18] : q[QS_DUB + i - 25];
-            act = (k < N) && fabs(bnd) < BIG;
-        } else {
-            int r = i - 32;
-            int np = (int)q[QS_NPOLY];
-            bnd = (r < np) ? q[QS_POLY + POLY_W * r + 14] : INF;
-            act = (k < N) && (r < np) && fabs(bnd) < BIG;
-        }
-        double* is = ISb + (size_t)k * IS;
-        is[IS_BND + i] = bnd;
-        is[IS_ACT + i] = act ? 1.0 : 0.0;
-        mcount += act ? 1.0 : 0.0;
-    }
-    mcount = wave_sum(mcount);
-    // rollout
-    if (lane < 16) sh.xv[0][lane] = 0.0;
-    for (int e = lane; e < NS * 24; e += 64) ISb[(size_t)(e / 24) * IS + IS_Z + (e % 24)] = 0.0;
-    __syncthreads();
-    for (int k = 0; k < N; k++) {
-        const double* q = QSb + (size_t)k * QS;
-        double yn = 0;
-        if (lane < 9) {
-            double s = 0;
-            for (int m = 0; m < 9; m++) s += sh.M[lane * 9 + m] * sh.xv[k & 1][m];
-            yn = s + q[QS_B + lane];
-        }
-        __syncthreads();
-        if (lane < 9) {
-            sh.xv[(k + 1) & 1][lane] = yn;
-            ISb[(size_t)(k + 1) * IS + IS_Z + lane] = yn;
-        }
-        __syncthreads();
-    }
-    for (int e = lane; e < nslots; e += 64) {
-        const int k = e / NSLOT, i = e - k * NSLOT;
-        double* is = ISb + (size_t)k * IS;
-        if (is[IS_ACT + i] != 0.0) {
-            double g = slot_sgn(i) * slot_cz(i, k, is + IS_Z, QSb + (size_t)k * QS) - slot_sgn(i) * is[IS_BND + i];
-            is[IS_S + i] = fmax(-g, 1.0);
-            is[IS_L + i] = 1.0;
-        } else {
-            is[IS_S + i] = 1.0;
-            is[IS_L + i] = 0.0;
-        }
-    }
-    __syncthreads();
-
-    double last_dz = 1e30;
-    bool conv = false;
-    int it;
-    const double HcBase = -2. * rddq;
-    for (it = 0; it < IPM_MAX_IT; it++) {
-        // ---- pass A: primal residuals, complementarity, barrier weights
-        double mus = 0, rpm = 0;
-        for (int e = lane; e < nslots; e += 64) {
-            const int k = e / NSLOT, i = e - k * NSLOT;
-            double* is = ISb + (size_t)k * IS;
-            if (is[IS_ACT + i] == 0.0) { is[IS_W + i] = 0.0; continue; }
-            double sg = slot_sgn(i);
-            double rp = sg * slot_cz(i, k, is + IS_Z, QSb + (size_t)k * QS) - sg * is[IS_BND + i] + is[IS_S + i];
-            is[IS_RP + i] = rp;
-            mus += is[IS_S + i] * is[IS_L + i];
-            rpm = fmax(rpm, fabs(rp));
-            is[IS_W + i] = is[IS_L + i] / is[IS_S + i];
-        }
-        mus = wave_sum(mus);
-        rpm = wave_max(rpm);
-        const double mu = (mcount > 0) ? mus / mcount : 0.0;
-        if (it > 0 && mu < IPM_TOL_MU && rpm < IPM_TOL_P && last_dz < IPM_TOL_STEP) { conv = true; break; }
-        // ---- objective gradient g0 = H z + h (per stage component)
-        for (int e = lane; e < NS * 24; e += 64) {
-            const int k = e / 24, a = e - k * 24;
-            const double* q = QSb + (size_t)k * QS;
-            double* is = ISb + (size_t)k * IS;
-            const double* z = is + IS_Z;
-            double g = 0;
-            if (a < 9) {
-                double s = 0;
-                for (int m = 0; m < 9; m++) s += q[QS_Q + a * 9 + m] * z[m];
-                g = s + q[QS_q + a];
-            } else if (a < 16) {
-                int j = a - 9;
-                g = (k >= 1 && k <= N - 1) ? (Tu[j] * HcBase * Tu[j]) * z[16 + j] : 0.0;
-            } else if (k < N) {
-                int j = a - 16;
-                g = q[QS_R + j] * z[a] + q[QS_r + j];
-                if (k >= 1 && j < DOF) g += (Tu[j] * HcBase * Tu[j]) * z[9 + j];
-            }
-            is[IS_G0 + a] = g;
-        }
-        __syncthreads();
-
-        // ---- Riccati factorization with barrier-augmented stage Hessians
-        // terminal stage: P = [[Q_N + diag(W_y), 0], [0, 0]]
-        {
-            const double* q = QSb + (size_t)N * QS;
-            const double* is = ISb + (size_t)N * IS;
-            for (int e = lane; e < 256; e += 64) {
-                int a = e >> 4, cc = e & 15;
-                double v = 0;
-                if (a < 9 && cc < 9) {
-                    v = q[QS_Q + a * 9 + cc];
-                    if (a == cc) v += is[IS_W + SL_YL + a] + is[IS_W + SL_YU + a];
-                }
-                sh.P[e] = v;
-            }
-        }
-        __syncthreads();
-        for (int k = N - 1; k >= 0; k--) {
-            const double* q = QSb + (size_t)k * QS;
-            double* is = ISb + (size_t)k * IS;
-            for (int e = lane; e < QS; e += 64) sh.st[e] = q[e];
-            if (lane < NSLOT) sh.W[lane] = is[IS_W + lane];
-            // (1) PB = P B~ (16x8), PM = P_yy M (9x9)
-            for (int e = lane; e < 128 + 81; e += 64) {
-                if (e < 128) {
-                    int a = e >> 3, j = e & 7;
-                    double s = 0;
-                    for (int m = 0; m < 9; m++) s += sh.P[a * 16 + m] * sh.G[m * 8 + j];
-                    if (j < 7) s += sh.P[a * 16 + 9 + j];
-                    sh.PB[e] = s;
-                } else {
-                    int e2 = e - 128, a = e2 / 9, cc = e2 - a * 9;
-                    double s = 0;
-                    for (int m = 0; m < 9; m++) s += sh.P[a * 16 + m] * sh.M[m * 9 + cc];
-                    sh.PM[e2] = s;
-                }
-            }
-            __syncthreads();
-            const int np = (int)sh.st[QS_NPOLY];
-            // (2) F = R~ + B~^T P B~, Gm = S~ + B~^T P A~, Hb_yy = Q~_yy + M^T P_yy M
-            for (int e = lane; e < 64 + 128 + 81; e += 64) {
-                if (e < 64) {
-                    int i = e >> 3, j = e & 7;
-                    double rt = 0;
-                    if (i == j) {
-                        rt = sh.st[QS_R + i];
-                        if (i < 7) rt += sh.W[SL_DL + i] + sh.W[SL_DU + i];
-                    }
-                    if (i < 7 && j < 7)
-                        for (int r = 0; r < np; r++) {
-                            const double* row = sh.st + QS_POLY + POLY_W * r;
-                            rt += sh.W[SL_P + r] * row[7 + i] * row[7 + j];
-                        }
-                    double s = 0;
-                    for (int m = 0; m < 9; m++) s += sh.G[m * 8 + i] * sh.PB[m * 8 + j];
-                    if (i < 7) s += sh.PB[(9 + i) * 8 + j];
-                    sh.F[e] = rt + s;
-                } else if (e < 192) {
-                    int e2 = e - 64, i = e2 >> 4, cc = e2 & 15;
-                    double v;
-                    if (cc < 9) {
-                        double st_ = 0;
-                        if (i < 7 && cc < 7)
-                            for (int r = 0; r < np; r++) {
-                                const double* row = sh.st + QS_POLY + POLY_W * r;
-                                st_ += sh.W[SL_P + r] * row[7 + i] * row[cc];
-                            }
-                        double s = 0;
-                        for (int m = 0; m < 9; m++) s += sh.PB[m * 8 + i] * sh.M[m * 9 + cc];
-                        v = st_ + s;
-                    } else {
-                        int j = cc - 9;
-                        v = 0;
-                        if (i == j && k >= 1) v = Tu[j] * HcBase * Tu[j] - (sh.W[SL_DL + j] + sh.W[SL_DU + j]);
-                    }
-                    sh.Gm[e2] = v;
-                } else {
-                    int e2 = e - 192, a = e2 / 9, cc = e2 - a * 9;
-                    double v = sh.st[QS_Q + a * 9 + cc];
-                    if (a == cc) v += sh.W[SL_YL + a] + sh.W[SL_YU + a];
-                    if (a < 7 && cc < 7)
-                        for (int r = 0; r < np; r++) {
-                            const double* row = sh.st + QS_POLY + POLY_W * r;
-                            v += sh.W[SL_P + r] * row[a] * row[cc];
-                        }
-                    double s = 0;
-                    for (int m = 0; m < 9; m++) s += sh.M[m * 9 + a] * sh.PM[m * 9 + cc];
-                    sh.Hb[e2] = v + s;
-                }
-            }
-            __syncthreads();
-            // (3) LF = chol(F) (every lane, registers); U = LF^-1 Gm (lane = column)
-            double Lf[36];
-            {
-                int idx = 0;
-#pragma unroll
-                for (int i = 0; i < 8; i++)
-#pragma unroll
-                    for (int j = 0; j <= i; j++) Lf[idx++] = sh.F[i * 8 + j];
-#pragma unroll
-                for (int j = 0; j < 8; j++) {
-                    const int jj = j * (j + 1) / 2;
-                    double dg = Lf[jj + j];
-#pragma unroll
-                    for (int m = 0; m < j; m++) dg -= Lf[jj + m] * Lf[jj + m];
-                    dg = sqrt(dg);
-                    Lf[jj + j] = dg;
-                    const double inv = 1.0 / dg;
-#pragma unroll
-                    for (int i = j + 1; i < 8; i++) {
-                        const int ii = i * (i + 1) / 2;
-                        double s = Lf[ii + j];
-#pragma unroll
-                        for (int m = 0; m < j; m++) s -= Lf[ii + m] * Lf[jj + m];
-                        Lf[ii + j] = s * inv;
-                    }
-                }
-            }
-            if (lane < 16) {
-                double u[8];
-#pragma unroll
-                for (int i = 0; i < 8; i++) {
-                    const int ii = i * (i + 1) / 2;
-                    double s = sh.Gm[i * 16 + lane];
-#pragma unroll
-                    for (int m = 0; m < i; m++) s -= Lf[ii + m] * u[m];
-                    u[i] = s / Lf[ii + i];
-                }
-#pragma unroll
-                for (int i = 0; i < 8; i++) {
-                    sh.U[i * 16 + lane] = u[i];
-                    is[IS_U + i * 16 + lane] = u[i];
-                }
-            } else if (lane < 16 + 36) {
-                // spread the packed factor to global (one entry per lane, select from registers)
-                const int e = lane - 16;
-                double v = 0;
-#pragma unroll
-                for (int m = 0; m < 36; m++) v = (m == e) ? Lf[m] : v;
-                is[IS_LF + e] = v;
-            }
-            __syncthreads();
-            // (4) P = Hb - U^T U  (not needed at k = 0)
-            if (k > 0) {
-                for (int e = lane; e < 256; e += 64) {
-                    int a = e >> 4, cc = e & 15;
-                    double v = 0;
-                    if (a < 9 && cc < 9) v = sh.Hb[a * 9 + cc];
-                    else if (a >= 9 && a == cc) v = (sh.W[SL_DL + a - 9] + sh.W[SL_DU + a - 9]);
-                    double s = 0;
-#pragma unroll
-                    for (int i = 0; i < 8; i++) s += sh.U[i * 16 + a] * sh.U[i * 16 + cc];
-                    sh.P[e] = v - s;
-                }
-            }
-            __syncthreads();
-        }
-
-        // ---- two solves (predictor, corrector) with the same factorization
-        double sigma_mu = 0.0;
-        double alpha = 0.0, dzmax = 0.0;
-        for (int phase = 0; phase < 2; phase++) {
-            // slot pass: rc, signed coefficient for the gradient
-            for (int e = lane; e < nslots; e += 64) {
-                const int k = e / NSLOT, i = e - k * NSLOT;
-                double* is = ISb + (size_t)k * IS;
-                if (is[IS_ACT + i] == 0.0) { is[IS_COEF + i] = 0.0; continue; }
-                double s = is[IS_S + i], l = is[IS_L + i];
-                double rc = (phase == 0) ? s * l : s * l + is[IS_DSA + i] * is[IS_DLA + i] - sigma_mu;
-                is[IS_RC + i] = rc;
-                double coef = l + is[IS_W + i] * is[IS_RP + i] - rc / s;
-                is[IS_COEF + i] = slot_sgn(i) * coef;
-            }
-            __syncthreads();
-            // gradient of the step system
-            for (int e = lane; e < NS * 24; e += 64) {
-                const int k = e / 24, a = e - k * 24;
-                const double* q = QSb + (size_t)k * QS;
-                double* is = ISb + (size_t)k * IS;
-                double g = is[IS_G0 + a];
-                const double* sc = is + IS_COEF;
-                const int np = (k < N) ? (int)q[QS_NPOLY] : 0;
-                if (a < 9) {
-                    g += sc[SL_YL + a] + sc[SL_YU + a];
-                    if (a < 7)
-                        for (int r = 0; r < np; r++) g += sc[SL_P + r] * q[QS_POLY + POLY_W * r + a];
-                } else if (a < 16) {
-                    int j = a - 9;
-                    if (k >= 1 && k < N) g -= sc[SL_DL + j] + sc[SL_DU + j];
-                } else if (k < N) {
-                    int j = a - 16;
-                    if (j < 7) {
-                        g += sc[SL_DL + j] + sc[SL_DU + j];
-                        for (int r = 0; r < np; r++) g += sc[SL_P + r] * q[QS_POLY + POLY_W * r + 7 + j];
-                    }
-                }
-                is[IS_G + a] = g;
-            }
-            __syncthreads();
-            // backward vector recursion: p_N = g_x~(N); f = g_v + B~^T p; t = LF^-1 f; p = g_x~ + A~^T p - U^T t
-            if (lane < 16) sh.pv[N & 1][lane] = ISb[(size_t)N * IS + IS_G + lane];
-            __syncthreads();
-            for (int k = N - 1; k >= 0; k--) {
-                double* is = ISb + (size_t)k * IS;
-                const double* pn = sh.pv[(k + 1) & 1];
-                if (lane < 8) {
-                    double s = 0;
-                    for (int m = 0; m < 9; m++) s += sh.G[m * 8 + lane] * pn[m];
-                    if (lane < 7) s += pn[9 + lane];
-                    sh.fv[lane] = is[IS_G + 16 + lane] + s;
-                }
-                __syncthreads();
-                double Lf[36], t[8];
-#pragma unroll
-                for (int m = 0; m < 36; m++) Lf[m] = is[IS_LF + m];
-#pragma unroll
-                for (int i = 0; i < 8; i++) {
-                    const int ii = i * (i + 1) / 2;
-                    double s = sh.fv[i];
-#pragma unroll
-                    for (int m = 0; m < i; m++) s -= Lf[ii + m] * t[m];
-                    t[i] = s / Lf[ii + i];
-                }
-                if (lane < 8) {
-                    double tv = 0;
-#pragma unroll
-                    for (int m = 0; m < 8; m++) tv = (m == lane) ? t[m] : tv;
-                    is[IS_T + lane] = tv;
-                }
-                if (k > 0 && lane < 16) {
-                    double s = is[IS_G + lane];
-                    if (lane < 9)
-                        for (int m = 0; m < 9; m++) s += sh.M[m * 9 + lane] * pn[m];
-#pragma unroll
-                    for (int i = 0; i < 8; i++) s -= is[IS_U + i * 16 + lane] * t[i];
-                    sh.pv[k & 1][lane] = s;
-                }
-                __syncthreads();
-            }
-            // forward rollout: x~_0 = 0; v = -LF^-T (U x~ + t); x~_{k+1} = A~ x~ + B~ v
-            if (lane < 16) sh.xv[0][lane] = 0.0;
-            __syncthreads();
-            double dzm = 0.0;
-            for (int k = 0; k < N; k++) {
-                double* is = ISb + (size_t)k * IS;
-                const double* xc = sh.xv[k & 1];
-                if (lane < 8) {
-                    double s = is[IS_T + lane];
-                    for (int a = 0; a < 16; a++) s += is[IS_U + lane * 16 + a] * xc[a];
-                    sh.hv[lane] = s;
-                }
-                __syncthreads();
-                double Lf[36], v[8];
-#pragma unroll
-                for (int m = 0; m < 36; m++) Lf[m] = is[IS_LF + m];
-#pragma unroll
-                for (int i = 7; i >= 0; i--) {
-                    double s = sh.hv[i];
-#pragma unroll
-                    for (int m = i + 1; m < 8; m++) s -= Lf[m * (m + 1) / 2 + i] * v[m];
-                    v[i] = s / Lf[i * (i + 1) / 2 + i];
-                }
-#pragma unroll
-                for (int i = 0; i < 8; i++) v[i] = -v[i];
-                if (lane < 16) {
-                    double xn;
-                    if (lane < 9) {
-                        double s = 0;
-                        for (int m = 0; m < 9; m++) s += sh.M[lane * 9 + m] * xc[m];
-                        for (int j = 0; j < 8; j++) s += sh.G[lane * 8 + j] * v[j];
-                        xn = s;
-                    } else {
-                        double vv = 0;
-#pragma unroll
-                        for (int j = 0; j < 7; j++) vv = (j == lane - 9) ? v[j] : vv;
-                        xn = vv;
-                    }
-                    sh.xv[(k + 1) & 1][lane] = xn;
-                    is[IS_DZ + lane] = xc[lane];
-                    dzm = fmax(dzm, fabs(xc[lane]));
-                } else if (lane < 24) {
-                    double vv = 0;
-#pragma unroll
-                    for (int j = 0; j < 8; j++) vv = (j == lane - 16) ? v[j] : vv;
-                    is[IS_DZ + lane] = vv;
-                    dzm = fmax(dzm, fabs(vv));
-                }
-                __syncthreads();
-            }
-            if (lane < 24) {
-                double v = (lane < 16) ? sh.xv[N & 1][lane] : 0.0;
-                ISb[(size_t)N * IS + IS_DZ + lane] = v;
-                dzm = fmax(dzm, fabs(v));
-            }
-            __syncthreads();
-            // slot pass: recover ds, dl; step length
-            double amax = (phase == 0) ? 1.0 : 1e30;
-            for (int e = lane; e < nslots; e += 64) {
-                const int k = e / NSLOT, i = e - k * NSLOT;
-                double* is = ISb + (size_t)k * IS;
-                if (is[IS_ACT + i] == 0.0) continue;
-                double cd = slot_sgn(i) * slot_cz(i, k, is + IS_DZ, QSb + (size_t)k * QS);
-                double rp = is[IS_RP + i];
-                double s = is[IS_S + i], l = is[IS_L + i];
-                double ds = -rp - cd;
-                double dl = is[IS_W + i] * (cd + rp) - is[IS_RC + i] / s;
-                if (phase == 0) { is[IS_DSA + i] = ds; is[IS_DLA + i] = dl; }
-                else { is[IS_DS + i] = ds; is[IS_DL + i] = dl; }
-                if (ds < 0) amax = fmin(amax, -s / ds);
-                if (dl < 0) amax = fmin(amax, -l / dl);
-            }
-            amax = wave_min(amax);
-            if (phase == 0) {
-                double mua = 0;
-                for (int e = lane; e < nslots; e += 64) {
-                    const int k = e / NSLOT, i = e - k * NSLOT;
-                    const double* is = ISb + (size_t)k * IS;
-                    if (is[IS_ACT + i] == 0.0) continue;
-                    mua += (is[IS_S + i] + amax * is[IS_DSA + i]) * (is[IS_L + i] + amax * is[IS_DLA + i]);
-                }
-                mua = wave_sum(mua);
-                mua = (mcount > 0) ? mua / mcount : 0.0;
-                double ratio = (mu > 0) ? mua / mu : 0.0;
-                double sigma = (mu > 0) ? ratio * ratio * ratio : 0.0;
-                sigma_mu = sigma * mu;
-            } else {
-                alpha = fmin(1.0, 0.995 * amax);
-                dzmax = wave_max(dzm);
-            }
-            __syncthreads();
-        }
-        // ---- update
-        for (int e = lane; e < NS * 24; e += 64) {
-            const int k = e / 24, a = e - k * 24;
-            double* is = ISb + (size_t)k * IS;
-            is[IS_Z + a] += alpha * is[IS_DZ + a];
-        }
-        for (int e = lane; e < nslots; e += 64) {
-            const int k = e / NSLOT, i = e - k * NSLOT;
-            double* is = ISb + (size_t)k * IS;
-            if (is[IS_ACT + i] == 0.0) continue;
-            is[IS_S + i] += alpha * is[IS_DS + i];
-            is[IS_L + i] += alpha * is[IS_DL + i];
-        }
-        last_dz = dzmax;
-        __syncthreads();
-    }
-    if (lane == 0) si[SQ_IPMIT] = it;
-    if (!conv) {
-        if (lane == 0) si[SQ_QPSTAT] = MPCC_QP_MaxIterReached;  // keep the previous step (Q6)
-        return;
-    }
-    if (lane == 0) si[SQ_QPSTAT] = 0;
-    double* stp = d.step + (size_t)b * NS * 17;
-    for (int e = lane; e < NS * 17; e += 64) {
-        const int k = e / 17, a = e - k * 17;
-        const double* z = ISb + (size_t)k * IS + IS_Z;
-        stp[e] = (a < 9) ? z[a] : ((k < N) ? z[16 + a - 9] : 0.0);
-    }
-}
-
-// ------------------------------------------------------------------------------------------------
 // k_trial: filterLineSearch trial (osqp_interface.cpp:759-808) — objective and l1 constraint
 // violation (:824-833) of setQP(obj, constr) at guess + alpha * T * step, one lane per stage.
 // Rows owned by stage k: dynamics block k, state bounds k, input bounds (Q1) k, ddq block k,
@@ -1204,9 +659,6 @@ void launch_stage_records(const DevConst& c, const DevBuffers& d, hipStream_t s)
 }
 void launch_setqp(const DevConst& c, const DevBuffers& d, const double* u_cur, hipStream_t s) {
     hipLaunchKernelGGL(k_setqp, dim3(nblk(c.S, 64)), dim3(64), 0, s, c, d, u_cur);
-}
-void launch_ipm(const DevConst& c, const DevBuffers& d, hipStream_t s) {
-    hipLaunchKernelGGL(k_ipm, dim3(c.Bn), dim3(64), 0, s, c, d);
 }
 void launch_trial(const DevConst& c, const DevBuffers& d, const double* u_cur, double alpha, int dead, hipStream_t s) {
     hipLaunchKernelGGL(k_trial, dim3(nblk(c.S, 64)), dim3(64), 0, s, c, d, u_cur, alpha, dead);

@@ -110,6 +110,10 @@ def lib():
         "mpcc_solve": (C.c_int, [V, C.c_int, DP, DP, DP, DP, DP, IP, IP, C.POINTER(MpccTiming)]),
         "mpcc_solve_device": (C.c_int, [V, C.c_int, V, V, V, V, V, V, V, V]),
         "mpcc_sim_time_step": (C.c_int, [V, C.c_int, DP, DP, D, DP]),
+        "mpcc_set_warmstart_device": (C.c_int, [V, C.c_int, V, V, V, V]),
+        "mpcc_timing_begin": (C.c_int, [V]),
+        "mpcc_timing_end": (C.c_int, [V, C.POINTER(MpccTiming), IP, IP]),
+        "mpcc_get_solve_stats": (C.c_int, [V, C.c_int, IP, IP, IP]),
         "mpcc_debug_robot_records": (C.c_int, [V, C.c_int, DP, DP, DP]),
         "mpcc_debug_spline": (C.c_int, [V, C.c_int, DP, DP, DP, DP, DP, DP]),
         "mpcc_debug_stage_cost": (C.c_int, [V, C.c_int, DP, DP, DP, IP, DP, DP, DP, DP, DP]),
@@ -336,6 +340,27 @@ class Engine:
         s = C.c_void_p(stream.cuda_stream) if stream is not None else None
         _check(self.L.mpcc_solve_device(self.h, int(B), ptr(x0), ptr(u0), ptr(obs), ptr(u_out), ptr(horizon),
                                         ptr(status), ptr(ok), s), "mpcc_solve_device")
+
+    def set_warmstart_device(self, B, guess, valid, fails, stream=None):
+        ptr = lambda t: C.c_void_p(t.data_ptr()) if t is not None else None
+        s = C.c_void_p(stream.cuda_stream) if stream is not None else None
+        _check(self.L.mpcc_set_warmstart_device(self.h, int(B), ptr(guess), ptr(valid), ptr(fails), s),
+               "mpcc_set_warmstart_device")
+
+    def timing_begin(self):
+        _check(self.L.mpcc_timing_begin(self.h), "mpcc_timing_begin")
+
+    def timing_end(self):
+        t = MpccTiming()
+        nc = C.c_int32()
+        ni = C.c_int32()
+        _check(self.L.mpcc_timing_end(self.h, C.byref(t), C.byref(nc), C.byref(ni)), "mpcc_timing_end")
+        return t.as_dict(), nc.value, ni.value
+
+    def solve_stats(self, B):
+        a, b, c = np.zeros(B, np.int32), np.zeros(B, np.int32), np.zeros(B, np.int32)
+        _check(self.L.mpcc_get_solve_stats(self.h, int(B), _ip(a), _ip(b), _ip(c)), "mpcc_get_solve_stats")
+        return dict(sqp_iter=a, ipm_iters=b, qp_status=c)
 
     def sim_time_step(self, x, u, ts):
         B = x.shape[0]
