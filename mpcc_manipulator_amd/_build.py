@@ -9,13 +9,14 @@ import subprocess
 PKG = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(PKG)
 CSRC = os.path.join(PKG, "csrc")
-BUILD = os.path.join(PKG, "_build")
+PROF = os.environ.get("MPCC_PROF_BUILD", "0") == "1"  # cycle-accounting variant (tools/ipm_prof.py)
+BUILD = os.path.join(PKG, "_build_prof" if PROF else "_build")
 LIB = os.path.join(BUILD, "libmpcc_engine.so")
 SOURCES = ["kernels.hip", "ipm.hip", "engine.cpp", "host_params.cpp", "host_spline.cpp", "mpc.cpp"]
 ARCH = os.environ.get("MPCC_OFFLOAD_ARCH", "gfx950")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 CFLAGS = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-I", os.path.join(ROOT, "include"),
-          "-I", CSRC, "-Wno-unused-result"]
+          "-I", CSRC, "-Wno-unused-result"] + (["-DMPCC_IPM_PROF"] if PROF else [])
 
 
 def _compile(src):

@@ -106,6 +106,15 @@ struct mpcc_engine {
             for (int b = 0; b < 9; b++) M[a * 9 + b] = (1.0 / p.Tx[a]) * A[a * 9 + b] * p.Tx[b];
             for (int b = 0; b < 8; b++) G[a * 8 + b] = (1.0 / p.Tx[a]) * B[a * 8 + b] * p.Tu[b];
         }
+        // k_ipm writes the Riccati products for M = diag(m) + m78 e7 e8^T, G = diag(g) + g87 e8 e7^T
+        for (int a = 0; a < 9; a++) {
+            for (int b = 0; b < 9; b++)
+                if (M[a * 9 + b] != 0.0 && a != b && !(a == 7 && b == 8))
+                    throw std::logic_error("discrete model outside the structure k_ipm assumes (M)");
+            for (int b = 0; b < 8; b++)
+                if (G[a * 8 + b] != 0.0 && a != b && !(a == 8 && b == 7))
+                    throw std::logic_error("discrete model outside the structure k_ipm assumes (G)");
+        }
     }
 
     DevConst make_const(int Bn) const {
@@ -200,7 +209,7 @@ int fail(int code, const std::string& m) {
 void validate_params(const mpcc_params& p) {
     if (p.N < 1 || p.N > NMAX) throw std::invalid_argument("N out of range [1, 64]");
     if (ipm_lds_bytes(p.N, poly_rows_max(p.constraint_mask)) > 160 * 1024)
-        throw std::invalid_argument("horizon too long for the LDS-resident interior point (N x constraint rows)");
+        throw std::invalid_argument("too many constraint rows for the interior-point LDS block");
     if (!(p.Ts > 0)) throw std::invalid_argument("Ts must be > 0");
     for (int i = 0; i < 9; i++) if (!(p.Tx[i] > 0)) throw std::invalid_argument("T_x must be > 0");
     for (int i = 0; i < 8; i++) if (!(p.Tu[i] > 0)) throw std::invalid_argument("T_u must be > 0");
@@ -382,13 +391,16 @@ int mpcc_set_params(mpcc_engine* e, const mpcc_params* p) {
     np.Ts = e->params.Ts;
     if ((np.constraint_mask & (MPCC_CON_SELFCOL | MPCC_CON_ENVCOL)) && !(e->nn_self.loaded && e->nn_env.loaded))
         return fail(MPCC_E_INVALID, "mpcc_set_params: collision rows need NN weights loaded at create");
+    const mpcc_params old = e->params;
     try {
         validate_params(np);
+        e->params = np;
+        e->set_model();
     } catch (const std::exception& x) {
+        e->params = old;
+        e->set_model();
         return fail(MPCC_E_INVALID, std::string("mpcc_set_params: ") + x.what());
     }
-    e->params = np;
-    e->set_model();
     return MPCC_OK;
 }
 

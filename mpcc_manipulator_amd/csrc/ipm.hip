@@ -1,16 +1,26 @@
 // ipm.hip — k_ipm: the per-instance QP solve that replaces OSQP (osqp_interface.cpp:592-656).
 //
-// Mehrotra predictor-corrector interior point on the stage-structured normalized QP,
-// one wavefront per instance.  Step systems are solved by a Riccati recursion over the augmented stage
-// state z~ = [y(9), w(7)] (w_k = v_{k-1}[0:7] carries the ddq rate coupling) with input v(8).
-// Same algorithm, tolerances and iteration rule as oracle/mpcc_oracle.cpp solve_struct_ipm.
+// Mehrotra predictor-corrector interior point on the stage-structured normalized QP;
+// same start point, tolerances, step rule and iteration-count rule as oracle/mpcc_oracle.cpp
+// solve_struct_ipm.  Step systems are solved by a Riccati recursion over the augmented stage state
+// x~ = [y(9), w(7)] (w_k = v_{k-1}[0:7] carries the ddq coupling) with input v(8).
 //
-// MI355X design: everything the sequential sweeps touch repeatedly lives in LDS (slot slacks and
-// multipliers, primal iterate and directions, gradients, Riccati work matrices); per-stage read-only
-// QP records and the Riccati factors (U, LF) stream from global memory through double-buffered LDS
-// staging, issued one stage ahead so their latency hides under the current stage's arithmetic.
-// Backward solves compute the stage gradient on the fly and forward solves recover the slack /
-// multiplier steps of the stage they just produced (fused sweeps, no whole-horizon passes between).
+// MI355X mapping:
+//  * one 16-lane DPP row per instance, 4 instances per wavefront.  Lane t owns row t of the stage
+//    (t < 9: box row on y_t, t >= 9: ddq row j = t-9), poly row t, column t of the 16x16 Riccati
+//    matrices and component t of the stage vectors.  Cross-lane traffic inside an instance uses DPP
+//    row shifts / rotations or the instance's private LDS block; there are no workgroup barriers.
+//  * the dynamics are sparse (M = diag(m) + m78 e7 e8^T, G = diag(g) + g87 e8 e7^T, checked on the
+//    host): the Riccati products are written out structurally; the dense work per stage is chol(F)
+//    (8x8, redundant per lane), U = LF^-1 Gm and K = -F^-1 Gm (lane = column) and P = Hb - U^T U
+//    (lane = row).
+//  * per-stage state (slacks, multipliers, iterate, steps, gains) streams through a coalesced
+//    [field][16 lanes] global workspace.  Backward solves are mat-vecs (p = g + A~^T p + K^T f,
+//    kff = -F^-1 f) and so are forward solves (v = K x~ + kff): no division chains outside chol(F).
+//  * the predictor backward solve is fused into the factorization sweep, and the iterate update of
+//    iteration i is applied lazily by the factorization sweep of iteration i+1.  The convergence test
+//    uses mu(alpha) = (S0 + alpha S1 + alpha^2 S2)/m and rp(alpha) = (1 - alpha) rp, accumulated by
+//    the corrector forward sweep (exact identities of the oracle's update, rounding aside).
 #include "dev_common.h"
 #include "kernels.h"
 
@@ -18,649 +28,889 @@ namespace mpcc {
 
 constexpr int IPM_MAX_IT = 60;
 constexpr double IPM_TOL_MU = 1e-13, IPM_TOL_P = 1e-11, IPM_TOL_STEP = 1e-11;
-constexpr int BND_U = 0, BND_LF = 128, BND_POLY = 164;  // stage bundle: U(8x16) | LF(36) | poly rows
-constexpr int BND_SZ = 336;
-constexpr int PF_QS = (QS + 63) / 64, PF_BND = (BND_SZ + 63) / 64;  // prefetch registers per lane
+constexpr int IPW = 4;  // instances per wavefront (16 lanes each)
 
-struct IpmLayout {
-    int NS, ns, npmax;
-    int oM, oG, oP, oPB, oPM, oF, oGm, oHb, oU, oSt, oBd, oW, oCf, oVec;
-    int oS, oL, oDSA, oDLA, oDS, oDL, oBND, oZ, oDZ, oG0, oT, total;
+// workspace fields, ws[((b*(N+1) + k)*IS + field*16 + lane]
+enum : int {
+    WF_SL = 0, WF_LL, WF_SU, WF_LU, WF_SP, WF_LP,  // slack / multiplier of the lower, upper and poly slot of row t
+    WF_ZX, WF_ZV,                                 // iterate: lane c -> x~_c (y, w); lane j < 8 -> v_j
+    WF_DX, WF_DV,                                 // corrector step (same layout)
+    WF_AX, WF_AV,                                 // predictor step
+    WF_GX, WF_GV,                                 // objective gradient H z + h
+    WF_KFF,                                       // kff (lanes 0..7)
+    WF_KC,                                        // 8 fields: K column layout, field i lane c = K[i][c]
+    WF_KR = WF_KC + 8,                            // 8 fields: K row halves, field m: lane i -> K[i][m], lane 8+i -> K[i][8+m]
+    WF_FI = WF_KR + 8,                            // 4 fields: F^-1 row halves, field m: lane i -> Fi[i][m], lane 8+i -> Fi[i][4+m]
+    NWF = WF_FI + 4
 };
+static_assert(NWF * 16 <= IS, "IPM workspace must fit the per-stage IS allocation");
 
-__host__ __device__ inline IpmLayout ipm_layout(int N, int npmax) {
-    IpmLayout L;
-    L.NS = N + 1;
-    L.npmax = npmax;
-    L.ns = SL_P + npmax;
-    int o = 0;
-    auto take = [&](int n) { int r = o; o += (n + 1) & ~1; return r; };  // keep 16-B alignment
-    L.oM = take(81); L.oG = take(72);
-    L.oP = take(256); L.oPB = take(128); L.oPM = take(81); L.oF = take(64); L.oGm = take(128); L.oHb = take(81);
-    L.oU = take(128);
-    L.oSt = take(2 * QS);
-    L.oBd = take(2 * BND_SZ);
-    L.oW = take(64); L.oCf = take(64);
-    L.oVec = take(96);
-    const int nsl = L.NS * L.ns;
-    L.oS = take(nsl); L.oL = take(nsl); L.oDSA = take(nsl); L.oDLA = take(nsl); L.oDS = take(nsl); L.oDL = take(nsl);
-    L.oBND = take(nsl);
-    L.oZ = take(L.NS * 24); L.oDZ = take(L.NS * 24); L.oG0 = take(L.NS * 24);
-    L.oT = take(L.NS * 8);
-    L.total = o;
-    return L;
+// per-instance LDS block (doubles)
+constexpr int L_P = 0;      // 16x16 Riccati P (full, symmetric)
+constexpr int L_U = 256;    // 8x16  Y = B~^T P scratch, then U = LF^-1 Gm, [i*16 + c]
+constexpr int L_K = 384;    // 8x16  K, [i*16 + c]
+constexpr int L_F = 512;    // 8x8   F, [i*8 + j]
+constexpr int L_Z = 576;    // 24    stage iterate z = [y, w, v]
+constexpr int L_DZ = 600;   // 24    corrector step
+constexpr int L_DA = 624;   // 24    predictor step
+constexpr int L_X = 648;    // 2x16  forward x~ (ping-pong)
+constexpr int L_PV = 680;   // 2x16  backward p (ping-pong)
+constexpr int L_FV = 712;   // 8     f
+constexpr int L_WD = 720;   // 16    row barrier weights W_lo + W_up
+constexpr int L_PC = 736;   // 16    poly coefficients
+constexpr int L_POLY = 752; // npmax x 16: a[7], bv[7], ub, W
+__host__ __device__ constexpr int grp_lds(int npmax) { return L_POLY + 16 * (npmax > 0 ? npmax : 1); }
+
+size_t ipm_lds_bytes(int /*N*/, int npmax) { return (size_t)IPW * grp_lds(npmax) * sizeof(double); }
+
+#ifdef MPCC_IPM_PROF
+// cycle accounting per k_ipm section (profiling build only, see _build.py / tools/ipm_prof.py)
+__device__ unsigned long long g_ipm_prof[16];
+#define PMARK(i) do { const long long t_ = clock64(); prof_acc[i] += t_ - prof_t; prof_t = t_; } while (0)
+#else
+#define PMARK(i) do { } while (0)
+#endif
+
+namespace {
+
+// ---- 16-lane row primitives (DPP rows coincide with instances) ---------------------------------
+template <int CTRL>
+__device__ __forceinline__ double dpp_d(double v) {
+    const unsigned long long x = (unsigned long long)__double_as_longlong(v);
+    int lo = (int)(unsigned)(x & 0xffffffffull), hi = (int)(unsigned)(x >> 32);
+    lo = __builtin_amdgcn_update_dpp(0, lo, CTRL, 0xF, 0xF, true);
+    hi = __builtin_amdgcn_update_dpp(0, hi, CTRL, 0xF, 0xF, true);
+    return __longlong_as_double((long long)(((unsigned long long)(unsigned)hi << 32) | (unsigned)lo));
+}
+template <int n> __device__ __forceinline__ double from_up(double v) { return dpp_d<0x100 + n>(v); }    // row_shl: lane t <- t+n
+template <int n> __device__ __forceinline__ double from_down(double v) { return dpp_d<0x110 + n>(v); } // row_shr: lane t <- t-n
+template <int n> __device__ __forceinline__ double rot16(double v) { return dpp_d<0x120 + n>(v); }     // row_ror
+__device__ __forceinline__ double g_sum(double v) {
+    v += rot16<8>(v); v += rot16<4>(v); v += rot16<2>(v); v += rot16<1>(v);
+    return v;
+}
+__device__ __forceinline__ double g_max(double v) {
+    v = fmax(v, rot16<8>(v)); v = fmax(v, rot16<4>(v)); v = fmax(v, rot16<2>(v)); v = fmax(v, rot16<1>(v));
+    return v;
+}
+__device__ __forceinline__ double g_min(double v) {
+    v = fmin(v, rot16<8>(v)); v = fmin(v, rot16<4>(v)); v = fmin(v, rot16<2>(v)); v = fmin(v, rot16<1>(v));
+    return v;
 }
 
-size_t ipm_lds_bytes(int N, int npmax) { return (size_t)ipm_layout(N, npmax).total * sizeof(double); }
+// One wavefront per workgroup: cross-lane LDS hand-offs only need this wave's LDS operations retired
+// and a compiler barrier; __syncthreads() would also drain outstanding global loads (vmcnt(0)).
+__device__ __forceinline__ void lds_sync() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
 
-// The workgroup is ONE wavefront: lanes run in lockstep, so cross-lane LDS hand-offs only need this
-// wave's LDS operations retired (lgkmcnt) and a compiler memory barrier.  __syncthreads() would also
-// wait vmcnt(0) and drain the global prefetches the sweeps keep in flight (cdna_hip_programming.md §5).
-__device__ __forceinline__ void wave_sync() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
+// ---- slot algebra (oracle solve_struct_ipm), slot: sgn*(c^T z) <= sgn*bnd ----------------------
+struct SlotStep {
+    double ds, dl;
+};
+__device__ __forceinline__ double slot_rp(double sgn, double cz, double bnd, double s) { return sgn * cz - sgn * bnd + s; }
+__device__ __forceinline__ SlotStep slot_recover(double s, double l, double rp, double cd, double rc) {
+    const double W = l / s;
+    return {-rp - cd, W * (cd + rp) - rc / s};
+}
+__device__ __forceinline__ double slot_coef(double s, double l, double rp, double rc) { return l + (l / s) * rp - rc / s; }
+__device__ __forceinline__ double step_bound(double a, double s, double l, SlotStep d) {
+    if (d.ds < 0) a = fmin(a, -s / d.ds);
+    if (d.dl < 0) a = fmin(a, -l / d.dl);
+    return a;
+}
+// corrector step of a slot given the iterate (cz), the predictor step (ca) and the corrector step (cd)
+__device__ __forceinline__ SlotStep slot_corr(double sgn, double bnd, double cz, double ca, double cd, double s, double l,
+                                              double smu, double* rp_out) {
+    const double rp = slot_rp(sgn, cz, bnd, s);
+    const SlotStep pa = slot_recover(s, l, rp, sgn * ca, s * l);
+    const double rc = s * l + pa.ds * pa.dl - smu;
+    *rp_out = rp;
+    return slot_recover(s, l, rp, sgn * cd, rc);
+}
 
-__device__ __forceinline__ double slot_sgn(int i) { return (i < SL_YU || (i >= SL_DL && i < SL_DU)) ? -1.0 : 1.0; }
-
-// c_i^T z for slot i of stage k (unsigned); z = [y(9) w(7) v(8)]; poly = the stage's poly rows
-__device__ __forceinline__ double slot_cz(int i, int k, const double* z, const double* poly) {
-    if (i < SL_DL) return z[(i < SL_YU) ? i : i - SL_YU];
-    if (i < SL_P) {
-        const int j = (i < SL_DU) ? i - SL_DL : i - SL_DU;
-        return (k == 0) ? z[16 + j] : z[16 + j] - z[9 + j];
-    }
-    const double* row = poly + POLY_W * (i - SL_P);
-    double s = 0;
+// Cholesky of the 8x8 stage F (lower triangle read from LDS), packed; reciprocal pivots
+__device__ __forceinline__ bool chol8(const double* F, double* L, double* dinv) {
+    bool ok = true;
 #pragma unroll
-    for (int j = 0; j < 7; j++) s += row[j] * z[j] + row[7 + j] * z[16 + j];
-    return s;
+    for (int i = 0; i < 8; i++)
+#pragma unroll
+        for (int j = 0; j <= i; j++) L[i * (i + 1) / 2 + j] = F[i * 8 + j];
+#pragma unroll
+    for (int j = 0; j < 8; j++) {
+        const int jj = j * (j + 1) / 2;
+        double d = L[jj + j];
+#pragma unroll
+        for (int m = 0; m < j; m++) d -= L[jj + m] * L[jj + m];
+        ok = ok && (d > 0);
+        d = sqrt(d);
+        L[jj + j] = d;
+        const double inv = 1.0 / d;
+        dinv[j] = inv;
+#pragma unroll
+        for (int i = j + 1; i < 8; i++) {
+            const int ii = i * (i + 1) / 2;
+            double s = L[ii + j];
+#pragma unroll
+            for (int m = 0; m < j; m++) s -= L[ii + m] * L[jj + m];
+            L[ii + j] = s * inv;
+        }
+    }
+    return ok;
+}
+__device__ __forceinline__ void fwd8(const double* L, const double* dinv, double* x) {  // x = LF^-1 x
+#pragma unroll
+    for (int i = 0; i < 8; i++) {
+        const int ii = i * (i + 1) / 2;
+        double s = x[i];
+#pragma unroll
+        for (int m = 0; m < i; m++) s -= L[ii + m] * x[m];
+        x[i] = s * dinv[i];
+    }
+}
+__device__ __forceinline__ void bwd8(const double* L, const double* dinv, double* x) {  // x = LF^-T x
+#pragma unroll
+    for (int i = 7; i >= 0; i--) {
+        double s = x[i];
+#pragma unroll
+        for (int m = i + 1; m < 8; m++) s -= L[m * (m + 1) / 2 + i] * x[m];
+        x[i] = s * dinv[i];
+    }
 }
 
-__global__ void __launch_bounds__(64) k_ipm(DevConst c, DevBuffers d, int npmax) {
+}  // namespace
+
+template <int NPM>
+__global__ void __launch_bounds__(64) k_ipm(DevConst c, DevBuffers d) {
+    constexpr int NPE = NPM > 0 ? NPM : 1;      // poly rows held in LDS (row 0 stays zero when NPM = 0)
+    constexpr int PFP = (15 * NPM + 15) / 16;   // poly prefetch registers per lane
     extern __shared__ __attribute__((aligned(16))) double smem[];
-    const int b = blockIdx.x;
     const int lane = threadIdx.x;
-    int32_t* si = d.sqi + (size_t)b * SQI;
-    if (!si[SQ_ACTIVE]) return;
+    const int grp = lane >> 4;
+    const int t = lane & 15;
+    const int b = blockIdx.x * IPW + grp;
     const int N = c.N;
-    const IpmLayout Ly = ipm_layout(N, npmax);
-    const int NS = Ly.NS, ns = Ly.ns;
-    double* sM = smem + Ly.oM;   double* sG = smem + Ly.oG;
-    double* sP = smem + Ly.oP;   double* sPB = smem + Ly.oPB; double* sPM = smem + Ly.oPM;
-    double* sF = smem + Ly.oF;   double* sGm = smem + Ly.oGm; double* sHb = smem + Ly.oHb;
-    double* sU = smem + Ly.oU;
-    double* sSt = smem + Ly.oSt;  // 2 x QS
-    double* sBd = smem + Ly.oBd;  // 2 x BND_SZ
-    double* sW = smem + Ly.oW;   double* sCf = smem + Ly.oCf;
-    double* sVec = smem + Ly.oVec;
-    double* pv0 = sVec;      double* pv1 = sVec + 16;  // backward p (ping-pong)
-    double* xv0 = sVec + 32; double* xv1 = sVec + 48;  // forward x~ (ping-pong)
-    double* sFv = sVec + 64; double* sH = sVec + 72; double* sGx = sVec + 80;
-    double* sS = smem + Ly.oS;   double* sL = smem + Ly.oL;
-    double* sDSA = smem + Ly.oDSA; double* sDLA = smem + Ly.oDLA;
-    double* sDS = smem + Ly.oDS; double* sDL = smem + Ly.oDL;
-    double* sBND = smem + Ly.oBND;
-    double* sZ = smem + Ly.oZ;   double* sDZ = smem + Ly.oDZ; double* sG0 = smem + Ly.oG0;
-    double* sT = smem + Ly.oT;
+    const int NS = N + 1;
+    double* const S = smem + grp * grp_lds(NPM);
+#ifdef MPCC_IPM_PROF
+    long long prof_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    long long prof_t = clock64();
+#endif
 
-    const double* QSb = d.qs + (size_t)b * NS * QS;
-    double* ISb = d.is + (size_t)b * NS * IS;
-    const double* Tu = c.p.Tu;
+    const bool valid = b < c.Bn;
+    int32_t* si = d.sqi + (size_t)(valid ? b : 0) * SQI;
+    bool run = valid && si[SQ_ACTIVE] != 0;
+    if (__ballot(run) == 0) return;
+
+    const double* QSb = d.qs + (size_t)(valid ? b : 0) * NS * QS;
+    double* WSb = d.is + (size_t)(valid ? b : 0) * NS * IS;
+    auto ws = [&](int k, int f) -> double* { return WSb + (size_t)k * IS + f * 16 + t; };
+
+    // ---- model constants of this lane (sparse M, G; selects keep the kernel-argument reads scalar)
+    const double m78 = c.M[7 * 9 + 8], m77 = c.M[7 * 10], m88 = c.M[8 * 10];
+    const double g77 = c.G[7 * 8 + 7], g87 = c.G[8 * 8 + 7];
+    double mt = 0.0, gt = 0.0, Hct = 0.0;
     const double HcB = -2. * c.p.qp_r_ddq;
-    auto Hc = [&](int j) { return Tu[j] * HcB * Tu[j]; };
+#pragma unroll
+    for (int a = 0; a < 9; a++)
+        if (t == a) mt = c.M[a * 10];
+#pragma unroll
+    for (int a = 0; a < 7; a++)
+        if (t == a || t == 9 + a) {
+            gt = (t < 7) ? c.G[a * 9] : 0.0;
+            Hct = c.p.Tu[a] * HcB * c.p.Tu[a];
+        }
+    if (t == 7) gt = g77;
+    const bool rowY = t < 9;
+    const int j9 = t - 9;
+    constexpr double sgnL = -1.0, sgnU = 1.0;
 
-    for (int e = lane; e < 81; e += 64) sM[e] = c.M[e];
-    for (int e = lane; e < 72; e += 64) sG[e] = c.G[e];
-
-    // ---- Hessian checks (osqp_interface.cpp:454-473): state blocks (k_setqp flags) + tridiagonal input blocks
+    // ---- Hessian checks (osqp_interface.cpp:454-473): stage flags from k_setqp + tridiagonal input blocks
     int fl = 0;
-    for (int k = lane; k < NS; k += 64) fl |= (int)QSb[(size_t)k * QS + QS_FLAG];
-    if (lane < 8) {
-        const int j = lane;
-        double prev_d = 0;
-        for (int k = 0; k < N; k++) {
-            const double dk = QSb[(size_t)k * QS + QS_R + j];
-            const double off = (k >= 1 && j < DOF) ? Hc(j) : 0.0;
-            const double l = (k >= 1) ? off / prev_d : 0.0;
-            const double dd = dk - l * l;
-            if (dd <= 0) { fl |= 2; break; }
-            prev_d = sqrt(dd);
+    if (run) {
+        for (int k = t; k < NS; k += 16) fl |= (int)QSb[(size_t)k * QS + QS_FLAG];
+        if (t < 8) {
+            double prev_d = 0;
+            for (int k = 0; k < N; k++) {
+                const double dk = QSb[(size_t)k * QS + QS_R + t];
+                const double off = (k >= 1 && t < DOF) ? Hct : 0.0;
+                const double l = (k >= 1) ? off / prev_d : 0.0;
+                const double dd = dk - l * l;
+                if (dd <= 0) { fl |= 2; break; }
+                prev_d = sqrt(dd);
+            }
         }
     }
-    fl = wave_or(fl);
-    if (fl & 2) { if (lane == 0) { si[SQ_STATUS] = MPCC_NON_PD_HESSIAN; si[SQ_ACTIVE] = 0; } return; }
-    if (fl & 1) { if (lane == 0) { si[SQ_STATUS] = MPCC_NAN_HESSIAN; si[SQ_ACTIVE] = 0; } return; }
-    if (fl & 4) { if (lane == 0) si[SQ_QPSTAT] = MPCC_QP_PrimalInfeasible; return; }  // keep old step (Q6)
+    {
+        int o = 0;
+#pragma unroll
+        for (int bit = 0; bit < 3; bit++)
+            if (g_max((double)((fl >> bit) & 1)) > 0.5) o |= 1 << bit;
+        fl = o;
+    }
+    if (run && (fl & 2)) { if (t == 0) { si[SQ_STATUS] = MPCC_NON_PD_HESSIAN; si[SQ_ACTIVE] = 0; } run = false; }
+    if (run && (fl & 1)) { if (t == 0) { si[SQ_STATUS] = MPCC_NAN_HESSIAN; si[SQ_ACTIVE] = 0; } run = false; }
+    if (run && (fl & 4)) { if (t == 0) si[SQ_QPSTAT] = MPCC_QP_PrimalInfeasible; run = false; }  // keep old step (Q6)
+    const bool entered = run;
 
-    // ---- global -> LDS staging helpers (issue into registers, commit later)
-    auto qs_issue = [&](int k, double* r) {
-        const double* src = QSb + (size_t)k * QS;
-#pragma unroll
-        for (int t = 0; t < PF_QS; t++) { const int e = lane + 64 * t; r[t] = (e < QS) ? src[e] : 0.0; }
-    };
-    auto qs_commit = [&](double* dst, const double* r) {
-#pragma unroll
-        for (int t = 0; t < PF_QS; t++) { const int e = lane + 64 * t; if (e < QS) dst[e] = r[t]; }
-    };
-    const int npw = POLY_W * npmax;
-    auto bd_issue = [&](int k, double* r) {
-        const double* is = ISb + (size_t)k * IS;
+    // ---- per-stage read-only data: row bounds, poly rows (staged into LDS)
+    auto load_bounds = [&](int k, double& lb, double& ub, int& np) {
         const double* q = QSb + (size_t)k * QS;
+        lb = q[rowY ? QS_YLB + t : QS_DLB + j9];
+        ub = q[rowY ? QS_YUB + t : QS_DUB + j9];
+        np = (int)q[QS_NPOLY];
+    };
+    auto load_poly = [&](int k, double* r) {
+        const double* q = QSb + (size_t)k * QS + QS_POLY;
 #pragma unroll
-        for (int t = 0; t < PF_BND; t++) {
-            const int e = lane + 64 * t;
-            double v = 0.0;
-            if (e >= BND_SZ) v = 0.0;
-            else if (e < 128) v = is[IS_U + e];
-            else if (e < 164) v = is[IS_LF + e - 128];
-            else if (e < 164 + npw) v = q[QS_POLY + e - 164];
-            r[t] = v;
+        for (int i = 0; i < PFP; i++) {
+            const int e = t + 16 * i;
+            r[i] = (e < 15 * NPM) ? q[e] : 0.0;
         }
     };
-    auto bd_commit = [&](double* dst, const double* r) {
+    // stage the poly rows (rows >= np zeroed); returns this lane's poly bound (INF: no live row t)
+    auto stage_poly = [&](const double* r, int np, int k) -> double {
 #pragma unroll
-        for (int t = 0; t < PF_BND; t++) { const int e = lane + 64 * t; if (e < BND_SZ) dst[e] = r[t]; }
+        for (int i = 0; i < PFP; i++) {
+            const int e = t + 16 * i;
+            if (e < 15 * NPM) {
+                const int p = e / 15, m = e - 15 * p;
+                S[L_POLY + p * 16 + m] = (p < np && k < N) ? r[i] : 0.0;
+            }
+        }
+        lds_sync();
+        return (t < np && t < NPM && k < N) ? S[L_POLY + t * 16 + 14] : INF;
     };
-
-    // ---- slots: bounds / activity
-    const int nsl = NS * ns;
-    double mcount = 0;
-    for (int e = lane; e < nsl; e += 64) {
-        const int k = e / ns, i = e - k * ns;
-        const double* q = QSb + (size_t)k * QS;
-        double bnd;
-        bool act;
-        if (i < SL_DL) {
-            bnd = (i < SL_YU) ? q[QS_YLB + i] : q[QS_YUB + i - SL_YU];
-            act = (k >= 1) && fabs(bnd) < BIG;
-        } else if (i < SL_P) {
-            bnd = (i < SL_DU) ? q[QS_DLB + i - SL_DL] : q[QS_DUB + i - SL_DU];
-            act = (k < N) && fabs(bnd) < BIG;
-        } else {
-            const int r = i - SL_P;
-            const int np = (int)q[QS_NPOLY];
-            bnd = (r < np) ? q[QS_POLY + POLY_W * r + 14] : INF;
-            act = (k < N) && (r < np) && fabs(bnd) < BIG;
-        }
-        sBND[e] = act ? bnd : INF;
-        mcount += act ? 1.0 : 0.0;
-    }
-    mcount = wave_sum(mcount);
-    // ---- primal start: dynamics rollout with v = 0
-    for (int e = lane; e < NS * 24; e += 64) sZ[e] = 0.0;
-    wave_sync();
-    for (int k = 0; k < N; k++) {
-        double yn = 0;
-        if (lane < 9) {
-            double s = 0;
-            for (int m = 0; m < 9; m++) s += sM[lane * 9 + m] * sZ[k * 24 + m];
-            yn = s + QSb[(size_t)k * QS + QS_B + lane];
-        }
-        if (lane < 9) sZ[(k + 1) * 24 + lane] = yn;
-        wave_sync();
-    }
-    for (int e = lane; e < nsl; e += 64) {
-        const int k = e / ns, i = e - k * ns;
-        if (fabs(sBND[e]) < BIG) {
-            const double sg = slot_sgn(i);
-            const double g = sg * slot_cz(i, k, sZ + 24 * k, QSb + (size_t)k * QS + QS_POLY) - sg * sBND[e];
-            sS[e] = fmax(-g, 1.0);
-            sL[e] = 1.0;
-        } else {
-            sS[e] = 1.0;
-            sL[e] = 0.0;
-        }
-        sDSA[e] = 0.0; sDLA[e] = 0.0;
-    }
-    wave_sync();
-
-    // per-slot residual / complementarity helpers for stage k, slot i (uses staged poly rows)
-    auto rp_of = [&](int k, int i, int e, const double* poly) {
-        const double sg = slot_sgn(i);
-        return sg * slot_cz(i, k, sZ + 24 * k, poly) - sg * sBND[e] + sS[e];
+    auto row_active = [&](int k, double bnd) { return (rowY ? (k >= 1) : (k < N)) && fabs(bnd) < BIG; };
+    // unsigned c^T z of this lane's box/ddq row and of poly row t; z = stage vector in LDS at off
+    auto row_cz = [&](int k, int off) -> double {
+        if (rowY) return S[off + t];
+        const double v = S[off + 16 + j9];
+        return (k == 0) ? v : v - S[off + 9 + j9];
     };
+    auto poly_cz = [&](int off) -> double {
+        if (t >= NPM) return 0.0;
+        const double* row = S + L_POLY + t * 16;
+        double s = 0;
+#pragma unroll
+        for (int m = 0; m < 7; m++) s += row[m] * S[off + m];
+#pragma unroll
+        for (int m = 0; m < 7; m++) s += row[7 + m] * S[off + 16 + m];
+        return s;
+    };
+    auto put_vec = [&](int off, double x, double v) {  // lane c: x~_c, lane j < 8: v_j
+        S[off + t] = x;
+        if (t < 8) S[off + 16 + t] = v;
+    };
+    double pvr[PFP > 0 ? PFP : 1];
 
-    double last_dz = 1e30;
+    // ---- start point: dynamics rollout with v = 0, s = max(-g, 1), lambda = 1
+    double mcount = 0.0;
+    if (run) {
+        double y = 0.0;  // lane a < 9: y_a of stage k
+        for (int k = 0; k <= N; k++) {
+            double lb, ub; int np;
+            load_bounds(k, lb, ub, np);
+            load_poly(k, pvr);
+            const double bk = (k < N && t < 9) ? QSb[(size_t)k * QS + QS_B + t] : 0.0;
+            put_vec(L_Z, rowY ? y : 0.0, 0.0);
+            const double pb = stage_poly(pvr, np, k);
+            const double cz = row_cz(k, L_Z);
+            const double pcz = poly_cz(L_Z);
+            const bool aL = row_active(k, lb), aU = row_active(k, ub), aP = fabs(pb) < BIG;
+            double sL = 1, lL = 0, sU = 1, lU = 0, sP = 1, lP = 0;
+            if (aL) { sL = fmax(-(sgnL * cz - sgnL * lb), 1.0); lL = 1.0; }
+            if (aU) { sU = fmax(-(sgnU * cz - sgnU * ub), 1.0); lU = 1.0; }
+            if (aP) { sP = fmax(-(sgnU * pcz - sgnU * pb), 1.0); lP = 1.0; }
+            mcount += (aL ? 1.0 : 0.0) + (aU ? 1.0 : 0.0) + (aP ? 1.0 : 0.0);
+            *ws(k, WF_SL) = sL; *ws(k, WF_LL) = lL; *ws(k, WF_SU) = sU; *ws(k, WF_LU) = lU;
+            *ws(k, WF_SP) = sP; *ws(k, WF_LP) = lP;
+            *ws(k, WF_ZX) = rowY ? y : 0.0;
+            *ws(k, WF_ZV) = 0.0;
+            // y_{k+1} = M y_k + b_k (oracle order: sum_b M[a][b] y_b, then + b_a)
+            const double y8 = from_up<1>(y);  // lane 7 <- y_8
+            const double yn = (t == 7) ? m77 * y + m78 * y8 : mt * y;
+            y = (t < 9) ? yn + bk : 0.0;
+            lds_sync();
+        }
+    }
+    mcount = g_sum(mcount);
+    PMARK(0);
+
+    int it = 0;
     bool conv = false;
-    int it;
-    double rq[PF_QS > PF_BND ? PF_QS : PF_BND];
-    for (it = 0; it < IPM_MAX_IT; it++) {
-        // ---- pass A: complementarity and primal residual
-        double mus = 0, rpm = 0;
-        for (int e = lane; e < nsl; e += 64) {
-            const int k = e / ns, i = e - k * ns;
-            if (fabs(sBND[e]) >= BIG) continue;
-            const double rp = rp_of(k, i, e, QSb + (size_t)k * QS + QS_POLY);
-            mus += sS[e] * sL[e];
-            rpm = fmax(rpm, fabs(rp));
-        }
-        mus = wave_sum(mus);
-        rpm = wave_max(rpm);
-        const double mu = (mcount > 0) ? mus / mcount : 0.0;
-        if (it > 0 && mu < IPM_TOL_MU && rpm < IPM_TOL_P && last_dz < IPM_TOL_STEP) { conv = true; break; }
-
-        // ================= Riccati factorization sweep (k = N .. 0), fused with g0 = H z + h
-        qs_issue(N, rq);
-        qs_commit(sSt + (N & 1) * QS, rq);
-        if (N >= 1) qs_issue(N - 1, rq);
-        wave_sync();
-        {
-            const double* st = sSt + (N & 1) * QS;
-            if (lane < ns) {
-                const int e = N * ns + lane;
-                sW[lane] = (fabs(sBND[e]) < BIG) ? sL[e] / sS[e] : 0.0;
-            }
-            if (lane < 24) {  // g0 of the terminal stage: y part only
-                double g = 0;
-                if (lane < 9) {
-                    double s = 0;
-                    for (int m = 0; m < 9; m++) s += st[QS_Q + lane * 9 + m] * sZ[N * 24 + m];
-                    g = s + st[QS_q + lane];
+    double alpha = 0.0, sigma_mu = 0.0;  // previous iteration's step length and sigma*mu (lazy update)
+    bool pending = false;
+    while (true) {
+        if (__ballot(run) == 0) break;
+        if (run) {
+            // ================= factorization sweep k = N..0 with the lazy update of the previous step,
+            // the objective gradient g0 = H z + h and the predictor backward solve
+            int pcur = 0;  // p ping-pong slot holding p_{k+1}
+            bool chol_ok = true;
+            for (int k = N; k >= 0; k--) {
+                const double* q = QSb + (size_t)k * QS;
+                double lb, ub; int np;
+                load_bounds(k, lb, ub, np);
+                load_poly(k, pvr);
+                double sL = *ws(k, WF_SL), lL = *ws(k, WF_LL), sU = *ws(k, WF_SU), lU = *ws(k, WF_LU);
+                double sP = *ws(k, WF_SP), lP = *ws(k, WF_LP);
+                double zx = *ws(k, WF_ZX), zv = *ws(k, WF_ZV);
+                double Qr[9];
+#pragma unroll
+                for (int m = 0; m < 9; m++) Qr[m] = (t < 9) ? q[QS_Q + t * 9 + m] : 0.0;
+                const double qt = (t < 9) ? q[QS_q + t] : 0.0;
+                const double Rt = (t < 8 && k < N) ? q[QS_R + t] : 0.0;
+                const double rt = (t < 8 && k < N) ? q[QS_r + t] : 0.0;
+                const double pb = stage_poly(pvr, np, k);
+                const bool aL = row_active(k, lb), aU = row_active(k, ub), aP = fabs(pb) < BIG;
+                if (pending) {
+                    // previous iteration's update at this stage (oracle: z += a dz, s += a ds, l += a dl)
+                    const double dx = *ws(k, WF_DX), dv = *ws(k, WF_DV);
+                    const double ax = *ws(k, WF_AX), av = *ws(k, WF_AV);
+                    put_vec(L_Z, zx, zv); put_vec(L_DZ, dx, dv); put_vec(L_DA, ax, av);
+                    lds_sync();
+                    const double cz = row_cz(k, L_Z), cd = row_cz(k, L_DZ), ca = row_cz(k, L_DA);
+                    const double pcz = poly_cz(L_Z), pcd = poly_cz(L_DZ), pca = poly_cz(L_DA);
+                    double rpd;
+                    if (aL) { const SlotStep st = slot_corr(sgnL, lb, cz, ca, cd, sL, lL, sigma_mu, &rpd); sL += alpha * st.ds; lL += alpha * st.dl; }
+                    if (aU) { const SlotStep st = slot_corr(sgnU, ub, cz, ca, cd, sU, lU, sigma_mu, &rpd); sU += alpha * st.ds; lU += alpha * st.dl; }
+                    if (aP) { const SlotStep st = slot_corr(sgnU, pb, pcz, pca, pcd, sP, lP, sigma_mu, &rpd); sP += alpha * st.ds; lP += alpha * st.dl; }
+                    zx += alpha * dx;
+                    zv += alpha * dv;
+                    *ws(k, WF_SL) = sL; *ws(k, WF_LL) = lL; *ws(k, WF_SU) = sU; *ws(k, WF_LU) = lU;
+                    *ws(k, WF_SP) = sP; *ws(k, WF_LP) = lP;
+                    *ws(k, WF_ZX) = zx; *ws(k, WF_ZV) = zv;
+                    lds_sync();
                 }
-                sG0[N * 24 + lane] = g;
-            }
-            wave_sync();
-            for (int e = lane; e < 256; e += 64) {
-                const int a = e >> 4, cc = e & 15;
-                double v = 0;
-                if (a < 9 && cc < 9) {
-                    v = st[QS_Q + a * 9 + cc];
-                    if (a == cc) v += sW[SL_YL + a] + sW[SL_YU + a];
-                }
-                sP[e] = v;
-            }
-        }
-        for (int k = N - 1; k >= 0; k--) {
-            double* st = sSt + (k & 1) * QS;
-            qs_commit(st, rq);
-            if (k >= 1) qs_issue(k - 1, rq);
-            wave_sync();
-            double* is = ISb + (size_t)k * IS;
-            // (a) barrier weights, g0, PB = P B~, PM = P_yy M
-            if (lane < ns) {
-                const int e = k * ns + lane;
-                sW[lane] = (fabs(sBND[e]) < BIG) ? sL[e] / sS[e] : 0.0;
-            }
-            if (lane < 24) {
-                const double* z = sZ + 24 * k;
-                const int a = lane;
-                double g;
-                if (a < 9) {
+                put_vec(L_Z, zx, zv);
+                lds_sync();
+                // ---- slots: barrier weights and predictor coefficients (rc = s l)
+                const double cz = row_cz(k, L_Z);
+                const double pcz = poly_cz(L_Z);
+                double WL = 0, WU = 0, WP = 0, cL = 0, cU = 0, cP = 0;
+                if (aL) { const double rp = slot_rp(sgnL, cz, lb, sL); WL = lL / sL; cL = slot_coef(sL, lL, rp, sL * lL); }
+                if (aU) { const double rp = slot_rp(sgnU, cz, ub, sU); WU = lU / sU; cU = slot_coef(sU, lU, rp, sU * lU); }
+                if (aP) { const double rp = slot_rp(sgnU, pcz, pb, sP); WP = lP / sP; cP = slot_coef(sP, lP, rp, sP * lP); }
+                const double wd = WL + WU;                 // diagonal weight of row t
+                const double dvr = sgnL * cL + sgnU * cU;  // signed coefficient of row t
+                S[L_PC + t] = cP;
+                if (t < NPE) S[L_POLY + t * 16 + 15] = WP;
+                // ---- objective gradient g0 = H z + h (f_xu = 0; oracle order: sum over z, then + h)
+                double g0x, g0v = 0.0;
+                if (t < 9) {
                     double s = 0;
-                    for (int m = 0; m < 9; m++) s += st[QS_Q + a * 9 + m] * z[m];
-                    g = s + st[QS_q + a];
-                } else if (a < 16) {
-                    const int j = a - 9;
-                    g = (k >= 1) ? Hc(j) * z[16 + j] : 0.0;
+#pragma unroll
+                    for (int m = 0; m < 9; m++) s += Qr[m] * S[L_Z + m];
+                    g0x = s + qt;
                 } else {
-                    const int j = a - 16;
-                    g = st[QS_R + j] * z[a] + st[QS_r + j];
-                    if (k >= 1 && j < DOF) g += Hc(j) * z[9 + j];
+                    g0x = (k >= 1 && k < N) ? Hct * S[L_Z + 16 + j9] : 0.0;
                 }
-                sG0[k * 24 + a] = g;
-            }
-            for (int e = lane; e < 128 + 81; e += 64) {
-                if (e < 128) {
-                    const int a = e >> 3, j = e & 7;
-                    double s = 0;
-                    for (int m = 0; m < 9; m++) s += sP[a * 16 + m] * sG[m * 8 + j];
-                    if (j < 7) s += sP[a * 16 + 9 + j];
-                    sPB[e] = s;
-                } else {
-                    const int e2 = e - 128, a = e2 / 9, cc = e2 - a * 9;
-                    double s = 0;
-                    for (int m = 0; m < 9; m++) s += sP[a * 16 + m] * sM[m * 9 + cc];
-                    sPM[e2] = s;
+                if (t < 8 && k < N) {
+                    double s = (k >= 1 && t < DOF) ? Hct * S[L_Z + 9 + t] : 0.0;
+                    s += Rt * zv;
+                    g0v = s + rt;
                 }
-            }
-            wave_sync();
-            const int np = (int)st[QS_NPOLY];
-            // (b) F = R~ + B~^T P B~, Gm = S~ + B~^T P A~, Hb_yy = Q~_yy + M^T P_yy M
-            for (int e = lane; e < 64 + 128 + 81; e += 64) {
-                if (e < 64) {
-                    const int i = e >> 3, j = e & 7;
-                    double rt = 0;
-                    if (i == j) {
-                        rt = st[QS_R + i];
-                        if (i < 7) rt += sW[SL_DL + i] + sW[SL_DU + i];
-                    }
-                    if (i < 7 && j < 7)
-                        for (int r = 0; r < np; r++) {
-                            const double* row = st + QS_POLY + POLY_W * r;
-                            rt += sW[SL_P + r] * row[7 + i] * row[7 + j];
+                *ws(k, WF_GX) = g0x;
+                *ws(k, WF_GV) = g0v;
+                lds_sync();
+                // ---- step-system gradient (predictor): g = g0 + sum_i sgn_i coef_i c_i
+                double gx = g0x, gv = g0v;
+                if (t < 9) {
+                    gx += dvr;
+                    if (t < 7)
+#pragma unroll
+                        for (int p = 0; p < NPM; p++) gx += S[L_PC + p] * S[L_POLY + p * 16 + t];
+                } else if (k >= 1) {
+                    gx -= dvr;
+                }
+                const double dv_up = from_up<9>(dvr);  // lane j <- ddq row j
+                if (t < 7 && k < N) {
+                    gv += dv_up;
+#pragma unroll
+                    for (int p = 0; p < NPM; p++) gv += S[L_PC + p] * S[L_POLY + p * 16 + 7 + t];
+                }
+                if (k == N) {
+                    // terminal stage: P = Hb_N (y block only), p = g_x~ (upper triangle mirrored, lane = row)
+#pragma unroll
+                    for (int cc = 0; cc < 16; cc++) {
+                        double v = 0.0;
+                        if (t < 9 && cc < 9) {
+                            v = Qr[cc];
+                            if (cc == t) v += wd;
                         }
-                    double s = 0;
-                    for (int m = 0; m < 9; m++) s += sG[m * 8 + i] * sPB[m * 8 + j];
-                    if (i < 7) s += sPB[(9 + i) * 8 + j];
-                    sF[e] = rt + s;
-                } else if (e < 192) {
-                    const int e2 = e - 64, i = e2 >> 4, cc = e2 & 15;
-                    double v;
-                    if (cc < 9) {
-                        double st_ = 0;
-                        if (i < 7 && cc < 7)
-                            for (int r = 0; r < np; r++) {
-                                const double* row = st + QS_POLY + POLY_W * r;
-                                st_ += sW[SL_P + r] * row[7 + i] * row[cc];
-                            }
-                        double s = 0;
-                        for (int m = 0; m < 9; m++) s += sPB[m * 8 + i] * sM[m * 9 + cc];
-                        v = st_ + s;
-                    } else {
-                        const int j = cc - 9;
-                        v = (i == j && k >= 1) ? Hc(j) - (sW[SL_DL + j] + sW[SL_DU + j]) : 0.0;
+                        if (cc >= t) { S[L_P + t * 16 + cc] = v; S[L_P + cc * 16 + t] = v; }
                     }
-                    sGm[e2] = v;
-                } else {
-                    const int e2 = e - 192, a = e2 / 9, cc = e2 - a * 9;
-                    double v = st[QS_Q + a * 9 + cc];
-                    if (a == cc) v += sW[SL_YL + a] + sW[SL_YU + a];
-                    if (a < 7 && cc < 7)
-                        for (int r = 0; r < np; r++) {
-                            const double* row = st + QS_POLY + POLY_W * r;
-                            v += sW[SL_P + r] * row[a] * row[cc];
-                        }
-                    double s = 0;
-                    for (int m = 0; m < 9; m++) s += sM[m * 9 + a] * sPM[m * 9 + cc];
-                    sHb[e2] = v + s;
+                    S[L_PV + t] = gx;
+                    pcur = 0;
+                    lds_sync();
+                    continue;
                 }
-            }
-            wave_sync();
-            // (c) LF = chol(F) in every lane (registers); U = LF^-1 Gm, lane = column
-            double Lf[36];
-            {
-                int idx = 0;
+                // ---- (1) Y = B~^T P (lane n: column n of Y from column n of P), f = g_v + B~^T p
+                double Pc[16];
 #pragma unroll
-                for (int i = 0; i < 8; i++)
-#pragma unroll
-                    for (int j = 0; j <= i; j++) Lf[idx++] = sF[i * 8 + j];
-#pragma unroll
-                for (int j = 0; j < 8; j++) {
-                    const int jj = j * (j + 1) / 2;
-                    double dg = Lf[jj + j];
-#pragma unroll
-                    for (int m = 0; m < j; m++) dg -= Lf[jj + m] * Lf[jj + m];
-                    dg = sqrt(dg);
-                    Lf[jj + j] = dg;
-                    const double inv = 1.0 / dg;
-#pragma unroll
-                    for (int i = j + 1; i < 8; i++) {
-                        const int ii = i * (i + 1) / 2;
-                        double s = Lf[ii + j];
-#pragma unroll
-                        for (int m = 0; m < j; m++) s -= Lf[ii + m] * Lf[jj + m];
-                        Lf[ii + j] = s * inv;
-                    }
-                }
-            }
-            if (lane < 16) {
-                double u[8];
-#pragma unroll
-                for (int i = 0; i < 8; i++) {
-                    const int ii = i * (i + 1) / 2;
-                    double s = sGm[i * 16 + lane];
-#pragma unroll
-                    for (int m = 0; m < i; m++) s -= Lf[ii + m] * u[m];
-                    u[i] = s / Lf[ii + i];
-                }
-#pragma unroll
-                for (int i = 0; i < 8; i++) {
-                    sU[i * 16 + lane] = u[i];
-                    is[IS_U + i * 16 + lane] = u[i];
-                }
-            } else if (lane < 16 + 36) {
-                const int e = lane - 16;
-                double v = 0;
-#pragma unroll
-                for (int m = 0; m < 36; m++) v = (m == e) ? Lf[m] : v;
-                is[IS_LF + e] = v;
-            }
-            wave_sync();
-            // (d) P = Hb - U^T U
-            if (k > 0) {
-                for (int e = lane; e < 256; e += 64) {
-                    const int a = e >> 4, cc = e & 15;
-                    double v = 0;
-                    if (a < 9 && cc < 9) v = sHb[a * 9 + cc];
-                    else if (a >= 9 && a == cc) v = sW[SL_DL + a - 9] + sW[SL_DU + a - 9];
-                    double s = 0;
-#pragma unroll
-                    for (int i = 0; i < 8; i++) s += sU[i * 16 + a] * sU[i * 16 + cc];
-                    sP[e] = v - s;
-                }
-            }
-        }
-        // U / LF stores of the sweep must be performed before the solves load them back
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        wave_sync();
-
-        // ================= two solves (predictor, corrector) with the same factorization
-        double sigma_mu = 0.0, alpha = 0.0, dzmax = 0.0;
-        for (int phase = 0; phase < 2; phase++) {
-            // slot coefficient of stage k slot i: sgn * (l + W rp - rc / s)
-            auto coef_of = [&](int k, int i, const double* poly) -> double {
-                const int e = k * ns + i;
-                if (fabs(sBND[e]) >= BIG) return 0.0;
-                const double s = sS[e], l = sL[e];
-                const double rp = rp_of(k, i, e, poly);
-                const double rc = (phase == 0) ? s * l : s * l + sDSA[e] * sDLA[e] - sigma_mu;
-                return slot_sgn(i) * (l + (l / s) * rp - rc / s);
-            };
-            // ---- backward sweep: p_N = g_x~(N); per stage f = g_v + B~^T p, t = LF^-1 f, p = g_x~ + A~^T p - U^T t
-            {
-                const double* poly = QSb + (size_t)N * QS + QS_POLY;  // unused at N (no poly slots)
-                if (lane < ns) sCf[lane] = coef_of(N, lane, poly);
-                bd_issue(N - 1, rq);
-                wave_sync();
-                if (lane < 16) {
-                    double g = sG0[N * 24 + lane];
-                    if (lane < 9) g += sCf[SL_YL + lane] + sCf[SL_YU + lane];
-                    pv0[lane] = g;  // p of stage N lives in pv[N & 1]; use pv0/pv1 by parity below
-                    if (N & 1) pv1[lane] = g;
-                }
-                wave_sync();
-            }
-            for (int k = N - 1; k >= 0; k--) {
-                double* bd = sBd + (k & 1) * BND_SZ;
-                bd_commit(bd, rq);
-                if (k >= 1) bd_issue(k - 1, rq);
-                wave_sync();
-                const double* pn = ((k + 1) & 1) ? pv1 : pv0;
-                double* pc = (k & 1) ? pv1 : pv0;
-                const double* poly = bd + BND_POLY;
-                if (lane < ns) sCf[lane] = coef_of(k, lane, poly);
-                wave_sync();
-                const int np = (int)QSb[(size_t)k * QS + QS_NPOLY];
-                if (lane < 24) {
-                    const int a = lane;
-                    double g = sG0[k * 24 + a];
-                    if (a < 9) {
-                        g += sCf[SL_YL + a] + sCf[SL_YU + a];
-                        if (a < 7)
-                            for (int r = 0; r < np; r++) g += sCf[SL_P + r] * poly[POLY_W * r + a];
-                        sGx[a] = g;
-                    } else if (a < 16) {
-                        const int j = a - 9;
-                        if (k >= 1) g -= sCf[SL_DL + j] + sCf[SL_DU + j];
-                        sGx[a] = g;
-                    } else {
-                        const int j = a - 16;
-                        if (j < 7) {
-                            g += sCf[SL_DL + j] + sCf[SL_DU + j];
-                            for (int r = 0; r < np; r++) g += sCf[SL_P + r] * poly[POLY_W * r + 7 + j];
-                        }
-                        double s = 0;
-                        for (int m = 0; m < 9; m++) s += sG[m * 8 + j] * pn[m];
-                        if (j < 7) s += pn[9 + j];
-                        sFv[j] = g + s;
-                    }
-                }
-                wave_sync();
-                double t[8];
+                for (int i = 0; i < 16; i++) Pc[i] = S[L_P + i * 16 + t];
                 {
-                    const double* Lf = bd + BND_LF;
+                    double Y[8];
+#pragma unroll
+                    for (int i = 0; i < 7; i++) Y[i] = c.G[i * 9] * Pc[i] + Pc[9 + i];
+                    Y[7] = g77 * Pc[7] + g87 * Pc[8];
+#pragma unroll
+                    for (int i = 0; i < 8; i++) S[L_U + i * 16 + t] = Y[i];
+                }
+                const double* pn = S + L_PV + 16 * pcur;
+                if (t < 8) {
+                    const double bp = (t < 7) ? gt * pn[t] + pn[9 + t] : g77 * pn[7] + g87 * pn[8];
+                    S[L_FV + t] = gv + bp;
+                }
+                lds_sync();
+                // ---- (2) Hb_yy row t, F column t (t < 8), Gm column t (t < 9)
+                double Hb[9];
+                {
+                    const double P77 = S[L_P + 7 * 16 + 7];
+#pragma unroll
+                    for (int cc = 0; cc < 9; cc++) {
+                        const double mc = c.M[cc * 10];
+                        double v = Qr[cc];
+                        if (cc == t) v += wd;
+                        if (t < 7 && cc < 7)
+#pragma unroll
+                            for (int p = 0; p < NPM; p++) {
+                                const double* row = S + L_POLY + p * 16;
+                                v += row[15] * (row[t] * row[cc]);
+                            }
+                        double mp = (mt * mc) * Pc[cc];
+                        if (cc == 8) mp += (mt * m78) * Pc[7];
+                        if (t == 8) mp += (m78 * mc) * S[L_P + 7 * 16 + cc];
+                        if (t == 8 && cc == 8) mp += (m78 * m78) * P77;
+                        Hb[cc] = v + mp;
+                    }
+                }
+                double gm[8];
+                {
+                    // F[:, t] = H_vv[:, t] + (Y B~)[:, t];  B~ column j = g_j e_j + e_{9+j} (j < 7), g77 e7 + g87 e8
+                    const bool fj = t < 7;
+                    const int c1 = fj ? t : 7, c2 = fj ? 9 + t : 8;
+                    const double w2 = fj ? 1.0 : g87;
+                    const double wdv = from_up<9>(wd);  // lane j <- ddq row j weight
+                    double Fc[8];
 #pragma unroll
                     for (int i = 0; i < 8; i++) {
-                        const int ii = i * (i + 1) / 2;
-                        double s = sFv[i];
+                        const double v = gt * S[L_U + i * 16 + c1] + w2 * S[L_U + i * 16 + c2];
+                        double h = 0.0;
+                        if (i == t) {
+                            h = Rt;
+                            if (fj) h += wdv;
+                        }
+                        if (i < 7 && fj)
 #pragma unroll
-                        for (int m = 0; m < i; m++) s -= Lf[ii + m] * t[m];
-                        t[i] = s / Lf[ii + i];
+                            for (int p = 0; p < NPM; p++) {
+                                const double* row = S + L_POLY + p * 16;
+                                h += row[15] * (row[7 + i] * row[7 + t]);
+                            }
+                        Fc[i] = h + v;
+                    }
+                    if (t < 8)
+#pragma unroll
+                        for (int i = 0; i < 8; i++) S[L_F + i * 8 + t] = Fc[i];
+                    // Gm[:, t] = H_vy[:, t] + (Y M)[:, t] (t < 9); w columns are diag(Hc - W_ddq) (k >= 1)
+                    const int ct = (t < 9) ? t : 0;
+#pragma unroll
+                    for (int i = 0; i < 8; i++) {
+                        double v = mt * S[L_U + i * 16 + ct];
+                        if (t == 8) v += m78 * S[L_U + i * 16 + 7];
+                        double h = 0.0;
+                        if (i < 7 && t < 7)
+#pragma unroll
+                            for (int p = 0; p < NPM; p++) {
+                                const double* row = S + L_POLY + p * 16;
+                                h += row[15] * (row[7 + i] * row[ct]);
+                            }
+                        gm[i] = h + v;
                     }
                 }
-                if (lane < 8) {
-                    double tv = 0;
+                lds_sync();
+                // ---- (3) chol(F); U = LF^-1 Gm; K = -LF^-T U; Finv column (t & 7); kff = -F^-1 f;
+                //          p = g_x~ + A~^T p + K^T f
+                double LF[36], dinv[8];
+                chol_ok = chol8(S + L_F, LF, dinv) && chol_ok;
+                double u[8];
+                const double gw = (k >= 1) ? Hct - wd : 0.0;
 #pragma unroll
-                    for (int m = 0; m < 8; m++) tv = (m == lane) ? t[m] : tv;
-                    sT[k * 8 + lane] = tv;
-                }
-                if (k > 0 && lane < 16) {
-                    double s = sGx[lane];
-                    if (lane < 9)
-                        for (int m = 0; m < 9; m++) s += sM[m * 9 + lane] * pn[m];
-                    const double* U = bd + BND_U;
+                for (int i = 0; i < 8; i++) u[i] = (t < 9) ? gm[i] : ((i == j9) ? gw : 0.0);
+                fwd8(LF, dinv, u);
+                double kc[8];
 #pragma unroll
-                    for (int i = 0; i < 8; i++) s -= U[i * 16 + lane] * t[i];
-                    pc[lane] = s;
-                }
-                wave_sync();
-            }
-            // ---- forward sweep: x~_0 = 0; v = -LF^-T (U x~ + t); x~_{k+1} = A~ x~ + B~ v; recover ds, dl
-            double amax = (phase == 0) ? 1.0 : 1e30;
-            double dzm = 0.0;
-            if (lane < 16) xv0[lane] = 0.0;
-            bd_issue(0, rq);
-            wave_sync();
-            double* sDSx = (phase == 0) ? sDSA : sDS;
-            double* sDLx = (phase == 0) ? sDLA : sDL;
-            auto recover = [&](int k, const double* poly) {
-                if (lane < ns) {
-                    const int i = lane, e = k * ns + i;
-                    if (fabs(sBND[e]) < BIG) {
-                        const double cd = slot_sgn(i) * slot_cz(i, k, sDZ + 24 * k, poly);
-                        const double s = sS[e], l = sL[e];
-                        const double rp = rp_of(k, i, e, poly);
-                        const double rc = (phase == 0) ? s * l : s * l + sDSA[e] * sDLA[e] - sigma_mu;
-                        const double ds = -rp - cd;
-                        const double dl = (l / s) * (cd + rp) - rc / s;
-                        sDSx[e] = ds;
-                        sDLx[e] = dl;
-                        if (ds < 0) amax = fmin(amax, -s / ds);
-                        if (dl < 0) amax = fmin(amax, -l / dl);
-                    }
-                }
-            };
-            for (int k = 0; k < N; k++) {
-                double* bd = sBd + (k & 1) * BND_SZ;
-                bd_commit(bd, rq);
-                if (k + 1 < N) bd_issue(k + 1, rq);
-                wave_sync();
-                const double* xc = (k & 1) ? xv1 : xv0;
-                double* xn_ = (k & 1) ? xv0 : xv1;
-                if (lane < 8) {
-                    double s = sT[k * 8 + lane];
-                    const double* U = bd + BND_U;
-                    for (int a = 0; a < 16; a++) s += U[lane * 16 + a] * xc[a];
-                    sH[lane] = s;
-                }
-                wave_sync();
-                double v[8];
+                for (int i = 0; i < 8; i++) kc[i] = u[i];
+                bwd8(LF, dinv, kc);
+#pragma unroll
+                for (int i = 0; i < 8; i++) kc[i] = -kc[i];
+                double fi[8];
+#pragma unroll
+                for (int i = 0; i < 8; i++) fi[i] = (i == (t & 7)) ? 1.0 : 0.0;
+                fwd8(LF, dinv, fi);
+                bwd8(LF, dinv, fi);
+                double f[8];
+#pragma unroll
+                for (int i = 0; i < 8; i++) f[i] = S[L_FV + i];
+                double kff = 0.0;
+#pragma unroll
+                for (int m = 0; m < 8; m++) kff -= fi[m] * f[m];
                 {
-                    const double* Lf = bd + BND_LF;
-#pragma unroll
-                    for (int i = 7; i >= 0; i--) {
-                        double s = sH[i];
-#pragma unroll
-                        for (int m = i + 1; m < 8; m++) s -= Lf[m * (m + 1) / 2 + i] * v[m];
-                        v[i] = s / Lf[i * (i + 1) / 2 + i];
+                    double atp = 0.0;
+                    if (t < 9) {
+                        atp = mt * pn[t];
+                        if (t == 8) atp += m78 * pn[7];
                     }
+                    double ktf = 0.0;
 #pragma unroll
-                    for (int i = 0; i < 8; i++) v[i] = -v[i];
+                    for (int i = 0; i < 8; i++) ktf += kc[i] * f[i];
+                    S[L_PV + 16 * (pcur ^ 1) + t] = gx + atp + ktf;
                 }
-                if (lane < 16) {
+#pragma unroll
+                for (int i = 0; i < 8; i++) {
+                    S[L_U + i * 16 + t] = u[i];
+                    S[L_K + i * 16 + t] = kc[i];
+                    *ws(k, WF_KC + i) = kc[i];
+                }
+                *ws(k, WF_KFF) = (t < 8) ? kff : 0.0;
+#pragma unroll
+                for (int m = 0; m < 4; m++) *ws(k, WF_FI + m) = (t < 8) ? fi[m] : fi[4 + m];
+                lds_sync();
+                {
+                    const int ri = t & 7, hoff = (t < 8) ? 0 : 8;
+#pragma unroll
+                    for (int m = 0; m < 8; m++) *ws(k, WF_KR + m) = S[L_K + ri * 16 + hoff + m];
+                }
+                // ---- (4) P = Hb - U^T U (lane = row t, upper triangle mirrored)
+                if (k > 0) {
+#pragma unroll
+                    for (int cc = 0; cc < 16; cc++) {
+                        if (cc < t) continue;
+                        double v = 0.0;
+                        if (t < 9 && cc < 9) v = Hb[cc];
+                        else if (t >= 9 && cc == t && k >= 1) v = wd;
+#pragma unroll
+                        for (int i = 0; i < 8; i++) v -= u[i] * S[L_U + i * 16 + cc];
+                        S[L_P + t * 16 + cc] = v;
+                        S[L_P + cc * 16 + t] = v;
+                    }
+                }
+                pcur ^= 1;
+                lds_sync();
+            }
+            if (!chol_ok) run = false;  // oracle: factorization failure ends the loop -> MaxIterReached
+        }
+        PMARK(2);
+        if (run) {
+            // ---- predictor forward: x~_0 = 0; v = K x~ + kff; x~' = A~ x~ + B~ v; recover dsa, dla
+            double S0 = 0, S1 = 0, S2 = 0, amax = 1.0;
+            int xc = 0;
+            S[L_X + t] = 0.0;
+            lds_sync();
+            for (int k = 0; k <= N; k++) {
+                double lb, ub; int np;
+                load_bounds(k, lb, ub, np);
+                load_poly(k, pvr);
+                const double sL = *ws(k, WF_SL), lL = *ws(k, WF_LL), sU = *ws(k, WF_SU), lU = *ws(k, WF_LU);
+                const double sP = *ws(k, WF_SP), lP = *ws(k, WF_LP);
+                const double zx = *ws(k, WF_ZX), zv = *ws(k, WF_ZV);
+                double kr[8];
+                double kff = 0.0;
+                if (k < N) {
+#pragma unroll
+                    for (int m = 0; m < 8; m++) kr[m] = *ws(k, WF_KR + m);
+                    kff = *ws(k, WF_KFF);
+                }
+                const double pb = stage_poly(pvr, np, k);
+                const bool aL = row_active(k, lb), aU = row_active(k, ub), aP = fabs(pb) < BIG;
+                const double* xs = S + L_X + 16 * xc;
+                const double xt = xs[t];
+                double v = 0.0;
+                if (k < N) {
+                    const int hoff = (t < 8) ? 0 : 8;
+                    double part = 0.0;
+#pragma unroll
+                    for (int m = 0; m < 8; m++) part += kr[m] * xs[hoff + m];
+                    v = part + from_up<8>(part) + kff;
+                    const double x8 = xs[8];
+                    const double v7 = from_down<1>(v);
+                    const double vj = from_down<9>(v);
                     double xn;
-                    if (lane < 9) {
-                        double s = 0;
-                        for (int m = 0; m < 9; m++) s += sM[lane * 9 + m] * xc[m];
+                    if (t < 7) xn = mt * xt + gt * v;
+                    else if (t == 7) xn = (m77 * xt + m78 * x8) + g77 * v;
+                    else if (t == 8) xn = m88 * xt + g87 * v7;
+                    else xn = vj;
+                    S[L_X + 16 * (xc ^ 1) + t] = xn;
+                }
+                const double dvv = (t < 8 && k < N) ? v : 0.0;
+                *ws(k, WF_AX) = xt;
+                *ws(k, WF_AV) = dvv;
+                put_vec(L_Z, zx, zv);
+                put_vec(L_DA, xt, dvv);
+                lds_sync();
+                const double cz = row_cz(k, L_Z), ca = row_cz(k, L_DA);
+                const double pcz = poly_cz(L_Z), pca = poly_cz(L_DA);
+                auto rec = [&](bool a, double sgn, double bnd, double czz, double caa, double s, double l) {
+                    if (!a) return;
+                    const double rp = slot_rp(sgn, czz, bnd, s);
+                    const SlotStep st = slot_recover(s, l, rp, sgn * caa, s * l);
+                    amax = step_bound(amax, s, l, st);
+                    S0 += s * l;
+                    S1 += s * st.dl + l * st.ds;
+                    S2 += st.ds * st.dl;
+                };
+                rec(aL, sgnL, lb, cz, ca, sL, lL);
+                rec(aU, sgnU, ub, cz, ca, sU, lU);
+                rec(aP, sgnU, pb, pcz, pca, sP, lP);
+                xc ^= 1;
+                lds_sync();
+            }
+            amax = g_min(amax);
+            S0 = g_sum(S0); S1 = g_sum(S1); S2 = g_sum(S2);
+            const double mu = (mcount > 0) ? S0 / mcount : 0.0;
+            double mua = S0 + amax * S1 + amax * amax * S2;
+            mua = (mcount > 0) ? mua / mcount : 0.0;
+            const double ratio = (mu > 0) ? mua / mu : 0.0;
+            const double sigma = (mu > 0) ? ratio * ratio * ratio : 0.0;
+            const double smu = sigma * mu;
+            PMARK(3);
+
+            // ---- corrector backward: coef with rc = s l + dsa dla - sigma mu; f = g_v + B~^T p;
+            //      kff = -F^-1 f; p = g_x~ + A~^T p + K^T f
+            int pcur = 0;
+            for (int k = N; k >= 0; k--) {
+                double lb, ub; int np;
+                load_bounds(k, lb, ub, np);
+                load_poly(k, pvr);
+                const double sL = *ws(k, WF_SL), lL = *ws(k, WF_LL), sU = *ws(k, WF_SU), lU = *ws(k, WF_LU);
+                const double sP = *ws(k, WF_SP), lP = *ws(k, WF_LP);
+                const double zx = *ws(k, WF_ZX), zv = *ws(k, WF_ZV);
+                const double ax = *ws(k, WF_AX), av = *ws(k, WF_AV);
+                const double g0x = *ws(k, WF_GX), g0v = *ws(k, WF_GV);
+                double kc[8], fir[4];
+                if (k < N) {
 #pragma unroll
-                        for (int j = 0; j < 8; j++) s += sG[lane * 8 + j] * v[j];
-                        xn = s;
-                    } else {
-                        double vv = 0;
+                    for (int i = 0; i < 8; i++) kc[i] = *ws(k, WF_KC + i);
 #pragma unroll
-                        for (int j = 0; j < 7; j++) vv = (j == lane - 9) ? v[j] : vv;
-                        xn = vv;
+                    for (int m = 0; m < 4; m++) fir[m] = *ws(k, WF_FI + m);
+                }
+                const double pb = stage_poly(pvr, np, k);
+                const bool aL = row_active(k, lb), aU = row_active(k, ub), aP = fabs(pb) < BIG;
+                put_vec(L_Z, zx, zv);
+                put_vec(L_DA, ax, av);
+                lds_sync();
+                const double cz = row_cz(k, L_Z), ca = row_cz(k, L_DA);
+                const double pcz = poly_cz(L_Z), pca = poly_cz(L_DA);
+                auto coef = [&](bool a, double sgn, double bnd, double czz, double caa, double s, double l) -> double {
+                    if (!a) return 0.0;
+                    const double rp = slot_rp(sgn, czz, bnd, s);
+                    const SlotStep pa = slot_recover(s, l, rp, sgn * caa, s * l);
+                    const double rc = s * l + pa.ds * pa.dl - smu;
+                    return slot_coef(s, l, rp, rc);
+                };
+                const double cL = coef(aL, sgnL, lb, cz, ca, sL, lL);
+                const double cU = coef(aU, sgnU, ub, cz, ca, sU, lU);
+                const double cP = coef(aP, sgnU, pb, pcz, pca, sP, lP);
+                const double dvr = sgnL * cL + sgnU * cU;
+                S[L_PC + t] = cP;
+                lds_sync();
+                double gx = g0x, gv = g0v;
+                if (t < 9) {
+                    gx += dvr;
+                    if (t < 7)
+#pragma unroll
+                        for (int p = 0; p < NPM; p++) gx += S[L_PC + p] * S[L_POLY + p * 16 + t];
+                } else if (k >= 1) {
+                    gx -= dvr;
+                }
+                const double dv_up = from_up<9>(dvr);
+                if (t < 7 && k < N) {
+                    gv += dv_up;
+#pragma unroll
+                    for (int p = 0; p < NPM; p++) gv += S[L_PC + p] * S[L_POLY + p * 16 + 7 + t];
+                }
+                if (k == N) {
+                    S[L_PV + t] = gx;
+                    pcur = 0;
+                    lds_sync();
+                    continue;
+                }
+                const double* pn = S + L_PV + 16 * pcur;
+                if (t < 8) {
+                    const double bp = (t < 7) ? gt * pn[t] + pn[9 + t] : g77 * pn[7] + g87 * pn[8];
+                    S[L_FV + t] = gv + bp;
+                }
+                lds_sync();
+                double f[8];
+#pragma unroll
+                for (int i = 0; i < 8; i++) f[i] = S[L_FV + i];
+                const int hoff = (t < 8) ? 0 : 4;
+                double part = 0.0;
+#pragma unroll
+                for (int m = 0; m < 4; m++) part -= fir[m] * f[hoff + m];
+                const double kff = part + from_up<8>(part);
+                *ws(k, WF_KFF) = (t < 8) ? kff : 0.0;
+                if (k > 0) {
+                    double atp = 0.0;
+                    if (t < 9) {
+                        atp = mt * pn[t];
+                        if (t == 8) atp += m78 * pn[7];
                     }
-                    xn_[lane] = xn;
-                    sDZ[k * 24 + lane] = xc[lane];
-                    dzm = fmax(dzm, fabs(xc[lane]));
-                } else if (lane < 24) {
-                    double vv = 0;
+                    double ktf = 0.0;
 #pragma unroll
-                    for (int j = 0; j < 8; j++) vv = (j == lane - 16) ? v[j] : vv;
-                    sDZ[k * 24 + lane] = vv;
-                    dzm = fmax(dzm, fabs(vv));
+                    for (int i = 0; i < 8; i++) ktf += kc[i] * f[i];
+                    S[L_PV + 16 * (pcur ^ 1) + t] = gx + atp + ktf;
                 }
-                wave_sync();
-                recover(k, bd + BND_POLY);
+                pcur ^= 1;
+                lds_sync();
             }
-            if (lane < 24) {
-                const double* xl = (N & 1) ? xv1 : xv0;
-                const double v = (lane < 16) ? xl[lane] : 0.0;
-                sDZ[N * 24 + lane] = v;
-                dzm = fmax(dzm, fabs(v));
-            }
-            wave_sync();
-            recover(N, QSb + (size_t)N * QS + QS_POLY);
-            amax = wave_min(amax);
-            wave_sync();
-            if (phase == 0) {
-                double mua = 0;
-                for (int e = lane; e < nsl; e += 64) {
-                    if (fabs(sBND[e]) >= BIG) continue;
-                    mua += (sS[e] + amax * sDSA[e]) * (sL[e] + amax * sDLA[e]);
+            PMARK(4);
+
+            // ---- corrector forward: dz, ds, dl, max step, mu(alpha) sums, max |rp|, max |dz|
+            double T0 = 0, T1 = 0, T2 = 0, amx = 1e30, rpm = 0, dzm = 0;
+            xc = 0;
+            S[L_X + t] = 0.0;
+            lds_sync();
+            for (int k = 0; k <= N; k++) {
+                double lb, ub; int np;
+                load_bounds(k, lb, ub, np);
+                load_poly(k, pvr);
+                const double sL = *ws(k, WF_SL), lL = *ws(k, WF_LL), sU = *ws(k, WF_SU), lU = *ws(k, WF_LU);
+                const double sP = *ws(k, WF_SP), lP = *ws(k, WF_LP);
+                const double zx = *ws(k, WF_ZX), zv = *ws(k, WF_ZV);
+                const double ax = *ws(k, WF_AX), av = *ws(k, WF_AV);
+                double kr[8];
+                double kff = 0.0;
+                if (k < N) {
+#pragma unroll
+                    for (int m = 0; m < 8; m++) kr[m] = *ws(k, WF_KR + m);
+                    kff = *ws(k, WF_KFF);
                 }
-                mua = wave_sum(mua);
-                mua = (mcount > 0) ? mua / mcount : 0.0;
-                const double ratio = (mu > 0) ? mua / mu : 0.0;
-                const double sigma = (mu > 0) ? ratio * ratio * ratio : 0.0;
-                sigma_mu = sigma * mu;
+                const double pb = stage_poly(pvr, np, k);
+                const bool aL = row_active(k, lb), aU = row_active(k, ub), aP = fabs(pb) < BIG;
+                const double* xs = S + L_X + 16 * xc;
+                const double xt = xs[t];
+                double v = 0.0;
+                if (k < N) {
+                    const int hoff = (t < 8) ? 0 : 8;
+                    double part = 0.0;
+#pragma unroll
+                    for (int m = 0; m < 8; m++) part += kr[m] * xs[hoff + m];
+                    v = part + from_up<8>(part) + kff;
+                    const double x8 = xs[8];
+                    const double v7 = from_down<1>(v);
+                    const double vj = from_down<9>(v);
+                    double xn;
+                    if (t < 7) xn = mt * xt + gt * v;
+                    else if (t == 7) xn = (m77 * xt + m78 * x8) + g77 * v;
+                    else if (t == 8) xn = m88 * xt + g87 * v7;
+                    else xn = vj;
+                    S[L_X + 16 * (xc ^ 1) + t] = xn;
+                }
+                const double dvv = (t < 8 && k < N) ? v : 0.0;
+                *ws(k, WF_DX) = xt;
+                *ws(k, WF_DV) = dvv;
+                dzm = fmax(dzm, fmax(fabs(xt), fabs(dvv)));
+                put_vec(L_Z, zx, zv);
+                put_vec(L_DZ, xt, dvv);
+                put_vec(L_DA, ax, av);
+                lds_sync();
+                const double cz = row_cz(k, L_Z), cd = row_cz(k, L_DZ), ca = row_cz(k, L_DA);
+                const double pcz = poly_cz(L_Z), pcd = poly_cz(L_DZ), pca = poly_cz(L_DA);
+                auto rec = [&](bool a, double sgn, double bnd, double czz, double caa, double cdd, double s, double l) {
+                    if (!a) return;
+                    double rp;
+                    const SlotStep st = slot_corr(sgn, bnd, czz, caa, cdd, s, l, smu, &rp);
+                    amx = step_bound(amx, s, l, st);
+                    T0 += s * l;
+                    T1 += s * st.dl + l * st.ds;
+                    T2 += st.ds * st.dl;
+                    rpm = fmax(rpm, fabs(rp));
+                };
+                rec(aL, sgnL, lb, cz, ca, cd, sL, lL);
+                rec(aU, sgnU, ub, cz, ca, cd, sU, lU);
+                rec(aP, sgnU, pb, pcz, pca, pcd, sP, lP);
+                xc ^= 1;
+                lds_sync();
+            }
+            amx = g_min(amx);
+            T0 = g_sum(T0); T1 = g_sum(T1); T2 = g_sum(T2);
+            rpm = g_max(rpm);
+            dzm = g_max(dzm);
+            alpha = fmin(1.0, 0.995 * amx);
+            sigma_mu = smu;
+            pending = true;
+            it++;
+            PMARK(5);
+            // convergence test at the start of the next iteration (oracle: only while it < IPM_MAX_IT)
+            if (it < IPM_MAX_IT) {
+                double mun = T0 + alpha * T1 + alpha * alpha * T2;
+                mun = (mcount > 0) ? mun / mcount : 0.0;
+                const double rpn = (1.0 - alpha) * rpm;
+                if (mun < IPM_TOL_MU && rpn < IPM_TOL_P && dzm < IPM_TOL_STEP) {
+                    conv = true;
+                    run = false;
+                }
             } else {
-                alpha = fmin(1.0, 0.995 * amax);
-                dzmax = wave_max(dzm);
+                run = false;
             }
         }
-        // ---- update
-        for (int e = lane; e < NS * 24; e += 64) sZ[e] += alpha * sDZ[e];
-        for (int e = lane; e < nsl; e += 64) {
-            if (fabs(sBND[e]) >= BIG) continue;
-            sS[e] += alpha * sDS[e];
-            sL[e] += alpha * sDL[e];
-        }
-        last_dz = dzmax;
-        wave_sync();
     }
-    if (lane == 0) si[SQ_IPMIT] = it;
+
+#ifdef MPCC_IPM_PROF
+    if (entered && t == 0) {
+        for (int i = 0; i < 6; i++) atomicAdd(&g_ipm_prof[i], (unsigned long long)prof_acc[i]);
+        atomicAdd(&g_ipm_prof[6], (unsigned long long)it);
+        atomicAdd(&g_ipm_prof[7], 1ull);
+    }
+#endif
+    if (!entered) return;
+    if (t == 0) si[SQ_IPMIT] = it;
     if (!conv) {
-        if (lane == 0) si[SQ_QPSTAT] = MPCC_QP_MaxIterReached;  // keep the previous step (Q6)
+        if (t == 0) si[SQ_QPSTAT] = MPCC_QP_MaxIterReached;  // keep the previous step (Q6)
         return;
     }
-    if (lane == 0) si[SQ_QPSTAT] = 0;
+    if (t == 0) si[SQ_QPSTAT] = 0;
     double* stp = d.step + (size_t)b * NS * 17;
-    for (int e = lane; e < NS * 17; e += 64) {
-        const int k = e / 17, a = e - k * 17;
-        const double* z = sZ + 24 * k;
-        stp[e] = (a < 9) ? z[a] : ((k < N) ? z[16 + a - 9] : 0.0);
+    for (int k = 0; k <= N; k++) {
+        const double zx = *ws(k, WF_ZX) + alpha * *ws(k, WF_DX);
+        const double zv = *ws(k, WF_ZV) + alpha * *ws(k, WF_DV);
+        if (t < 9) stp[k * 17 + t] = zx;
+        if (t < 8) stp[k * 17 + 9 + t] = (k < N) ? zv : 0.0;
     }
+}
+
+#ifdef MPCC_IPM_PROF
+extern "C" int mpcc_debug_ipm_prof(unsigned long long* out, int reset) {
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_ipm_prof), sizeof(unsigned long long) * 16) != hipSuccess) return -1;
+    if (reset) {
+        unsigned long long z[16] = {0};
+        if (hipMemcpyToSymbol(HIP_SYMBOL(g_ipm_prof), z, sizeof z) != hipSuccess) return -1;
+    }
+    return 0;
+}
+#endif
+
+template <int NPM>
+static void launch_ipm_t(const DevConst& c, const DevBuffers& d, hipStream_t s) {
+    const size_t lds = ipm_lds_bytes(c.N, NPM);
+    static bool configured = false;
+    if (!configured) {
+        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_ipm<NPM>), hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  (int)lds);
+        configured = true;
+    }
+    hipLaunchKernelGGL(k_ipm<NPM>, dim3((c.Bn + IPW - 1) / IPW), dim3(64), lds, s, c, d);
 }
 
 void launch_ipm(const DevConst& c, const DevBuffers& d, int npmax, hipStream_t s) {
-    const size_t lds = ipm_lds_bytes(c.N, npmax);
-    static size_t configured = 0;
-    if (lds > configured) {
-        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_ipm), hipFuncAttributeMaxDynamicSharedMemorySize,
-                                  (int)lds);
-        configured = lds;
+    switch (npmax) {
+        case 0: launch_ipm_t<0>(c, d, s); break;
+        case 1: launch_ipm_t<1>(c, d, s); break;
+        case 2: launch_ipm_t<2>(c, d, s); break;
+        case 9: launch_ipm_t<9>(c, d, s); break;
+        case 10: launch_ipm_t<10>(c, d, s); break;
+        default: launch_ipm_t<11>(c, d, s); break;
     }
-    hipLaunchKernelGGL(k_ipm, dim3(c.Bn), dim3(64), lds, s, c, d, npmax);
 }
 
 }  // namespace mpcc

@@ -13,7 +13,7 @@ DATA = os.path.join(PKG, "data")
 NN_DIR = os.path.join(DATA, "nn")
 DEFAULT_PARAMS = os.path.join(DATA, "params", "default_params.json")
 DEFAULT_TRACK = os.path.join(DATA, "params", "default_track.json")
-LIB_PATH = os.path.join(PKG, "_build", "libmpcc_engine.so")
+LIB_PATH = os.environ.get("MPCC_ENGINE_LIB", os.path.join(PKG, "_build", "libmpcc_engine.so"))
 
 REC_SIZE = 143
 NX, NU, PANDA_DOF, PANDA_NUM_LINKS = 9, 8, 7, 9

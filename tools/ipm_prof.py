@@ -1,0 +1,64 @@
+"""Cycle accounting of k_ipm sections (profiling build: MPCC_PROF_BUILD=1 python -m mpcc_manipulator_amd._build).
+
+    MPCC_ENGINE_LIB=mpcc_manipulator_amd/_build_prof/libmpcc_engine.so python tools/ipm_prof.py --batch 512
+"""
+import argparse
+import ctypes as C
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+import bench  # noqa: E402
+
+SECTIONS = ["setup", "passA", "factor", "backward", "forward", "update"]
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--batch", type=int, nargs="+", default=[256, 512, 1024, 4096])
+    ap.add_argument("--N", type=int, default=20)
+    ap.add_argument("--mask", type=int, default=2)
+    args = ap.parse_args()
+    import torch
+    import mpcc_manipulator_amd as m
+    from mpcc_manipulator_amd.engine import lib
+    L = lib()
+    prof = getattr(L, "mpcc_debug_ipm_prof", None)
+    params = m.load_params(args.N, overrides={"sqp": {"max_iter": 2}})
+    params.constraint_mask = args.mask
+    pool, track = bench.make_pool(m, params, args.mask, 400, 0)
+    for B in args.batch:
+        eng = m.Engine(params, max_batch=B, device=0, constraint_mask=args.mask)
+        eng.set_track(*track)
+        rng = np.random.default_rng(1)
+        idx = np.arange(B) % len(pool["x0"])
+        x0 = pool["x0"][idx].copy(); x0[:, :7] += rng.normal(0, 0.005, (B, 7))
+        args_ = (x0, pool["u0"][idx], np.tile([3., 3., 3., 0.], (B, 1)))
+        ws = (pool["guess"][idx], pool["valid"][idx].astype(np.int32), pool["fails"][idx].astype(np.int32))
+        for rep in range(3):
+            eng.set_warmstart(*ws)
+            if rep == 2 and prof:
+                buf = (C.c_ulonglong * 16)()
+                prof(buf, 1)
+            eng.timing_begin()
+            out = eng.solve(*[a.copy() for a in args_])
+            tm, ncalls, nipm = eng.timing_end()
+        res = {"batch": B, "solve_qp_ms": tm["solve_qp"] * 1e3, "ipm_launches": nipm, "total_ms": tm["total"] * 1e3}
+        if prof:
+            buf = (C.c_ulonglong * 16)()
+            prof(buf, 0)
+            n_inst, n_it = buf[7], buf[6]
+            res["instances"] = n_inst
+            res["ipm_iters"] = n_it
+            res["kcycles_per_iter"] = {s: round(buf[i] / max(1, n_it) / 1e3, 2) for i, s in enumerate(SECTIONS)}
+        print(json.dumps(res), flush=True)
+        eng.close()
+
+
+if __name__ == "__main__":
+    main()
