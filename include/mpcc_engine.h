@@ -191,10 +191,19 @@ int mpcc_debug_spline(mpcc_engine* e, int M, const double* s, double* pos, doubl
 /* Cost::getCost for M (x,u,rec,k) tuples: obj [M], fx [M*9], fu [M*8], fxx [M*81], fuu [M*64] */
 int mpcc_debug_stage_cost(mpcc_engine* e, int M, const double* x, const double* u, const double* rec, const int32_t* k,
                           double* obj, double* fx, double* fu, double* fxx, double* fuu);
+/* ArcLengthSpline::projectOnSpline (arc_length_spline.cpp:318-379) for M (s_guess, ee[3]) pairs */
+int mpcc_debug_project(mpcc_engine* e, int M, const double* s_guess, const double* ee, double* s_out);
+
 /* one QP of the SQP for B instances: guess [B*(N+1)*17], rec [B*(N+1)*143], u_cur [B*8]
  * -> step [B*(17N+9)] in the reference's stacked layout, qp_status [B], ipm_iters [B] */
 int mpcc_debug_solve_qp(mpcc_engine* e, int B, const double* guess, const double* rec, const double* u_cur,
                         double* step, int32_t* qp_status, int32_t* ipm_iters);
+
+/* SQP trace of the next solves (test instrumentation, off by default): per instance and SQP iteration
+ * (at most 4) 8 doubles: qp status, ipm iterations, trial objective and violation at alpha = 1,
+ * accepted, |step|_inf, alpha, alpha*|step|_inf (osqp_interface.cpp:540-574, 759-808). */
+int mpcc_debug_trace_enable(mpcc_engine* e, int enable);
+int mpcc_debug_trace_get(mpcc_engine* e, int B, double* out /* [B*4*8] */);
 
 #ifdef __cplusplus
 }

@@ -15,6 +15,10 @@ LIB = os.path.join(BUILD, "libmpcc_engine.so")
 SOURCES = ["kernels.hip", "ipm.hip", "engine.cpp", "host_params.cpp", "host_spline.cpp", "mpc.cpp"]
 ARCH = os.environ.get("MPCC_OFFLOAD_ARCH", "gfx950")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+# The stage kernels (projection, kinematics, records, QP assembly, line-search trials) follow the
+# oracle's operation order without FMA contraction, so their discrete decisions (projection Newton,
+# warm-start validity, filter comparisons) see the same values as the reference CPU arithmetic.
+FILE_FLAGS = {"kernels.hip": ["-ffp-contract=off"]}
 CFLAGS = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-I", os.path.join(ROOT, "include"),
           "-I", CSRC, "-Wno-unused-result"] + (["-DMPCC_IPM_PROF"] if PROF else [])
 
@@ -27,7 +31,7 @@ def _compile(src):
     if os.path.exists(obj) and os.path.getmtime(obj) >= max(os.path.getmtime(d) for d in deps):
         return obj
     lang = ["-x", "hip"] if src.endswith(".cpp") else []
-    cmd = [HIPCC] + CFLAGS + lang + ["-c", path, "-o", obj]
+    cmd = [HIPCC] + CFLAGS + lang + FILE_FLAGS.get(src, []) + ["-c", path, "-o", obj]
     r = subprocess.run(cmd, capture_output=True, text=True)
     if r.returncode != 0:
         raise RuntimeError(f"compile failed: {' '.join(cmd)}\n{r.stdout}\n{r.stderr}")

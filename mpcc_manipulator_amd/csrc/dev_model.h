@@ -245,7 +245,13 @@ __device__ inline void exp_skew(const double* v, double* E) {
 }
 
 // ---- regular cubic spline evaluation (cubic_spline.cpp:126-246, cubic_spline_rot.cpp:216-259) ----
-__device__ __forceinline__ double spl_unwrap(const SplineDev& sp, double x) { return fmax(0., fmin(x, sp.L)); }
+// unwrapInput (cubic_spline.cpp, arc_length_spline.cpp): std::max(0., std::min(x, L)) — comparison
+// semantics, so a NaN (0/0 Newton step at the track end, arc_length_spline.cpp:356-372) maps to 0,
+// where IEEE fmin/fmax would return L and end the projection there.
+__device__ __forceinline__ double spl_unwrap(const SplineDev& sp, double x) {
+    const double m = (sp.L < x) ? sp.L : x;
+    return (0. < m) ? m : 0.;
+}
 __device__ __forceinline__ int spl_index(const SplineDev& sp, double x) {
     if (x == sp.L) return sp.n - 1;
     return (int)floor(x / sp.delta);

@@ -85,6 +85,7 @@ struct mpcc_engine {
         auto f = [](void* p) { if (p) (void)hipFree(p); };
         f(d_spl);
         f(d.guess); f(d.valid); f(d.fails); f(d.rec); f(d.qs); f(d.is); f(d.step); f(d.trial); f(d.sqi); f(d.sqd);
+        f(d.dbg_trace);
         f(s_x0); f(s_u0); f(s_obs); f(s_u0out); f(s_hor); f(s_status); f(s_ok);
         f(nn_self.d); f(nn_env.d);
         for (auto ev : events) (void)hipEventDestroy(ev);
@@ -259,6 +260,7 @@ void run_batch(mpcc_engine* e, int B, hipStream_t st, mpcc_timing* timing) {
     std::vector<std::pair<int, int>> set_qp, solve_qp, get_alpha;
     int t0 = -1, t_env0 = -1, t_env1 = -1, t_end = -1;
     if (tm) t0 = mark();
+    if (d.dbg_trace) HIPCHK(hipMemsetAsync(d.dbg_trace, 0, sizeof(double) * B * TRACE_IT * TRACE_W, st));
     launch_prepare(c, d, st);
     if (tm) t_env0 = mark();
     launch_stage_records(c, d, st);
@@ -666,6 +668,28 @@ int mpcc_debug_robot_records(mpcc_engine* e, int M, const double* q, const doubl
     return MPCC_OK;
 }
 
+int mpcc_debug_project(mpcc_engine* e, int M, const double* s_guess, const double* ee, double* s_out) {
+    if (!e || M < 1 || !s_guess || !ee || !s_out) return fail(MPCC_E_INVALID, "mpcc_debug_project: invalid argument");
+    if (!e->has_track) return fail(MPCC_E_NOTRACK, "mpcc_debug_project: no track");
+    double *dg = nullptr, *de = nullptr, *dout = nullptr;
+    try {
+        dg = dmalloc<double>(M);
+        de = dmalloc<double>((size_t)M * 3);
+        dout = dmalloc<double>(M);
+        HIPCHK(hipMemcpy(dg, s_guess, M * sizeof(double), hipMemcpyHostToDevice));
+        HIPCHK(hipMemcpy(de, ee, (size_t)M * 3 * sizeof(double), hipMemcpyHostToDevice));
+        DevConst c = e->make_const(1);
+        launch_debug_project(c, M, dg, de, dout, e->stream);
+        HIPCHK(hipStreamSynchronize(e->stream));
+        HIPCHK(hipMemcpy(s_out, dout, M * sizeof(double), hipMemcpyDeviceToHost));
+    } catch (const std::exception& x) {
+        (void)hipFree(dg); (void)hipFree(de); (void)hipFree(dout);
+        return fail(MPCC_E_HIP, std::string("mpcc_debug_project: ") + x.what());
+    }
+    (void)hipFree(dg); (void)hipFree(de); (void)hipFree(dout);
+    return MPCC_OK;
+}
+
 int mpcc_debug_spline(mpcc_engine* e, int M, const double* s, double* pos, double* dd1, double* dd2, double* R, double* dR) {
     if (!e || M < 1 || !s) return fail(MPCC_E_INVALID, "mpcc_debug_spline: invalid argument");
     if (!e->has_track) return fail(MPCC_E_NOTRACK, "mpcc_debug_spline: no track");
@@ -782,3 +806,26 @@ int mpcc_debug_solve_qp(mpcc_engine* e, int B, const double* guess, const double
 }
 
 }  // extern "C"
+
+int mpcc_debug_trace_enable(mpcc_engine* e, int enable) {
+    if (!e) return fail(MPCC_E_INVALID, "mpcc_debug_trace_enable: null engine");
+    try {
+        if (enable && !e->d.dbg_trace) e->d.dbg_trace = dmalloc<double>((size_t)e->cfg.max_batch * TRACE_IT * TRACE_W);
+        if (!enable && e->d.dbg_trace) { HIPCHK(hipFree(e->d.dbg_trace)); e->d.dbg_trace = nullptr; }
+    } catch (const std::exception& x) {
+        return fail(MPCC_E_HIP, std::string("mpcc_debug_trace_enable: ") + x.what());
+    }
+    return MPCC_OK;
+}
+
+int mpcc_debug_trace_get(mpcc_engine* e, int B, double* out) {
+    if (!e || !out || B < 1 || B > e->cfg.max_batch || !e->d.dbg_trace)
+        return fail(MPCC_E_INVALID, "mpcc_debug_trace_get: invalid argument or trace disabled");
+    try {
+        HIPCHK(hipDeviceSynchronize());
+        HIPCHK(hipMemcpy(out, e->d.dbg_trace, sizeof(double) * B * TRACE_IT * TRACE_W, hipMemcpyDeviceToHost));
+    } catch (const std::exception& x) {
+        return fail(MPCC_E_HIP, std::string("mpcc_debug_trace_get: ") + x.what());
+    }
+    return MPCC_OK;
+}

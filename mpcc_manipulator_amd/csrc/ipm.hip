@@ -28,6 +28,7 @@ namespace mpcc {
 
 constexpr int IPM_MAX_IT = 60;
 constexpr double IPM_TOL_MU = 1e-13, IPM_TOL_P = 1e-11, IPM_TOL_STEP = 1e-11;
+constexpr double IPM_TOL_FB = 1e-9;  // P2: a converged iterate is accepted when the Riccati factor breaks down
 constexpr int IPW = 4;  // instances per wavefront (16 lanes each)
 
 // workspace fields, ws[((b*(N+1) + k)*IS + field*16 + lane]
@@ -191,7 +192,7 @@ __global__ void __launch_bounds__(64) k_ipm(DevConst c, DevBuffers d) {
     const int NS = N + 1;
     double* const S = smem + grp * grp_lds(NPM);
 #ifdef MPCC_IPM_PROF
-    long long prof_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    long long prof_acc[16] = {0};
     long long prof_t = clock64();
 #endif
 
@@ -251,7 +252,29 @@ __global__ void __launch_bounds__(64) k_ipm(DevConst c, DevBuffers d) {
     if (run && (fl & 4)) { if (t == 0) si[SQ_QPSTAT] = MPCC_QP_PrimalInfeasible; run = false; }  // keep old step (Q6)
     const bool entered = run;
 
-    // ---- per-stage read-only data: row bounds, poly rows (staged into LDS)
+    // ---- per-stage inputs, loaded one stage ahead of their use (software pipelining of the sweeps)
+    struct StageIn {
+        double lb, ub;          // bounds of row t
+        int np;                 // live poly rows
+        double pv[PFP > 0 ? PFP : 1];
+        double sL, lL, sU, lU, sP, lP, zx, zv;
+        double x0, x1, x2, x3;  // sweep-specific pairs (dz / dza / g0)
+        double m[12];           // sweep-specific: Q row + q,R,r | K rows + kff | K column + Finv half
+    };
+    auto load_common = [&](int k, StageIn& o) {
+        const double* q = QSb + (size_t)k * QS;
+        o.lb = q[rowY ? QS_YLB + t : QS_DLB + j9];
+        o.ub = q[rowY ? QS_YUB + t : QS_DUB + j9];
+        o.np = (int)q[QS_NPOLY];
+#pragma unroll
+        for (int i = 0; i < PFP; i++) {
+            const int e = t + 16 * i;
+            o.pv[i] = (e < 15 * NPM) ? q[QS_POLY + e] : 0.0;
+        }
+        o.sL = *ws(k, WF_SL); o.lL = *ws(k, WF_LL); o.sU = *ws(k, WF_SU); o.lU = *ws(k, WF_LU);
+        o.sP = *ws(k, WF_SP); o.lP = *ws(k, WF_LP);
+        o.zx = *ws(k, WF_ZX); o.zv = *ws(k, WF_ZV);
+    };
     auto load_bounds = [&](int k, double& lb, double& ub, int& np) {
         const double* q = QSb + (size_t)k * QS;
         lb = q[rowY ? QS_YLB + t : QS_DLB + j9];
@@ -300,19 +323,64 @@ __global__ void __launch_bounds__(64) k_ipm(DevConst c, DevBuffers d) {
         S[off + t] = x;
         if (t < 8) S[off + 16 + t] = v;
     };
-    double pvr[PFP > 0 ? PFP : 1];
+    auto load_factor = [&](int k, StageIn& o, bool upd) {
+        load_common(k, o);
+        const double* q = QSb + (size_t)k * QS;
+#pragma unroll
+        for (int m = 0; m < 9; m++) o.m[m] = (t < 9) ? q[QS_Q + t * 9 + m] : 0.0;
+        o.m[9] = (t < 9) ? q[QS_q + t] : 0.0;
+        o.m[10] = (t < 8 && k < N) ? q[QS_R + t] : 0.0;
+        o.m[11] = (t < 8 && k < N) ? q[QS_r + t] : 0.0;
+        if (upd) {
+            o.x0 = *ws(k, WF_DX); o.x1 = *ws(k, WF_DV); o.x2 = *ws(k, WF_AX); o.x3 = *ws(k, WF_AV);
+        } else {
+            o.x0 = o.x1 = o.x2 = o.x3 = 0.0;
+        }
+    };
+    auto load_fwd = [&](int k, StageIn& o, bool corr) {
+        load_common(k, o);
+        if (k < N) {
+#pragma unroll
+            for (int m = 0; m < 8; m++) o.m[m] = *ws(k, WF_KR + m);
+            o.m[8] = *ws(k, WF_KFF);
+        } else {
+#pragma unroll
+            for (int m = 0; m < 9; m++) o.m[m] = 0.0;
+        }
+        if (corr) { o.x0 = *ws(k, WF_AX); o.x1 = *ws(k, WF_AV); } else { o.x0 = o.x1 = 0.0; }
+    };
+    auto load_bwd = [&](int k, StageIn& o) {
+        load_common(k, o);
+        o.x0 = *ws(k, WF_AX); o.x1 = *ws(k, WF_AV); o.x2 = *ws(k, WF_GX); o.x3 = *ws(k, WF_GV);
+        if (k < N) {
+#pragma unroll
+            for (int i = 0; i < 8; i++) o.m[i] = *ws(k, WF_KC + i);
+#pragma unroll
+            for (int m = 0; m < 4; m++) o.m[8 + m] = *ws(k, WF_FI + m);
+        } else {
+#pragma unroll
+            for (int m = 0; m < 12; m++) o.m[m] = 0.0;
+        }
+    };
 
     // ---- start point: dynamics rollout with v = 0, s = max(-g, 1), lambda = 1
     double mcount = 0.0;
     if (run) {
         double y = 0.0;  // lane a < 9: y_a of stage k
+        double lb, ub, bk; int np;
+        double pv[PFP > 0 ? PFP : 1];
+        auto load_start = [&](int k, double& lb_, double& ub_, int& np_, double* pv_, double& bk_) {
+            load_bounds(k, lb_, ub_, np_);
+            load_poly(k, pv_);
+            bk_ = (k < N && t < 9) ? QSb[(size_t)k * QS + QS_B + t] : 0.0;
+        };
+        load_start(0, lb, ub, np, pv, bk);
         for (int k = 0; k <= N; k++) {
-            double lb, ub; int np;
-            load_bounds(k, lb, ub, np);
-            load_poly(k, pvr);
-            const double bk = (k < N && t < 9) ? QSb[(size_t)k * QS + QS_B + t] : 0.0;
+            double lbn = 0, ubn = 0, bkn = 0; int npn = 0;
+            double pvn[PFP > 0 ? PFP : 1];
+            if (k < N) load_start(k + 1, lbn, ubn, npn, pvn, bkn);
             put_vec(L_Z, rowY ? y : 0.0, 0.0);
-            const double pb = stage_poly(pvr, np, k);
+            const double pb = stage_poly(pv, np, k);
             const double cz = row_cz(k, L_Z);
             const double pcz = poly_cz(L_Z);
             const bool aL = row_active(k, lb), aU = row_active(k, ub), aP = fabs(pb) < BIG;
@@ -329,6 +397,9 @@ __global__ void __launch_bounds__(64) k_ipm(DevConst c, DevBuffers d) {
             const double y8 = from_up<1>(y);  // lane 7 <- y_8
             const double yn = (t == 7) ? m77 * y + m78 * y8 : mt * y;
             y = (t < 9) ? yn + bk : 0.0;
+            lb = lbn; ub = ubn; np = npn; bk = bkn;
+#pragma unroll
+            for (int i = 0; i < PFP; i++) pv[i] = pvn[i];
             lds_sync();
         }
     }
@@ -338,7 +409,9 @@ __global__ void __launch_bounds__(64) k_ipm(DevConst c, DevBuffers d) {
     int it = 0;
     bool conv = false;
     double alpha = 0.0, sigma_mu = 0.0;  // previous iteration's step length and sigma*mu (lazy update)
+    double mu_cur = 1e30, rp_cur = 1e30; // mu and max |rp| of the current iterate (known for it > 0)
     bool pending = false;
+    StageIn cur, nxt;
     while (true) {
         if (__ballot(run) == 0) break;
         if (run) {
@@ -346,26 +419,20 @@ __global__ void __launch_bounds__(64) k_ipm(DevConst c, DevBuffers d) {
             // the objective gradient g0 = H z + h and the predictor backward solve
             int pcur = 0;  // p ping-pong slot holding p_{k+1}
             bool chol_ok = true;
+            load_factor(N, cur, pending);
+            PMARK(1);
             for (int k = N; k >= 0; k--) {
-                const double* q = QSb + (size_t)k * QS;
-                double lb, ub; int np;
-                load_bounds(k, lb, ub, np);
-                load_poly(k, pvr);
-                double sL = *ws(k, WF_SL), lL = *ws(k, WF_LL), sU = *ws(k, WF_SU), lU = *ws(k, WF_LU);
-                double sP = *ws(k, WF_SP), lP = *ws(k, WF_LP);
-                double zx = *ws(k, WF_ZX), zv = *ws(k, WF_ZV);
-                double Qr[9];
-#pragma unroll
-                for (int m = 0; m < 9; m++) Qr[m] = (t < 9) ? q[QS_Q + t * 9 + m] : 0.0;
-                const double qt = (t < 9) ? q[QS_q + t] : 0.0;
-                const double Rt = (t < 8 && k < N) ? q[QS_R + t] : 0.0;
-                const double rt = (t < 8 && k < N) ? q[QS_r + t] : 0.0;
-                const double pb = stage_poly(pvr, np, k);
+                if (k > 0) load_factor(k - 1, nxt, pending);
+                const double lb = cur.lb, ub = cur.ub;
+                const double* Qr = cur.m;
+                const double qt = cur.m[9], Rt = cur.m[10], rt = cur.m[11];
+                double sL = cur.sL, lL = cur.lL, sU = cur.sU, lU = cur.lU, sP = cur.sP, lP = cur.lP;
+                double zx = cur.zx, zv = cur.zv;
+                const double pb = stage_poly(cur.pv, cur.np, k);
                 const bool aL = row_active(k, lb), aU = row_active(k, ub), aP = fabs(pb) < BIG;
                 if (pending) {
                     // previous iteration's update at this stage (oracle: z += a dz, s += a ds, l += a dl)
-                    const double dx = *ws(k, WF_DX), dv = *ws(k, WF_DV);
-                    const double ax = *ws(k, WF_AX), av = *ws(k, WF_AV);
+                    const double dx = cur.x0, dv = cur.x1, ax = cur.x2, av = cur.x3;
                     put_vec(L_Z, zx, zv); put_vec(L_DZ, dx, dv); put_vec(L_DA, ax, av);
                     lds_sync();
                     const double cz = row_cz(k, L_Z), cd = row_cz(k, L_DZ), ca = row_cz(k, L_DA);
@@ -381,6 +448,7 @@ __global__ void __launch_bounds__(64) k_ipm(DevConst c, DevBuffers d) {
                     *ws(k, WF_ZX) = zx; *ws(k, WF_ZV) = zv;
                     lds_sync();
                 }
+                PMARK(8);
                 put_vec(L_Z, zx, zv);
                 lds_sync();
                 // ---- slots: barrier weights and predictor coefficients (rc = s l)
@@ -442,8 +510,10 @@ __global__ void __launch_bounds__(64) k_ipm(DevConst c, DevBuffers d) {
                     S[L_PV + t] = gx;
                     pcur = 0;
                     lds_sync();
+                    cur = nxt;
                     continue;
                 }
+                PMARK(9);
                 // ---- (1) Y = B~^T P (lane n: column n of Y from column n of P), f = g_v + B~^T p
                 double Pc[16];
 #pragma unroll
@@ -528,6 +598,7 @@ __global__ void __launch_bounds__(64) k_ipm(DevConst c, DevBuffers d) {
                     }
                 }
                 lds_sync();
+                PMARK(10);
                 // ---- (3) chol(F); U = LF^-1 Gm; K = -LF^-T U; Finv column (t & 7); kff = -F^-1 f;
                 //          p = g_x~ + A~^T p + K^T f
                 double LF[36], dinv[8];
@@ -565,6 +636,7 @@ __global__ void __launch_bounds__(64) k_ipm(DevConst c, DevBuffers d) {
                     for (int i = 0; i < 8; i++) ktf += kc[i] * f[i];
                     S[L_PV + 16 * (pcur ^ 1) + t] = gx + atp + ktf;
                 }
+                PMARK(11);
 #pragma unroll
                 for (int i = 0; i < 8; i++) {
                     S[L_U + i * 16 + t] = u[i];
@@ -580,6 +652,7 @@ __global__ void __launch_bounds__(64) k_ipm(DevConst c, DevBuffers d) {
 #pragma unroll
                     for (int m = 0; m < 8; m++) *ws(k, WF_KR + m) = S[L_K + ri * 16 + hoff + m];
                 }
+                PMARK(12);
                 // ---- (4) P = Hb - U^T U (lane = row t, upper triangle mirrored)
                 if (k > 0) {
 #pragma unroll
@@ -587,7 +660,7 @@ __global__ void __launch_bounds__(64) k_ipm(DevConst c, DevBuffers d) {
                         if (cc < t) continue;
                         double v = 0.0;
                         if (t < 9 && cc < 9) v = Hb[cc];
-                        else if (t >= 9 && cc == t && k >= 1) v = wd;
+                        else if (t >= 9 && cc == t) v = wd;
 #pragma unroll
                         for (int i = 0; i < 8; i++) v -= u[i] * S[L_U + i * 16 + cc];
                         S[L_P + t * 16 + cc] = v;
@@ -596,41 +669,31 @@ __global__ void __launch_bounds__(64) k_ipm(DevConst c, DevBuffers d) {
                 }
                 pcur ^= 1;
                 lds_sync();
+                cur = nxt;
+                PMARK(13);
             }
-            if (!chol_ok) run = false;  // oracle: factorization failure ends the loop -> MaxIterReached
+            if (!chol_ok) {
+                // Riccati breakdown: MaxIterReached unless the current iterate is converged to IPM_TOL_FB (P2);
+                // the sweep has already applied the pending update, so the iterate is the stored z
+                conv = it > 0 && mu_cur < IPM_TOL_FB && rp_cur < IPM_TOL_FB;
+                alpha = 0.0;
+                run = false;
+            }
         }
         PMARK(2);
         if (run) {
-            // ---- predictor forward: x~_0 = 0; v = K x~ + kff; x~' = A~ x~ + B~ v; recover dsa, dla
-            double S0 = 0, S1 = 0, S2 = 0, amax = 1.0;
-            int xc = 0;
-            S[L_X + t] = 0.0;
-            lds_sync();
-            for (int k = 0; k <= N; k++) {
-                double lb, ub; int np;
-                load_bounds(k, lb, ub, np);
-                load_poly(k, pvr);
-                const double sL = *ws(k, WF_SL), lL = *ws(k, WF_LL), sU = *ws(k, WF_SU), lU = *ws(k, WF_LU);
-                const double sP = *ws(k, WF_SP), lP = *ws(k, WF_LP);
-                const double zx = *ws(k, WF_ZX), zv = *ws(k, WF_ZV);
-                double kr[8];
-                double kff = 0.0;
-                if (k < N) {
-#pragma unroll
-                    for (int m = 0; m < 8; m++) kr[m] = *ws(k, WF_KR + m);
-                    kff = *ws(k, WF_KFF);
-                }
-                const double pb = stage_poly(pvr, np, k);
-                const bool aL = row_active(k, lb), aU = row_active(k, ub), aP = fabs(pb) < BIG;
+            // forward sweep body shared by the predictor and the corrector:
+            // x~_0 = 0; v = K x~ + kff; x~' = A~ x~ + B~ v; returns (x~_k, v_k) of stage k
+            auto fwd_step = [&](int k, const StageIn& in, int xc, double& xt, double& vv) {
                 const double* xs = S + L_X + 16 * xc;
-                const double xt = xs[t];
+                xt = xs[t];
                 double v = 0.0;
                 if (k < N) {
                     const int hoff = (t < 8) ? 0 : 8;
                     double part = 0.0;
 #pragma unroll
-                    for (int m = 0; m < 8; m++) part += kr[m] * xs[hoff + m];
-                    v = part + from_up<8>(part) + kff;
+                    for (int m = 0; m < 8; m++) part += in.m[m] * xs[hoff + m];
+                    v = part + from_up<8>(part) + in.m[8];
                     const double x8 = xs[8];
                     const double v7 = from_down<1>(v);
                     const double vj = from_down<9>(v);
@@ -641,10 +704,23 @@ __global__ void __launch_bounds__(64) k_ipm(DevConst c, DevBuffers d) {
                     else xn = vj;
                     S[L_X + 16 * (xc ^ 1) + t] = xn;
                 }
-                const double dvv = (t < 8 && k < N) ? v : 0.0;
+                vv = (t < 8 && k < N) ? v : 0.0;
+            };
+            // ---- predictor forward: recover dsa, dla; max step; mu(alpha) sums
+            double S0 = 0, S1 = 0, S2 = 0, amax = 1.0;
+            int xc = 0;
+            S[L_X + t] = 0.0;
+            load_fwd(0, cur, false);
+            lds_sync();
+            for (int k = 0; k <= N; k++) {
+                if (k < N) load_fwd(k + 1, nxt, false);
+                const double pb = stage_poly(cur.pv, cur.np, k);
+                const bool aL = row_active(k, cur.lb), aU = row_active(k, cur.ub), aP = fabs(pb) < BIG;
+                double xt, dvv;
+                fwd_step(k, cur, xc, xt, dvv);
                 *ws(k, WF_AX) = xt;
                 *ws(k, WF_AV) = dvv;
-                put_vec(L_Z, zx, zv);
+                put_vec(L_Z, cur.zx, cur.zv);
                 put_vec(L_DA, xt, dvv);
                 lds_sync();
                 const double cz = row_cz(k, L_Z), ca = row_cz(k, L_DA);
@@ -658,11 +734,12 @@ __global__ void __launch_bounds__(64) k_ipm(DevConst c, DevBuffers d) {
                     S1 += s * st.dl + l * st.ds;
                     S2 += st.ds * st.dl;
                 };
-                rec(aL, sgnL, lb, cz, ca, sL, lL);
-                rec(aU, sgnU, ub, cz, ca, sU, lU);
-                rec(aP, sgnU, pb, pcz, pca, sP, lP);
+                rec(aL, sgnL, cur.lb, cz, ca, cur.sL, cur.lL);
+                rec(aU, sgnU, cur.ub, cz, ca, cur.sU, cur.lU);
+                rec(aP, sgnU, pb, pcz, pca, cur.sP, cur.lP);
                 xc ^= 1;
                 lds_sync();
+                cur = nxt;
             }
             amax = g_min(amax);
             S0 = g_sum(S0); S1 = g_sum(S1); S2 = g_sum(S2);
@@ -677,26 +754,13 @@ __global__ void __launch_bounds__(64) k_ipm(DevConst c, DevBuffers d) {
             // ---- corrector backward: coef with rc = s l + dsa dla - sigma mu; f = g_v + B~^T p;
             //      kff = -F^-1 f; p = g_x~ + A~^T p + K^T f
             int pcur = 0;
+            load_bwd(N, cur);
             for (int k = N; k >= 0; k--) {
-                double lb, ub; int np;
-                load_bounds(k, lb, ub, np);
-                load_poly(k, pvr);
-                const double sL = *ws(k, WF_SL), lL = *ws(k, WF_LL), sU = *ws(k, WF_SU), lU = *ws(k, WF_LU);
-                const double sP = *ws(k, WF_SP), lP = *ws(k, WF_LP);
-                const double zx = *ws(k, WF_ZX), zv = *ws(k, WF_ZV);
-                const double ax = *ws(k, WF_AX), av = *ws(k, WF_AV);
-                const double g0x = *ws(k, WF_GX), g0v = *ws(k, WF_GV);
-                double kc[8], fir[4];
-                if (k < N) {
-#pragma unroll
-                    for (int i = 0; i < 8; i++) kc[i] = *ws(k, WF_KC + i);
-#pragma unroll
-                    for (int m = 0; m < 4; m++) fir[m] = *ws(k, WF_FI + m);
-                }
-                const double pb = stage_poly(pvr, np, k);
-                const bool aL = row_active(k, lb), aU = row_active(k, ub), aP = fabs(pb) < BIG;
-                put_vec(L_Z, zx, zv);
-                put_vec(L_DA, ax, av);
+                if (k > 0) load_bwd(k - 1, nxt);
+                const double pb = stage_poly(cur.pv, cur.np, k);
+                const bool aL = row_active(k, cur.lb), aU = row_active(k, cur.ub), aP = fabs(pb) < BIG;
+                put_vec(L_Z, cur.zx, cur.zv);
+                put_vec(L_DA, cur.x0, cur.x1);
                 lds_sync();
                 const double cz = row_cz(k, L_Z), ca = row_cz(k, L_DA);
                 const double pcz = poly_cz(L_Z), pca = poly_cz(L_DA);
@@ -707,13 +771,13 @@ __global__ void __launch_bounds__(64) k_ipm(DevConst c, DevBuffers d) {
                     const double rc = s * l + pa.ds * pa.dl - smu;
                     return slot_coef(s, l, rp, rc);
                 };
-                const double cL = coef(aL, sgnL, lb, cz, ca, sL, lL);
-                const double cU = coef(aU, sgnU, ub, cz, ca, sU, lU);
-                const double cP = coef(aP, sgnU, pb, pcz, pca, sP, lP);
+                const double cL = coef(aL, sgnL, cur.lb, cz, ca, cur.sL, cur.lL);
+                const double cU = coef(aU, sgnU, cur.ub, cz, ca, cur.sU, cur.lU);
+                const double cP = coef(aP, sgnU, pb, pcz, pca, cur.sP, cur.lP);
                 const double dvr = sgnL * cL + sgnU * cU;
                 S[L_PC + t] = cP;
                 lds_sync();
-                double gx = g0x, gv = g0v;
+                double gx = cur.x2, gv = cur.x3;
                 if (t < 9) {
                     gx += dvr;
                     if (t < 7)
@@ -732,6 +796,7 @@ __global__ void __launch_bounds__(64) k_ipm(DevConst c, DevBuffers d) {
                     S[L_PV + t] = gx;
                     pcur = 0;
                     lds_sync();
+                    cur = nxt;
                     continue;
                 }
                 const double* pn = S + L_PV + 16 * pcur;
@@ -746,7 +811,7 @@ __global__ void __launch_bounds__(64) k_ipm(DevConst c, DevBuffers d) {
                 const int hoff = (t < 8) ? 0 : 4;
                 double part = 0.0;
 #pragma unroll
-                for (int m = 0; m < 4; m++) part -= fir[m] * f[hoff + m];
+                for (int m = 0; m < 4; m++) part -= cur.m[8 + m] * f[hoff + m];
                 const double kff = part + from_up<8>(part);
                 *ws(k, WF_KFF) = (t < 8) ? kff : 0.0;
                 if (k > 0) {
@@ -757,11 +822,12 @@ __global__ void __launch_bounds__(64) k_ipm(DevConst c, DevBuffers d) {
                     }
                     double ktf = 0.0;
 #pragma unroll
-                    for (int i = 0; i < 8; i++) ktf += kc[i] * f[i];
+                    for (int i = 0; i < 8; i++) ktf += cur.m[i] * f[i];
                     S[L_PV + 16 * (pcur ^ 1) + t] = gx + atp + ktf;
                 }
                 pcur ^= 1;
                 lds_sync();
+                cur = nxt;
             }
             PMARK(4);
 
@@ -769,50 +835,20 @@ __global__ void __launch_bounds__(64) k_ipm(DevConst c, DevBuffers d) {
             double T0 = 0, T1 = 0, T2 = 0, amx = 1e30, rpm = 0, dzm = 0;
             xc = 0;
             S[L_X + t] = 0.0;
+            load_fwd(0, cur, true);
             lds_sync();
             for (int k = 0; k <= N; k++) {
-                double lb, ub; int np;
-                load_bounds(k, lb, ub, np);
-                load_poly(k, pvr);
-                const double sL = *ws(k, WF_SL), lL = *ws(k, WF_LL), sU = *ws(k, WF_SU), lU = *ws(k, WF_LU);
-                const double sP = *ws(k, WF_SP), lP = *ws(k, WF_LP);
-                const double zx = *ws(k, WF_ZX), zv = *ws(k, WF_ZV);
-                const double ax = *ws(k, WF_AX), av = *ws(k, WF_AV);
-                double kr[8];
-                double kff = 0.0;
-                if (k < N) {
-#pragma unroll
-                    for (int m = 0; m < 8; m++) kr[m] = *ws(k, WF_KR + m);
-                    kff = *ws(k, WF_KFF);
-                }
-                const double pb = stage_poly(pvr, np, k);
-                const bool aL = row_active(k, lb), aU = row_active(k, ub), aP = fabs(pb) < BIG;
-                const double* xs = S + L_X + 16 * xc;
-                const double xt = xs[t];
-                double v = 0.0;
-                if (k < N) {
-                    const int hoff = (t < 8) ? 0 : 8;
-                    double part = 0.0;
-#pragma unroll
-                    for (int m = 0; m < 8; m++) part += kr[m] * xs[hoff + m];
-                    v = part + from_up<8>(part) + kff;
-                    const double x8 = xs[8];
-                    const double v7 = from_down<1>(v);
-                    const double vj = from_down<9>(v);
-                    double xn;
-                    if (t < 7) xn = mt * xt + gt * v;
-                    else if (t == 7) xn = (m77 * xt + m78 * x8) + g77 * v;
-                    else if (t == 8) xn = m88 * xt + g87 * v7;
-                    else xn = vj;
-                    S[L_X + 16 * (xc ^ 1) + t] = xn;
-                }
-                const double dvv = (t < 8 && k < N) ? v : 0.0;
+                if (k < N) load_fwd(k + 1, nxt, true);
+                const double pb = stage_poly(cur.pv, cur.np, k);
+                const bool aL = row_active(k, cur.lb), aU = row_active(k, cur.ub), aP = fabs(pb) < BIG;
+                double xt, dvv;
+                fwd_step(k, cur, xc, xt, dvv);
                 *ws(k, WF_DX) = xt;
                 *ws(k, WF_DV) = dvv;
                 dzm = fmax(dzm, fmax(fabs(xt), fabs(dvv)));
-                put_vec(L_Z, zx, zv);
+                put_vec(L_Z, cur.zx, cur.zv);
                 put_vec(L_DZ, xt, dvv);
-                put_vec(L_DA, ax, av);
+                put_vec(L_DA, cur.x0, cur.x1);
                 lds_sync();
                 const double cz = row_cz(k, L_Z), cd = row_cz(k, L_DZ), ca = row_cz(k, L_DA);
                 const double pcz = poly_cz(L_Z), pcd = poly_cz(L_DZ), pca = poly_cz(L_DA);
@@ -826,11 +862,12 @@ __global__ void __launch_bounds__(64) k_ipm(DevConst c, DevBuffers d) {
                     T2 += st.ds * st.dl;
                     rpm = fmax(rpm, fabs(rp));
                 };
-                rec(aL, sgnL, lb, cz, ca, cd, sL, lL);
-                rec(aU, sgnU, ub, cz, ca, cd, sU, lU);
-                rec(aP, sgnU, pb, pcz, pca, pcd, sP, lP);
+                rec(aL, sgnL, cur.lb, cz, ca, cd, cur.sL, cur.lL);
+                rec(aU, sgnU, cur.ub, cz, ca, cd, cur.sU, cur.lU);
+                rec(aP, sgnU, pb, pcz, pca, pcd, cur.sP, cur.lP);
                 xc ^= 1;
                 lds_sync();
+                cur = nxt;
             }
             amx = g_min(amx);
             T0 = g_sum(T0); T1 = g_sum(T1); T2 = g_sum(T2);
@@ -846,6 +883,8 @@ __global__ void __launch_bounds__(64) k_ipm(DevConst c, DevBuffers d) {
                 double mun = T0 + alpha * T1 + alpha * alpha * T2;
                 mun = (mcount > 0) ? mun / mcount : 0.0;
                 const double rpn = (1.0 - alpha) * rpm;
+                mu_cur = mun;
+                rp_cur = rpn;
                 if (mun < IPM_TOL_MU && rpn < IPM_TOL_P && dzm < IPM_TOL_STEP) {
                     conv = true;
                     run = false;
@@ -858,7 +897,7 @@ __global__ void __launch_bounds__(64) k_ipm(DevConst c, DevBuffers d) {
 
 #ifdef MPCC_IPM_PROF
     if (entered && t == 0) {
-        for (int i = 0; i < 6; i++) atomicAdd(&g_ipm_prof[i], (unsigned long long)prof_acc[i]);
+        for (int i = 0; i < 16; i++) if (i != 6 && i != 7) atomicAdd(&g_ipm_prof[i], (unsigned long long)prof_acc[i]);
         atomicAdd(&g_ipm_prof[6], (unsigned long long)it);
         atomicAdd(&g_ipm_prof[7], 1ull);
     }

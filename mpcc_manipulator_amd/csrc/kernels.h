@@ -30,7 +30,10 @@ struct DevBuffers {
     // NN weights (device)
     const double* nn_self;  // packed W0,b0,W1,b1,W2,b2
     const double* nn_env;   // packed W0,b0,...,W4,b4
+    // debug: per-instance SQP trace (null unless mpcc_debug_trace_enable), TRACE_W doubles per iteration
+    double* dbg_trace;
 };
+constexpr int TRACE_W = 8, TRACE_IT = 4;  // qp status, ipm iters, obj, vio, accepted, |step|_inf, alpha, alpha*|step|
 
 constexpr int SQI = 8;  // int bookkeeping per instance: status, active, iter, nfilt, qp_status, ipm_iters, reject
 constexpr int SQ_REJECT = 6;
@@ -59,6 +62,7 @@ void launch_finalize(const DevConst& c, const DevBuffers& d, hipStream_t s);
 void launch_sim_step(int B, const double* x, const double* u, double ts, double* xn, hipStream_t s);
 void launch_debug_records(const DevConst& c, int M, const double* q, const double* obs, double* rec, hipStream_t s);
 void launch_debug_spline(const DevConst& c, int M, const double* sv, double* out, hipStream_t s);
+void launch_debug_project(const DevConst& c, int M, const double* sg, const double* ee, double* out, hipStream_t s);
 void launch_debug_cost(const DevConst& c, int M, const double* x, const double* u, const double* rec, const int32_t* k,
                        double* out, hipStream_t s);
 

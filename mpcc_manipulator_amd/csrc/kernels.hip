@@ -502,6 +502,10 @@ __global__ void __launch_bounds__(64) k_accept(DevConst c, DevBuffers d) {
     }
     sd[SQ_ALPHA] = alpha;
     si[SQ_REJECT] = accepted ? 0 : 1;
+    if (d.dbg_trace && si[SQ_ITER] < TRACE_IT) {
+        double* tr = d.dbg_trace + ((size_t)b * TRACE_IT + si[SQ_ITER]) * TRACE_W;
+        tr[0] = si[SQ_QPSTAT]; tr[1] = si[SQ_IPMIT]; tr[2] = obj; tr[3] = vio; tr[4] = accepted ? 1 : 0;
+    }
 }
 
 // take step (osqp_interface.cpp:549-573): guess += alpha * deNormalizeStep(step); termination test
@@ -530,6 +534,10 @@ __global__ void __launch_bounds__(64) k_apply(DevConst c, DevBuffers d) {
     }
     const double pn = alpha * nrm;
     int iter = si[SQ_ITER];
+    if (d.dbg_trace && iter < TRACE_IT) {
+        double* tr = d.dbg_trace + ((size_t)b * TRACE_IT + iter) * TRACE_W;
+        tr[5] = nrm; tr[6] = alpha; tr[7] = pn;
+    }
     if (pn < p.eps_prim) {
         si[SQ_STATUS] = MPCC_SOLVED;
         si[SQ_ACTIVE] = 0;
@@ -634,6 +642,13 @@ __global__ void k_debug_spline(DevConst c, int M, const double* __restrict__ sv,
     spline_rot(c.spl, sv[t], o + 9, o + 18);
 }
 
+__global__ void k_debug_project(DevConst c, int M, const double* __restrict__ sg, const double* __restrict__ ee,
+                                double* __restrict__ out) {
+    const int t = blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= M) return;
+    out[t] = project_on_spline(c.spl, c.p.proj_max_dist, sg[t], ee + 3 * t);
+}
+
 __global__ void k_debug_cost(DevConst c, int M, const double* __restrict__ x, const double* __restrict__ u,
                              const double* __restrict__ rec, const int32_t* __restrict__ kk, double* __restrict__ out) {
     const int t = blockIdx.x * blockDim.x + threadIdx.x;
@@ -681,6 +696,9 @@ void launch_finalize(const DevConst& c, const DevBuffers& d, hipStream_t s) {
 }
 void launch_sim_step(int B, const double* x, const double* u, double ts, double* xn, hipStream_t s) {
     hipLaunchKernelGGL(k_sim_step, dim3(nblk(B, 64)), dim3(64), 0, s, B, x, u, ts, xn);
+}
+void launch_debug_project(const DevConst& c, int M, const double* sg, const double* ee, double* out, hipStream_t s) {
+    hipLaunchKernelGGL(k_debug_project, dim3(nblk(M, 64)), dim3(64), 0, s, c, M, sg, ee, out);
 }
 void launch_debug_spline(const DevConst& c, int M, const double* sv, double* out, hipStream_t s) {
     hipLaunchKernelGGL(k_debug_spline, dim3(nblk(M, 64)), dim3(64), 0, s, c, M, sv, out);

@@ -118,6 +118,9 @@ def lib():
         "mpcc_debug_spline": (C.c_int, [V, C.c_int, DP, DP, DP, DP, DP, DP]),
         "mpcc_debug_stage_cost": (C.c_int, [V, C.c_int, DP, DP, DP, IP, DP, DP, DP, DP, DP]),
         "mpcc_debug_solve_qp": (C.c_int, [V, C.c_int, DP, DP, DP, DP, IP, IP]),
+        "mpcc_debug_trace_enable": (C.c_int, [V, C.c_int]),
+        "mpcc_debug_project": (C.c_int, [V, C.c_int, DP, DP, DP]),
+        "mpcc_debug_trace_get": (C.c_int, [V, C.c_int, DP]),
     }
     for name, (res, args) in sig.items():
         f = getattr(L, name)
@@ -410,3 +413,22 @@ class Engine:
         _check(self.L.mpcc_debug_solve_qp(self.h, B, _dp(g), _dp(r), _dp(u), _dp(step), _ip(st), _ip(it)),
                "mpcc_debug_solve_qp")
         return step, st, it
+
+    def project(self, s_guess, ee):
+        """projectOnSpline for M (s_guess, ee) pairs (arc_length_spline.cpp:318-379)."""
+        sg = _f64(np.atleast_1d(s_guess))
+        M = sg.shape[0]
+        e = _f64(ee, (M, 3))
+        out = np.zeros(M)
+        _check(self.L.mpcc_debug_project(self.h, M, _dp(sg), _dp(e), _dp(out)), "mpcc_debug_project")
+        return out
+
+    def trace_enable(self, on=True):
+        """Record per-SQP-iteration decisions of the next solves (test instrumentation)."""
+        _check(self.L.mpcc_debug_trace_enable(self.h, 1 if on else 0), "mpcc_debug_trace_enable")
+
+    def trace_get(self, B):
+        """[B, 4, 8]: qp status, ipm iters, trial obj, trial vio, accepted, |step|_inf, alpha, alpha*|step|_inf."""
+        out = np.zeros((B, 4, 8))
+        _check(self.L.mpcc_debug_trace_get(self.h, B, _dp(out)), "mpcc_debug_trace_get")
+        return out

@@ -1086,6 +1086,7 @@ static double constraint_norm(const DenseQP& q, double floor_) {
 constexpr double BIG = 1e20;  // |bound| >= BIG is treated as infinite (OSQP_INFTY semantics)
 constexpr int IPM_MAX_IT = 60;
 constexpr double IPM_TOL_MU = 1e-13, IPM_TOL_P = 1e-11, IPM_TOL_STEP = 1e-11;
+constexpr double IPM_TOL_FB = 1e-9;  // P2: accept a converged iterate when the Riccati factor breaks down
 constexpr double FEAS_TOL = 1e-9;
 
 // ---------------- stage-structured primal-dual IPM with a Riccati factorization ----------------
@@ -1445,7 +1446,12 @@ static int solve_struct_ipm(const StructQP& S, std::vector<double>& step, int* i
                 for (int b = 0; b < NZ; b++) H[a * NZ + b] += W[i] * row.c[a] * row.c[b];
             }
         }
-        if (!R.factor(S, Hs)) break;
+        if (!R.factor(S, Hs)) {
+            // Riccati breakdown (chol(F) loses definiteness at extreme barrier weights near the end of the
+            // solve): an iterate that is already converged to IPM_TOL_FB is the QP solution
+            if (it > 0 && mu < IPM_TOL_FB && rpmax < IPM_TOL_FB) conv = true;
+            break;
+        }
         std::vector<double> g0 = gs;
         auto add_rows = [&](std::vector<double>& g, const std::vector<double>& coef) {
             for (int i = 0; i < m; i++) {
@@ -1640,6 +1646,10 @@ static void denorm_add(const Oracle& o, const double* base, const std::vector<do
     }
 }
 
+// optional per-instance SQP trace (test instrumentation): 4 iterations x 8 doubles, same fields as
+// the engine's mpcc_debug_trace_get
+static thread_local double* g_trace = nullptr;
+
 static int solve_ocp(const Oracle& o, double* guess, const double* recs, const double* ucur, double* opt_sol, int* iters_out) {
     const OracleParams& p = o.p;
     const int N = p.N;
@@ -1676,7 +1686,9 @@ static int solve_ocp(const Oracle& o, double* guess, const double* recs, const d
             if (!pd) { status = NON_PD_HESSIAN; status_set = true; break; }
             if (nan) { status = NAN_HESSIAN; status_set = true; break; }
             std::vector<double> st;
-            int qs = solve_dense_ipm(q, st, nullptr);
+            int qit = 0;
+            int qs = solve_dense_ipm(q, st, &qit);
+            if (g_trace && it < 4) { g_trace[8 * it] = qs; g_trace[8 * it + 1] = qit; }
             if (qs == 0) step = st; else { status = qs; status_set = true; }  // Q6: keep old step
         } else {
             StructQP S;
@@ -1713,7 +1725,9 @@ static int solve_ocp(const Oracle& o, double* guess, const double* recs, const d
             if (!pd) { status = NON_PD_HESSIAN; status_set = true; break; }
             if (nan) { status = NAN_HESSIAN; status_set = true; break; }
             std::vector<double> st;
-            int qs = solve_struct_ipm(S, st, nullptr);
+            int qit = 0;
+            int qs = solve_struct_ipm(S, st, &qit);
+            if (g_trace && it < 4) { g_trace[8 * it] = qs; g_trace[8 * it + 1] = qit; }
             if (qs == 0) step = st; else { status = qs; status_set = true; }
         }
         // filterLineSearch :759-808
@@ -1725,6 +1739,7 @@ static int solve_ocp(const Oracle& o, double* guess, const double* recs, const d
             DenseQP q;
             set_qp(o, trial.data(), recs, ucur, false, q);
             Filter f{q.obj, constraint_norm(q, p.vio_floor)};
+            if (g_trace && it < 4 && ls == 0) { g_trace[8 * it + 2] = f.obj; g_trace[8 * it + 3] = f.vio; }
             for (size_t j = 0; j < filter.size(); j++)
                 if (f.obj >= filter[j].obj && f.vio >= filter[j].vio) { accepted = false; break; }
             if (accepted) {
@@ -1744,6 +1759,7 @@ static int solve_ocp(const Oracle& o, double* guess, const double* recs, const d
         double nrm = 0;
         for (int i = 0; i < nv; i++) nrm = std::max(nrm, std::fabs(step[i]));
         double pn = alpha * nrm;
+        if (g_trace && it < 4) { g_trace[8 * it + 4] = (alpha == 1.0) ? 1 : 0; g_trace[8 * it + 5] = nrm; g_trace[8 * it + 6] = alpha; g_trace[8 * it + 7] = pn; }
         if (pn < p.eps_prim) { status = SOLVED; status_set = true; break; }
     }
     if (it == p.max_iter) status = MAX_ITER_EXCEEDED;
@@ -1772,8 +1788,9 @@ static void rk4(const double* x, const double* u, double ts, double* out) {
 }
 
 // MPC::runMPC_ — mpc.cpp:104-190 for one instance
-static int run_mpc_one(const Oracle& o, double* x0, const double* u0, const double* obs, double* guess, int* valid,
-                       int* fails, double* u0_out, double* horizon, int* ok, int* iters) {
+// runMPC_ up to the solve (mpc.cpp:104-130): projection, warm start, frozen robot records (Q4)
+static void prepare_one(const Oracle& o, double* x0, const double* u0, const double* obs, double* guess, int* valid,
+                        int* fails, double* recs) {
     const OracleParams& p = o.p;
     const int N = p.N;
     double last_s = x0[7];
@@ -1803,8 +1820,15 @@ static int run_mpc_one(const Oracle& o, double* x0, const double* u0, const doub
     }
     for (int i = 1; i <= N; i++) guess[17 * i + 7] = std::min(guess[17 * i + 7], L);  // unwrapInitialGuess
     // setInitialGuess + setEnvData: robot records at the warm start (Q4)
-    std::vector<double> recs((size_t)REC * (N + 1));
     for (int i = 0; i <= N; i++) robot_record(o, guess + 17 * i, obs, obs[3], &recs[(size_t)REC * i]);
+}
+
+static int run_mpc_one(const Oracle& o, double* x0, const double* u0, const double* obs, double* guess, int* valid,
+                       int* fails, double* u0_out, double* horizon, int* ok, int* iters) {
+    const OracleParams& p = o.p;
+    const int N = p.N;
+    std::vector<double> recs((size_t)REC * (N + 1));
+    prepare_one(o, x0, u0, obs, guess, valid, fails, recs.data());
     std::vector<double> sol((size_t)(N + 1) * 17);
     int status = solve_ocp(o, guess, recs.data(), u0, sol.data(), iters);
     std::memcpy(guess, sol.data(), sizeof(double) * 17 * (N + 1));  // initial_guess_ = opt_sol
@@ -1914,8 +1938,8 @@ void oracle_sim_time_step(const double* x9, const double* u8, double ts, double*
     for (int i = 0; i < steps; i++) { double t[9]; rk4(x, u8, fine, t); std::memcpy(x, t, 72); }
     std::memcpy(out9, x, 72);
 }
-int oracle_run_mpc(void* h, int B, double* x0, const double* u0, const double* obs, double* guess, int* valid, int* fails,
-                   double* u0_out, double* horizon, int* status, int* ok, int* sqp_iters) {
+int oracle_run_mpc_trace(void* h, int B, double* x0, const double* u0, const double* obs, double* guess, int* valid,
+                         int* fails, double* u0_out, double* horizon, int* status, int* ok, int* sqp_iters, double* trace) {
     Oracle* o = (Oracle*)h;
     const int N = o->p.N;
 #ifdef _OPENMP
@@ -1924,12 +1948,28 @@ int oracle_run_mpc(void* h, int B, double* x0, const double* u0, const double* o
 #endif
     for (int b = 0; b < B; b++) {
         int it = 0;
+        g_trace = trace ? trace + (size_t)32 * b : nullptr;
+        if (g_trace) for (int i = 0; i < 32; i++) g_trace[i] = 0.0;
         status[b] = run_mpc_one(*o, x0 + 9 * b, u0 + 8 * b, obs + 4 * b, guess + (size_t)17 * (N + 1) * b, valid + b,
                                 fails + b, u0_out + 8 * b, horizon + (size_t)17 * (N + 1) * b, ok + b, &it);
         if (sqp_iters) sqp_iters[b] = it;
+        g_trace = nullptr;
     }
     return 0;
 }
+int oracle_run_mpc(void* h, int B, double* x0, const double* u0, const double* obs, double* guess, int* valid, int* fails,
+                   double* u0_out, double* horizon, int* status, int* ok, int* sqp_iters) {
+    return oracle_run_mpc_trace(h, B, x0, u0, obs, guess, valid, fails, u0_out, horizon, status, ok, sqp_iters, nullptr);
+}
 int oracle_rec_size(void) { return REC; }
+int oracle_prepare(void* h, int B, double* x0, const double* u0, const double* obs, double* guess, int* valid, int* fails,
+                   double* recs) {
+    Oracle* o = (Oracle*)h;
+    const int N = o->p.N;
+    for (int b = 0; b < B; b++)
+        prepare_one(*o, x0 + 9 * b, u0 + 8 * b, obs + 4 * b, guess + (size_t)17 * (N + 1) * b, valid + b, fails + b,
+                    recs + (size_t)REC * (N + 1) * b);
+    return 0;
+}
 
 }  // extern "C"

@@ -103,6 +103,13 @@ void   oracle_sim_time_step(const double* x9, const double* u8, double ts, doubl
 int    oracle_run_mpc(void* h, int B, double* x0, const double* u0, const double* obs,
                       double* guess, int* valid, int* fails,
                       double* u0_out, double* horizon, int* status, int* ok, int* sqp_iters);
+/* runMPC_ up to the SQP (projection, warm start, robot records at the warm start) -> recs [B*(N+1)*REC] */
+int    oracle_prepare(void* h, int B, double* x0, const double* u0, const double* obs, double* guess, int* valid,
+                      int* fails, double* recs);
+/* same, plus a per-instance SQP trace [B*4*8] (see mpcc_debug_trace_get) */
+int    oracle_run_mpc_trace(void* h, int B, double* x0, const double* u0, const double* obs, double* guess, int* valid,
+                            int* fails, double* u0_out, double* horizon, int* status, int* ok, int* sqp_iters,
+                            double* trace);
 
 int    oracle_rec_size(void);
 

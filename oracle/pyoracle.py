@@ -88,6 +88,10 @@ def lib():
         L.oracle_sim_time_step.argtypes = [DP, DP, D, DP]
         L.oracle_run_mpc.restype = C.c_int
         L.oracle_run_mpc.argtypes = [C.c_void_p, C.c_int, DP, DP, DP, DP, IP, IP, DP, DP, IP, IP, IP]
+        L.oracle_prepare.restype = C.c_int
+        L.oracle_prepare.argtypes = [C.c_void_p, C.c_int, DP, DP, DP, DP, IP, IP, DP]
+        L.oracle_run_mpc_trace.restype = C.c_int
+        L.oracle_run_mpc_trace.argtypes = [C.c_void_p, C.c_int, DP, DP, DP, DP, IP, IP, DP, DP, IP, IP, IP, DP]
         L.oracle_rec_size.restype = C.c_int
         assert L.oracle_rec_size() == REC_SIZE
         _lib = L
@@ -245,7 +249,15 @@ class Oracle:
         self.L.oracle_sim_time_step(_dp(_f64(x)), _dp(_f64(u)), float(ts), _dp(out))
         return out
 
-    def run_mpc(self, x0, u0, obs, guess, valid, fails):
+    def prepare(self, x0, u0, obs, guess, valid, fails):
+        """runMPC_ up to the SQP (in place on x0, guess, valid, fails); returns the frozen records."""
+        B = x0.shape[0]
+        recs = np.zeros((B, self.N + 1, self.L.oracle_rec_size()))
+        self.L.oracle_prepare(self.h, B, _dp(x0), _dp(_f64(u0, (B, 8))), _dp(_f64(obs, (B, 4))), _dp(guess),
+                              _ip(valid), _ip(fails), _dp(recs))
+        return recs
+
+    def run_mpc(self, x0, u0, obs, guess, valid, fails, trace=False):
         """Batched runMPC_.  All arrays are modified in place where the reference mutates them
         (x0, guess, valid, fails).  Returns dict of outputs."""
         B = x0.shape[0]
@@ -260,6 +272,11 @@ class Oracle:
         status = np.zeros(B, dtype=np.int32)
         ok = np.zeros(B, dtype=np.int32)
         iters = np.zeros(B, dtype=np.int32)
-        self.L.oracle_run_mpc(self.h, B, _dp(x0), _dp(u0), _dp(obs), _dp(guess), _ip(valid), _ip(fails),
-                              _dp(u0_out), _dp(hor), _ip(status), _ip(ok), _ip(iters))
-        return dict(u0=u0_out, horizon=hor, status=status, ok=ok, sqp_iters=iters)
+        tr = np.zeros((B, 4, 8)) if trace else None
+        self.L.oracle_run_mpc_trace(self.h, B, _dp(x0), _dp(u0), _dp(obs), _dp(guess), _ip(valid), _ip(fails),
+                                    _dp(u0_out), _dp(hor), _ip(status), _ip(ok), _ip(iters),
+                                    _dp(tr) if trace else None)
+        out = dict(u0=u0_out, horizon=hor, status=status, ok=ok, sqp_iters=iters)
+        if trace:
+            out["trace"] = tr
+        return out
