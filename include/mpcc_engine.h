@@ -203,6 +203,8 @@ int mpcc_debug_solve_qp(mpcc_engine* e, int B, const double* guess, const double
  * (at most 4) 8 doubles: qp status, ipm iterations, trial objective and violation at alpha = 1,
  * accepted, |step|_inf, alpha, alpha*|step|_inf (osqp_interface.cpp:540-574, 759-808). */
 int mpcc_debug_trace_enable(mpcc_engine* e, int enable);
+/* raw interior-point workspace of the last solve [B*(N+1)*816] (layout: csrc/ipm.hip WF_*) */
+int mpcc_debug_workspace(mpcc_engine* e, int B, double* out);
 int mpcc_debug_trace_get(mpcc_engine* e, int B, double* out /* [B*4*8] */);
 
 #ifdef __cplusplus

@@ -829,3 +829,14 @@ int mpcc_debug_trace_get(mpcc_engine* e, int B, double* out) {
     }
     return MPCC_OK;
 }
+
+int mpcc_debug_workspace(mpcc_engine* e, int B, double* out) {
+    if (!e || !out || B < 1 || B > e->cfg.max_batch) return fail(MPCC_E_INVALID, "mpcc_debug_workspace: invalid argument");
+    try {
+        HIPCHK(hipDeviceSynchronize());
+        HIPCHK(hipMemcpy(out, e->d.is, sizeof(double) * (size_t)B * (e->N + 1) * IS, hipMemcpyDeviceToHost));
+    } catch (const std::exception& x) {
+        return fail(MPCC_E_HIP, std::string("mpcc_debug_workspace: ") + x.what());
+    }
+    return MPCC_OK;
+}

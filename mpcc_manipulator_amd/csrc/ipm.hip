@@ -7,16 +7,18 @@
 //
 // MI355X mapping:
 //  * one 16-lane DPP row per instance, 4 instances per wavefront.  Lane t owns row t of the stage
-//    (t < 9: box row on y_t, t >= 9: ddq row j = t-9), poly row t, column t of the 16x16 Riccati
-//    matrices and component t of the stage vectors.  Cross-lane traffic inside an instance uses DPP
-//    row shifts / rotations or the instance's private LDS block; there are no workgroup barriers.
+//    (t < 9: box row on y_t, t >= 9: ddq row j = t-9), poly row t, component t of every stage vector
+//    and column t of every 16x16 / 8x16 stage matrix.  All of it lives in registers: P is carried
+//    from stage to stage as one column per lane, and every exchange inside an instance is a DPP row
+//    broadcast (row_newbcast) or row shift — no LDS round trip, so no lgkmcnt waits on the chain.
+//    The only LDS traffic is U (8x16) for P = Hb - U^T U (broadcast ds_read_b128 of U's rows) and
+//    the K transpose for the forward-solve layout.
 //  * the dynamics are sparse (M = diag(m) + m78 e7 e8^T, G = diag(g) + g87 e8 e7^T, checked on the
 //    host): the Riccati products are written out structurally; the dense work per stage is chol(F)
-//    (8x8, redundant per lane), U = LF^-1 Gm and K = -F^-1 Gm (lane = column) and P = Hb - U^T U
-//    (lane = row).
+//    (8x8, redundant per lane), U = LF^-1 Gm, K = -F^-1 Gm (lane = column) and P = Hb - U^T U.
 //  * per-stage state (slacks, multipliers, iterate, steps, gains) streams through a coalesced
-//    [field][16 lanes] global workspace.  Backward solves are mat-vecs (p = g + A~^T p + K^T f,
-//    kff = -F^-1 f) and so are forward solves (v = K x~ + kff): no division chains outside chol(F).
+//    [field][16 lanes] global workspace, prefetched one stage ahead.  Backward solves are mat-vecs
+//    (p = g + A~^T p + K^T f, kff = -F^-1 f) and so are forward solves (v = K x~ + kff).
 //  * the predictor backward solve is fused into the factorization sweep, and the iterate update of
 //    iteration i is applied lazily by the factorization sweep of iteration i+1.  The convergence test
 //    uses mu(alpha) = (S0 + alpha S1 + alpha^2 S2)/m and rp(alpha) = (1 - alpha) rp, accumulated by
@@ -26,12 +28,15 @@
 
 namespace mpcc {
 
-constexpr int IPM_MAX_IT = 60;
+#ifndef MPCC_IPM_MAXIT
+#define MPCC_IPM_MAXIT 60
+#endif
+constexpr int IPM_MAX_IT = MPCC_IPM_MAXIT;  // 60 (oracle); a debug build may cap it
 constexpr double IPM_TOL_MU = 1e-13, IPM_TOL_P = 1e-11, IPM_TOL_STEP = 1e-11;
 constexpr double IPM_TOL_FB = 1e-9;  // P2: a converged iterate is accepted when the Riccati factor breaks down
-constexpr int IPW = 4;  // instances per wavefront (16 lanes each)
+constexpr int IPW = 4;               // instances per wavefront (16 lanes each)
 
-// workspace fields, ws[((b*(N+1) + k)*IS + field*16 + lane]
+// workspace fields, ws[(b*(N+1) + k)*IS + field*16 + lane]
 enum : int {
     WF_SL = 0, WF_LL, WF_SU, WF_LU, WF_SP, WF_LP,  // slack / multiplier of the lower, upper and poly slot of row t
     WF_ZX, WF_ZV,                                 // iterate: lane c -> x~_c (y, w); lane j < 8 -> v_j
@@ -46,23 +51,11 @@ enum : int {
 };
 static_assert(NWF * 16 <= IS, "IPM workspace must fit the per-stage IS allocation");
 
-// per-instance LDS block (doubles)
-constexpr int L_P = 0;      // 16x16 Riccati P (full, symmetric)
-constexpr int L_U = 256;    // 8x16  Y = B~^T P scratch, then U = LF^-1 Gm, [i*16 + c]
-constexpr int L_K = 384;    // 8x16  K, [i*16 + c]
-constexpr int L_F = 512;    // 8x8   F, [i*8 + j]
-constexpr int L_Z = 576;    // 24    stage iterate z = [y, w, v]
-constexpr int L_DZ = 600;   // 24    corrector step
-constexpr int L_DA = 624;   // 24    predictor step
-constexpr int L_X = 648;    // 2x16  forward x~ (ping-pong)
-constexpr int L_PV = 680;   // 2x16  backward p (ping-pong)
-constexpr int L_FV = 712;   // 8     f
-constexpr int L_WD = 720;   // 16    row barrier weights W_lo + W_up
-constexpr int L_PC = 736;   // 16    poly coefficients
-constexpr int L_POLY = 752; // npmax x 16: a[7], bv[7], ub, W
-__host__ __device__ constexpr int grp_lds(int npmax) { return L_POLY + 16 * (npmax > 0 ? npmax : 1); }
+// per-instance LDS block (doubles): U and K of the current stage, [i*16 + c]
+constexpr int L_U = 0, L_K = 128;
+constexpr int GRP_LDS = 256 + 16;  // 16 mod 32 doubles: the two instances of a half-wave start 32 banks apart
 
-size_t ipm_lds_bytes(int /*N*/, int npmax) { return (size_t)IPW * grp_lds(npmax) * sizeof(double); }
+size_t ipm_lds_bytes(int /*N*/, int /*npmax*/) { return (size_t)IPW * GRP_LDS * sizeof(double); }
 
 #ifdef MPCC_IPM_PROF
 // cycle accounting per k_ipm section (profiling build only, see _build.py / tools/ipm_prof.py)
@@ -86,6 +79,16 @@ __device__ __forceinline__ double dpp_d(double v) {
 template <int n> __device__ __forceinline__ double from_up(double v) { return dpp_d<0x100 + n>(v); }    // row_shl: lane t <- t+n
 template <int n> __device__ __forceinline__ double from_down(double v) { return dpp_d<0x110 + n>(v); } // row_shr: lane t <- t-n
 template <int n> __device__ __forceinline__ double rot16(double v) { return dpp_d<0x120 + n>(v); }     // row_ror
+template <int n> __device__ __forceinline__ double bc(double v) { return dpp_d<0x150 + n>(v); }        // row_newbcast: lane n
+// lane n of the row for an n that is a constant after unrolling
+__device__ __forceinline__ double bcn(double v, int n) {
+    switch (n) {
+        case 0: return bc<0>(v);   case 1: return bc<1>(v);   case 2: return bc<2>(v);   case 3: return bc<3>(v);
+        case 4: return bc<4>(v);   case 5: return bc<5>(v);   case 6: return bc<6>(v);   case 7: return bc<7>(v);
+        case 8: return bc<8>(v);   case 9: return bc<9>(v);   case 10: return bc<10>(v); case 11: return bc<11>(v);
+        case 12: return bc<12>(v); case 13: return bc<13>(v); case 14: return bc<14>(v); default: return bc<15>(v);
+    }
+}
 __device__ __forceinline__ double g_sum(double v) {
     v += rot16<8>(v); v += rot16<4>(v); v += rot16<2>(v); v += rot16<1>(v);
     return v;
@@ -99,6 +102,10 @@ __device__ __forceinline__ double g_min(double v) {
     return v;
 }
 
+// NOTE: every DPP read must execute with the whole 16-lane row active — a lane reading from a lane that
+// is masked off at that instruction gets 0.  Shifts/broadcasts are therefore evaluated unconditionally
+// and consumed through selects.
+
 // One wavefront per workgroup: cross-lane LDS hand-offs only need this wave's LDS operations retired
 // and a compiler barrier; __syncthreads() would also drain outstanding global loads (vmcnt(0)).
 __device__ __forceinline__ void lds_sync() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
@@ -108,11 +115,12 @@ struct SlotStep {
     double ds, dl;
 };
 __device__ __forceinline__ double slot_rp(double sgn, double cz, double bnd, double s) { return sgn * cz - sgn * bnd + s; }
-__device__ __forceinline__ SlotStep slot_recover(double s, double l, double rp, double cd, double rc) {
-    const double W = l / s;
-    return {-rp - cd, W * (cd + rp) - rc / s};
+// ri = 1/s is formed once per slot and sweep (W = l/s, rc/s become products)
+__device__ __forceinline__ SlotStep slot_recover(double ri, double l, double rp, double cd, double rc) {
+    const double W = l * ri;
+    return {-rp - cd, W * (cd + rp) - rc * ri};
 }
-__device__ __forceinline__ double slot_coef(double s, double l, double rp, double rc) { return l + (l / s) * rp - rc / s; }
+__device__ __forceinline__ double slot_coef(double ri, double l, double rp, double rc) { return l + (l * ri) * rp - rc * ri; }
 __device__ __forceinline__ double step_bound(double a, double s, double l, SlotStep d) {
     if (d.ds < 0) a = fmin(a, -s / d.ds);
     if (d.dl < 0) a = fmin(a, -l / d.dl);
@@ -121,20 +129,17 @@ __device__ __forceinline__ double step_bound(double a, double s, double l, SlotS
 // corrector step of a slot given the iterate (cz), the predictor step (ca) and the corrector step (cd)
 __device__ __forceinline__ SlotStep slot_corr(double sgn, double bnd, double cz, double ca, double cd, double s, double l,
                                               double smu, double* rp_out) {
+    const double ri = 1.0 / s;
     const double rp = slot_rp(sgn, cz, bnd, s);
-    const SlotStep pa = slot_recover(s, l, rp, sgn * ca, s * l);
+    const SlotStep pa = slot_recover(ri, l, rp, sgn * ca, s * l);
     const double rc = s * l + pa.ds * pa.dl - smu;
     *rp_out = rp;
-    return slot_recover(s, l, rp, sgn * cd, rc);
+    return slot_recover(ri, l, rp, sgn * cd, rc);
 }
 
-// Cholesky of the 8x8 stage F (lower triangle read from LDS), packed; reciprocal pivots
-__device__ __forceinline__ bool chol8(const double* F, double* L, double* dinv) {
+// Cholesky of the 8x8 stage F (lower triangle, packed row-major in L on entry); reciprocal pivots
+__device__ __forceinline__ bool chol8(double* L, double* dinv) {
     bool ok = true;
-#pragma unroll
-    for (int i = 0; i < 8; i++)
-#pragma unroll
-        for (int j = 0; j <= i; j++) L[i * (i + 1) / 2 + j] = F[i * 8 + j];
 #pragma unroll
     for (int j = 0; j < 8; j++) {
         const int jj = j * (j + 1) / 2;
@@ -177,12 +182,23 @@ __device__ __forceinline__ void bwd8(const double* L, const double* dinv, double
     }
 }
 
+// per-stage inputs of one lane, loaded one stage ahead of their use
+template <int NPE>
+struct StageIn {
+    double lb, ub, np;            // bounds of row t, live poly rows
+    double pa[NPE], pb[NPE];      // poly rows p: a_p[t], bv_p[t] (t < 7)
+    double pub;                   // upper bound of poly row t (t < npmax)
+    double sL, lL, sU, lU, sP, lP, zx, zv;
+    double x0, x1, x2, x3;        // sweep-specific pairs (dz, dza, g0)
+    double m[12];                 // sweep-specific: Q row + q, R, r | K row halves + kff | K column + F^-1 half
+};
+
 }  // namespace
 
 template <int NPM>
 __global__ void __launch_bounds__(64) k_ipm(DevConst c, DevBuffers d) {
-    constexpr int NPE = NPM > 0 ? NPM : 1;      // poly rows held in LDS (row 0 stays zero when NPM = 0)
-    constexpr int PFP = (15 * NPM + 15) / 16;   // poly prefetch registers per lane
+    constexpr int NPE = NPM > 0 ? NPM : 1;
+    using In = StageIn<NPE>;
     extern __shared__ __attribute__((aligned(16))) double smem[];
     const int lane = threadIdx.x;
     const int grp = lane >> 4;
@@ -190,7 +206,7 @@ __global__ void __launch_bounds__(64) k_ipm(DevConst c, DevBuffers d) {
     const int b = blockIdx.x * IPW + grp;
     const int N = c.N;
     const int NS = N + 1;
-    double* const S = smem + grp * grp_lds(NPM);
+    double* const S = smem + grp * GRP_LDS;
 #ifdef MPCC_IPM_PROF
     long long prof_acc[16] = {0};
     long long prof_t = clock64();
@@ -210,15 +226,20 @@ __global__ void __launch_bounds__(64) k_ipm(DevConst c, DevBuffers d) {
     const double g77 = c.G[7 * 8 + 7], g87 = c.G[8 * 8 + 7];
     double mt = 0.0, gt = 0.0, Hct = 0.0;
     const double HcB = -2. * c.p.qp_r_ddq;
+    double mdiag[9], gdiag[7];
 #pragma unroll
-    for (int a = 0; a < 9; a++)
-        if (t == a) mt = c.M[a * 10];
+    for (int a = 0; a < 9; a++) {
+        mdiag[a] = c.M[a * 10];
+        if (t == a) mt = mdiag[a];
+    }
 #pragma unroll
-    for (int a = 0; a < 7; a++)
+    for (int a = 0; a < 7; a++) {
+        gdiag[a] = c.G[a * 9];
         if (t == a || t == 9 + a) {
-            gt = (t < 7) ? c.G[a * 9] : 0.0;
+            gt = (t < 7) ? gdiag[a] : 0.0;
             Hct = c.p.Tu[a] * HcB * c.p.Tu[a];
         }
+    }
     if (t == 7) gt = g77;
     const bool rowY = t < 9;
     const int j9 = t - 9;
@@ -252,78 +273,23 @@ __global__ void __launch_bounds__(64) k_ipm(DevConst c, DevBuffers d) {
     if (run && (fl & 4)) { if (t == 0) si[SQ_QPSTAT] = MPCC_QP_PrimalInfeasible; run = false; }  // keep old step (Q6)
     const bool entered = run;
 
-    // ---- per-stage inputs, loaded one stage ahead of their use (software pipelining of the sweeps)
-    struct StageIn {
-        double lb, ub;          // bounds of row t
-        int np;                 // live poly rows
-        double pv[PFP > 0 ? PFP : 1];
-        double sL, lL, sU, lU, sP, lP, zx, zv;
-        double x0, x1, x2, x3;  // sweep-specific pairs (dz / dza / g0)
-        double m[12];           // sweep-specific: Q row + q,R,r | K rows + kff | K column + Finv half
-    };
-    auto load_common = [&](int k, StageIn& o) {
+    // ---- stage loaders
+    auto load_common = [&](int k, In& o) {
         const double* q = QSb + (size_t)k * QS;
         o.lb = q[rowY ? QS_YLB + t : QS_DLB + j9];
         o.ub = q[rowY ? QS_YUB + t : QS_DUB + j9];
-        o.np = (int)q[QS_NPOLY];
+        o.np = q[QS_NPOLY];
 #pragma unroll
-        for (int i = 0; i < PFP; i++) {
-            const int e = t + 16 * i;
-            o.pv[i] = (e < 15 * NPM) ? q[QS_POLY + e] : 0.0;
+        for (int p = 0; p < NPE; p++) {
+            o.pa[p] = (NPM > 0 && t < 7) ? q[QS_POLY + 15 * p + t] : 0.0;
+            o.pb[p] = (NPM > 0 && t < 7) ? q[QS_POLY + 15 * p + 7 + t] : 0.0;
         }
+        o.pub = (t < NPM) ? q[QS_POLY + 15 * t + 14] : INF;
         o.sL = *ws(k, WF_SL); o.lL = *ws(k, WF_LL); o.sU = *ws(k, WF_SU); o.lU = *ws(k, WF_LU);
         o.sP = *ws(k, WF_SP); o.lP = *ws(k, WF_LP);
         o.zx = *ws(k, WF_ZX); o.zv = *ws(k, WF_ZV);
     };
-    auto load_bounds = [&](int k, double& lb, double& ub, int& np) {
-        const double* q = QSb + (size_t)k * QS;
-        lb = q[rowY ? QS_YLB + t : QS_DLB + j9];
-        ub = q[rowY ? QS_YUB + t : QS_DUB + j9];
-        np = (int)q[QS_NPOLY];
-    };
-    auto load_poly = [&](int k, double* r) {
-        const double* q = QSb + (size_t)k * QS + QS_POLY;
-#pragma unroll
-        for (int i = 0; i < PFP; i++) {
-            const int e = t + 16 * i;
-            r[i] = (e < 15 * NPM) ? q[e] : 0.0;
-        }
-    };
-    // stage the poly rows (rows >= np zeroed); returns this lane's poly bound (INF: no live row t)
-    auto stage_poly = [&](const double* r, int np, int k) -> double {
-#pragma unroll
-        for (int i = 0; i < PFP; i++) {
-            const int e = t + 16 * i;
-            if (e < 15 * NPM) {
-                const int p = e / 15, m = e - 15 * p;
-                S[L_POLY + p * 16 + m] = (p < np && k < N) ? r[i] : 0.0;
-            }
-        }
-        lds_sync();
-        return (t < np && t < NPM && k < N) ? S[L_POLY + t * 16 + 14] : INF;
-    };
-    auto row_active = [&](int k, double bnd) { return (rowY ? (k >= 1) : (k < N)) && fabs(bnd) < BIG; };
-    // unsigned c^T z of this lane's box/ddq row and of poly row t; z = stage vector in LDS at off
-    auto row_cz = [&](int k, int off) -> double {
-        if (rowY) return S[off + t];
-        const double v = S[off + 16 + j9];
-        return (k == 0) ? v : v - S[off + 9 + j9];
-    };
-    auto poly_cz = [&](int off) -> double {
-        if (t >= NPM) return 0.0;
-        const double* row = S + L_POLY + t * 16;
-        double s = 0;
-#pragma unroll
-        for (int m = 0; m < 7; m++) s += row[m] * S[off + m];
-#pragma unroll
-        for (int m = 0; m < 7; m++) s += row[7 + m] * S[off + 16 + m];
-        return s;
-    };
-    auto put_vec = [&](int off, double x, double v) {  // lane c: x~_c, lane j < 8: v_j
-        S[off + t] = x;
-        if (t < 8) S[off + 16 + t] = v;
-    };
-    auto load_factor = [&](int k, StageIn& o, bool upd) {
+    auto load_factor = [&](int k, In& o, bool upd) {
         load_common(k, o);
         const double* q = QSb + (size_t)k * QS;
 #pragma unroll
@@ -337,7 +303,7 @@ __global__ void __launch_bounds__(64) k_ipm(DevConst c, DevBuffers d) {
             o.x0 = o.x1 = o.x2 = o.x3 = 0.0;
         }
     };
-    auto load_fwd = [&](int k, StageIn& o, bool corr) {
+    auto load_fwd = [&](int k, In& o, bool corr) {
         load_common(k, o);
         if (k < N) {
 #pragma unroll
@@ -349,7 +315,7 @@ __global__ void __launch_bounds__(64) k_ipm(DevConst c, DevBuffers d) {
         }
         if (corr) { o.x0 = *ws(k, WF_AX); o.x1 = *ws(k, WF_AV); } else { o.x0 = o.x1 = 0.0; }
     };
-    auto load_bwd = [&](int k, StageIn& o) {
+    auto load_bwd = [&](int k, In& o) {
         load_common(k, o);
         o.x0 = *ws(k, WF_AX); o.x1 = *ws(k, WF_AV); o.x2 = *ws(k, WF_GX); o.x3 = *ws(k, WF_GV);
         if (k < N) {
@@ -363,44 +329,97 @@ __global__ void __launch_bounds__(64) k_ipm(DevConst c, DevBuffers d) {
         }
     };
 
+    // ---- stage-local helpers (registers + DPP only)
+    auto row_active = [&](int k, double bnd) { return (rowY ? (k >= 1) : (k < N)) && fabs(bnd) < BIG; };
+    // unsigned c^T z of this lane's box / ddq row; (x, v) = lane components of a stage vector
+    auto row_cz = [&](int k, double x, double v) -> double {
+        const double vj = from_down<9>(v);  // lane 9+j <- v_j
+        if (rowY) return x;
+        return (k == 0) ? vj : vj - x;
+    };
+    // c^T z of poly row t (= p), reduced over the row's 16 lanes: sum_m a_p[m] y_m + bv_p[m] v_m
+    auto poly_cz = [&](const In& in, int k, double x, double v) -> double {
+        double r = 0.0;
+#pragma unroll
+        for (int p = 0; p < NPM; p++) {
+            const bool live = (double)p < in.np && k < N;
+            const double term = live ? in.pa[p] * x + in.pb[p] * v : 0.0;
+            const double s = g_sum(term);
+            if (t == p) r = s;
+        }
+        return r;
+    };
+    auto poly_slot_active = [&](const In& in, int k) {
+        return t < NPM && (double)t < in.np && k < N && fabs(in.pub) < BIG;
+    };
+    // gradient of the step system: g = g0 + sum_i sgn_i coef_i c_i (dvr: signed coefficient of row t,
+    // cP: coefficient of poly row t)
+    auto assemble_grad = [&](const In& in, int k, double g0x, double g0v, double dvr, double cP, double& gx, double& gv) {
+        gx = g0x;
+        if (t < 9) gx += dvr;
+        else if (k >= 1) gx -= dvr;
+        gv = g0v;
+        const double dv_up = from_up<9>(dvr);  // lane j <- ddq row j
+        if (t < 7 && k < N) gv += dv_up;
+#pragma unroll
+        for (int p = 0; p < NPM; p++) {
+            const double cp = bcn(cP, p);
+            const bool live = (double)p < in.np && k < N;
+            if (live) {
+                gx += cp * in.pa[p];  // zero for lanes >= 7
+                gv += cp * in.pb[p];
+            }
+        }
+    };
+    // forward step: v = K x~ + kff (lanes 0..7) and x~' = A~ x~ + B~ v (all lanes)
+    auto fwd_step = [&](const In& in, double xt, double& v, double& xn) {
+        double xb[16];
+#pragma unroll
+        for (int m = 0; m < 16; m++) xb[m] = bcn(xt, m);
+        double part = 0.0;
+#pragma unroll
+        for (int m = 0; m < 8; m++) part += in.m[m] * ((t < 8) ? xb[m] : xb[8 + m]);
+        v = part + from_up<8>(part) + in.m[8];
+        const double v7 = from_down<1>(v);
+        const double vj = from_down<9>(v);
+        if (t < 7) xn = mt * xt + gt * v;
+        else if (t == 7) xn = (m77 * xt + m78 * xb[8]) + g77 * v;
+        else if (t == 8) xn = m88 * xt + g87 * v7;
+        else xn = vj;
+    };
+
     // ---- start point: dynamics rollout with v = 0, s = max(-g, 1), lambda = 1
     double mcount = 0.0;
+    In cur, nxt;
     if (run) {
         double y = 0.0;  // lane a < 9: y_a of stage k
-        double lb, ub, bk; int np;
-        double pv[PFP > 0 ? PFP : 1];
-        auto load_start = [&](int k, double& lb_, double& ub_, int& np_, double* pv_, double& bk_) {
-            load_bounds(k, lb_, ub_, np_);
-            load_poly(k, pv_);
-            bk_ = (k < N && t < 9) ? QSb[(size_t)k * QS + QS_B + t] : 0.0;
-        };
-        load_start(0, lb, ub, np, pv, bk);
+        double bk = 0, bkn = 0;
+        load_common(0, cur);
+        bk = (N > 0 && t < 9) ? QSb[QS_B + t] : 0.0;
         for (int k = 0; k <= N; k++) {
-            double lbn = 0, ubn = 0, bkn = 0; int npn = 0;
-            double pvn[PFP > 0 ? PFP : 1];
-            if (k < N) load_start(k + 1, lbn, ubn, npn, pvn, bkn);
-            put_vec(L_Z, rowY ? y : 0.0, 0.0);
-            const double pb = stage_poly(pv, np, k);
-            const double cz = row_cz(k, L_Z);
-            const double pcz = poly_cz(L_Z);
-            const bool aL = row_active(k, lb), aU = row_active(k, ub), aP = fabs(pb) < BIG;
+            if (k < N) {
+                load_common(k + 1, nxt);
+                bkn = (k + 1 < N && t < 9) ? QSb[(size_t)(k + 1) * QS + QS_B + t] : 0.0;
+            }
+            const double yx = rowY ? y : 0.0;
+            const double cz = row_cz(k, yx, 0.0);
+            const double pcz = poly_cz(cur, k, yx, 0.0);
+            const bool aL = row_active(k, cur.lb), aU = row_active(k, cur.ub), aP = poly_slot_active(cur, k);
             double sL = 1, lL = 0, sU = 1, lU = 0, sP = 1, lP = 0;
-            if (aL) { sL = fmax(-(sgnL * cz - sgnL * lb), 1.0); lL = 1.0; }
-            if (aU) { sU = fmax(-(sgnU * cz - sgnU * ub), 1.0); lU = 1.0; }
-            if (aP) { sP = fmax(-(sgnU * pcz - sgnU * pb), 1.0); lP = 1.0; }
+            if (aL) { sL = fmax(-(sgnL * cz - sgnL * cur.lb), 1.0); lL = 1.0; }
+            if (aU) { sU = fmax(-(sgnU * cz - sgnU * cur.ub), 1.0); lU = 1.0; }
+            if (aP) { sP = fmax(-(sgnU * pcz - sgnU * cur.pub), 1.0); lP = 1.0; }
             mcount += (aL ? 1.0 : 0.0) + (aU ? 1.0 : 0.0) + (aP ? 1.0 : 0.0);
             *ws(k, WF_SL) = sL; *ws(k, WF_LL) = lL; *ws(k, WF_SU) = sU; *ws(k, WF_LU) = lU;
             *ws(k, WF_SP) = sP; *ws(k, WF_LP) = lP;
-            *ws(k, WF_ZX) = rowY ? y : 0.0;
+            *ws(k, WF_ZX) = yx;
             *ws(k, WF_ZV) = 0.0;
             // y_{k+1} = M y_k + b_k (oracle order: sum_b M[a][b] y_b, then + b_a)
             const double y8 = from_up<1>(y);  // lane 7 <- y_8
             const double yn = (t == 7) ? m77 * y + m78 * y8 : mt * y;
             y = (t < 9) ? yn + bk : 0.0;
-            lb = lbn; ub = ubn; np = npn; bk = bkn;
-#pragma unroll
-            for (int i = 0; i < PFP; i++) pv[i] = pvn[i];
-            lds_sync();
+            cur = nxt;
+            bk = bkn;
         }
     }
     mcount = g_sum(mcount);
@@ -411,16 +430,15 @@ __global__ void __launch_bounds__(64) k_ipm(DevConst c, DevBuffers d) {
     double alpha = 0.0, sigma_mu = 0.0;  // previous iteration's step length and sigma*mu (lazy update)
     double mu_cur = 1e30, rp_cur = 1e30; // mu and max |rp| of the current iterate (known for it > 0)
     bool pending = false;
-    StageIn cur, nxt;
     while (true) {
         if (__ballot(run) == 0) break;
         if (run) {
             // ================= factorization sweep k = N..0 with the lazy update of the previous step,
             // the objective gradient g0 = H z + h and the predictor backward solve
-            int pcur = 0;  // p ping-pong slot holding p_{k+1}
+            double Pc[16];   // column t of P_{k+1}
+            double pv = 0.0; // p_{k+1}, component t
             bool chol_ok = true;
             load_factor(N, cur, pending);
-            PMARK(1);
             for (int k = N; k >= 0; k--) {
                 if (k > 0) load_factor(k - 1, nxt, pending);
                 const double lb = cur.lb, ub = cur.ub;
@@ -428,181 +446,118 @@ __global__ void __launch_bounds__(64) k_ipm(DevConst c, DevBuffers d) {
                 const double qt = cur.m[9], Rt = cur.m[10], rt = cur.m[11];
                 double sL = cur.sL, lL = cur.lL, sU = cur.sU, lU = cur.lU, sP = cur.sP, lP = cur.lP;
                 double zx = cur.zx, zv = cur.zv;
-                const double pb = stage_poly(cur.pv, cur.np, k);
-                const bool aL = row_active(k, lb), aU = row_active(k, ub), aP = fabs(pb) < BIG;
+                const bool aL = row_active(k, lb), aU = row_active(k, ub), aP = poly_slot_active(cur, k);
                 if (pending) {
                     // previous iteration's update at this stage (oracle: z += a dz, s += a ds, l += a dl)
                     const double dx = cur.x0, dv = cur.x1, ax = cur.x2, av = cur.x3;
-                    put_vec(L_Z, zx, zv); put_vec(L_DZ, dx, dv); put_vec(L_DA, ax, av);
-                    lds_sync();
-                    const double cz = row_cz(k, L_Z), cd = row_cz(k, L_DZ), ca = row_cz(k, L_DA);
-                    const double pcz = poly_cz(L_Z), pcd = poly_cz(L_DZ), pca = poly_cz(L_DA);
+                    const double cz = row_cz(k, zx, zv), cd = row_cz(k, dx, dv), ca = row_cz(k, ax, av);
+                    const double pcz = poly_cz(cur, k, zx, zv), pcd = poly_cz(cur, k, dx, dv), pca = poly_cz(cur, k, ax, av);
                     double rpd;
                     if (aL) { const SlotStep st = slot_corr(sgnL, lb, cz, ca, cd, sL, lL, sigma_mu, &rpd); sL += alpha * st.ds; lL += alpha * st.dl; }
                     if (aU) { const SlotStep st = slot_corr(sgnU, ub, cz, ca, cd, sU, lU, sigma_mu, &rpd); sU += alpha * st.ds; lU += alpha * st.dl; }
-                    if (aP) { const SlotStep st = slot_corr(sgnU, pb, pcz, pca, pcd, sP, lP, sigma_mu, &rpd); sP += alpha * st.ds; lP += alpha * st.dl; }
+                    if (aP) { const SlotStep st = slot_corr(sgnU, cur.pub, pcz, pca, pcd, sP, lP, sigma_mu, &rpd); sP += alpha * st.ds; lP += alpha * st.dl; }
                     zx += alpha * dx;
                     zv += alpha * dv;
                     *ws(k, WF_SL) = sL; *ws(k, WF_LL) = lL; *ws(k, WF_SU) = sU; *ws(k, WF_LU) = lU;
                     *ws(k, WF_SP) = sP; *ws(k, WF_LP) = lP;
                     *ws(k, WF_ZX) = zx; *ws(k, WF_ZV) = zv;
-                    lds_sync();
                 }
                 PMARK(8);
-                put_vec(L_Z, zx, zv);
-                lds_sync();
                 // ---- slots: barrier weights and predictor coefficients (rc = s l)
-                const double cz = row_cz(k, L_Z);
-                const double pcz = poly_cz(L_Z);
+                const double cz = row_cz(k, zx, zv);
+                const double pcz = poly_cz(cur, k, zx, zv);
                 double WL = 0, WU = 0, WP = 0, cL = 0, cU = 0, cP = 0;
-                if (aL) { const double rp = slot_rp(sgnL, cz, lb, sL); WL = lL / sL; cL = slot_coef(sL, lL, rp, sL * lL); }
-                if (aU) { const double rp = slot_rp(sgnU, cz, ub, sU); WU = lU / sU; cU = slot_coef(sU, lU, rp, sU * lU); }
-                if (aP) { const double rp = slot_rp(sgnU, pcz, pb, sP); WP = lP / sP; cP = slot_coef(sP, lP, rp, sP * lP); }
+                if (aL) { const double rp = slot_rp(sgnL, cz, lb, sL); const double ri = 1.0 / sL; WL = lL * ri; cL = slot_coef(ri, lL, rp, sL * lL); }
+                if (aU) { const double rp = slot_rp(sgnU, cz, ub, sU); const double ri = 1.0 / sU; WU = lU * ri; cU = slot_coef(ri, lU, rp, sU * lU); }
+                if (aP) { const double rp = slot_rp(sgnU, pcz, cur.pub, sP); const double ri = 1.0 / sP; WP = lP * ri; cP = slot_coef(ri, lP, rp, sP * lP); }
                 const double wd = WL + WU;                 // diagonal weight of row t
                 const double dvr = sgnL * cL + sgnU * cU;  // signed coefficient of row t
-                S[L_PC + t] = cP;
-                if (t < NPE) S[L_POLY + t * 16 + 15] = WP;
                 // ---- objective gradient g0 = H z + h (f_xu = 0; oracle order: sum over z, then + h)
                 double g0x, g0v = 0.0;
-                if (t < 9) {
-                    double s = 0;
+                {
+                    double zb[9];
 #pragma unroll
-                    for (int m = 0; m < 9; m++) s += Qr[m] * S[L_Z + m];
-                    g0x = s + qt;
-                } else {
-                    g0x = (k >= 1 && k < N) ? Hct * S[L_Z + 16 + j9] : 0.0;
-                }
-                if (t < 8 && k < N) {
-                    double s = (k >= 1 && t < DOF) ? Hct * S[L_Z + 9 + t] : 0.0;
-                    s += Rt * zv;
-                    g0v = s + rt;
+                    for (int m = 0; m < 9; m++) zb[m] = bcn(zx, m);
+                    const double vj = from_down<9>(zv);  // lane 9+j <- v_j
+                    const double wj = from_up<9>(zx);    // lane j <- w_j
+                    if (t < 9) {
+                        double s = 0;
+#pragma unroll
+                        for (int m = 0; m < 9; m++) s += Qr[m] * zb[m];
+                        g0x = s + qt;
+                    } else {
+                        g0x = (k >= 1 && k < N) ? Hct * vj : 0.0;
+                    }
+                    if (t < 8 && k < N) {
+                        double s = (k >= 1 && t < DOF) ? Hct * wj : 0.0;
+                        s += Rt * zv;
+                        g0v = s + rt;
+                    }
                 }
                 *ws(k, WF_GX) = g0x;
                 *ws(k, WF_GV) = g0v;
-                lds_sync();
-                // ---- step-system gradient (predictor): g = g0 + sum_i sgn_i coef_i c_i
-                double gx = g0x, gv = g0v;
-                if (t < 9) {
-                    gx += dvr;
-                    if (t < 7)
-#pragma unroll
-                        for (int p = 0; p < NPM; p++) gx += S[L_PC + p] * S[L_POLY + p * 16 + t];
-                } else if (k >= 1) {
-                    gx -= dvr;
-                }
-                const double dv_up = from_up<9>(dvr);  // lane j <- ddq row j
-                if (t < 7 && k < N) {
-                    gv += dv_up;
-#pragma unroll
-                    for (int p = 0; p < NPM; p++) gv += S[L_PC + p] * S[L_POLY + p * 16 + 7 + t];
-                }
+                double gx, gv;
+                assemble_grad(cur, k, g0x, g0v, dvr, cP, gx, gv);
+                PMARK(9);
                 if (k == N) {
-                    // terminal stage: P = Hb_N (y block only), p = g_x~ (upper triangle mirrored, lane = row)
+                    // terminal stage: P = Hb_N (y block only; Q row t used as column t), p = g_x~
 #pragma unroll
-                    for (int cc = 0; cc < 16; cc++) {
+                    for (int a = 0; a < 16; a++) {
                         double v = 0.0;
-                        if (t < 9 && cc < 9) {
-                            v = Qr[cc];
-                            if (cc == t) v += wd;
+                        if (t < 9 && a < 9) {
+                            v = Qr[a];
+                            if (a == t) v += wd;
                         }
-                        if (cc >= t) { S[L_P + t * 16 + cc] = v; S[L_P + cc * 16 + t] = v; }
+                        Pc[a] = v;
                     }
-                    S[L_PV + t] = gx;
-                    pcur = 0;
-                    lds_sync();
+                    pv = gx;
                     cur = nxt;
                     continue;
                 }
-                PMARK(9);
-                // ---- (1) Y = B~^T P (lane n: column n of Y from column n of P), f = g_v + B~^T p
-                double Pc[16];
+                // ---- (1) Y = B~^T P (column t), f = g_v + B~^T p (lanes 0..7)
+                double Y[8];
 #pragma unroll
-                for (int i = 0; i < 16; i++) Pc[i] = S[L_P + i * 16 + t];
-                {
-                    double Y[8];
+                for (int i = 0; i < 7; i++) Y[i] = gdiag[i] * Pc[i] + Pc[9 + i];
+                Y[7] = g77 * Pc[7] + g87 * Pc[8];
+                const double pu9 = from_up<9>(pv), pu1 = from_up<1>(pv);  // DPP in uniform control flow
+                const double fv = gv + gt * pv + ((t < 7) ? pu9 : g87 * pu1);
+                // ---- (2) F column t (t < 8), Gm column t (t < 9); poly terms W_p bv_p bv_p^T, W_p bv_p a_p^T
+                double Wb[NPE], bvb[NPE][8];
 #pragma unroll
-                    for (int i = 0; i < 7; i++) Y[i] = c.G[i * 9] * Pc[i] + Pc[9 + i];
-                    Y[7] = g77 * Pc[7] + g87 * Pc[8];
+                for (int p = 0; p < NPM; p++) {
+                    const bool live = (double)p < cur.np && k < N;
+                    const double wp = bcn(WP, p);
+                    Wb[p] = live ? wp : 0.0;
 #pragma unroll
-                    for (int i = 0; i < 8; i++) S[L_U + i * 16 + t] = Y[i];
+                    for (int i = 0; i < 8; i++) bvb[p][i] = bcn(cur.pb[p], i);
                 }
-                const double* pn = S + L_PV + 16 * pcur;
-                if (t < 8) {
-                    const double bp = (t < 7) ? gt * pn[t] + pn[9 + t] : g77 * pn[7] + g87 * pn[8];
-                    S[L_FV + t] = gv + bp;
-                }
-                lds_sync();
-                // ---- (2) Hb_yy row t, F column t (t < 8), Gm column t (t < 9)
-                double Hb[9];
-                {
-                    const double P77 = S[L_P + 7 * 16 + 7];
+                const double wdv = from_up<9>(wd);  // lane j <- ddq row j weight
+                double Fc[8], gm[8];
 #pragma unroll
-                    for (int cc = 0; cc < 9; cc++) {
-                        const double mc = c.M[cc * 10];
-                        double v = Qr[cc];
-                        if (cc == t) v += wd;
-                        if (t < 7 && cc < 7)
+                for (int i = 0; i < 8; i++) {
+                    const double yu9 = from_up<9>(Y[i]);
+                    const double yu1 = from_up<1>(Y[i]);
+                    const double yd = from_down<1>(Y[i]);
+                    double h = 0.0, hv = 0.0;
+                    if (i == t) h = Rt + ((t < 7) ? wdv : 0.0);
+                    if (i < 7)
 #pragma unroll
-                            for (int p = 0; p < NPM; p++) {
-                                const double* row = S + L_POLY + p * 16;
-                                v += row[15] * (row[t] * row[cc]);
-                            }
-                        double mp = (mt * mc) * Pc[cc];
-                        if (cc == 8) mp += (mt * m78) * Pc[7];
-                        if (t == 8) mp += (m78 * mc) * S[L_P + 7 * 16 + cc];
-                        if (t == 8 && cc == 8) mp += (m78 * m78) * P77;
-                        Hb[cc] = v + mp;
-                    }
-                }
-                double gm[8];
-                {
-                    // F[:, t] = H_vv[:, t] + (Y B~)[:, t];  B~ column j = g_j e_j + e_{9+j} (j < 7), g77 e7 + g87 e8
-                    const bool fj = t < 7;
-                    const int c1 = fj ? t : 7, c2 = fj ? 9 + t : 8;
-                    const double w2 = fj ? 1.0 : g87;
-                    const double wdv = from_up<9>(wd);  // lane j <- ddq row j weight
-                    double Fc[8];
-#pragma unroll
-                    for (int i = 0; i < 8; i++) {
-                        const double v = gt * S[L_U + i * 16 + c1] + w2 * S[L_U + i * 16 + c2];
-                        double h = 0.0;
-                        if (i == t) {
-                            h = Rt;
-                            if (fj) h += wdv;
+                        for (int p = 0; p < NPM; p++) {
+                            h += Wb[p] * (bvb[p][i] * cur.pb[p]);   // bv_p[t]: zero for lanes >= 7
+                            hv += Wb[p] * (bvb[p][i] * cur.pa[p]);  // a_p[t]: zero for lanes >= 7
                         }
-                        if (i < 7 && fj)
-#pragma unroll
-                            for (int p = 0; p < NPM; p++) {
-                                const double* row = S + L_POLY + p * 16;
-                                h += row[15] * (row[7 + i] * row[7 + t]);
-                            }
-                        Fc[i] = h + v;
-                    }
-                    if (t < 8)
-#pragma unroll
-                        for (int i = 0; i < 8; i++) S[L_F + i * 8 + t] = Fc[i];
-                    // Gm[:, t] = H_vy[:, t] + (Y M)[:, t] (t < 9); w columns are diag(Hc - W_ddq) (k >= 1)
-                    const int ct = (t < 9) ? t : 0;
-#pragma unroll
-                    for (int i = 0; i < 8; i++) {
-                        double v = mt * S[L_U + i * 16 + ct];
-                        if (t == 8) v += m78 * S[L_U + i * 16 + 7];
-                        double h = 0.0;
-                        if (i < 7 && t < 7)
-#pragma unroll
-                            for (int p = 0; p < NPM; p++) {
-                                const double* row = S + L_POLY + p * 16;
-                                h += row[15] * (row[7 + i] * row[ct]);
-                            }
-                        gm[i] = h + v;
-                    }
+                    Fc[i] = h + (gt * Y[i] + ((t < 7) ? yu9 : g87 * yu1));
+                    gm[i] = hv + (mt * Y[i] + ((t == 8) ? m78 * yd : 0.0));
                 }
-                lds_sync();
                 PMARK(10);
-                // ---- (3) chol(F); U = LF^-1 Gm; K = -LF^-T U; Finv column (t & 7); kff = -F^-1 f;
-                //          p = g_x~ + A~^T p + K^T f
+                // ---- (3) chol(F) from the broadcast columns; U = LF^-1 Gm; K = -LF^-T U; Finv column (t & 7);
+                //          kff = -F^-1 f; p = g_x~ + A~^T p + K^T f
                 double LF[36], dinv[8];
-                chol_ok = chol8(S + L_F, LF, dinv) && chol_ok;
+#pragma unroll
+                for (int i = 0; i < 8; i++)
+#pragma unroll
+                    for (int j = 0; j <= i; j++) LF[i * (i + 1) / 2 + j] = bcn(Fc[i], j);
+                chol_ok = chol8(LF, dinv) && chol_ok;
                 double u[8];
                 const double gw = (k >= 1) ? Hct - wd : 0.0;
 #pragma unroll
@@ -619,24 +574,30 @@ __global__ void __launch_bounds__(64) k_ipm(DevConst c, DevBuffers d) {
                 for (int i = 0; i < 8; i++) fi[i] = (i == (t & 7)) ? 1.0 : 0.0;
                 fwd8(LF, dinv, fi);
                 bwd8(LF, dinv, fi);
-                double f[8];
+                double fb[8];
 #pragma unroll
-                for (int i = 0; i < 8; i++) f[i] = S[L_FV + i];
+                for (int i = 0; i < 8; i++) fb[i] = bcn(fv, i);
                 double kff = 0.0;
 #pragma unroll
-                for (int m = 0; m < 8; m++) kff -= fi[m] * f[m];
+                for (int m = 0; m < 8; m++) kff -= fi[m] * fb[m];
+                double pnew;
                 {
                     double atp = 0.0;
+                    const double p7 = from_down<1>(pv);
                     if (t < 9) {
-                        atp = mt * pn[t];
-                        if (t == 8) atp += m78 * pn[7];
+                        atp = mt * pv;
+                        if (t == 8) atp += m78 * p7;
                     }
                     double ktf = 0.0;
 #pragma unroll
-                    for (int i = 0; i < 8; i++) ktf += kc[i] * f[i];
-                    S[L_PV + 16 * (pcur ^ 1) + t] = gx + atp + ktf;
+                    for (int i = 0; i < 8; i++) ktf += kc[i] * fb[i];
+                    pnew = gx + atp + ktf;
                 }
                 PMARK(11);
+#ifdef MPCC_IPM_DBGF
+                *ws(k, 35) = gx; *ws(k, 36) = gv; *ws(k, 37) = pv; *ws(k, 38) = fv; *ws(k, 39) = dvr; *ws(k, 40) = cP;
+                *ws(k, 41) = wd; *ws(k, 42) = pnew; *ws(k, 43) = kff;
+#endif
 #pragma unroll
                 for (int i = 0; i < 8; i++) {
                     S[L_U + i * 16 + t] = u[i];
@@ -646,28 +607,68 @@ __global__ void __launch_bounds__(64) k_ipm(DevConst c, DevBuffers d) {
                 *ws(k, WF_KFF) = (t < 8) ? kff : 0.0;
 #pragma unroll
                 for (int m = 0; m < 4; m++) *ws(k, WF_FI + m) = (t < 8) ? fi[m] : fi[4 + m];
-                lds_sync();
+                // ---- (4) Hb column t and P = Hb - U^T U (column t); U rows are broadcast LDS reads
+                double hb[16];
                 {
-                    const int ri = t & 7, hoff = (t < 8) ? 0 : 8;
+                    double Pc7[9];
 #pragma unroll
-                    for (int m = 0; m < 8; m++) *ws(k, WF_KR + m) = S[L_K + ri * 16 + hoff + m];
-                }
-                PMARK(12);
-                // ---- (4) P = Hb - U^T U (lane = row t, upper triangle mirrored)
-                if (k > 0) {
+                    for (int a = 0; a < 9; a++) Pc7[a] = from_down<1>(Pc[a]);  // lane 8 <- P[a][7]
+                    double pab[NPE][7];
 #pragma unroll
-                    for (int cc = 0; cc < 16; cc++) {
-                        if (cc < t) continue;
+                    for (int p = 0; p < NPM; p++)
+#pragma unroll
+                        for (int a = 0; a < 7; a++) pab[p][a] = bcn(cur.pa[p], a);
+#pragma unroll
+                    for (int a = 0; a < 16; a++) {
                         double v = 0.0;
-                        if (t < 9 && cc < 9) v = Hb[cc];
-                        else if (t >= 9 && cc == t) v = wd;
+                        if (a < 9) {
+                            if (t < 9) {
+                                v = Qr[a];
+                                if (a == t) v += wd;
+                                if (a < 7)
 #pragma unroll
-                        for (int i = 0; i < 8; i++) v -= u[i] * S[L_U + i * 16 + cc];
-                        S[L_P + t * 16 + cc] = v;
-                        S[L_P + cc * 16 + t] = v;
+                                    for (int p = 0; p < NPM; p++) v += Wb[p] * (pab[p][a] * cur.pa[p]);
+                                double mp = (mdiag[a] * mt) * Pc[a];
+                                if (t == 8) mp += (mdiag[a] * m78) * Pc7[a];
+                                if (a == 8) mp += (m78 * mt) * Pc[7];
+                                if (a == 8 && t == 8) mp += (m78 * m78) * Pc7[7];
+                                v += mp;
+                            }
+                        } else if (a == t) {
+                            v = wd;
+                        }
+                        hb[a] = v;
                     }
                 }
-                pcur ^= 1;
+                lds_sync();
+                if (k > 0) {
+#pragma unroll
+                    for (int i = 0; i < 8; i++) {
+                        const double2* row = reinterpret_cast<const double2*>(S + L_U + i * 16);
+                        double ur[16];
+#pragma unroll
+                        for (int q2 = 0; q2 < 8; q2++) {
+                            const double2 w = row[q2];
+                            ur[2 * q2] = w.x;
+                            ur[2 * q2 + 1] = w.y;
+                        }
+#pragma unroll
+                        for (int a = 0; a < 16; a++) hb[a] -= ur[a] * u[i];
+                    }
+#pragma unroll
+                    for (int a = 0; a < 16; a++) Pc[a] = hb[a];
+                }
+                {
+                    const int ri = t & 7, hoff = (t < 8) ? 0 : 8;
+                    const double2* row = reinterpret_cast<const double2*>(S + L_K + ri * 16 + hoff);
+#pragma unroll
+                    for (int q2 = 0; q2 < 4; q2++) {
+                        const double2 w = row[q2];
+                        *ws(k, WF_KR + 2 * q2) = w.x;
+                        *ws(k, WF_KR + 2 * q2 + 1) = w.y;
+                    }
+                }
+                pv = pnew;
                 lds_sync();
                 cur = nxt;
                 PMARK(13);
@@ -682,53 +683,24 @@ __global__ void __launch_bounds__(64) k_ipm(DevConst c, DevBuffers d) {
         }
         PMARK(2);
         if (run) {
-            // forward sweep body shared by the predictor and the corrector:
-            // x~_0 = 0; v = K x~ + kff; x~' = A~ x~ + B~ v; returns (x~_k, v_k) of stage k
-            auto fwd_step = [&](int k, const StageIn& in, int xc, double& xt, double& vv) {
-                const double* xs = S + L_X + 16 * xc;
-                xt = xs[t];
-                double v = 0.0;
-                if (k < N) {
-                    const int hoff = (t < 8) ? 0 : 8;
-                    double part = 0.0;
-#pragma unroll
-                    for (int m = 0; m < 8; m++) part += in.m[m] * xs[hoff + m];
-                    v = part + from_up<8>(part) + in.m[8];
-                    const double x8 = xs[8];
-                    const double v7 = from_down<1>(v);
-                    const double vj = from_down<9>(v);
-                    double xn;
-                    if (t < 7) xn = mt * xt + gt * v;
-                    else if (t == 7) xn = (m77 * xt + m78 * x8) + g77 * v;
-                    else if (t == 8) xn = m88 * xt + g87 * v7;
-                    else xn = vj;
-                    S[L_X + 16 * (xc ^ 1) + t] = xn;
-                }
-                vv = (t < 8 && k < N) ? v : 0.0;
-            };
-            // ---- predictor forward: recover dsa, dla; max step; mu(alpha) sums
+            // ---- predictor forward: x~_0 = 0; recover dsa, dla; max step; mu(alpha) sums
             double S0 = 0, S1 = 0, S2 = 0, amax = 1.0;
-            int xc = 0;
-            S[L_X + t] = 0.0;
+            double xt = 0.0;
             load_fwd(0, cur, false);
-            lds_sync();
             for (int k = 0; k <= N; k++) {
                 if (k < N) load_fwd(k + 1, nxt, false);
-                const double pb = stage_poly(cur.pv, cur.np, k);
-                const bool aL = row_active(k, cur.lb), aU = row_active(k, cur.ub), aP = fabs(pb) < BIG;
-                double xt, dvv;
-                fwd_step(k, cur, xc, xt, dvv);
+                const bool aL = row_active(k, cur.lb), aU = row_active(k, cur.ub), aP = poly_slot_active(cur, k);
+                double v = 0.0, xn = 0.0;
+                if (k < N) fwd_step(cur, xt, v, xn);
+                const double dvv = (t < 8 && k < N) ? v : 0.0;
                 *ws(k, WF_AX) = xt;
                 *ws(k, WF_AV) = dvv;
-                put_vec(L_Z, cur.zx, cur.zv);
-                put_vec(L_DA, xt, dvv);
-                lds_sync();
-                const double cz = row_cz(k, L_Z), ca = row_cz(k, L_DA);
-                const double pcz = poly_cz(L_Z), pca = poly_cz(L_DA);
+                const double cz = row_cz(k, cur.zx, cur.zv), ca = row_cz(k, xt, dvv);
+                const double pcz = poly_cz(cur, k, cur.zx, cur.zv), pca = poly_cz(cur, k, xt, dvv);
                 auto rec = [&](bool a, double sgn, double bnd, double czz, double caa, double s, double l) {
                     if (!a) return;
                     const double rp = slot_rp(sgn, czz, bnd, s);
-                    const SlotStep st = slot_recover(s, l, rp, sgn * caa, s * l);
+                    const SlotStep st = slot_recover(1.0 / s, l, rp, sgn * caa, s * l);
                     amax = step_bound(amax, s, l, st);
                     S0 += s * l;
                     S1 += s * st.dl + l * st.ds;
@@ -736,9 +708,8 @@ __global__ void __launch_bounds__(64) k_ipm(DevConst c, DevBuffers d) {
                 };
                 rec(aL, sgnL, cur.lb, cz, ca, cur.sL, cur.lL);
                 rec(aU, sgnU, cur.ub, cz, ca, cur.sU, cur.lU);
-                rec(aP, sgnU, pb, pcz, pca, cur.sP, cur.lP);
-                xc ^= 1;
-                lds_sync();
+                rec(aP, sgnU, cur.pub, pcz, pca, cur.sP, cur.lP);
+                xt = xn;
                 cur = nxt;
             }
             amax = g_min(amax);
@@ -753,105 +724,72 @@ __global__ void __launch_bounds__(64) k_ipm(DevConst c, DevBuffers d) {
 
             // ---- corrector backward: coef with rc = s l + dsa dla - sigma mu; f = g_v + B~^T p;
             //      kff = -F^-1 f; p = g_x~ + A~^T p + K^T f
-            int pcur = 0;
+            double pv = 0.0;
             load_bwd(N, cur);
             for (int k = N; k >= 0; k--) {
                 if (k > 0) load_bwd(k - 1, nxt);
-                const double pb = stage_poly(cur.pv, cur.np, k);
-                const bool aL = row_active(k, cur.lb), aU = row_active(k, cur.ub), aP = fabs(pb) < BIG;
-                put_vec(L_Z, cur.zx, cur.zv);
-                put_vec(L_DA, cur.x0, cur.x1);
-                lds_sync();
-                const double cz = row_cz(k, L_Z), ca = row_cz(k, L_DA);
-                const double pcz = poly_cz(L_Z), pca = poly_cz(L_DA);
+                const bool aL = row_active(k, cur.lb), aU = row_active(k, cur.ub), aP = poly_slot_active(cur, k);
+                const double cz = row_cz(k, cur.zx, cur.zv), ca = row_cz(k, cur.x0, cur.x1);
+                const double pcz = poly_cz(cur, k, cur.zx, cur.zv), pca = poly_cz(cur, k, cur.x0, cur.x1);
                 auto coef = [&](bool a, double sgn, double bnd, double czz, double caa, double s, double l) -> double {
                     if (!a) return 0.0;
                     const double rp = slot_rp(sgn, czz, bnd, s);
-                    const SlotStep pa = slot_recover(s, l, rp, sgn * caa, s * l);
+                    const double ri = 1.0 / s;
+                    const SlotStep pa = slot_recover(ri, l, rp, sgn * caa, s * l);
                     const double rc = s * l + pa.ds * pa.dl - smu;
-                    return slot_coef(s, l, rp, rc);
+                    return slot_coef(ri, l, rp, rc);
                 };
                 const double cL = coef(aL, sgnL, cur.lb, cz, ca, cur.sL, cur.lL);
                 const double cU = coef(aU, sgnU, cur.ub, cz, ca, cur.sU, cur.lU);
-                const double cP = coef(aP, sgnU, pb, pcz, pca, cur.sP, cur.lP);
+                const double cP = coef(aP, sgnU, cur.pub, pcz, pca, cur.sP, cur.lP);
                 const double dvr = sgnL * cL + sgnU * cU;
-                S[L_PC + t] = cP;
-                lds_sync();
-                double gx = cur.x2, gv = cur.x3;
-                if (t < 9) {
-                    gx += dvr;
-                    if (t < 7)
-#pragma unroll
-                        for (int p = 0; p < NPM; p++) gx += S[L_PC + p] * S[L_POLY + p * 16 + t];
-                } else if (k >= 1) {
-                    gx -= dvr;
-                }
-                const double dv_up = from_up<9>(dvr);
-                if (t < 7 && k < N) {
-                    gv += dv_up;
-#pragma unroll
-                    for (int p = 0; p < NPM; p++) gv += S[L_PC + p] * S[L_POLY + p * 16 + 7 + t];
-                }
+                double gx, gv;
+                assemble_grad(cur, k, cur.x2, cur.x3, dvr, cP, gx, gv);
                 if (k == N) {
-                    S[L_PV + t] = gx;
-                    pcur = 0;
-                    lds_sync();
+                    pv = gx;
                     cur = nxt;
                     continue;
                 }
-                const double* pn = S + L_PV + 16 * pcur;
-                if (t < 8) {
-                    const double bp = (t < 7) ? gt * pn[t] + pn[9 + t] : g77 * pn[7] + g87 * pn[8];
-                    S[L_FV + t] = gv + bp;
-                }
-                lds_sync();
-                double f[8];
+                const double pu9 = from_up<9>(pv), pu1 = from_up<1>(pv);  // DPP in uniform control flow
+                const double fv = gv + gt * pv + ((t < 7) ? pu9 : g87 * pu1);
+                double fb[8];
 #pragma unroll
-                for (int i = 0; i < 8; i++) f[i] = S[L_FV + i];
-                const int hoff = (t < 8) ? 0 : 4;
+                for (int i = 0; i < 8; i++) fb[i] = bcn(fv, i);
                 double part = 0.0;
 #pragma unroll
-                for (int m = 0; m < 4; m++) part -= cur.m[8 + m] * f[hoff + m];
+                for (int m = 0; m < 4; m++) part -= cur.m[8 + m] * ((t < 8) ? fb[m] : fb[4 + m]);
                 const double kff = part + from_up<8>(part);
                 *ws(k, WF_KFF) = (t < 8) ? kff : 0.0;
-                if (k > 0) {
-                    double atp = 0.0;
-                    if (t < 9) {
-                        atp = mt * pn[t];
-                        if (t == 8) atp += m78 * pn[7];
-                    }
-                    double ktf = 0.0;
-#pragma unroll
-                    for (int i = 0; i < 8; i++) ktf += cur.m[i] * f[i];
-                    S[L_PV + 16 * (pcur ^ 1) + t] = gx + atp + ktf;
+                double atp = 0.0;
+                const double p7 = from_down<1>(pv);
+                if (t < 9) {
+                    atp = mt * pv;
+                    if (t == 8) atp += m78 * p7;
                 }
-                pcur ^= 1;
-                lds_sync();
+                double ktf = 0.0;
+#pragma unroll
+                for (int i = 0; i < 8; i++) ktf += cur.m[i] * fb[i];
+                pv = gx + atp + ktf;
                 cur = nxt;
             }
             PMARK(4);
 
             // ---- corrector forward: dz, ds, dl, max step, mu(alpha) sums, max |rp|, max |dz|
             double T0 = 0, T1 = 0, T2 = 0, amx = 1e30, rpm = 0, dzm = 0;
-            xc = 0;
-            S[L_X + t] = 0.0;
+            xt = 0.0;
             load_fwd(0, cur, true);
-            lds_sync();
             for (int k = 0; k <= N; k++) {
                 if (k < N) load_fwd(k + 1, nxt, true);
-                const double pb = stage_poly(cur.pv, cur.np, k);
-                const bool aL = row_active(k, cur.lb), aU = row_active(k, cur.ub), aP = fabs(pb) < BIG;
-                double xt, dvv;
-                fwd_step(k, cur, xc, xt, dvv);
+                const bool aL = row_active(k, cur.lb), aU = row_active(k, cur.ub), aP = poly_slot_active(cur, k);
+                double v = 0.0, xn = 0.0;
+                if (k < N) fwd_step(cur, xt, v, xn);
+                const double dvv = (t < 8 && k < N) ? v : 0.0;
                 *ws(k, WF_DX) = xt;
                 *ws(k, WF_DV) = dvv;
                 dzm = fmax(dzm, fmax(fabs(xt), fabs(dvv)));
-                put_vec(L_Z, cur.zx, cur.zv);
-                put_vec(L_DZ, xt, dvv);
-                put_vec(L_DA, cur.x0, cur.x1);
-                lds_sync();
-                const double cz = row_cz(k, L_Z), cd = row_cz(k, L_DZ), ca = row_cz(k, L_DA);
-                const double pcz = poly_cz(L_Z), pcd = poly_cz(L_DZ), pca = poly_cz(L_DA);
+                const double cz = row_cz(k, cur.zx, cur.zv), cd = row_cz(k, xt, dvv), ca = row_cz(k, cur.x0, cur.x1);
+                const double pcz = poly_cz(cur, k, cur.zx, cur.zv), pcd = poly_cz(cur, k, xt, dvv);
+                const double pca = poly_cz(cur, k, cur.x0, cur.x1);
                 auto rec = [&](bool a, double sgn, double bnd, double czz, double caa, double cdd, double s, double l) {
                     if (!a) return;
                     double rp;
@@ -864,9 +802,8 @@ __global__ void __launch_bounds__(64) k_ipm(DevConst c, DevBuffers d) {
                 };
                 rec(aL, sgnL, cur.lb, cz, ca, cd, cur.sL, cur.lL);
                 rec(aU, sgnU, cur.ub, cz, ca, cd, cur.sU, cur.lU);
-                rec(aP, sgnU, pb, pcz, pca, pcd, cur.sP, cur.lP);
-                xc ^= 1;
-                lds_sync();
+                rec(aP, sgnU, cur.pub, pcz, pca, pcd, cur.sP, cur.lP);
+                xt = xn;
                 cur = nxt;
             }
             amx = g_min(amx);
@@ -931,14 +868,7 @@ extern "C" int mpcc_debug_ipm_prof(unsigned long long* out, int reset) {
 
 template <int NPM>
 static void launch_ipm_t(const DevConst& c, const DevBuffers& d, hipStream_t s) {
-    const size_t lds = ipm_lds_bytes(c.N, NPM);
-    static bool configured = false;
-    if (!configured) {
-        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_ipm<NPM>), hipFuncAttributeMaxDynamicSharedMemorySize,
-                                  (int)lds);
-        configured = true;
-    }
-    hipLaunchKernelGGL(k_ipm<NPM>, dim3((c.Bn + IPW - 1) / IPW), dim3(64), lds, s, c, d);
+    hipLaunchKernelGGL(k_ipm<NPM>, dim3((c.Bn + IPW - 1) / IPW), dim3(64), ipm_lds_bytes(c.N, NPM), s, c, d);
 }
 
 void launch_ipm(const DevConst& c, const DevBuffers& d, int npmax, hipStream_t s) {

@@ -119,6 +119,7 @@ def lib():
         "mpcc_debug_stage_cost": (C.c_int, [V, C.c_int, DP, DP, DP, IP, DP, DP, DP, DP, DP]),
         "mpcc_debug_solve_qp": (C.c_int, [V, C.c_int, DP, DP, DP, DP, IP, IP]),
         "mpcc_debug_trace_enable": (C.c_int, [V, C.c_int]),
+        "mpcc_debug_workspace": (C.c_int, [V, C.c_int, DP]),
         "mpcc_debug_project": (C.c_int, [V, C.c_int, DP, DP, DP]),
         "mpcc_debug_trace_get": (C.c_int, [V, C.c_int, DP]),
     }
@@ -421,6 +422,12 @@ class Engine:
         e = _f64(ee, (M, 3))
         out = np.zeros(M)
         _check(self.L.mpcc_debug_project(self.h, M, _dp(sg), _dp(e), _dp(out)), "mpcc_debug_project")
+        return out
+
+    def workspace(self, B):
+        """Interior-point workspace of the last solve, [B, N+1, 816] (test instrumentation)."""
+        out = np.zeros((B, self.N + 1, 816))
+        _check(self.L.mpcc_debug_workspace(self.h, B, _dp(out)), "mpcc_debug_workspace")
         return out
 
     def trace_enable(self, on=True):
