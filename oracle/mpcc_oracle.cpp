@@ -1962,6 +1962,16 @@ int oracle_run_mpc(void* h, int B, double* x0, const double* u0, const double* o
     return oracle_run_mpc_trace(h, B, x0, u0, obs, guess, valid, fails, u0_out, horizon, status, ok, sqp_iters, nullptr);
 }
 int oracle_rec_size(void) { return REC; }
+// CubicSpline (cubic_spline.cpp:126-246) on (x, y): value, first and second derivative at xq
+void oracle_cubic_spline(int n, const double* x, const double* y, int regular, int m, const double* xq, double* out3) {
+    CubicSpline sp;
+    sp.gen(std::vector<double>(x, x + n), std::vector<double>(y, y + n), regular != 0);
+    for (int i = 0; i < m; i++) {
+        out3[3 * i] = sp.point(xq[i]);
+        out3[3 * i + 1] = sp.deriv(xq[i]);
+        out3[3 * i + 2] = sp.deriv2(xq[i]);
+    }
+}
 int oracle_prepare(void* h, int B, double* x0, const double* u0, const double* obs, double* guess, int* valid, int* fails,
                    double* recs) {
     Oracle* o = (Oracle*)h;

@@ -112,6 +112,8 @@ int    oracle_run_mpc_trace(void* h, int B, double* x0, const double* u0, const 
                             double* trace);
 
 int    oracle_rec_size(void);
+/* CubicSpline (cubic_spline.cpp) fit to (x, y) [n], evaluated at xq [m] -> out [m*3]: y, y', y'' */
+void   oracle_cubic_spline(int n, const double* x, const double* y, int regular, int m, const double* xq, double* out3);
 
 #ifdef __cplusplus
 }

@@ -88,6 +88,8 @@ def lib():
         L.oracle_sim_time_step.argtypes = [DP, DP, D, DP]
         L.oracle_run_mpc.restype = C.c_int
         L.oracle_run_mpc.argtypes = [C.c_void_p, C.c_int, DP, DP, DP, DP, IP, IP, DP, DP, IP, IP, IP]
+        L.oracle_cubic_spline.restype = None
+        L.oracle_cubic_spline.argtypes = [C.c_int, DP, DP, C.c_int, C.c_int, DP, DP]
         L.oracle_prepare.restype = C.c_int
         L.oracle_prepare.argtypes = [C.c_void_p, C.c_int, DP, DP, DP, DP, IP, IP, DP]
         L.oracle_run_mpc_trace.restype = C.c_int
@@ -247,6 +249,14 @@ class Oracle:
     def sim_time_step(self, x, u, ts):
         out = np.zeros(9)
         self.L.oracle_sim_time_step(_dp(_f64(x)), _dp(_f64(u)), float(ts), _dp(out))
+        return out
+
+    @staticmethod
+    def cubic_spline(x, y, xq, regular=True):
+        """CubicSpline (cubic_spline.cpp) fit to (x, y), evaluated at xq -> [m, 3] (y, y', y'')."""
+        x, y, xq = _f64(x), _f64(y), _f64(xq)
+        out = np.zeros((xq.shape[0], 3))
+        lib().oracle_cubic_spline(x.shape[0], _dp(x), _dp(y), 1 if regular else 0, xq.shape[0], _dp(xq), _dp(out))
         return out
 
     def prepare(self, x0, u0, obs, guess, valid, fails):

@@ -204,3 +204,55 @@ def test_benchmark_batch_parity(built_lib, oracle_lib, mask, B):
     assert np.abs(xg - xo).max() <= 1e-9
     assert np.array_equal(vg, vo) and np.array_equal(fg, fo)
     eng.close()
+
+
+# ---------------------------------------------------------------- committed golden vectors
+def _gold(name):
+    import os
+    return np.load(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", name), allow_pickle=False)
+
+
+def test_golden_records_gpu(setup20):
+    m, o, eng, pool = setup20
+    g = _gold("records.npz")
+    rec = eng.robot_records(g["q"], g["obs"])
+    assert np.allclose(rec[:, :55], g["rec"][:, :55], rtol=1e-11, atol=1e-13)
+    assert np.allclose(rec[:, 55:62], g["rec"][:, 55:62], rtol=1e-7, atol=1e-9)
+    assert np.allclose(rec[:, 62:], g["rec"][:, 62:], rtol=1e-10, atol=1e-10)
+
+
+def test_golden_qp_step_gpu(setup20):
+    m, o, eng, pool = setup20
+    g = _gold("qp_step.npz")
+    step, st, it = eng.solve_qp(g["guess"], g["rec"], g["ucur"])
+    assert np.array_equal(st, g["status"])
+    assert np.abs(step - g["step"]).max() < 1e-8
+
+
+def test_golden_batch_mask2_gpu(built_lib, oracle_lib):
+    import mpcc_manipulator_amd as m
+    g = _gold("batch_mask2.npz")
+    o, P, track = make_oracle(N=20, max_iter=2, mask=2)
+    params = m.load_params(N=20, overrides={"sqp": {"max_iter": 2}})
+    eng = m.Engine(params, max_batch=64, constraint_mask=2)
+    eng.set_track(*track)
+    eng.set_warmstart(g["guess"], g["valid"], g["fails"])
+    xg = g["x0"].copy()
+    out = eng.solve(xg, g["u0"], g["obs"])
+    assert np.array_equal(out["status"], g["status"])
+    assert np.abs(out["horizon"][:, :-1, 9:] - g["horizon"][:, :-1, 9:]).max() <= 1e-6
+    assert np.abs(xg - g["x0_out"]).max() <= 1e-9
+    eng.close()
+
+
+def test_golden_closed_loop_gpu(setup20):
+    """The engine drives the 60-step closed loop of the fixture (status and u0 at every step)."""
+    m, o, eng, pool = setup20
+    g = _gold("closed_loop_n20.npz")
+    eng.reset_warmstart(1)
+    for step in range(g["x"].shape[0]):
+        x = g["x"][step:step + 1].copy()
+        u = g["u0"][step - 1:step].copy() if step else np.zeros((1, 8))
+        out = eng.solve(x, u, g["obs"][None, :])
+        assert out["status"][0] == g["status"][step], step
+        assert np.abs(out["u0"][0] - g["u0"][step]).max() <= 1e-6, step
