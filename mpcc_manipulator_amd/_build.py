@@ -27,7 +27,8 @@ def _compile(src):
     path = os.path.join(CSRC, src)
     obj = os.path.join(BUILD, os.path.splitext(src)[0] + ".o")
     deps = [path] + [os.path.join(CSRC, h) for h in os.listdir(CSRC) if h.endswith(".h")]
-    deps.append(os.path.join(ROOT, "include", "mpcc_engine.h"))
+    inc = os.path.join(ROOT, "include")
+    deps += [os.path.join(inc, h) for h in os.listdir(inc)]
     if os.path.exists(obj) and os.path.getmtime(obj) >= max(os.path.getmtime(d) for d in deps):
         return obj
     lang = ["-x", "hip"] if src.endswith(".cpp") else []
@@ -42,15 +43,39 @@ def build(verbose=False):
     os.makedirs(BUILD, exist_ok=True)
     with cf.ThreadPoolExecutor(max_workers=min(8, len(SOURCES))) as ex:
         objs = list(ex.map(_compile, SOURCES))
-    if os.path.exists(LIB) and os.path.getmtime(LIB) >= max(os.path.getmtime(o) for o in objs):
-        return LIB
-    cmd = [HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", LIB] + objs
-    r = subprocess.run(cmd, capture_output=True, text=True)
-    if r.returncode != 0:
-        raise RuntimeError(f"link failed: {' '.join(cmd)}\n{r.stdout}\n{r.stderr}")
-    if verbose:
-        print("built", LIB)
+    if not (os.path.exists(LIB) and os.path.getmtime(LIB) >= max(os.path.getmtime(o) for o in objs)):
+        cmd = [HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", LIB] + objs
+        r = subprocess.run(cmd, capture_output=True, text=True)
+        if r.returncode != 0:
+            raise RuntimeError(f"link failed: {' '.join(cmd)}\n{r.stdout}\n{r.stderr}")
+        if verbose:
+            print("built", LIB)
+    build_examples(verbose)
     return LIB
+
+
+EXAMPLES = os.path.join(ROOT, "examples")
+
+
+def build_examples(verbose=False):
+    """C++ programs on the host surface (include/mpcc_mpc.hpp), linked against the engine with g++."""
+    out = []
+    for src in sorted(os.listdir(EXAMPLES)) if os.path.isdir(EXAMPLES) else []:
+        if not src.endswith(".cpp"):
+            continue
+        exe = os.path.join(BUILD, os.path.splitext(src)[0])
+        path = os.path.join(EXAMPLES, src)
+        deps = [path, LIB] + [os.path.join(ROOT, "include", h) for h in os.listdir(os.path.join(ROOT, "include"))]
+        if not (os.path.exists(exe) and os.path.getmtime(exe) >= max(os.path.getmtime(d) for d in deps)):
+            cmd = ["g++", "-O2", "-std=c++17", "-I", os.path.join(ROOT, "include"), path, "-o", exe,
+                   "-L", BUILD, "-lmpcc_engine", "-Wl,-rpath,$ORIGIN"]
+            r = subprocess.run(cmd, capture_output=True, text=True)
+            if r.returncode != 0:
+                raise RuntimeError(f"example build failed: {' '.join(cmd)}\n{r.stdout}\n{r.stderr}")
+            if verbose:
+                print("built", exe)
+        out.append(exe)
+    return out
 
 
 if __name__ == "__main__":

@@ -8,12 +8,15 @@ validity, filter decisions, eps_prim test): the stage kernels follow the oracle'
 without FMA contraction, and parity policies P1 (violation noise floor) and P2 (Riccati breakdown at a
 converged iterate) are shared by both sides.
 """
+import os
+
 import numpy as np
 import pytest
 
 from helpers import Q0, SEED, batch_from_pool, make_oracle, max_rel, oracle_pool
 
 pytestmark = pytest.mark.gpu
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
 @pytest.fixture(scope="module")
@@ -256,3 +259,20 @@ def test_golden_closed_loop_gpu(setup20):
         out = eng.solve(x, u, g["obs"][None, :])
         assert out["status"][0] == g["status"][step], step
         assert np.abs(out["u0"][0] - g["u0"][step]).max() <= 1e-6, step
+
+
+def test_cpp_mpc_closed_loop_golden(built_lib):
+    """The C++ host surface (mpcc_amd::MPC, examples/mpc_closed_loop.cpp: the reference main.cpp loop)
+    reproduces the golden closed loop: status at every step, u0 within 1e-6, states within 1e-6."""
+    import subprocess
+    g = _gold("closed_loop_n20.npz")
+    exe = os.path.join(os.path.dirname(built_lib), "mpc_closed_loop")
+    steps = g["x"].shape[0]
+    r = subprocess.run([exe, os.path.join(ROOT, "mpcc_manipulator_amd", "data"), str(steps)] +
+                       [repr(float(v)) for v in g["obs"]], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr
+    rows = np.array([[float(v) for v in line.split(",")] for line in r.stdout.strip().splitlines()])
+    assert rows.shape == (steps, 1 + 9 + 8 + 2)
+    assert np.abs(rows[:, 1:10] - g["x"]).max() <= 1e-6
+    assert np.abs(rows[:, 10:18] - g["u0"]).max() <= 1e-6
+    assert np.array_equal(rows[:, 18].astype(np.int32), g["status"])

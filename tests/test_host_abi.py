@@ -135,3 +135,23 @@ def test_host_integrator_matches_oracle(built_lib, oracle_lib):
     xs = sim_time_step(x, u, 0.01)
     for i in range(6):
         assert np.allclose(xs[i], o.sim_time_step(x[i], u[i], 0.01), rtol=0, atol=1e-15)
+
+
+def test_cpp_surface_exported(built_lib):
+    """The C++ host mirror (include/mpcc_mpc.hpp) is compiled into the same library."""
+    import subprocess
+    syms = subprocess.run(["nm", "-DC", built_lib], capture_output=True, text=True, check=True).stdout
+    for s in ("mpcc_amd::MPC::runMPC_(", "mpcc_amd::MPC::setTrack(", "mpcc_amd::MPC::setParam(",
+              "mpcc_amd::BatchMPC::runMPCBatch(", "mpcc_amd::loadTrack(", "mpcc_amd::defaultPaths("):
+        assert s in syms, s
+
+
+@pytest.mark.skipif(torch.cuda.device_count() > 0, reason="checks the no-GPU failure path")
+def test_cpp_example_fails_loudly_without_gpu(built_lib):
+    """examples/mpc_closed_loop on a machine without a GPU exits 1 with the HIP error (no fallback)."""
+    import subprocess
+    exe = os.path.join(os.path.dirname(built_lib), "mpc_closed_loop")
+    r = subprocess.run([exe, os.path.join(ROOT, "mpcc_manipulator_amd", "data"), "1"], capture_output=True,
+                       text=True, timeout=60)
+    assert r.returncode == 1
+    assert "mpcc_create" in r.stderr and r.stdout == ""
