@@ -143,6 +143,11 @@ int  mpcc_get_params(mpcc_engine* e, mpcc_params* out);
  * the host (gen6DSpline, arc_length_spline.cpp:213-265) and uploads its tables.  Invalidates
  * every instance's warm start (mpc.cpp:196). */
 int    mpcc_set_track(mpcc_engine* e, int n, const double* X, const double* Y, const double* Z, const double* R9);
+/* SolverInterface::setTrack(const ArcLengthSpline) (solver_interface.h:46): the spline's regular path
+ * data (ArcLengthSpline::getPathData(), arc_length_spline.h:108) — n = 100 points — refit exactly as
+ * the reference's final fit (arc_length_spline.cpp:245-252).  Invalidates every warm start. */
+int    mpcc_set_track_path(mpcc_engine* e, int n, const double* s, const double* X, const double* Y, const double* Z,
+                           const double* R9);
 double mpcc_track_length(mpcc_engine* e);
 /* final regular path data (getPathData): s, X, Y, Z [100], R9 [100*9] */
 /* host-only: build the arc-length spline from way-points without an engine (no GPU needed) and
@@ -178,6 +183,15 @@ int mpcc_solve(mpcc_engine* e, int B, double* x0, const double* u0, const double
  * Instances [0, B) of the engine's warm-start state are used. */
 int mpcc_solve_device(mpcc_engine* e, int B, double* d_x0, const double* d_u0, const double* d_obs,
                       double* d_u0_out, double* d_horizon, int32_t* d_status, int32_t* d_ok, void* stream);
+
+/* SolverInterface granularity (solver_interface.h:44-54): for B instances, setInitialGuess(guess) +
+ * setCurrentInput(u_cur) + setEnvData(obs) + solveOCP(opt_sol, status, time)
+ * (osqp_interface.cpp:102-127, 398-590).  No projection, warm-start shift or valid/fail bookkeeping:
+ * that stays with the caller's MPC (mpc.cpp:104-189), as in the reference.  guess, opt_sol
+ * [B*(N+1)*17]; u_cur [B*8]; obs [B*4]; status [B]; solved [B] = solveOCP's bool (may be NULL).
+ * Uses the engine's warm-start slots [0, B) as the iterate (they are overwritten). */
+int mpcc_solve_ocp(mpcc_engine* e, int B, const double* guess, const double* u_cur, const double* obs,
+                   double* opt_sol, int32_t* status, int32_t* solved, mpcc_timing* timing);
 
 /* Integrator::simTimeStep (integrator.cpp:55-68) for B states, host arrays (closed-loop driver). */
 int mpcc_sim_time_step(mpcc_engine* e, int B, const double* x, const double* u, double ts, double* x_next);

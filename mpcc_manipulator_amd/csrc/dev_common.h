@@ -83,6 +83,7 @@ struct DevConst {
     int S;                           // record stride = B*(N+1) of this call
     int Bn;                          // batch size of this call
     int faithful_dead_trials;
+    int ocp;                         // 1: SolverInterface::solveOCP only (mpcc_solve_ocp), no MPC bookkeeping
 };
 
 // ------------------------------------------------------------------------------------------------

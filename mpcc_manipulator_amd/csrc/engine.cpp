@@ -215,6 +215,8 @@ void validate_params(const mpcc_params& p) {
     for (int i = 0; i < 9; i++) if (!(p.Tx[i] > 0)) throw std::invalid_argument("T_x must be > 0");
     for (int i = 0; i < 8; i++) if (!(p.Tu[i] > 0)) throw std::invalid_argument("T_u must be > 0");
     if (p.max_iter < 0 || p.line_search_max_iter < 0) throw std::invalid_argument("negative iteration limit");
+    if (p.do_SOC || p.use_BFGS)  // off in the reference's sqp.json and off the benchmark path
+        throw std::invalid_argument("do_SOC / use_BFGS (osqp_interface.cpp:658-757) are not supported by this engine");
 }
 
 void upload_track(mpcc_engine* e) {
@@ -243,8 +245,9 @@ void upload_track(mpcc_engine* e) {
     s.L = t.length();
 }
 
-void run_batch(mpcc_engine* e, int B, hipStream_t st, mpcc_timing* timing) {
+void run_batch(mpcc_engine* e, int B, hipStream_t st, mpcc_timing* timing, bool ocp = false) {
     DevConst c = e->make_const(B);
+    c.ocp = ocp ? 1 : 0;
     DevBuffers& d = e->d;
     // Event recording: 'timing' (one synchronous call) or live mode (pairs kept until timing_end).
     const bool tm = timing != nullptr || e->live;
@@ -423,6 +426,22 @@ int mpcc_set_track(mpcc_engine* e, int n, const double* X, const double* Y, cons
         return fail(MPCC_E_HIP, std::string("mpcc_set_track: ") + x.what());
     } catch (const std::exception& x) {
         return fail(MPCC_E_INVALID, std::string("mpcc_set_track: ") + x.what());
+    }
+    return MPCC_OK;
+}
+
+int mpcc_set_track_path(mpcc_engine* e, int n, const double* s, const double* X, const double* Y, const double* Z,
+                        const double* R9) {
+    if (!e || !s || !X || !Y || !Z || !R9) return fail(MPCC_E_INVALID, "mpcc_set_track_path: invalid argument");
+    try {
+        e->track = build_track_from_path(n, s, X, Y, Z, R9);
+        upload_track(e);
+        e->has_track = true;
+        HIPCHK(hipMemset(e->d.valid, 0, (size_t)e->maxB * sizeof(int32_t)));
+    } catch (const HipError& x) {
+        return fail(MPCC_E_HIP, std::string("mpcc_set_track_path: ") + x.what());
+    } catch (const std::exception& x) {
+        return fail(MPCC_E_INVALID, std::string("mpcc_set_track_path: ") + x.what());
     }
     return MPCC_OK;
 }
@@ -616,6 +635,30 @@ int mpcc_solve(mpcc_engine* e, int B, double* x0, const double* u0, const double
         HIPCHK(hipStreamSynchronize(st));
     } catch (const HipError& x) {
         return fail(MPCC_E_HIP, std::string("mpcc_solve: ") + x.what());
+    }
+    return MPCC_OK;
+}
+
+int mpcc_solve_ocp(mpcc_engine* e, int B, const double* guess, const double* u_cur, const double* obs,
+                   double* opt_sol, int32_t* status, int32_t* solved, mpcc_timing* timing) {
+    if (!e || B < 1 || B > e->maxB || !guess || !u_cur || !obs || !opt_sol)
+        return fail(MPCC_E_INVALID, "mpcc_solve_ocp: invalid argument");
+    if (!e->has_track) return fail(MPCC_E_NOTRACK, "mpcc_solve_ocp: set_track first");
+    try {
+        hipStream_t st = e->stream;
+        const size_t NS = e->N + 1;
+        HIPCHK(hipMemcpyAsync(e->d.guess, guess, B * NS * 17 * sizeof(double), hipMemcpyHostToDevice, st));
+        HIPCHK(hipMemcpyAsync(e->s_u0, u_cur, B * 8 * sizeof(double), hipMemcpyHostToDevice, st));
+        HIPCHK(hipMemcpyAsync(e->s_obs, obs, B * 4 * sizeof(double), hipMemcpyHostToDevice, st));
+        e->d.x0 = e->s_x0; e->d.u0 = e->s_u0; e->d.obs = e->s_obs;
+        e->d.u0_out = e->s_u0out; e->d.horizon = e->s_hor; e->d.status = e->s_status; e->d.ok = e->s_ok;
+        run_batch(e, B, st, timing, true);
+        HIPCHK(hipMemcpyAsync(opt_sol, e->s_hor, B * NS * 17 * sizeof(double), hipMemcpyDeviceToHost, st));
+        if (status) HIPCHK(hipMemcpyAsync(status, e->s_status, B * sizeof(int32_t), hipMemcpyDeviceToHost, st));
+        if (solved) HIPCHK(hipMemcpyAsync(solved, e->s_ok, B * sizeof(int32_t), hipMemcpyDeviceToHost, st));
+        HIPCHK(hipStreamSynchronize(st));
+    } catch (const HipError& x) {
+        return fail(MPCC_E_HIP, std::string("mpcc_solve_ocp: ") + x.what());
     }
     return MPCC_OK;
 }

@@ -5,6 +5,7 @@
 #include <cmath>
 #include <cstring>
 #include <map>
+#include <stdexcept>
 
 namespace mpcc {
 
@@ -256,6 +257,21 @@ SplineTables build_track_spline(int n, const double* X, const double* Y, const d
     CubicRot f2r;
     f2x.gen(sa, p1.X, false); f2y.gen(sa, p1.Y, false); f2z.gen(sa, p1.Z, false); f2r.gen(sa, p1.R, false);
     Path p2 = resample(f2x, f2y, f2z, f2r, total);
+    std::vector<double> R2((size_t)NSPLINE * 9);
+    for (int i = 0; i < NSPLINE; i++) std::memcpy(&R2[(size_t)9 * i], p2.R[i].data(), sizeof(double) * 9);
+    return build_track_from_path(NSPLINE, p2.s.data(), p2.X.data(), p2.Y.data(), p2.Z.data(), R2.data());
+}
+
+SplineTables build_track_from_path(int n, const double* s, const double* X, const double* Y, const double* Z,
+                                   const double* R9) {
+    if (n != NSPLINE) throw std::invalid_argument("path data must have N_SPLINE = 100 points (config.h:38)");
+    for (int i = 1; i < n; i++)
+        if (!(s[i] > s[i - 1])) throw std::invalid_argument("path data s must be strictly increasing");
+    Path p2;
+    p2.s.assign(s, s + n); p2.X.assign(X, X + n); p2.Y.assign(Y, Y + n); p2.Z.assign(Z, Z + n);
+    p2.R.resize(n);
+    for (int i = 0; i < n; i++) std::memcpy(p2.R[i].data(), R9 + 9 * i, sizeof(double) * 9);
+    // final spline fit with fixed delta s (arc_length_spline.cpp:245-252)
     Cubic fx, fy, fz;
     CubicRot fr;
     fx.gen(p2.s, p2.X, true); fy.gen(p2.s, p2.Y, true); fz.gen(p2.s, p2.Z, true); fr.gen(p2.s, p2.R, true);

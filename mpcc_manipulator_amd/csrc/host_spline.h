@@ -23,6 +23,11 @@ struct SplineTables {
 // Build from way-points (MPC::setTrack(X, Y, Z, R)); R9 = n row-major 3x3 matrices.
 SplineTables build_track_spline(int n, const double* X, const double* Y, const double* Z, const double* R9);
 
+// Final regular fit only (arc_length_spline.cpp:245-252) from ArcLengthSpline::getPathData():
+// n = N_SPLINE points, s strictly increasing.  build_track_spline ends with this call.
+SplineTables build_track_from_path(int n, const double* s, const double* X, const double* Y, const double* Z,
+                                   const double* R9);
+
 // quaternion (x, y, z, w) -> rotation as Eigen Quaterniond::normalized().toRotationMatrix() (track.cpp:45-53)
 void quat_to_rot(double qx, double qy, double qz, double qw, double* R9);
 

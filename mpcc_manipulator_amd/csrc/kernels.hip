@@ -19,9 +19,8 @@ namespace mpcc {
 // ------------------------------------------------------------------------------------------------
 // k_prepare
 // ------------------------------------------------------------------------------------------------
-__global__ void __launch_bounds__(64) k_prepare(DevConst c, DevBuffers d) {
-    const int b = blockIdx.x * blockDim.x + threadIdx.x;
-    if (b >= c.Bn) return;
+// MPC::runMPC_ before solveOCP (mpc.cpp:104-124, 54-89): projection, vs estimate, guess shift
+__device__ inline void prepare_mpc(const DevConst& c, const DevBuffers& d, int b) {
     const int N = c.N;
     double x[9], u[8];
 #pragma unroll
@@ -65,6 +64,13 @@ __global__ void __launch_bounds__(64) k_prepare(DevConst c, DevBuffers d) {
     for (int i = 0; i < 9; i++) d.x0[9 * b + i] = x[i];
     d.valid[b] = valid;
     d.fails[b] = fails;
+}
+
+__global__ void __launch_bounds__(64) k_prepare(DevConst c, DevBuffers d) {
+    const int b = blockIdx.x * blockDim.x + threadIdx.x;
+    if (b >= c.Bn) return;
+    const int N = c.N;
+    if (!c.ocp) prepare_mpc(c, d, b);
     int32_t* si = d.sqi + (size_t)b * SQI;
     si[SQ_STATUS] = MPCC_MAX_ITER_EXCEEDED;
     si[SQ_ACTIVE] = 1;
@@ -573,12 +579,16 @@ __global__ void __launch_bounds__(64) k_finalize(DevConst c, DevBuffers d) {
     } else {
         for (int a = 0; a < 8; a++) g[17 * N + 9 + a] = 0.0;
     }
-    int fails = d.fails[b];
-    if (status == MPCC_SOLVED) { d.valid[b] = 1; fails = 0; }
-    else { d.valid[b] = 0; fails++; }
-    d.fails[b] = fails;
     if (d.status) d.status[b] = status;
-    if (d.ok) d.ok[b] = (status == MPCC_SOLVED || (status == MPCC_MAX_ITER_EXCEEDED && fails < 5)) ? 1 : 0;
+    if (c.ocp) {  // solveOCP's return value only; the MPC bookkeeping belongs to the caller
+        if (d.ok) d.ok[b] = (status == MPCC_SOLVED) ? 1 : 0;
+    } else {
+        int fails = d.fails[b];
+        if (status == MPCC_SOLVED) { d.valid[b] = 1; fails = 0; }
+        else { d.valid[b] = 0; fails++; }
+        d.fails[b] = fails;
+        if (d.ok) d.ok[b] = (status == MPCC_SOLVED || (status == MPCC_MAX_ITER_EXCEEDED && fails < 5)) ? 1 : 0;
+    }
     if (d.u0_out)
         for (int a = 0; a < 8; a++) d.u0_out[8 * b + a] = g[9 + a];
     if (d.horizon)

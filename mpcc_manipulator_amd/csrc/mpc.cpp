@@ -26,8 +26,11 @@ mpcc_params load(int N, double Ts, const PathToJson& path, const ParamValue& pv,
     p.sqp_path = cs(path.sqp_path);
     p.merged_path = cs(path.merged_path);
     std::vector<mpcc_override> ov;
-    for (const auto& sec : pv)
-        for (const auto& kv : sec.second) ov.push_back({sec.first.c_str(), kv.first.c_str(), kv.second});
+    const std::pair<const char*, const std::map<std::string, double>*> secs[] = {
+        {"param", &pv.param}, {"cost", &pv.cost}, {"bounds", &pv.bounds},
+        {"normalization", &pv.normalization}, {"sqp", &pv.sqp}};
+    for (const auto& sec : secs)
+        for (const auto& kv : *sec.second) ov.push_back({sec.first, kv.first.c_str(), kv.second});
     mpcc_params out;
     check(mpcc_params_load_json(&p, ov.empty() ? nullptr : ov.data(), (int)ov.size(), ctor ? 1 : 0, N, &out),
           "mpcc_params_load_json");
@@ -133,6 +136,62 @@ std::array<double, 3> BatchMPC::eePosition(const std::array<double, 7>& q) {
     std::vector<double> rec(MPCC_REC_SIZE);
     check(mpcc_debug_robot_records(e_, 1, q.data(), obs, rec.data()), "mpcc_debug_robot_records");
     return {rec[0], rec[1], rec[2]};
+}
+
+// ------------------------------------------------------------------------------------------------
+OcpSolver::OcpSolver(int N, double Ts, const PathToJson& path, const ParamValue& param_value, int device,
+                     int constraint_mask)
+    : impl_(N, Ts, 1, path, param_value, device, constraint_mask), guess_((size_t)(N + 1) * 17, 0.0) {}
+
+void OcpSolver::setTrack(const std::vector<double>& s, const std::vector<double>& X, const std::vector<double>& Y,
+                         const std::vector<double>& Z, const std::vector<Rot>& R) {
+    const size_t n = s.size();
+    if (X.size() != n || Y.size() != n || Z.size() != n || R.size() != n) throw Error("setTrack: size mismatch");
+    std::vector<double> R9(9 * n);
+    for (size_t i = 0; i < n; i++) std::memcpy(&R9[9 * i], R[i].data(), 9 * sizeof(double));
+    check(mpcc_set_track_path(impl_.engine(), (int)n, s.data(), X.data(), Y.data(), Z.data(), R9.data()),
+          "mpcc_set_track_path");
+}
+
+void OcpSolver::setParam(const ParamValue& param_value) { impl_.setParam(param_value); }
+
+void OcpSolver::setEnvData(const std::array<double, 3>& obs_position, const double& obs_radius) {
+    obs_[0] = obs_position[0]; obs_[1] = obs_position[1]; obs_[2] = obs_position[2]; obs_[3] = obs_radius;
+}
+
+void OcpSolver::setInitialGuess(const std::vector<OptVariables>& g) {
+    const int N = impl_.horizon();
+    if ((int)g.size() != N + 1) throw Error("setInitialGuess: expected N+1 stages");
+    for (int k = 0; k <= N; k++) {
+        const State& x = g[k].xk;
+        const Input& u = g[k].uk;
+        const double v[17] = {x.q1, x.q2, x.q3, x.q4, x.q5, x.q6, x.q7, x.s, x.vs,
+                              u.dq1, u.dq2, u.dq3, u.dq4, u.dq5, u.dq6, u.dq7, u.dVs};
+        std::memcpy(&guess_[(size_t)17 * k], v, sizeof v);
+    }
+}
+
+void OcpSolver::setCurrentInput(const Input& u) {
+    const double v[NU] = {u.dq1, u.dq2, u.dq3, u.dq4, u.dq5, u.dq6, u.dq7, u.dVs};
+    std::memcpy(ucur_, v, sizeof v);
+}
+
+bool OcpSolver::solveOCP(std::vector<OptVariables>& opt_sol, Status* status, ComputeTime* mpc_time) {
+    const int N = impl_.horizon();
+    std::vector<double> sol((size_t)(N + 1) * 17);
+    int32_t st = 0, ok = 0;
+    mpcc_timing tm{};
+    check(mpcc_solve_ocp(impl_.engine(), 1, guess_.data(), ucur_, obs_, sol.data(), &st, &ok, mpc_time ? &tm : nullptr),
+          "mpcc_solve_ocp");
+    opt_sol.resize(N + 1);
+    for (int k = 0; k <= N; k++) {
+        const double* h = &sol[(size_t)17 * k];
+        opt_sol[k].xk = {h[0], h[1], h[2], h[3], h[4], h[5], h[6], h[7], h[8]};
+        opt_sol[k].uk = {h[9], h[10], h[11], h[12], h[13], h[14], h[15], h[16]};
+    }
+    if (status) *status = (Status)st;
+    if (mpc_time) *mpc_time = {tm.set_env, tm.set_qp, tm.solve_qp, tm.get_alpha, tm.total};
+    return ok != 0;
 }
 
 // ------------------------------------------------------------------------------------------------

@@ -109,6 +109,8 @@ def lib():
         "mpcc_reset_warmstart": (C.c_int, [V, C.c_int, C.POINTER(C.c_uint8)]),
         "mpcc_solve": (C.c_int, [V, C.c_int, DP, DP, DP, DP, DP, IP, IP, C.POINTER(MpccTiming)]),
         "mpcc_solve_device": (C.c_int, [V, C.c_int, V, V, V, V, V, V, V, V]),
+        "mpcc_set_track_path": (C.c_int, [V, C.c_int, DP, DP, DP, DP, DP]),
+        "mpcc_solve_ocp": (C.c_int, [V, C.c_int, DP, DP, DP, DP, IP, IP, C.POINTER(MpccTiming)]),
         "mpcc_sim_time_step": (C.c_int, [V, C.c_int, DP, DP, D, DP]),
         "mpcc_set_warmstart_device": (C.c_int, [V, C.c_int, V, V, V, V]),
         "mpcc_timing_begin": (C.c_int, [V]),
@@ -290,6 +292,13 @@ class Engine:
         R = _f64(R).reshape(-1, 9)
         _check(self.L.mpcc_set_track(self.h, len(X), _dp(X), _dp(Y), _dp(Z), _dp(R)), "mpcc_set_track")
 
+    def set_track_path(self, s, X, Y, Z, R):
+        """SolverInterface::setTrack(ArcLengthSpline): from getPathData() (100 regular points)."""
+        s, X, Y, Z = _f64(s), _f64(X), _f64(Y), _f64(Z)
+        R = _f64(R).reshape(-1, 9)
+        _check(self.L.mpcc_set_track_path(self.h, len(s), _dp(s), _dp(X), _dp(Y), _dp(Z), _dp(R)),
+               "mpcc_set_track_path")
+
     def track_length(self):
         return self.L.mpcc_track_length(self.h)
 
@@ -337,6 +346,20 @@ class Engine:
         if timing:
             out["timing"] = tm.as_dict()
         return out
+
+    def solve_ocp(self, guess, u_cur, obs):
+        """SolverInterface::setInitialGuess/setCurrentInput/setEnvData/solveOCP for B instances
+        (solver_interface.h:44-54).  Returns dict(opt_sol [B,N+1,17], status, solved)."""
+        B = guess.shape[0]
+        guess = _f64(guess, (B, self.N + 1, 17))
+        u_cur = _f64(u_cur, (B, 8))
+        obs = _f64(obs, (B, 4))
+        sol = np.zeros((B, self.N + 1, 17))
+        st = np.zeros(B, np.int32)
+        ok = np.zeros(B, np.int32)
+        _check(self.L.mpcc_solve_ocp(self.h, B, _dp(guess), _dp(u_cur), _dp(obs), _dp(sol), _ip(st), _ip(ok), None),
+               "mpcc_solve_ocp")
+        return dict(opt_sol=sol, status=st, solved=ok)
 
     def solve_device(self, B, x0, u0, obs, u_out=None, horizon=None, status=None, ok=None, stream=None):
         """Batched runMPC_ on device-resident torch tensors (float64 / int32), asynchronous on 'stream'."""

@@ -52,6 +52,23 @@ def test_spline_eval(setup20):
         assert np.allclose(dR[i], dRo, rtol=1e-11, atol=1e-12)
 
 
+def test_set_track_path_equivalent(setup20):
+    """mpcc_set_track_path (SolverInterface::setTrack(ArcLengthSpline) via getPathData()) reproduces
+    the tables of mpcc_set_track on the way-points bit for bit (the reference's final regular fit)."""
+    m, o, eng, pool = setup20
+    eng2 = m.Engine(m.load_params(N=20, overrides={"sqp": {"max_iter": 2}}), max_batch=4, constraint_mask=7)
+    eng2.set_track_path(*eng.track_path())
+    assert eng2.track_length() == eng.track_length()
+    L = eng.track_length()
+    sv = np.concatenate([np.linspace(0, L, 257), [-0.1, L + 0.1]])
+    for a, b in zip(eng.spline_eval(sv), eng2.spline_eval(sv)):
+        assert np.array_equal(a, b)
+    with pytest.raises(m.MpccError):
+        s, X, Y, Z, R = eng.track_path()
+        eng2.set_track_path(s[:50], X[:50], Y[:50], Z[:50], R[:50])
+    eng2.close()
+
+
 def test_projection(setup20):
     """projectOnSpline (arc_length_spline.cpp:318-379) incl. the far branch (Q12) and the 0/0 Newton step
     at the track end that the reference's unwrapInput maps to s = 0."""
@@ -246,6 +263,59 @@ def test_golden_batch_mask2_gpu(built_lib, oracle_lib):
     assert np.abs(out["horizon"][:, :-1, 9:] - g["horizon"][:, :-1, 9:]).max() <= 1e-6
     assert np.abs(xg - g["x0_out"]).max() <= 1e-9
     eng.close()
+
+
+def test_solve_ocp_plugin_boundary(built_lib, oracle_lib):
+    """mpcc_solve_ocp (the SolverInterface::solveOCP granularity, solver_interface.h:44-54): given the
+    guess the reference MPC would pass after its own projection and shift (here: the oracle's
+    runMPC_ prefix), it returns the same opt_sol and status as the full runMPC_ path, and as the fixture."""
+    import mpcc_manipulator_amd as m
+    g = _gold("batch_mask2.npz")
+    o, P, track = make_oracle(N=20, max_iter=2, mask=2)
+    xo, go, vo, fo = g["x0"].copy(), g["guess"].copy(), g["valid"].copy(), g["fails"].copy()
+    o.prepare(xo, g["u0"], g["obs"], go, vo, fo)           # MPC side: projection + warm start (mpc.cpp:104-124)
+    params = m.load_params(N=20, overrides={"sqp": {"max_iter": 2}})
+    eng = m.Engine(params, max_batch=64, constraint_mask=2)
+    eng.set_track(*track)
+    res = eng.solve_ocp(go, g["u0"], g["obs"])
+    assert np.array_equal(res["status"], g["status"])
+    assert np.array_equal(res["solved"], (g["status"] == 0).astype(np.int32))
+    assert np.abs(res["opt_sol"][:, :-1, 9:] - g["horizon"][:, :-1, 9:]).max() <= 1e-6
+    eng.set_warmstart(g["guess"], g["valid"], g["fails"])
+    full = eng.solve(g["x0"].copy(), g["u0"], g["obs"])
+    assert np.array_equal(full["status"], res["status"])
+    assert np.abs(full["horizon"] - res["opt_sol"]).max() <= 1e-12
+    eng.close()
+
+
+def test_cpp_ocp_solver_plugin(built_lib, oracle_lib, tmp_path):
+    """mpcc_amd::OcpSolver (SolverInterface mirror; examples/ocp_solver_io.cpp drives it as MPC::runMPC_
+    drives solver_interface_) on the golden configs[1] batch, one instance at a time on one solver:
+    status, solveOCP's bool and opt_sol match the fixture (u <= 1e-6)."""
+    import subprocess
+    g = _gold("batch_mask2.npz")
+    o, P, track = make_oracle(N=20, max_iter=2, mask=2)
+    xo, go, vo, fo = g["x0"].copy(), g["guess"].copy(), g["valid"].copy(), g["fails"].copy()
+    o.prepare(xo, g["u0"], g["obs"], go, vo, fo)
+    B, N = go.shape[0], 20
+    s, X, Y, Z, R = o.track_path()
+    blob = [np.array([N, B], np.int32).tobytes()] + [np.asarray(a, np.float64).tobytes() for a in (s, X, Y, Z, R)]
+    for b in range(B):
+        blob += [go[b].tobytes(), np.asarray(g["u0"][b], np.float64).tobytes(), g["obs"][b].tobytes()]
+    fin, fout = tmp_path / "in.bin", tmp_path / "out.bin"
+    fin.write_bytes(b"".join(blob))
+    exe = os.path.join(os.path.dirname(built_lib), "ocp_solver_io")
+    r = subprocess.run([exe, os.path.join(ROOT, "mpcc_manipulator_amd", "data"), "2", "2", str(fin), str(fout)],
+                       capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr
+    raw = fout.read_bytes()
+    rec = 8 + (N + 1) * 17 * 8
+    assert len(raw) == B * rec
+    for b in range(B):
+        st, ok = np.frombuffer(raw[b * rec:b * rec + 8], np.int32)
+        sol = np.frombuffer(raw[b * rec + 8:(b + 1) * rec], np.float64).reshape(N + 1, 17)
+        assert st == g["status"][b] and ok == (st == 0), b
+        assert np.abs(sol[:-1, 9:] - g["horizon"][b, :-1, 9:]).max() <= 1e-6, b
 
 
 def test_golden_closed_loop_gpu(setup20):

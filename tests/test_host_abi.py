@@ -126,6 +126,16 @@ def test_engine_fails_loudly_without_gpu(built_lib):
         m.Engine(params, max_batch=4, constraint_mask=2)
 
 
+@pytest.mark.parametrize("key", ["do_SOC", "use_BFGS"])
+def test_unsupported_sqp_variants_rejected(built_lib, key):
+    """SOC / BFGS (osqp_interface.cpp:658-757) are off the path; enabling them is an error raised before
+    any device work, never a silent fallback to plain SQP."""
+    import mpcc_manipulator_amd as m
+    params = m.load_params(N=20, overrides={"sqp": {key: 1.0}})
+    with pytest.raises(m.MpccError, match="not supported"):
+        m.Engine(params, max_batch=4, constraint_mask=2)
+
+
 def test_host_integrator_matches_oracle(built_lib, oracle_lib):
     """integrator.py (Integrator::simTimeStep, integrator.cpp:55-68) vs the oracle, batched."""
     from mpcc_manipulator_amd.integrator import sim_time_step
