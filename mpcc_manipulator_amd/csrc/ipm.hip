@@ -34,6 +34,7 @@ namespace mpcc {
 constexpr int IPM_MAX_IT = MPCC_IPM_MAXIT;  // 60 (oracle); a debug build may cap it
 constexpr double IPM_TOL_MU = 1e-13, IPM_TOL_P = 1e-11, IPM_TOL_STEP = 1e-11;
 constexpr double IPM_TOL_FB = 1e-9;  // P2: a converged iterate is accepted when the Riccati factor breaks down
+constexpr double IPM_DIV = 1e6;      // P3: mu > IPM_DIV * mu_0 -> primal infeasible (divergent multipliers)
 constexpr int IPW = 4;               // instances per wavefront (16 lanes each)
 
 // workspace fields, ws[(b*(N+1) + k)*IS + field*16 + lane]
@@ -74,6 +75,10 @@ __device__ __forceinline__ double dpp_d(double v) {
     int lo = (int)(unsigned)(x & 0xffffffffull), hi = (int)(unsigned)(x >> 32);
     lo = __builtin_amdgcn_update_dpp(0, lo, CTRL, 0xF, 0xF, true);
     hi = __builtin_amdgcn_update_dpp(0, hi, CTRL, 0xF, 0xF, true);
+    // Pin the DPP where it is written: the optimizer may otherwise sink it into a lane-divergent branch
+    // of its only consumer (e.g. the t >= 9 side of a select), where the source lanes are masked off
+    // and read as 0.  An empty volatile asm on the result cannot be moved across control flow.
+    asm volatile("" : "+v"(lo), "+v"(hi));
     return __longlong_as_double((long long)(((unsigned long long)(unsigned)hi << 32) | (unsigned)lo));
 }
 template <int n> __device__ __forceinline__ double from_up(double v) { return dpp_d<0x100 + n>(v); }    // row_shl: lane t <- t+n
@@ -192,6 +197,19 @@ struct StageIn {
     double x0, x1, x2, x3;        // sweep-specific pairs (dz, dza, g0)
     double m[12];                 // sweep-specific: Q row + q, R, r | K row halves + kff | K column + F^-1 half
 };
+
+// Stage sweep i = 0..N in the order s(i) (forward or backward), next stage prefetched one ahead.
+// (A deeper, unrolled three-buffer pipeline measured slower: 5.1 -> 6.1 ms per k_ipm launch.)
+template <class In, class LoadF, class BodyF>
+__device__ __forceinline__ void sweep_simple(int N, bool backward, In& b0, In& b1, LoadF load, BodyF body) {
+    auto s = [&](int i) { return backward ? N - i : i; };
+    load(s(0), b0);
+    for (int i = 0; i <= N; i++) {
+        if (i < N) load(s(i + 1), b1);
+        body(s(i), b0);
+        b0 = b1;
+    }
+}
 
 }  // namespace
 
@@ -391,6 +409,8 @@ __global__ void __launch_bounds__(64) k_ipm(DevConst c, DevBuffers d) {
     // ---- start point: dynamics rollout with v = 0, s = max(-g, 1), lambda = 1
     double mcount = 0.0;
     In cur, nxt;
+    // light sweeps (predictor forward, corrector backward / forward)
+    auto sweep = [&](bool backward, auto load, auto body) { sweep_simple(N, backward, cur, nxt, load, body); };
     if (run) {
         double y = 0.0;  // lane a < 9: y_a of stage k
         double bk = 0, bkn = 0;
@@ -426,7 +446,8 @@ __global__ void __launch_bounds__(64) k_ipm(DevConst c, DevBuffers d) {
     PMARK(0);
 
     int it = 0;
-    bool conv = false;
+    bool conv = false, diverged = false;
+    double mu0 = 0.0;                    // mu of the starting point (P3)
     double alpha = 0.0, sigma_mu = 0.0;  // previous iteration's step length and sigma*mu (lazy update)
     double mu_cur = 1e30, rp_cur = 1e30; // mu and max |rp| of the current iterate (known for it > 0)
     bool pending = false;
@@ -686,9 +707,7 @@ __global__ void __launch_bounds__(64) k_ipm(DevConst c, DevBuffers d) {
             // ---- predictor forward: x~_0 = 0; recover dsa, dla; max step; mu(alpha) sums
             double S0 = 0, S1 = 0, S2 = 0, amax = 1.0;
             double xt = 0.0;
-            load_fwd(0, cur, false);
-            for (int k = 0; k <= N; k++) {
-                if (k < N) load_fwd(k + 1, nxt, false);
+            sweep(false, [&](int k, In& o) { load_fwd(k, o, false); }, [&](int k, const In& cur) {
                 const bool aL = row_active(k, cur.lb), aU = row_active(k, cur.ub), aP = poly_slot_active(cur, k);
                 double v = 0.0, xn = 0.0;
                 if (k < N) fwd_step(cur, xt, v, xn);
@@ -710,11 +729,11 @@ __global__ void __launch_bounds__(64) k_ipm(DevConst c, DevBuffers d) {
                 rec(aU, sgnU, cur.ub, cz, ca, cur.sU, cur.lU);
                 rec(aP, sgnU, cur.pub, pcz, pca, cur.sP, cur.lP);
                 xt = xn;
-                cur = nxt;
-            }
+            });
             amax = g_min(amax);
             S0 = g_sum(S0); S1 = g_sum(S1); S2 = g_sum(S2);
             const double mu = (mcount > 0) ? S0 / mcount : 0.0;
+            if (it == 0) mu0 = mu;
             double mua = S0 + amax * S1 + amax * amax * S2;
             mua = (mcount > 0) ? mua / mcount : 0.0;
             const double ratio = (mu > 0) ? mua / mu : 0.0;
@@ -725,9 +744,7 @@ __global__ void __launch_bounds__(64) k_ipm(DevConst c, DevBuffers d) {
             // ---- corrector backward: coef with rc = s l + dsa dla - sigma mu; f = g_v + B~^T p;
             //      kff = -F^-1 f; p = g_x~ + A~^T p + K^T f
             double pv = 0.0;
-            load_bwd(N, cur);
-            for (int k = N; k >= 0; k--) {
-                if (k > 0) load_bwd(k - 1, nxt);
+            sweep(true, [&](int k, In& o) { load_bwd(k, o); }, [&](int k, const In& cur) {
                 const bool aL = row_active(k, cur.lb), aU = row_active(k, cur.ub), aP = poly_slot_active(cur, k);
                 const double cz = row_cz(k, cur.zx, cur.zv), ca = row_cz(k, cur.x0, cur.x1);
                 const double pcz = poly_cz(cur, k, cur.zx, cur.zv), pca = poly_cz(cur, k, cur.x0, cur.x1);
@@ -747,8 +764,7 @@ __global__ void __launch_bounds__(64) k_ipm(DevConst c, DevBuffers d) {
                 assemble_grad(cur, k, cur.x2, cur.x3, dvr, cP, gx, gv);
                 if (k == N) {
                     pv = gx;
-                    cur = nxt;
-                    continue;
+                    return;
                 }
                 const double pu9 = from_up<9>(pv), pu1 = from_up<1>(pv);  // DPP in uniform control flow
                 const double fv = gv + gt * pv + ((t < 7) ? pu9 : g87 * pu1);
@@ -770,16 +786,13 @@ __global__ void __launch_bounds__(64) k_ipm(DevConst c, DevBuffers d) {
 #pragma unroll
                 for (int i = 0; i < 8; i++) ktf += cur.m[i] * fb[i];
                 pv = gx + atp + ktf;
-                cur = nxt;
-            }
+            });
             PMARK(4);
 
             // ---- corrector forward: dz, ds, dl, max step, mu(alpha) sums, max |rp|, max |dz|
             double T0 = 0, T1 = 0, T2 = 0, amx = 1e30, rpm = 0, dzm = 0;
             xt = 0.0;
-            load_fwd(0, cur, true);
-            for (int k = 0; k <= N; k++) {
-                if (k < N) load_fwd(k + 1, nxt, true);
+            sweep(false, [&](int k, In& o) { load_fwd(k, o, true); }, [&](int k, const In& cur) {
                 const bool aL = row_active(k, cur.lb), aU = row_active(k, cur.ub), aP = poly_slot_active(cur, k);
                 double v = 0.0, xn = 0.0;
                 if (k < N) fwd_step(cur, xt, v, xn);
@@ -804,8 +817,7 @@ __global__ void __launch_bounds__(64) k_ipm(DevConst c, DevBuffers d) {
                 rec(aU, sgnU, cur.ub, cz, ca, cd, cur.sU, cur.lU);
                 rec(aP, sgnU, cur.pub, pcz, pca, pcd, cur.sP, cur.lP);
                 xt = xn;
-                cur = nxt;
-            }
+            });
             amx = g_min(amx);
             T0 = g_sum(T0); T1 = g_sum(T1); T2 = g_sum(T2);
             rpm = g_max(rpm);
@@ -825,6 +837,9 @@ __global__ void __launch_bounds__(64) k_ipm(DevConst c, DevBuffers d) {
                 if (mun < IPM_TOL_MU && rpn < IPM_TOL_P && dzm < IPM_TOL_STEP) {
                     conv = true;
                     run = false;
+                } else if (mun > IPM_DIV * mu0) {  // P3: divergent multipliers, primal infeasible
+                    diverged = true;
+                    run = false;
                 }
             } else {
                 run = false;
@@ -841,8 +856,8 @@ __global__ void __launch_bounds__(64) k_ipm(DevConst c, DevBuffers d) {
 #endif
     if (!entered) return;
     if (t == 0) si[SQ_IPMIT] = it;
-    if (!conv) {
-        if (t == 0) si[SQ_QPSTAT] = MPCC_QP_MaxIterReached;  // keep the previous step (Q6)
+    if (!conv) {  // keep the previous step (Q6)
+        if (t == 0) si[SQ_QPSTAT] = diverged ? MPCC_QP_PrimalInfeasible : MPCC_QP_MaxIterReached;
         return;
     }
     if (t == 0) si[SQ_QPSTAT] = 0;

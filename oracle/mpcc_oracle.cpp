@@ -10,6 +10,7 @@
 #include <algorithm>
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <fstream>
 #include <limits>
@@ -1087,6 +1088,7 @@ constexpr double BIG = 1e20;  // |bound| >= BIG is treated as infinite (OSQP_INF
 constexpr int IPM_MAX_IT = 60;
 constexpr double IPM_TOL_MU = 1e-13, IPM_TOL_P = 1e-11, IPM_TOL_STEP = 1e-11;
 constexpr double IPM_TOL_FB = 1e-9;  // P2: accept a converged iterate when the Riccati factor breaks down
+constexpr double IPM_DIV = 1e6;      // P3: mu > IPM_DIV * mu_0 -> primal infeasible (divergent multipliers)
 constexpr double FEAS_TOL = 1e-9;
 
 // ---------------- stage-structured primal-dual IPM with a Riccati factorization ----------------
@@ -1379,6 +1381,8 @@ struct Riccati {
 };
 
 // Returns 0 on success (step filled in reference layout: [y_0..y_N | v_0..v_{N-1}]), else Status.
+static const bool g_ipm_debug = std::getenv("MPCC_ORACLE_IPM_DEBUG") != nullptr;  // per-iteration log (debug)
+
 static int solve_struct_ipm(const StructQP& S, std::vector<double>& step, int* iters_out) {
     const int N = S.N;
     if (S.infeasible) return QP_PrimalInfeasible;
@@ -1414,8 +1418,8 @@ static int solve_struct_ipm(const StructQP& S, std::vector<double>& step, int* i
     std::vector<double> Hs((size_t)(N + 1) * NZ * NZ), gs((size_t)(N + 1) * NZ), dz, dza;
     Riccati R;
     int it;
-    bool conv = false;
-    double last_dz = 1e30;
+    bool conv = false, diverged = false;
+    double last_dz = 1e30, mu0 = 0.0;
     for (it = 0; it < IPM_MAX_IT; it++) {
         double mu = 0, rpmax = 0;
         for (int i = 0; i < m; i++) {
@@ -1424,8 +1428,22 @@ static int solve_struct_ipm(const StructQP& S, std::vector<double>& step, int* i
             rpmax = std::max(rpmax, std::fabs(rp[i]));
         }
         mu = (m > 0) ? mu / m : 0.0;
+        if (g_ipm_debug) {
+            double lmax = 0, smin = 1e300;
+            for (int i = 0; i < m; i++) { lmax = std::max(lmax, lam[i]); smin = std::min(smin, sl[i]); }
+            std::fprintf(stderr, "ipm it %2d mu %.3e rp %.3e dz %.3e lam_max %.3e s_min %.3e\n", it, mu, rpmax,
+                         last_dz, lmax, smin);
+        }
         if (it > 0 && mu < IPM_TOL_MU && rpmax < IPM_TOL_P && last_dz < IPM_TOL_STEP) {
             conv = true;
+            break;
+        }
+        // P3: the complementarity of a primal-infeasible QP grows without bound while rp
+        // stalls; OSQP reports such a QP PrimalInfeasible (osqp_interface.cpp:497-499).  Converged
+        // solves never exceed ~1.1 mu_0, so 1e6 mu_0 cannot cut a solve that would converge.
+        if (it == 0) mu0 = mu;
+        else if (mu > IPM_DIV * mu0) {
+            diverged = true;
             break;
         }
         for (int i = 0; i < m; i++) W[i] = lam[i] / sl[i];
@@ -1499,6 +1517,8 @@ static int solve_struct_ipm(const StructQP& S, std::vector<double>& step, int* i
         last_dz = dzmax;
     }
     if (iters_out) *iters_out = it;
+    if (g_ipm_debug) std::fprintf(stderr, "ipm end conv %d it %d div %d\n", conv ? 1 : 0, it, diverged ? 1 : 0);
+    if (diverged) return QP_PrimalInfeasible;
     if (!conv) return QP_MaxIterReached;
     // export in reference layout
     step.assign((size_t)(N + 1) * NX + N * NU, 0.0);
@@ -1564,8 +1584,8 @@ static int solve_dense_ipm(const DenseQP& q, std::vector<double>& step, int* ite
     auto rowdot = [&](int r, const std::vector<double>& v) { const double* a = Arow(r); double t = 0; for (int j = 0; j < nv; j++) t += a[j] * v[j]; return t; };
     for (int i = 0; i < m; i++) s[i] = std::max(-(I[i].sgn * rowdot(I[i].row, x) - I[i].sgn * I[i].bnd), 1.0);
     int n = nv + ne;
-    int it; bool conv = false;
-    double last_dx = 1e30;
+    int it; bool conv = false, diverged = false;
+    double last_dx = 1e30, mu0 = 0.0;
     for (it = 0; it < IPM_MAX_IT; it++) {
         double mu = 0, rpmax = 0;
         for (int i = 0; i < m; i++) { rp[i] = I[i].sgn * rowdot(I[i].row, x) - I[i].sgn * I[i].bnd + s[i]; mu += s[i] * lam[i]; rpmax = std::max(rpmax, std::fabs(rp[i])); }
@@ -1574,6 +1594,8 @@ static int solve_dense_ipm(const DenseQP& q, std::vector<double>& step, int* ite
         double remax = 0;
         for (int e = 0; e < ne; e++) { re[e] = rowdot(eq[e], x) - beq[e]; remax = std::max(remax, std::fabs(re[e])); }
         if (it > 0 && mu < IPM_TOL_MU && rpmax < IPM_TOL_P && remax < IPM_TOL_P && last_dx < IPM_TOL_STEP) { conv = true; break; }
+        if (it == 0) mu0 = mu;
+        else if (mu > IPM_DIV * mu0) { diverged = true; break; }  // P3
         for (int i = 0; i < m; i++) W[i] = lam[i] / s[i];
         std::vector<double> K((size_t)n * n, 0.0);
         for (int i = 0; i < nv; i++) for (int j = 0; j < nv; j++) K[(size_t)i * n + j] = q.P[(size_t)i * nv + j];
@@ -1626,6 +1648,8 @@ static int solve_dense_ipm(const DenseQP& q, std::vector<double>& step, int* ite
         for (int i = 0; i < m; i++) { s[i] += a * dS[i]; lam[i] += a * dL[i]; }
     }
     if (iters_out) *iters_out = it;
+    if (g_ipm_debug) std::fprintf(stderr, "ipm end conv %d it %d div %d\n", conv ? 1 : 0, it, diverged ? 1 : 0);
+    if (diverged) return QP_PrimalInfeasible;
     if (!conv) return QP_MaxIterReached;
     step = x;
     return 0;

@@ -11,9 +11,10 @@ sys.path.insert(0, os.path.join(ROOT, "tests"))
 from helpers import SEED, make_oracle, oracle_pool  # noqa: E402
 import mpcc_manipulator_amd as m  # noqa: E402
 
-o, P, track = make_oracle(N=20, max_iter=2, mask=7)
+MASK = int(os.environ.get("WS_MASK", "7"))
+o, P, track = make_oracle(N=20, max_iter=2, mask=MASK)
 params = m.load_params(N=20, overrides={"sqp": {"max_iter": 2}})
-eng = m.Engine(params, max_batch=8, constraint_mask=7)
+eng = m.Engine(params, max_batch=8, constraint_mask=MASK)
 eng.set_track(*track)
 pool = oracle_pool(o, 40)
 rng = np.random.default_rng(SEED + 2)
