@@ -31,7 +31,7 @@ def algorithmic_qp_flops(N):
     return 2 * (96 * N ** 3 + 324 * N ** 2) + 616 * N ** 2 + n ** 3 / 3 + 4 * n ** 2
 
 
-def make_pool(m, params, mask, steps, device):
+def make_pool(m, params, mask, steps, device, pool_obs=(3.0, 3.0, 3.0, 0.0)):
     """State pool of the reference closed loop (main.cpp:100-114): the committed file for configs[1]
     (tools/make_bench_pool.py), else a B = 1 closed loop on the GPU.  Returns (pool, track)."""
     N = params.N
@@ -49,7 +49,7 @@ def make_pool(m, params, mask, steps, device):
     from mpcc_manipulator_amd.integrator import sim_time_step
     x = np.zeros((1, 9)); x[0, :7] = Q0
     u = np.zeros((1, 8))
-    obs = np.array([[3.0, 3.0, 3.0, 0.0]])
+    obs = np.array([pool_obs])
     pool = {k: [] for k in ["x0", "u0", "guess", "valid", "fails", "status"]}
     for _ in range(steps):
         g, v, fl = eng.get_warmstart(1)
@@ -90,9 +90,12 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--batch", type=int, default=4096, help="instances per GPU")
-    ap.add_argument("--N", type=int, default=20)
-    ap.add_argument("--mask", type=int, default=2, help="polytopic rows: 1 self, 2 singularity, 4 env (configs[1] = 2)")
+    ap.add_argument("--config", type=int, default=1, choices=[1, 2],
+                    help="BASELINE configs[i] preset: 1 = B 4096, N 20, mask 2 (the metric); "
+                         "2 = B 65536, N 40, mask 7, per-instance obstacles (parity case, timing only)")
+    ap.add_argument("--batch", type=int, default=None, help="instances per GPU")
+    ap.add_argument("--N", type=int, default=None)
+    ap.add_argument("--mask", type=int, default=None, help="polytopic rows: 1 self, 2 singularity, 4 env (configs[1] = 2)")
     ap.add_argument("--max-iter", type=int, default=2)
     ap.add_argument("--pool-steps", type=int, default=400)
     ap.add_argument("--cpu-threads", type=int, default=16)
@@ -101,6 +104,10 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "pmc_traffic_k_ipm.json"))
     args = ap.parse_args()
+    preset = {1: dict(batch=4096, N=20, mask=2), 2: dict(batch=65536, N=40, mask=7)}[args.config]
+    for k, v in preset.items():
+        if getattr(args, k) is None:
+            setattr(args, k, v)
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -118,7 +125,8 @@ def main():
     N, B = args.N, args.batch
     params = m.load_params(N, overrides={"sqp": {"max_iter": args.max_iter}})
     params.constraint_mask = args.mask
-    pool, track = make_pool(m, params, args.mask, args.pool_steps, local)
+    pool_obs = (0.48, 0.218, 0.521, 5.0) if args.config == 2 else (3.0, 3.0, 3.0, 0.0)
+    pool, track = make_pool(m, params, args.mask, args.pool_steps, local, pool_obs)
     eng = m.Engine(params, max_batch=B, device=local, constraint_mask=args.mask)
     eng.set_track(*track)
 
@@ -133,7 +141,11 @@ def main():
     guess = pool["guess"][idx].copy()
     valid = pool["valid"][idx].astype(np.int32)
     fails = pool["fails"][idx].astype(np.int32)
-    obs = np.tile(np.array([3.0, 3.0, 3.0, 0.0]), (B, 1))
+    if args.config == 2:  # main_w_sim.py:42-45 scenario: xyz = (0.48, 0.218, z), z ~ U[0.421, 0.621], r = 5 cm
+        z = rng.uniform(0.421, 0.621, B)
+        obs = np.column_stack([np.full(B, 0.48), np.full(B, 0.218), z, np.full(B, 5.0)])
+    else:  # dummy obstacle of MPC::runMPC (mpc.cpp:97-100)
+        obs = np.tile(np.array([3.0, 3.0, 3.0, 0.0]), (B, 1))
 
     dev = torch.device("cuda", local)
     t = lambda a, dt=torch.float64: torch.from_numpy(np.ascontiguousarray(a)).to(dev, dt)
@@ -233,8 +245,10 @@ def main():
             "value": value, "unit": "solves/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
             "ms_per_step": ms, "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f64",
             "data": "synthetic (closed-loop state pool on the default track, q + N(0, 0.005 rad))",
-            "config": {"workload": f"configs[1]: batch={B}/GPU Panda MPCC instances, N={N}, bounds+singularity "
-                                   f"constraints (mask={args.mask}), {args.max_iter} SQP iters",
+            "config": {"workload": (f"configs[1]: batch={B}/GPU Panda MPCC instances, N={N}, bounds+singularity "
+                                    f"constraints (mask={args.mask}), {args.max_iter} SQP iters") if args.config == 1 else
+                                   (f"configs[2]: batch={B}/GPU Panda MPCC instances, N={N}, self+env collision NN "
+                                    f"constraints (mask={args.mask}), per-instance obstacles, {args.max_iter} SQP iters"),
                        "batch_per_gpu": B, "global_batch": B * world, "horizon": N, "sqp_iters": args.max_iter,
                        "parallelism": f"instance-sharded x{world}" + (", RCCL all_gather(u0)" if world > 1 else "")},
             "roofline": roof,

@@ -226,6 +226,73 @@ def test_benchmark_batch_parity(built_lib, oracle_lib, mask, B):
     eng.close()
 
 
+# ---------------------------------------------------------------- configs[2]: N = 40, both MLPs, obstacles
+def _obstacles(rng, B):
+    """main_w_sim.py:42-45 scenario: xyz = (0.48, 0.218, z), z ~ U[0.421, 0.621], r = 5 cm."""
+    z = rng.uniform(0.421, 0.621, B)
+    return np.column_stack([np.full(B, 0.48), np.full(B, 0.218), z, np.full(B, 5.0)])
+
+
+@pytest.fixture(scope="module")
+def setup40(built_lib, oracle_lib):
+    import mpcc_manipulator_amd as m
+    o, P, track = make_oracle(N=40, max_iter=2, mask=7, nthreads=16)
+    pool = oracle_pool(o, 120, obs=(0.48, 0.218, 0.521, 5.0))
+    return m, o, track, pool
+
+
+def test_config2_parity(setup40):
+    """BASELINE configs[2] shape (N = 40, self + env collision rows, per-instance obstacles): status,
+    optimal input sequence (1e-6), x0 update and controller state match the oracle per instance."""
+    m, o, track, pool = setup40
+    B = 512
+    rng = np.random.default_rng(SEED + 40)
+    x0, u0, obs, guess, valid, fails = batch_from_pool(pool, B, rng, obs=_obstacles(rng, B))
+    eng = m.Engine(m.load_params(N=40, overrides={"sqp": {"max_iter": 2}}), max_batch=B, constraint_mask=7)
+    eng.set_track(*track)
+    (xg, outg, gg, vg, fg), (xo, outo, go, vo, fo) = _run_both(eng, o, x0, u0, obs, guess, valid, fails)
+    assert np.array_equal(outg["status"], outo["status"])
+    assert np.abs(outg["horizon"][:, :-1, 9:] - outo["horizon"][:, :-1, 9:]).max() <= 1e-6
+    assert np.abs(outg["horizon"] - outo["horizon"]).max() <= 1e-6
+    assert np.abs(xg - xo).max() <= 1e-9
+    assert np.array_equal(vg, vo) and np.array_equal(fg, fo) and np.array_equal(outg["ok"], outo["ok"])
+    eng.close()
+
+
+def test_config2_full_scale(setup40):
+    """configs[2] at full size (B = 65,536, N = 40): size-independent properties.
+    (1) instance independence: a random subset re-solved alone is bitwise identical to its rows of the
+    full batch (outputs, x0 update, warm-start state); (2) every output finite with a valid status;
+    (3) a seeded sample of 64 instances matches the oracle (status, u <= 1e-6)."""
+    m, o, track, pool = setup40
+    B = 65536
+    rng = np.random.default_rng(SEED + 65536)
+    x0, u0, obs, guess, valid, fails = batch_from_pool(pool, B, rng, obs=_obstacles(rng, B))
+    params = m.load_params(N=40, overrides={"sqp": {"max_iter": 2}})
+    eng = m.Engine(params, max_batch=B, constraint_mask=7)
+    eng.set_track(*track)
+    eng.set_warmstart(guess, valid, fails)
+    xf = x0.copy()
+    full = eng.solve(xf, u0, obs)
+    gf, vf, ff = eng.get_warmstart(B)
+    assert np.all(np.isfinite(full["horizon"])) and np.all(np.isfinite(xf))
+    assert set(np.unique(full["status"]).tolist()) <= {0, 1, 10, 11}
+    sub = np.sort(rng.choice(B, 256, replace=False))
+    eng.set_warmstart(guess[sub], valid[sub], fails[sub])
+    xs = x0[sub].copy()
+    part = eng.solve(xs, u0[sub], obs[sub])
+    gs, vs, fs = eng.get_warmstart(len(sub))
+    assert np.array_equal(part["status"], full["status"][sub])
+    assert np.array_equal(part["horizon"], full["horizon"][sub]) and np.array_equal(xs, xf[sub])
+    assert np.array_equal(gs, gf[sub]) and np.array_equal(vs, vf[sub]) and np.array_equal(fs, ff[sub])
+    smp = sub[:64]
+    xo = x0[smp].copy(); go = guess[smp].copy(); vo = valid[smp].copy(); fo = fails[smp].copy()
+    outo = o.run_mpc(xo, u0[smp], obs[smp], go, vo, fo)
+    assert np.array_equal(outo["status"], full["status"][smp])
+    assert np.abs(outo["horizon"][:, :-1, 9:] - full["horizon"][smp, :-1, 9:]).max() <= 1e-6
+    eng.close()
+
+
 # ---------------------------------------------------------------- committed golden vectors
 def _gold(name):
     import os
