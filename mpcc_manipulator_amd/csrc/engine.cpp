@@ -164,6 +164,10 @@ bool read_doubles_txt(const std::string& path, std::vector<double>& out, size_t 
 }
 
 void load_nn(mpcc_engine* e, const std::string& dir, int nin, int nout, std::vector<int> hidden, NNWeights& w) {
+    // k_mlp_self / k_mlp_env are specialized for the reference architectures (osqp_interface.cpp:35-43)
+    const bool self_arch = nin == 7 && nout == 1 && hidden == std::vector<int>{256, 64};
+    const bool env_arch = nin == 10 && nout == 9 && hidden == std::vector<int>{256, 256, 256, 256};
+    if (!self_arch && !env_arch) throw std::runtime_error("unsupported MLP architecture under " + dir);
     std::vector<int> dims;
     dims.push_back(3 * nin);
     for (int h : hidden) dims.push_back(h);
@@ -189,11 +193,19 @@ void load_nn(mpcc_engine* e, const std::string& dir, int nin, int nout, std::vec
                      read_doubles_txt(base + "bias_" + std::to_string(l) + ".txt", b, R);
         }
         if (!ok) throw std::runtime_error("cannot read MLP layer " + std::to_string(l) + " under " + dir);
+        // MFMA fragment order (mlp.hip): [row tile t][k-step s][lane l] = W[16t + (l & 15)][4s + (l >> 4)],
+        // zero-padded to 16-row tiles and 16-deep k-tiles; bias zero-padded to the row tiles
+        const int RT = (R + 15) / 16, KS = 4 * ((C + 15) / 16);
         nd.offW[l] = (long)packed.size();
-        for (int k = 0; k < C; k++)  // transpose: W^T[k][r]
-            for (int r = 0; r < R; r++) packed.push_back(W[(size_t)r * C + k]);
+        for (int t = 0; t < RT; t++)
+            for (int s = 0; s < KS; s++)
+                for (int ln = 0; ln < 64; ln++) {
+                    const int r = 16 * t + (ln & 15), k = 4 * s + (ln >> 4);
+                    packed.push_back((r < R && k < C) ? W[(size_t)r * C + k] : 0.0);
+                }
         nd.offb[l] = (long)packed.size();
-        packed.insert(packed.end(), b.begin(), b.end());
+        for (int r = 0; r < 16 * RT; r++) packed.push_back(r < R ? b[r] : 0.0);
+        while (packed.size() % 8) packed.push_back(0.0);  // 64-byte aligned layers
     }
     w.d = dmalloc<double>(packed.size());
     HIPCHK(hipMemcpy(w.d, packed.data(), packed.size() * sizeof(double), hipMemcpyHostToDevice));

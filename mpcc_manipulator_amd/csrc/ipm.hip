@@ -24,6 +24,7 @@
 //    uses mu(alpha) = (S0 + alpha S1 + alpha^2 S2)/m and rp(alpha) = (1 - alpha) rp, accumulated by
 //    the corrector forward sweep (exact identities of the oracle's update, rounding aside).
 #include "dev_common.h"
+#include "dev_dpp.h"
 #include "kernels.h"
 
 namespace mpcc {
@@ -68,48 +69,7 @@ __device__ unsigned long long g_ipm_prof[16];
 
 namespace {
 
-// ---- 16-lane row primitives (DPP rows coincide with instances) ---------------------------------
-template <int CTRL>
-__device__ __forceinline__ double dpp_d(double v) {
-    const unsigned long long x = (unsigned long long)__double_as_longlong(v);
-    int lo = (int)(unsigned)(x & 0xffffffffull), hi = (int)(unsigned)(x >> 32);
-    lo = __builtin_amdgcn_update_dpp(0, lo, CTRL, 0xF, 0xF, true);
-    hi = __builtin_amdgcn_update_dpp(0, hi, CTRL, 0xF, 0xF, true);
-    // Pin the DPP where it is written: the optimizer may otherwise sink it into a lane-divergent branch
-    // of its only consumer (e.g. the t >= 9 side of a select), where the source lanes are masked off
-    // and read as 0.  An empty volatile asm on the result cannot be moved across control flow.
-    asm volatile("" : "+v"(lo), "+v"(hi));
-    return __longlong_as_double((long long)(((unsigned long long)(unsigned)hi << 32) | (unsigned)lo));
-}
-template <int n> __device__ __forceinline__ double from_up(double v) { return dpp_d<0x100 + n>(v); }    // row_shl: lane t <- t+n
-template <int n> __device__ __forceinline__ double from_down(double v) { return dpp_d<0x110 + n>(v); } // row_shr: lane t <- t-n
-template <int n> __device__ __forceinline__ double rot16(double v) { return dpp_d<0x120 + n>(v); }     // row_ror
-template <int n> __device__ __forceinline__ double bc(double v) { return dpp_d<0x150 + n>(v); }        // row_newbcast: lane n
-// lane n of the row for an n that is a constant after unrolling
-__device__ __forceinline__ double bcn(double v, int n) {
-    switch (n) {
-        case 0: return bc<0>(v);   case 1: return bc<1>(v);   case 2: return bc<2>(v);   case 3: return bc<3>(v);
-        case 4: return bc<4>(v);   case 5: return bc<5>(v);   case 6: return bc<6>(v);   case 7: return bc<7>(v);
-        case 8: return bc<8>(v);   case 9: return bc<9>(v);   case 10: return bc<10>(v); case 11: return bc<11>(v);
-        case 12: return bc<12>(v); case 13: return bc<13>(v); case 14: return bc<14>(v); default: return bc<15>(v);
-    }
-}
-__device__ __forceinline__ double g_sum(double v) {
-    v += rot16<8>(v); v += rot16<4>(v); v += rot16<2>(v); v += rot16<1>(v);
-    return v;
-}
-__device__ __forceinline__ double g_max(double v) {
-    v = fmax(v, rot16<8>(v)); v = fmax(v, rot16<4>(v)); v = fmax(v, rot16<2>(v)); v = fmax(v, rot16<1>(v));
-    return v;
-}
-__device__ __forceinline__ double g_min(double v) {
-    v = fmin(v, rot16<8>(v)); v = fmin(v, rot16<4>(v)); v = fmin(v, rot16<2>(v)); v = fmin(v, rot16<1>(v));
-    return v;
-}
-
-// NOTE: every DPP read must execute with the whole 16-lane row active — a lane reading from a lane that
-// is masked off at that instruction gets 0.  Shifts/broadcasts are therefore evaluated unconditionally
-// and consumed through selects.
+using namespace dpp;
 
 // One wavefront per workgroup: cross-lane LDS hand-offs only need this wave's LDS operations retired
 // and a compiler barrier; __syncthreads() would also drain outstanding global loads (vmcnt(0)).

@@ -4,7 +4,7 @@
 // controllers.  Kernel sequence:
 //   k_prepare      thread / instance        projection, vs estimate, warm-start shift  (mpc.cpp:104-124, 54-89)
 //   k_records      thread / (instance,stage) RobotData::update: FK, J, manipulability + FD gradient (robot_data.h:55-71)
-//   k_nn           wave / (instance,stage)  self / env collision MLPs + input Jacobians (SelfCollisionModel.cpp:140-250)
+//   k_mlp_*        (mlp.hip) 2 samples / wave, FP64 MFMA: self / env collision MLPs + input Jacobians
 //   per SQP iteration (osqp_interface.cpp:431-574):
 //     k_setqp      thread / (instance,stage) stage QP record: cost, constraint rows, bounds, dynamics residual
 //     k_ipm        wave / instance           Mehrotra interior point, Riccati factorization (replaces OSQP)
@@ -123,111 +123,6 @@ __global__ void __launch_bounds__(64) k_records(DevConst c, DevBuffers d) {
     if (!(c.p.constraint_mask & MPCC_CON_ENVCOL)) {
         for (int m = 0; m < 9; m++) rec[(size_t)(R_ENV + m) * S] = inf;
         for (int m = 0; m < 63; m++) rec[(size_t)(R_DENV + m) * S] = 0.0;
-    }
-}
-
-// ------------------------------------------------------------------------------------------------
-// k_nn: NeRF MLP value + 7-column forward-mode input Jacobian, one wave per (instance, stage).
-// Weights are stored transposed per layer (W^T[k][r]) so that a wave's lanes read consecutive
-// output rows.  Activations [width][8] (value + 7 tangents) live in LDS.
-// ------------------------------------------------------------------------------------------------
-
-
-template <int MAXW>
-__device__ inline void nn_eval_wave(const NNDesc& nd, const double* __restrict__ W, const double* in, double* lds_a,
-                                    double* lds_b, double* out_val, double* out_jac /* nout x 7 */) {
-    const int lane = threadIdx.x;
-    const int nin = nd.nin;
-    // layer 0 (NeRF input [x, sin x, cos x]; SelfCollisionModel.cpp:143-151, 162-188)
-    {
-        const int R = nd.dims[1], C = nd.dims[0];
-        const double* WT = W + nd.offW[0];
-        const double* bb = W + nd.offb[0];
-        for (int r = lane; r < R; r += 64) {
-            double h = 0;
-            for (int k = 0; k < C; k++) {
-                int kk = k % nin, part = k / nin;
-                double xk = in[kk];
-                double f = (part == 0) ? xk : (part == 1 ? sin(xk) : cos(xk));
-                h += WT[(size_t)k * R + r] * f;
-            }
-            h += bb[r];
-            double gsw = h > 0 ? 1.0 : 0.0;
-            lds_a[r * 8] = fmax(0.0, h);
-#pragma unroll
-            for (int j = 0; j < 7; j++) {
-                double w0 = gsw * WT[(size_t)j * R + r];
-                double w1 = gsw * WT[(size_t)(nin + j) * R + r];
-                double w2 = gsw * WT[(size_t)(2 * nin + j) * R + r];
-                lds_a[r * 8 + 1 + j] = w0 * 1.0 + w1 * cos(in[j]) + w2 * (-sin(in[j]));
-            }
-        }
-    }
-    __syncthreads();
-    double* src = lds_a;
-    double* dst = lds_b;
-    for (int l = 1; l < nd.L; l++) {
-        const int R = nd.dims[l + 1], C = nd.dims[l];
-        const double* WT = W + nd.offW[l];
-        const double* bb = W + nd.offb[l];
-        const bool last = (l == nd.L - 1);
-        for (int r = lane; r < R; r += 64) {
-            double acc[8];
-#pragma unroll
-            for (int j = 0; j < 8; j++) acc[j] = 0.0;
-            for (int k = 0; k < C; k++) {
-                double w = WT[(size_t)k * R + r];
-#pragma unroll
-                for (int j = 0; j < 8; j++) acc[j] += w * src[k * 8 + j];
-            }
-            double h = acc[0] + bb[r];
-            if (last) {
-                out_val[r] = h;
-#pragma unroll
-                for (int j = 0; j < 7; j++) out_jac[r * 7 + j] = acc[1 + j];
-            } else {
-                double gsw = h > 0 ? 1.0 : 0.0;
-                dst[r * 8] = fmax(0.0, h);
-#pragma unroll
-                for (int j = 0; j < 7; j++) dst[r * 8 + 1 + j] = gsw * acc[1 + j];
-            }
-        }
-        __syncthreads();
-        double* t = src; src = dst; dst = t;
-    }
-}
-
-__global__ void __launch_bounds__(64) k_nn(DevConst c, DevBuffers d, NNDesc nd, const double* __restrict__ W, int which,
-                                          int M, const double* __restrict__ qin, const double* __restrict__ obsin,
-                                          double* __restrict__ recout, int rec_stride) {
-    __shared__ double lds[2 * 256 * 8];
-    const int t = blockIdx.x;
-    if (t >= M) return;
-    __shared__ double outv[16], outj[16 * 7];
-    double in[10];
-    int S = rec_stride;
-    const double* obs;
-    if (qin) {  // debug path: explicit q / obs lists
-        for (int j = 0; j < 7; j++) in[j] = qin[7 * t + j];
-        obs = obsin + 4 * t;
-    } else {
-        const int N = c.N;
-        const int b = t / (N + 1), k = t - b * (N + 1);
-        const double* g = d.guess + ((size_t)b * (N + 1) + k) * 17;
-        for (int j = 0; j < 7; j++) in[j] = g[j];
-        obs = d.obs + 4 * b;
-    }
-    if (which == 1) { in[7] = obs[0]; in[8] = obs[1]; in[9] = obs[2]; }
-    nn_eval_wave<256>(nd, W, in, lds, lds + 256 * 8, outv, outj);
-    __syncthreads();
-    double* rec = recout + t;
-    const int lane = threadIdx.x;
-    if (which == 0) {
-        if (lane == 0) rec[(size_t)R_SEL * S] = outv[0];
-        if (lane < 7) rec[(size_t)(R_DSEL + lane) * S] = outj[lane];
-    } else {
-        if (lane < 9) rec[(size_t)(R_ENV + lane) * S] = outv[lane];
-        if (lane < 63) rec[(size_t)(R_DENV + lane) * S] = outj[lane];
     }
 }
 
@@ -693,10 +588,6 @@ void launch_accept(const DevConst& c, const DevBuffers& d, hipStream_t s) {
 }
 void launch_apply(const DevConst& c, const DevBuffers& d, hipStream_t s) {
     hipLaunchKernelGGL(k_apply, dim3(nblk(c.Bn, 64)), dim3(64), 0, s, c, d);
-}
-void launch_nn(const DevConst& c, const DevBuffers& d, const NNDesc& nd, const double* W, int which, int M,
-               const double* q, const double* obs, double* rec, int rec_stride, hipStream_t s) {
-    hipLaunchKernelGGL(k_nn, dim3(M), dim3(64), 0, s, c, d, nd, W, which, M, q, obs, rec, rec_stride);
 }
 void launch_debug_records(const DevConst& c, int M, const double* q, const double* obs, double* rec, hipStream_t s) {
     hipLaunchKernelGGL(k_debug_records, dim3(nblk(M, 64)), dim3(64), 0, s, c, M, q, obs, rec);

@@ -1,0 +1,188 @@
+// mlp.hip — k_mlp: the collision MLPs (SelCollNNmodel / EnvCollNNmodel::calculateMlpOutput,
+// SelfCollisionModel.cpp:140-250, EnvCollisionModel.cpp:137-247) with their forward-mode input
+// Jacobian, as FP64 MFMA GEMMs over (instance, stage) samples.
+//
+// One wave carries 2 samples x 8 columns (value + 7 tangent directions dq_0..dq_6) = one 16-column
+// tile through every layer: Z = W X is v_mfma_f64_16x16x4f64 over 16-row tiles of W and 4-deep k-steps.
+//  * The f64 C/D layout (lane l, reg r -> row (l>>4) + 4r of the tile, column l&15) is exactly the
+//    B-operand layout of the next layer's k-step 4t + r, so activations stay in registers from layer
+//    to layer — no LDS.  Bias, ReLU (value columns) and ReLU' gating (tangent columns, the value of
+//    the same sample broadcast over the 16-lane row by DPP) are applied in place between layers.
+//  * W is packed on the host in fragment order ([row tile][k-step][lane]), zero-padded to 16-row /
+//    4-column multiples: every A fragment is one coalesced 512-byte line.  Both networks' weights
+//    (1.84 MB) stay L2-resident; a weight element feeds 16 columns = 2 samples per load.
+//  * v_mfma_f64_16x16x4f64 accumulates as an ascending fma chain over k (bitwise,
+//    tools/probes/mfma_f64_probe.hip); the oracle's MLP uses the same chain.
+#include "dev_common.h"
+#include "dev_dpp.h"
+#include "kernels.h"
+
+namespace mpcc {
+namespace {
+
+using namespace dpp;
+typedef double d4 __attribute__((ext_vector_type(4)));
+
+// out[t] = sum_k W[16t + row][k] in[k] over KT k-tiles (4 k-steps of 4 each), RT 16-row output tiles
+template <int KT, int RT>
+__device__ __forceinline__ void mfma_layer(const double* __restrict__ Wp, const d4 (&in)[KT], d4 (&out)[RT],
+                                           int lane) {
+    constexpr int KS = 4 * KT;
+#pragma unroll
+    for (int t = 0; t < RT; t++) out[t] = d4{0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+    for (int kt = 0; kt < KT; kt++)
+#pragma unroll
+        for (int r = 0; r < 4; r++) {
+            const int s = 4 * kt + r;
+#pragma unroll
+            for (int t = 0; t < RT; t++)
+                out[t] = __builtin_amdgcn_mfma_f64_16x16x4f64(Wp[((size_t)t * KS + s) * 64 + lane], in[kt][r], out[t], 0,
+                                                              0, 0);
+        }
+}
+
+// hidden-layer epilogue: value columns h = relu(z + b); tangent columns dh = (z + b > 0) ? dz : 0
+template <int RT>
+__device__ __forceinline__ void relu_gate(d4 (&a)[RT], const double* __restrict__ bias, int lane) {
+    const bool isv = (lane & 7) == 0;
+    const bool hi = (lane & 8) != 0;
+#pragma unroll
+    for (int t = 0; t < RT; t++)
+#pragma unroll
+        for (int r = 0; r < 4; r++) {
+            const double z = a[t][r] + bias[16 * t + (lane >> 4) + 4 * r];
+            const double z0 = bc<0>(z), z8 = bc<8>(z);  // this row's value of sample 0 / sample 1
+            const bool on = (hi ? z8 : z0) > 0.0;
+            a[t][r] = isv ? (z > 0.0 ? z : 0.0) : (on ? a[t][r] : 0.0);  // std::max(0., h) of the oracle
+        }
+}
+
+// NeRF input [x, sin x, cos x] (3 NIN rows, zero-padded to 32) with its Jacobian columns for dq_0..dq_6
+// (nerf_jac = [I; diag(cos x); diag(-sin x)], SelfCollisionModel.cpp:143-151, 177-188)
+template <int NIN>
+__device__ __forceinline__ void nerf_input(const double (&x)[NIN], d4 (&in)[2], int lane) {
+    double sx[NIN], cx[NIN];
+#pragma unroll
+    for (int i = 0; i < NIN; i++) {
+        sx[i] = sin(x[i]);
+        cx[i] = cos(x[i]);
+    }
+    const int j = lane & 7;  // 0: value column, 1 + d: tangent of q_d
+    const int d = j - 1;
+#pragma unroll
+    for (int kt = 0; kt < 2; kt++)
+#pragma unroll
+        for (int r = 0; r < 4; r++) {
+            const int k = 16 * kt + 4 * r + (lane >> 4);
+            double v = 0.0;
+#pragma unroll
+            for (int i = 0; i < NIN; i++) {
+                if (j == 0) {
+                    if (k == i) v = x[i];
+                    if (k == NIN + i) v = sx[i];
+                    if (k == 2 * NIN + i) v = cx[i];
+                } else if (d == i) {
+                    if (k == i) v = 1.0;
+                    if (k == NIN + i) v = cx[i];
+                    if (k == 2 * NIN + i) v = -sx[i];
+                }
+            }
+            in[kt][r] = v;
+        }
+}
+
+// output tile: rows i < NOUT; value column -> out_i + b_i, tangent column 1 + d -> J[i][d]
+template <int NOUT>
+__device__ __forceinline__ void write_out(const d4& o, const double* __restrict__ bias, int lane, int m, int M,
+                                          double* __restrict__ rec, int S, int r_val, int r_jac) {
+    if (m >= M) return;
+    const int j = lane & 7;
+#pragma unroll
+    for (int r = 0; r < 4; r++) {
+        const int i = (lane >> 4) + 4 * r;
+        if (i >= NOUT) continue;
+        if (j == 0) rec[(size_t)(r_val + i) * S + m] = o[r] + bias[i];
+        else rec[(size_t)(r_jac + 7 * i + (j - 1)) * S + m] = o[r];
+    }
+}
+
+// sample m of the call: q (and the obstacle for the env network)
+__device__ __forceinline__ void sample_input(const DevConst& c, const DevBuffers& d, int m, int M, const double* qin,
+                                             const double* obsin, double* x /* 10 */) {
+    const int mm = m < M ? m : 0;
+    const double* q;
+    const double* obs;
+    if (qin) {  // debug path: explicit q / obs lists
+        q = qin + 7 * mm;
+        obs = obsin + 4 * mm;
+    } else {
+        const int b = mm / (c.N + 1), k = mm - b * (c.N + 1);
+        q = d.guess + ((size_t)b * (c.N + 1) + k) * 17;
+        obs = d.obs + 4 * b;
+    }
+#pragma unroll
+    for (int i = 0; i < 7; i++) x[i] = q[i];
+    x[7] = obs[0]; x[8] = obs[1]; x[9] = obs[2];
+}
+
+}  // namespace
+
+// self network 21 -> 256 -> 64 -> 1 (osqp_interface.cpp:35-38)
+__global__ void __launch_bounds__(256) k_mlp_self(DevConst c, DevBuffers d, NNDesc nd, const double* __restrict__ W, int M,
+                                                  const double* __restrict__ qin, const double* __restrict__ obsin,
+                                                  double* __restrict__ rec, int S) {
+    const int lane = threadIdx.x & 63;
+    const int wave = blockIdx.x * 4 + (threadIdx.x >> 6);
+    const int m = 2 * wave + ((lane >> 3) & 1);
+    if (2 * wave >= M) return;  // wave-uniform
+    double xin[10];
+    sample_input(c, d, m, M, qin, obsin, xin);
+    double x[7];
+#pragma unroll
+    for (int i = 0; i < 7; i++) x[i] = xin[i];
+    d4 a0[2], a1[16], a2[4], o[1];
+    nerf_input<7>(x, a0, lane);
+    mfma_layer<2, 16>(W + nd.offW[0], a0, a1, lane);
+    relu_gate<16>(a1, W + nd.offb[0], lane);
+    mfma_layer<16, 4>(W + nd.offW[1], a1, a2, lane);
+    relu_gate<4>(a2, W + nd.offb[1], lane);
+    mfma_layer<4, 1>(W + nd.offW[2], a2, o, lane);
+    write_out<1>(o[0], W + nd.offb[2], lane, m, M, rec, S, R_SEL, R_DSEL);
+}
+
+// env network 30 -> 256 -> 256 -> 256 -> 256 -> 9 (osqp_interface.cpp:40-43)
+__global__ void __launch_bounds__(256) k_mlp_env(DevConst c, DevBuffers d, NNDesc nd, const double* __restrict__ W, int M,
+                                                 const double* __restrict__ qin, const double* __restrict__ obsin,
+                                                 double* __restrict__ rec, int S) {
+    const int lane = threadIdx.x & 63;
+    const int wave = blockIdx.x * 4 + (threadIdx.x >> 6);
+    const int m = 2 * wave + ((lane >> 3) & 1);
+    if (2 * wave >= M) return;
+    double x[10];
+    sample_input(c, d, m, M, qin, obsin, x);
+    d4 a0[2], a[16], h[16], o[1];
+    nerf_input<10>(x, a0, lane);
+    mfma_layer<2, 16>(W + nd.offW[0], a0, a, lane);
+    relu_gate<16>(a, W + nd.offb[0], lane);
+    for (int l = 1; l <= 3; l++) {  // three 256 x 256 hidden layers share one unrolled body
+        mfma_layer<16, 16>(W + nd.offW[l], a, h, lane);
+        relu_gate<16>(h, W + nd.offb[l], lane);
+#pragma unroll
+        for (int t = 0; t < 16; t++) a[t] = h[t];
+    }
+    mfma_layer<16, 1>(W + nd.offW[4], a, o, lane);
+    write_out<9>(o[0], W + nd.offb[4], lane, m, M, rec, S, R_ENV, R_DENV);
+}
+
+void launch_nn(const DevConst& c, const DevBuffers& d, const NNDesc& nd, const double* W, int which, int M,
+               const double* q, const double* obs, double* rec, int rec_stride, hipStream_t s) {
+    const int blocks = (M + 7) / 8;  // 4 waves x 2 samples
+    if (blocks == 0) return;
+    if (which == 0)
+        hipLaunchKernelGGL(k_mlp_self, dim3(blocks), dim3(256), 0, s, c, d, nd, W, M, q, obs, rec, rec_stride);
+    else
+        hipLaunchKernelGGL(k_mlp_env, dim3(blocks), dim3(256), 0, s, c, d, nd, W, M, q, obs, rec, rec_stride);
+}
+
+}  // namespace mpcc

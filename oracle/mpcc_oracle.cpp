@@ -521,6 +521,9 @@ static void dmanipulability(const double* q, double* d) {
 
 // ------------------------------------------------------------------------------------------------
 // NeRF MLP with forward-mode input Jacobian — SelfCollisionModel.cpp:140-250 (Env identical)
+// Every dot product is an fma chain in ascending k (s = fma(W[i][k], x[k], s)), bitwise the
+// accumulation of v_mfma_f64_16x16x4f64 k-step by k-step (tools/probes/mfma_f64_probe.hip); the
+// reference's own order is Eigen-internal, so this is the restatement's choice.
 // ------------------------------------------------------------------------------------------------
 struct MLP {
     int n_in = 0, n_out = 0;
@@ -565,7 +568,7 @@ struct MLP {
             hid.assign(r, 0.0);
             for (int i = 0; i < r; i++) {
                 double s = 0;
-                for (int k = 0; k < c; k++) s += W[l][(size_t)i * c + k] * x[k];
+                for (int k = 0; k < c; k++) s = std::fma(W[l][(size_t)i * c + k], x[k], s);
                 hid[i] = s + b[l][i];
             }
             if (l == L - 1) {  // output layer :194-203
@@ -573,7 +576,7 @@ struct MLP {
                 for (int i = 0; i < r; i++)
                     for (int j = 0; j < n_in; j++) {
                         double s = 0;
-                        for (int k = 0; k < c; k++) s += W[l][(size_t)i * c + k] * temp[(size_t)k * n_in + j];
+                        for (int k = 0; k < c; k++) s = std::fma(W[l][(size_t)i * c + k], temp[(size_t)k * n_in + j], s);
                         jac[i * n_in + j] = s;
                     }
                 break;
@@ -582,22 +585,24 @@ struct MLP {
             std::vector<double> nt((size_t)r * n_in, 0.0);
             if (l == 0) {
                 // temp = hd0 * nerf_jac, nerf_jac = [I; diag(cos x); diag(-sin x)]  :177-188
+                // (the fma chain over the full nerf_jac column: its zero entries leave the sum unchanged)
                 for (int i = 0; i < r; i++) {
-                    double g = hid[i] > 0 ? 1.0 : 0.0;
+                    const bool g = hid[i] > 0;
                     for (int j = 0; j < n_in; j++) {
-                        double h0 = g * W[0][(size_t)i * c + j];
-                        double h1 = g * W[0][(size_t)i * c + n_in + j];
-                        double h2 = g * W[0][(size_t)i * c + 2 * n_in + j];
-                        nt[(size_t)i * n_in + j] = h0 * 1.0 + h1 * std::cos(in[j]) + h2 * (-std::sin(in[j]));
+                        const double* w = &W[0][(size_t)i * c];
+                        double s = std::fma(w[j], 1.0, 0.0);
+                        s = std::fma(w[n_in + j], std::cos(in[j]), s);
+                        s = std::fma(w[2 * n_in + j], -std::sin(in[j]), s);
+                        nt[(size_t)i * n_in + j] = g ? s : 0.0;
                     }
                 }
             } else {
                 for (int i = 0; i < r; i++) {
-                    double g = hid[i] > 0 ? 1.0 : 0.0;
+                    const bool g = hid[i] > 0;
                     for (int j = 0; j < n_in; j++) {
                         double s = 0;
-                        for (int k = 0; k < c; k++) s += (g * W[l][(size_t)i * c + k]) * temp[(size_t)k * n_in + j];
-                        nt[(size_t)i * n_in + j] = s;
+                        for (int k = 0; k < c; k++) s = std::fma(W[l][(size_t)i * c + k], temp[(size_t)k * n_in + j], s);
+                        nt[(size_t)i * n_in + j] = g ? s : 0.0;
                     }
                 }
             }
