@@ -158,16 +158,28 @@ struct StageIn {
     double m[12];                 // sweep-specific: Q row + q, R, r | K row halves + kff | K column + F^-1 half
 };
 
-// Stage sweep i = 0..N in the order s(i) (forward or backward), next stage prefetched one ahead.
-// (A deeper, unrolled three-buffer pipeline measured slower: 5.1 -> 6.1 ms per k_ipm launch.)
-template <class In, class LoadF, class BodyF>
-__device__ __forceinline__ void sweep_simple(int N, bool backward, In& b0, In& b1, LoadF load, BodyF body) {
+// Stage sweep i = 0..N in the order s(i) (forward or backward) with the next stage prefetched into the
+// other of two buffers.  Unrolled by two so that the buffers swap roles instead of being copied (a copy
+// of an in-flight buffer waits for its loads), and every load is issued unconditionally (the last one
+// re-reads stage s(N)): loads behind branches make the waitcnt pass drain all loads at the join.
+template <bool PINGPONG, class In, class LoadF, class BodyF>
+__device__ __forceinline__ void sweep(int N, bool backward, In& b0, In& b1, LoadF load, BodyF body) {
     auto s = [&](int i) { return backward ? N - i : i; };
     load(s(0), b0);
-    for (int i = 0; i <= N; i++) {
-        if (i < N) load(s(i + 1), b1);
+    if constexpr (!PINGPONG) {  // wide-poly variants: the unrolled factor body doubles their spills
+        for (int i = 0; i <= N; i++) {
+            load(s(i + 1 <= N ? i + 1 : N), b1);
+            body(s(i), b0);
+            b0 = b1;
+        }
+        return;
+    }
+    for (int i = 0; i <= N; i += 2) {
+        load(s(i + 1 <= N ? i + 1 : N), b1);
         body(s(i), b0);
-        b0 = b1;
+        if (i + 1 > N) break;
+        load(s(i + 2 <= N ? i + 2 : N), b0);
+        body(s(i + 1), b1);
     }
 }
 
@@ -251,18 +263,22 @@ __global__ void __launch_bounds__(64) k_ipm(DevConst c, DevBuffers d) {
     if (run && (fl & 4)) { if (t == 0) si[SQ_QPSTAT] = MPCC_QP_PrimalInfeasible; run = false; }  // keep old step (Q6)
     const bool entered = run;
 
-    // ---- stage loaders
+    // ---- stage loaders: every load unconditional (addresses clamped inside the stage record), the
+    //      lane/stage conditions applied as selects afterwards (see sweep())
     auto load_common = [&](int k, In& o) {
         const double* q = QSb + (size_t)k * QS;
         o.lb = q[rowY ? QS_YLB + t : QS_DLB + j9];
         o.ub = q[rowY ? QS_YUB + t : QS_DUB + j9];
         o.np = q[QS_NPOLY];
+        const int tp = t < 7 ? t : 0;  // keep the address inside row p (15 p + 7 + t would leave the record)
 #pragma unroll
         for (int p = 0; p < NPE; p++) {
-            o.pa[p] = (NPM > 0 && t < 7) ? q[QS_POLY + 15 * p + t] : 0.0;
-            o.pb[p] = (NPM > 0 && t < 7) ? q[QS_POLY + 15 * p + 7 + t] : 0.0;
+            const double a = q[QS_POLY + 15 * p + tp], bv = q[QS_POLY + 15 * p + 7 + tp];
+            o.pa[p] = (NPM > 0 && t < 7) ? a : 0.0;
+            o.pb[p] = (NPM > 0 && t < 7) ? bv : 0.0;
         }
-        o.pub = (t < NPM) ? q[QS_POLY + 15 * t + 14] : INF;
+        const double pu = q[QS_POLY + 15 * (t < NPE ? t : 0) + 14];
+        o.pub = (t < NPM) ? pu : INF;
         o.sL = *ws(k, WF_SL); o.lL = *ws(k, WF_LL); o.sU = *ws(k, WF_SU); o.lU = *ws(k, WF_LU);
         o.sP = *ws(k, WF_SP); o.lP = *ws(k, WF_LP);
         o.zx = *ws(k, WF_ZX); o.zv = *ws(k, WF_ZV);
@@ -271,39 +287,40 @@ __global__ void __launch_bounds__(64) k_ipm(DevConst c, DevBuffers d) {
         load_common(k, o);
         const double* q = QSb + (size_t)k * QS;
 #pragma unroll
-        for (int m = 0; m < 9; m++) o.m[m] = (t < 9) ? q[QS_Q + t * 9 + m] : 0.0;
-        o.m[9] = (t < 9) ? q[QS_q + t] : 0.0;
-        o.m[10] = (t < 8 && k < N) ? q[QS_R + t] : 0.0;
-        o.m[11] = (t < 8 && k < N) ? q[QS_r + t] : 0.0;
-        if (upd) {
-            o.x0 = *ws(k, WF_DX); o.x1 = *ws(k, WF_DV); o.x2 = *ws(k, WF_AX); o.x3 = *ws(k, WF_AV);
-        } else {
-            o.x0 = o.x1 = o.x2 = o.x3 = 0.0;
+        for (int m = 0; m < 9; m++) {
+            const double v = q[QS_Q + t * 9 + m];
+            o.m[m] = (t < 9) ? v : 0.0;
         }
+        const double qv = q[QS_q + t], rv = q[QS_R + t], rr = q[QS_r + t];
+        o.m[9] = (t < 9) ? qv : 0.0;
+        o.m[10] = (t < 8 && k < N) ? rv : 0.0;
+        o.m[11] = (t < 8 && k < N) ? rr : 0.0;
+        const double x0 = *ws(k, WF_DX), x1 = *ws(k, WF_DV), x2 = *ws(k, WF_AX), x3 = *ws(k, WF_AV);
+        o.x0 = upd ? x0 : 0.0; o.x1 = upd ? x1 : 0.0; o.x2 = upd ? x2 : 0.0; o.x3 = upd ? x3 : 0.0;
     };
     auto load_fwd = [&](int k, In& o, bool corr) {
         load_common(k, o);
-        if (k < N) {
 #pragma unroll
-            for (int m = 0; m < 8; m++) o.m[m] = *ws(k, WF_KR + m);
-            o.m[8] = *ws(k, WF_KFF);
-        } else {
-#pragma unroll
-            for (int m = 0; m < 9; m++) o.m[m] = 0.0;
+        for (int m = 0; m < 8; m++) {
+            const double v = *ws(k, WF_KR + m);
+            o.m[m] = (k < N) ? v : 0.0;
         }
-        if (corr) { o.x0 = *ws(k, WF_AX); o.x1 = *ws(k, WF_AV); } else { o.x0 = o.x1 = 0.0; }
+        const double kf = *ws(k, WF_KFF);
+        o.m[8] = (k < N) ? kf : 0.0;
+        if (corr) { o.x0 = *ws(k, WF_AX); o.x1 = *ws(k, WF_AV); } else { o.x0 = o.x1 = 0.0; }  // corr: constant
     };
     auto load_bwd = [&](int k, In& o) {
         load_common(k, o);
         o.x0 = *ws(k, WF_AX); o.x1 = *ws(k, WF_AV); o.x2 = *ws(k, WF_GX); o.x3 = *ws(k, WF_GV);
-        if (k < N) {
 #pragma unroll
-            for (int i = 0; i < 8; i++) o.m[i] = *ws(k, WF_KC + i);
+        for (int i = 0; i < 8; i++) {
+            const double v = *ws(k, WF_KC + i);
+            o.m[i] = (k < N) ? v : 0.0;
+        }
 #pragma unroll
-            for (int m = 0; m < 4; m++) o.m[8 + m] = *ws(k, WF_FI + m);
-        } else {
-#pragma unroll
-            for (int m = 0; m < 12; m++) o.m[m] = 0.0;
+        for (int m = 0; m < 4; m++) {
+            const double v = *ws(k, WF_FI + m);
+            o.m[8 + m] = (k < N) ? v : 0.0;
         }
     };
 
@@ -369,8 +386,6 @@ __global__ void __launch_bounds__(64) k_ipm(DevConst c, DevBuffers d) {
     // ---- start point: dynamics rollout with v = 0, s = max(-g, 1), lambda = 1
     double mcount = 0.0;
     In cur, nxt;
-    // light sweeps (predictor forward, corrector backward / forward)
-    auto sweep = [&](bool backward, auto load, auto body) { sweep_simple(N, backward, cur, nxt, load, body); };
     if (run) {
         double y = 0.0;  // lane a < 9: y_a of stage k
         double bk = 0, bkn = 0;
@@ -419,9 +434,7 @@ __global__ void __launch_bounds__(64) k_ipm(DevConst c, DevBuffers d) {
             double Pc[16];   // column t of P_{k+1}
             double pv = 0.0; // p_{k+1}, component t
             bool chol_ok = true;
-            load_factor(N, cur, pending);
-            for (int k = N; k >= 0; k--) {
-                if (k > 0) load_factor(k - 1, nxt, pending);
+            sweep<(NPM <= 2)>(N, true, cur, nxt, [&](int k, In& o) { load_factor(k, o, pending); }, [&](int k, const In& cur) {
                 const double lb = cur.lb, ub = cur.ub;
                 const double* Qr = cur.m;
                 const double qt = cur.m[9], Rt = cur.m[10], rt = cur.m[11];
@@ -492,8 +505,7 @@ __global__ void __launch_bounds__(64) k_ipm(DevConst c, DevBuffers d) {
                         Pc[a] = v;
                     }
                     pv = gx;
-                    cur = nxt;
-                    continue;
+                    return;
                 }
                 // ---- (1) Y = B~^T P (column t), f = g_v + B~^T p (lanes 0..7)
                 double Y[8];
@@ -651,9 +663,8 @@ __global__ void __launch_bounds__(64) k_ipm(DevConst c, DevBuffers d) {
                 }
                 pv = pnew;
                 lds_sync();
-                cur = nxt;
                 PMARK(13);
-            }
+            });
             if (!chol_ok) {
                 // Riccati breakdown: MaxIterReached unless the current iterate is converged to IPM_TOL_FB (P2);
                 // the sweep has already applied the pending update, so the iterate is the stored z
@@ -667,7 +678,7 @@ __global__ void __launch_bounds__(64) k_ipm(DevConst c, DevBuffers d) {
             // ---- predictor forward: x~_0 = 0; recover dsa, dla; max step; mu(alpha) sums
             double S0 = 0, S1 = 0, S2 = 0, amax = 1.0;
             double xt = 0.0;
-            sweep(false, [&](int k, In& o) { load_fwd(k, o, false); }, [&](int k, const In& cur) {
+            sweep<(NPM <= 2)>(N, false, cur, nxt, [&](int k, In& o) { load_fwd(k, o, false); }, [&](int k, const In& cur) {
                 const bool aL = row_active(k, cur.lb), aU = row_active(k, cur.ub), aP = poly_slot_active(cur, k);
                 double v = 0.0, xn = 0.0;
                 if (k < N) fwd_step(cur, xt, v, xn);
@@ -704,7 +715,7 @@ __global__ void __launch_bounds__(64) k_ipm(DevConst c, DevBuffers d) {
             // ---- corrector backward: coef with rc = s l + dsa dla - sigma mu; f = g_v + B~^T p;
             //      kff = -F^-1 f; p = g_x~ + A~^T p + K^T f
             double pv = 0.0;
-            sweep(true, [&](int k, In& o) { load_bwd(k, o); }, [&](int k, const In& cur) {
+            sweep<(NPM <= 2)>(N, true, cur, nxt, [&](int k, In& o) { load_bwd(k, o); }, [&](int k, const In& cur) {
                 const bool aL = row_active(k, cur.lb), aU = row_active(k, cur.ub), aP = poly_slot_active(cur, k);
                 const double cz = row_cz(k, cur.zx, cur.zv), ca = row_cz(k, cur.x0, cur.x1);
                 const double pcz = poly_cz(cur, k, cur.zx, cur.zv), pca = poly_cz(cur, k, cur.x0, cur.x1);
@@ -752,7 +763,7 @@ __global__ void __launch_bounds__(64) k_ipm(DevConst c, DevBuffers d) {
             // ---- corrector forward: dz, ds, dl, max step, mu(alpha) sums, max |rp|, max |dz|
             double T0 = 0, T1 = 0, T2 = 0, amx = 1e30, rpm = 0, dzm = 0;
             xt = 0.0;
-            sweep(false, [&](int k, In& o) { load_fwd(k, o, true); }, [&](int k, const In& cur) {
+            sweep<(NPM <= 2)>(N, false, cur, nxt, [&](int k, In& o) { load_fwd(k, o, true); }, [&](int k, const In& cur) {
                 const bool aL = row_active(k, cur.lb), aU = row_active(k, cur.ub), aP = poly_slot_active(cur, k);
                 double v = 0.0, xn = 0.0;
                 if (k < N) fwd_step(cur, xt, v, xn);
