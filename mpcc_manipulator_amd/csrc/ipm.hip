@@ -86,15 +86,35 @@ __device__ __forceinline__ SlotStep slot_recover(double ri, double l, double rp,
     return {-rp - cd, W * (cd + rp) - rc * ri};
 }
 __device__ __forceinline__ double slot_coef(double ri, double l, double rp, double rc) { return l + (l * ri) * rp - rc * ri; }
-__device__ __forceinline__ double step_bound(double a, double s, double l, SlotStep d) {
-    if (d.ds < 0) a = fmin(a, -s / d.ds);
-    if (d.dl < 0) a = fmin(a, -l / d.dl);
-    return a;
+// Fraction-to-boundary ratio test min(a, -s/ds, -l/dl) without a division per slot: the running
+// minimum is kept as a ratio num/den (den > 0) and candidates are compared by cross-multiplication;
+// value() divides once.  It is the oracle's min over the same quotients (max_step, solve_struct_ipm),
+// exact unless two candidates tie to within rounding of the products.
+struct MinRatio {
+    double num, den;
+    __device__ __forceinline__ explicit MinRatio(double cap) : num(cap), den(1.0) {}
+    __device__ __forceinline__ void add(double n, double dneg) {  // candidate n / (-dneg), dneg < 0
+        const double d = -dneg;
+        const bool take = dneg < 0 && n * den < num * d;
+        num = take ? n : num;
+        den = take ? d : den;
+    }
+    __device__ __forceinline__ double value() const { return num / den; }
+};
+__device__ __forceinline__ void step_bound(MinRatio& a, double s, double l, SlotStep d) {
+    a.add(s, d.ds);
+    a.add(l, d.dl);
+}
+// 1/x for x > 0: v_rcp_f64 refined by two Newton steps (vs the ~10-instruction IEEE division sequence)
+__device__ __forceinline__ double rcp(double x) {
+    double r = __builtin_amdgcn_rcp(x);
+    r = fma(fma(-x, r, 1.0), r, r);
+    return fma(fma(-x, r, 1.0), r, r);
 }
 // corrector step of a slot given the iterate (cz), the predictor step (ca) and the corrector step (cd)
 __device__ __forceinline__ SlotStep slot_corr(double sgn, double bnd, double cz, double ca, double cd, double s, double l,
                                               double smu, double* rp_out) {
-    const double ri = 1.0 / s;
+    const double ri = rcp(s);
     const double rp = slot_rp(sgn, cz, bnd, s);
     const SlotStep pa = slot_recover(ri, l, rp, sgn * ca, s * l);
     const double rc = s * l + pa.ds * pa.dl - smu;
@@ -114,7 +134,7 @@ __device__ __forceinline__ bool chol8(double* L, double* dinv) {
         ok = ok && (d > 0);
         d = sqrt(d);
         L[jj + j] = d;
-        const double inv = 1.0 / d;
+        const double inv = rcp(d);
         dinv[j] = inv;
 #pragma unroll
         for (int i = j + 1; i < 8; i++) {
@@ -461,9 +481,9 @@ __global__ void __launch_bounds__(64) k_ipm(DevConst c, DevBuffers d) {
                 const double cz = row_cz(k, zx, zv);
                 const double pcz = poly_cz(cur, k, zx, zv);
                 double WL = 0, WU = 0, WP = 0, cL = 0, cU = 0, cP = 0;
-                if (aL) { const double rp = slot_rp(sgnL, cz, lb, sL); const double ri = 1.0 / sL; WL = lL * ri; cL = slot_coef(ri, lL, rp, sL * lL); }
-                if (aU) { const double rp = slot_rp(sgnU, cz, ub, sU); const double ri = 1.0 / sU; WU = lU * ri; cU = slot_coef(ri, lU, rp, sU * lU); }
-                if (aP) { const double rp = slot_rp(sgnU, pcz, cur.pub, sP); const double ri = 1.0 / sP; WP = lP * ri; cP = slot_coef(ri, lP, rp, sP * lP); }
+                if (aL) { const double rp = slot_rp(sgnL, cz, lb, sL); const double ri = rcp(sL); WL = lL * ri; cL = slot_coef(ri, lL, rp, sL * lL); }
+                if (aU) { const double rp = slot_rp(sgnU, cz, ub, sU); const double ri = rcp(sU); WU = lU * ri; cU = slot_coef(ri, lU, rp, sU * lU); }
+                if (aP) { const double rp = slot_rp(sgnU, pcz, cur.pub, sP); const double ri = rcp(sP); WP = lP * ri; cP = slot_coef(ri, lP, rp, sP * lP); }
                 const double wd = WL + WU;                 // diagonal weight of row t
                 const double dvr = sgnL * cL + sgnU * cU;  // signed coefficient of row t
                 // ---- objective gradient g0 = H z + h (f_xu = 0; oracle order: sum over z, then + h)
@@ -676,7 +696,8 @@ __global__ void __launch_bounds__(64) k_ipm(DevConst c, DevBuffers d) {
         PMARK(2);
         if (run) {
             // ---- predictor forward: x~_0 = 0; recover dsa, dla; max step; mu(alpha) sums
-            double S0 = 0, S1 = 0, S2 = 0, amax = 1.0;
+            double S0 = 0, S1 = 0, S2 = 0;
+            MinRatio amr(1.0);
             double xt = 0.0;
             sweep<(NPM <= 2)>(N, false, cur, nxt, [&](int k, In& o) { load_fwd(k, o, false); }, [&](int k, const In& cur) {
                 const bool aL = row_active(k, cur.lb), aU = row_active(k, cur.ub), aP = poly_slot_active(cur, k);
@@ -690,8 +711,8 @@ __global__ void __launch_bounds__(64) k_ipm(DevConst c, DevBuffers d) {
                 auto rec = [&](bool a, double sgn, double bnd, double czz, double caa, double s, double l) {
                     if (!a) return;
                     const double rp = slot_rp(sgn, czz, bnd, s);
-                    const SlotStep st = slot_recover(1.0 / s, l, rp, sgn * caa, s * l);
-                    amax = step_bound(amax, s, l, st);
+                    const SlotStep st = slot_recover(rcp(s), l, rp, sgn * caa, s * l);
+                    step_bound(amr, s, l, st);
                     S0 += s * l;
                     S1 += s * st.dl + l * st.ds;
                     S2 += st.ds * st.dl;
@@ -701,7 +722,7 @@ __global__ void __launch_bounds__(64) k_ipm(DevConst c, DevBuffers d) {
                 rec(aP, sgnU, cur.pub, pcz, pca, cur.sP, cur.lP);
                 xt = xn;
             });
-            amax = g_min(amax);
+            const double amax = g_min(amr.value());
             S0 = g_sum(S0); S1 = g_sum(S1); S2 = g_sum(S2);
             const double mu = (mcount > 0) ? S0 / mcount : 0.0;
             if (it == 0) mu0 = mu;
@@ -722,7 +743,7 @@ __global__ void __launch_bounds__(64) k_ipm(DevConst c, DevBuffers d) {
                 auto coef = [&](bool a, double sgn, double bnd, double czz, double caa, double s, double l) -> double {
                     if (!a) return 0.0;
                     const double rp = slot_rp(sgn, czz, bnd, s);
-                    const double ri = 1.0 / s;
+                    const double ri = rcp(s);
                     const SlotStep pa = slot_recover(ri, l, rp, sgn * caa, s * l);
                     const double rc = s * l + pa.ds * pa.dl - smu;
                     return slot_coef(ri, l, rp, rc);
@@ -761,7 +782,8 @@ __global__ void __launch_bounds__(64) k_ipm(DevConst c, DevBuffers d) {
             PMARK(4);
 
             // ---- corrector forward: dz, ds, dl, max step, mu(alpha) sums, max |rp|, max |dz|
-            double T0 = 0, T1 = 0, T2 = 0, amx = 1e30, rpm = 0, dzm = 0;
+            double T0 = 0, T1 = 0, T2 = 0, rpm = 0, dzm = 0;
+            MinRatio amc(1e30);
             xt = 0.0;
             sweep<(NPM <= 2)>(N, false, cur, nxt, [&](int k, In& o) { load_fwd(k, o, true); }, [&](int k, const In& cur) {
                 const bool aL = row_active(k, cur.lb), aU = row_active(k, cur.ub), aP = poly_slot_active(cur, k);
@@ -778,7 +800,7 @@ __global__ void __launch_bounds__(64) k_ipm(DevConst c, DevBuffers d) {
                     if (!a) return;
                     double rp;
                     const SlotStep st = slot_corr(sgn, bnd, czz, caa, cdd, s, l, smu, &rp);
-                    amx = step_bound(amx, s, l, st);
+                    step_bound(amc, s, l, st);
                     T0 += s * l;
                     T1 += s * st.dl + l * st.ds;
                     T2 += st.ds * st.dl;
@@ -789,7 +811,7 @@ __global__ void __launch_bounds__(64) k_ipm(DevConst c, DevBuffers d) {
                 rec(aP, sgnU, cur.pub, pcz, pca, pcd, cur.sP, cur.lP);
                 xt = xn;
             });
-            amx = g_min(amx);
+            const double amx = g_min(amc.value());
             T0 = g_sum(T0); T1 = g_sum(T1); T2 = g_sum(T2);
             rpm = g_max(rpm);
             dzm = g_max(dzm);
