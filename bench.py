@@ -55,10 +55,11 @@ def make_pool(m, params, mask, steps, device, pool_obs=(3.0, 3.0, 3.0, 0.0)):
         g, v, fl = eng.get_warmstart(1)
         pool["x0"].append(x[0].copy()); pool["u0"].append(u[0].copy())
         pool["guess"].append(g[0]); pool["valid"].append(v[0]); pool["fails"].append(fl[0])
-        out = eng.solve(x.copy(), u, obs)
+        xin = x.copy()
+        out = eng.solve(xin, u, obs)
         pool["status"].append(out["status"][0])
         u = out["u0"].copy()
-        x = sim_time_step(x, u, params.Ts)
+        x = sim_time_step(xin, u, params.Ts)  # the state runMPC mutated (main.cpp:103-105)
     eng.close()
     return {k: np.array(v) for k, v in pool.items()}, track
 

@@ -66,11 +66,14 @@ int main(int argc, char** argv) {
             std::printf("%d", k);
             for (double v : x) std::printf(",%.17g", v);
             const bool ok = mpc.runMPC_(ret, xs, u0, obs_p, obs_r);
+            x[7] = xs.s;  // runMPC_ updates s and vs of its state argument; the reference integrates that
+            x[8] = xs.vs; // state (main.cpp:103-105)
             u0 = ret.u0;
             const double u[8] = {u0.dq1, u0.dq2, u0.dq3, u0.dq4, u0.dq5, u0.dq6, u0.dq7, u0.dVs};
             for (double v : u) std::printf(",%.17g", v);
             std::printf(",%d,%d\n", (int)mpc.lastStatus(), ok ? 1 : 0);
             sim_time_step(x, u, Ts);
+            if (!ok) break;  // main.cpp:108-112
         }
     } catch (const Error& e) {
         std::fprintf(stderr, "error: %s\n", e.what());

@@ -193,6 +193,16 @@ int mpcc_solve_device(mpcc_engine* e, int B, double* d_x0, const double* d_u0, c
 int mpcc_solve_ocp(mpcc_engine* e, int B, const double* guess, const double* u_cur, const double* obs,
                    double* opt_sol, int32_t* status, int32_t* solved, mpcc_timing* timing);
 
+/* The reference's closed-loop driver (main.cpp:100-114) for B instances, device resident: each step runs
+ * runMPC_ (the engine's warm-start state carries over; x's s and vs are updated as mpc.cpp:107-115), takes
+ * u0 and integrates the updated state with simTimeStep (integrator.cpp:55-68).  An instance whose runMPC_
+ * returns false stops (main.cpp:108-112): its state stays the one that entered that step and later steps
+ * report status -1.  x0 [B*9] / u0 [B*8] in, out: final state / input; obs [B*4] constant;
+ * x_traj [(steps+1)*B*9], u_traj [steps*B*8], status_traj [steps*B] (any may be NULL).
+ * use_graph = 1 captures one control step in a hipGraph and replays it (same results, fewer launches). */
+int mpcc_closed_loop(mpcc_engine* e, int B, int steps, double* x0, double* u0, const double* obs, double* x_traj,
+                     double* u_traj, int32_t* status_traj, int use_graph);
+
 /* Integrator::simTimeStep (integrator.cpp:55-68) for B states, host arrays (closed-loop driver). */
 int mpcc_sim_time_step(mpcc_engine* e, int B, const double* x, const double* u, double ts, double* x_next);
 

@@ -675,6 +675,69 @@ int mpcc_solve_ocp(mpcc_engine* e, int B, const double* guess, const double* u_c
     return MPCC_OK;
 }
 
+int mpcc_closed_loop(mpcc_engine* e, int B, int steps, double* x0, double* u0, const double* obs, double* x_traj,
+                     double* u_traj, int32_t* status_traj, int use_graph) {
+    if (!e || B < 1 || B > e->maxB || steps < 0 || !x0 || !u0 || !obs)
+        return fail(MPCC_E_INVALID, "mpcc_closed_loop: invalid argument");
+    if (!e->has_track) return fail(MPCC_E_NOTRACK, "mpcc_closed_loop: set_track first");
+    std::vector<void*> owned;
+    auto dev = [&](size_t bytes) { void* p = dmalloc<char>(bytes ? bytes : 1); owned.push_back(p); return p; };
+    hipGraph_t graph = nullptr;
+    hipGraphExec_t exec = nullptr;
+    int rc = MPCC_OK;
+    try {
+        hipStream_t st = e->stream;
+        double* dx = (double*)dev((size_t)B * 9 * 8);
+        double* du = (double*)dev((size_t)B * 8 * 8);
+        double* dobs = (double*)dev((size_t)B * 4 * 8);
+        int32_t* alive = (int32_t*)dev((size_t)B * 4);
+        int* kstep = (int*)dev(sizeof(int));
+        double* xtraj = (double*)dev((size_t)(steps + 1) * B * 9 * 8);
+        double* utraj = (double*)dev((size_t)steps * B * 8 * 8);
+        int32_t* straj = (int32_t*)dev((size_t)steps * B * 4);
+        HIPCHK(hipMemcpyAsync(dx, x0, (size_t)B * 9 * 8, hipMemcpyHostToDevice, st));
+        HIPCHK(hipMemcpyAsync(du, u0, (size_t)B * 8 * 8, hipMemcpyHostToDevice, st));
+        HIPCHK(hipMemcpyAsync(dobs, obs, (size_t)B * 4 * 8, hipMemcpyHostToDevice, st));
+        std::vector<int32_t> ones(B, 1);
+        HIPCHK(hipMemcpyAsync(alive, ones.data(), (size_t)B * 4, hipMemcpyHostToDevice, st));
+        HIPCHK(hipMemsetAsync(kstep, 0, sizeof(int), st));
+        DevBuffers& d = e->d;
+        d.x0 = dx; d.u0 = du; d.obs = dobs;
+        d.u0_out = e->s_u0out; d.horizon = nullptr; d.status = e->s_status; d.ok = e->s_ok;
+        const double ts = e->params.Ts;
+        auto step = [&]() {
+            launch_loop_pre(B, dx, xtraj, kstep, st);
+            run_batch(e, B, st, nullptr);
+            launch_loop_post(B, ts, dx, du, xtraj, e->s_u0out, e->s_status, e->s_ok, alive, utraj, straj, kstep, st);
+        };
+        if (use_graph && steps > 0) {
+            HIPCHK(hipStreamSynchronize(st));
+            HIPCHK(hipStreamBeginCapture(st, hipStreamCaptureModeThreadLocal));
+            step();
+            HIPCHK(hipStreamEndCapture(st, &graph));
+            HIPCHK(hipGraphInstantiate(&exec, graph, nullptr, nullptr, 0));
+            for (int k = 0; k < steps; k++) HIPCHK(hipGraphLaunch(exec, st));
+        } else {
+            for (int k = 0; k < steps; k++) step();
+        }
+        launch_loop_pre(B, dx, xtraj, kstep, st);  // x_traj[steps] = final state
+        HIPCHK(hipGetLastError());
+        HIPCHK(hipMemcpyAsync(x0, dx, (size_t)B * 9 * 8, hipMemcpyDeviceToHost, st));
+        HIPCHK(hipMemcpyAsync(u0, du, (size_t)B * 8 * 8, hipMemcpyDeviceToHost, st));
+        if (x_traj) HIPCHK(hipMemcpyAsync(x_traj, xtraj, (size_t)(steps + 1) * B * 9 * 8, hipMemcpyDeviceToHost, st));
+        if (u_traj && steps) HIPCHK(hipMemcpyAsync(u_traj, utraj, (size_t)steps * B * 8 * 8, hipMemcpyDeviceToHost, st));
+        if (status_traj && steps)
+            HIPCHK(hipMemcpyAsync(status_traj, straj, (size_t)steps * B * 4, hipMemcpyDeviceToHost, st));
+        HIPCHK(hipStreamSynchronize(st));
+    } catch (const HipError& x) {
+        rc = fail(MPCC_E_HIP, std::string("mpcc_closed_loop: ") + x.what());
+    }
+    if (exec) (void)hipGraphExecDestroy(exec);
+    if (graph) (void)hipGraphDestroy(graph);
+    for (void* p : owned) (void)hipFree(p);
+    return rc;
+}
+
 int mpcc_sim_time_step(mpcc_engine* e, int B, const double* x, const double* u, double ts, double* x_next) {
     if (!e || B < 1 || !x || !u || !x_next) return fail(MPCC_E_INVALID, "mpcc_sim_time_step: invalid argument");
     try {

@@ -60,6 +60,10 @@ void launch_accept(const DevConst& c, const DevBuffers& d, hipStream_t s);
 void launch_apply(const DevConst& c, const DevBuffers& d, hipStream_t s);
 void launch_finalize(const DevConst& c, const DevBuffers& d, hipStream_t s);
 void launch_sim_step(int B, const double* x, const double* u, double ts, double* xn, hipStream_t s);
+void launch_loop_pre(int B, const double* x, double* xtraj, const int* kstep, hipStream_t s);
+void launch_loop_post(int B, double ts, double* x, double* u, const double* xtraj, const double* u0out,
+                      const int32_t* status, const int32_t* ok, int32_t* alive, double* utraj, int32_t* straj,
+                      int* kstep, hipStream_t s);
 void launch_debug_records(const DevConst& c, int M, const double* q, const double* obs, double* rec, hipStream_t s);
 void launch_debug_spline(const DevConst& c, int M, const double* sv, double* out, hipStream_t s);
 void launch_debug_project(const DevConst& c, int M, const double* sg, const double* ee, double* out, hipStream_t s);

@@ -509,6 +509,47 @@ __global__ void k_sim_step(int B, const double* __restrict__ x, const double* __
     for (int a = 0; a < 9; a++) xn[9 * b + a] = xc[a];
 }
 
+// ---- device closed loop (main.cpp:100-114; mpcc_closed_loop).  The step index lives in device memory
+//      so that one captured control step (hipGraph) can be replayed: k_loop_tick advances it.
+__global__ void k_loop_pre(int B, const double* __restrict__ x, double* __restrict__ xtraj, const int* __restrict__ kstep) {
+    const int b = blockIdx.x * blockDim.x + threadIdx.x;
+    if (b >= B) return;
+    const size_t o = ((size_t)*kstep * B + b) * 9;
+    for (int a = 0; a < 9; a++) xtraj[o + a] = x[9 * b + a];
+}
+// after runMPC_: a live instance takes u0 and integrates the state runMPC_ updated (simTimeStep); an
+// instance whose runMPC_ returned false stops (main.cpp:108-112) — its state is frozen at the state
+// that entered the failing step and later steps report status -1
+__global__ void k_loop_post(int B, double ts, double* __restrict__ x, double* __restrict__ u,
+                            const double* __restrict__ xtraj, const double* __restrict__ u0out,
+                            const int32_t* __restrict__ status, const int32_t* __restrict__ ok, int32_t* __restrict__ alive,
+                            double* __restrict__ utraj, int32_t* __restrict__ straj, const int* __restrict__ kstep) {
+    const int b = blockIdx.x * blockDim.x + threadIdx.x;
+    if (b >= B) return;
+    const int k = *kstep;
+    const bool live = alive[b] != 0;
+    const bool go = live && ok[b] != 0;
+    if (go) {
+        double xc[9], uu[8];
+        for (int a = 0; a < 8; a++) uu[a] = u0out[8 * b + a];
+        for (int a = 0; a < 9; a++) xc[a] = x[9 * b + a];
+        const int steps = (int)(ts / 0.001);
+        for (int i = 0; i < steps; i++) {
+            double t[9];
+            rk4_step(xc, uu, 0.001, t);
+            for (int a = 0; a < 9; a++) xc[a] = t[a];
+        }
+        for (int a = 0; a < 9; a++) x[9 * b + a] = xc[a];
+        for (int a = 0; a < 8; a++) u[8 * b + a] = uu[a];
+    } else {
+        for (int a = 0; a < 9; a++) x[9 * b + a] = xtraj[((size_t)k * B + b) * 9 + a];
+    }
+    if (live && !go) alive[b] = 0;
+    straj[(size_t)k * B + b] = live ? status[b] : -1;
+    for (int a = 0; a < 8; a++) utraj[((size_t)k * B + b) * 8 + a] = u[8 * b + a];
+}
+__global__ void k_loop_tick(int* kstep) { *kstep += 1; }
+
 // ---- debug kernels (stage-level parity) ----
 __global__ void k_debug_records(DevConst c, int M, const double* __restrict__ qin, const double* __restrict__ obsin,
                                 double* __restrict__ rec) {
@@ -597,6 +638,16 @@ void launch_finalize(const DevConst& c, const DevBuffers& d, hipStream_t s) {
 }
 void launch_sim_step(int B, const double* x, const double* u, double ts, double* xn, hipStream_t s) {
     hipLaunchKernelGGL(k_sim_step, dim3(nblk(B, 64)), dim3(64), 0, s, B, x, u, ts, xn);
+}
+void launch_loop_pre(int B, const double* x, double* xtraj, const int* kstep, hipStream_t s) {
+    hipLaunchKernelGGL(k_loop_pre, dim3(nblk(B, 64)), dim3(64), 0, s, B, x, xtraj, kstep);
+}
+void launch_loop_post(int B, double ts, double* x, double* u, const double* xtraj, const double* u0out,
+                      const int32_t* status, const int32_t* ok, int32_t* alive, double* utraj, int32_t* straj,
+                      int* kstep, hipStream_t s) {
+    hipLaunchKernelGGL(k_loop_post, dim3(nblk(B, 64)), dim3(64), 0, s, B, ts, x, u, xtraj, u0out, status, ok, alive,
+                       utraj, straj, kstep);
+    hipLaunchKernelGGL(k_loop_tick, dim3(1), dim3(1), 0, s, kstep);
 }
 void launch_debug_project(const DevConst& c, int M, const double* sg, const double* ee, double* out, hipStream_t s) {
     hipLaunchKernelGGL(k_debug_project, dim3(nblk(M, 64)), dim3(64), 0, s, c, M, sg, ee, out);

@@ -109,6 +109,7 @@ def lib():
         "mpcc_reset_warmstart": (C.c_int, [V, C.c_int, C.POINTER(C.c_uint8)]),
         "mpcc_solve": (C.c_int, [V, C.c_int, DP, DP, DP, DP, DP, IP, IP, C.POINTER(MpccTiming)]),
         "mpcc_solve_device": (C.c_int, [V, C.c_int, V, V, V, V, V, V, V, V]),
+        "mpcc_closed_loop": (C.c_int, [V, C.c_int, C.c_int, DP, DP, DP, DP, DP, IP, C.c_int]),
         "mpcc_set_track_path": (C.c_int, [V, C.c_int, DP, DP, DP, DP, DP]),
         "mpcc_solve_ocp": (C.c_int, [V, C.c_int, DP, DP, DP, DP, IP, IP, C.POINTER(MpccTiming)]),
         "mpcc_sim_time_step": (C.c_int, [V, C.c_int, DP, DP, D, DP]),
@@ -346,6 +347,18 @@ class Engine:
         if timing:
             out["timing"] = tm.as_dict()
         return out
+
+    def closed_loop(self, x0, u0, obs, steps, graph=True):
+        """main.cpp:100-114 on the device for B instances (mpcc_closed_loop).  Returns dict(x [steps+1,B,9],
+        u [steps,B,8], status [steps,B] (-1 after an instance stopped), x_final, u_final)."""
+        B = x0.shape[0]
+        x = _f64(x0, (B, 9)).copy()
+        u = _f64(u0, (B, 8)).copy()
+        obs = _f64(obs, (B, 4))
+        xt = np.zeros((steps + 1, B, 9)); ut = np.zeros((steps, B, 8)); stt = np.zeros((steps, B), np.int32)
+        _check(self.L.mpcc_closed_loop(self.h, B, int(steps), _dp(x), _dp(u), _dp(obs), _dp(xt), _dp(ut), _ip(stt),
+                                       int(bool(graph))), "mpcc_closed_loop")
+        return dict(x=xt, u=ut, status=stt, x_final=x, u_final=u)
 
     def solve_ocp(self, guess, u_cur, obs):
         """SolverInterface::setInitialGuess/setCurrentInput/setEnvData/solveOCP for B instances

@@ -20,8 +20,9 @@ def make_oracle(N=20, max_iter=2, mask=7, qp_mode=0, nthreads=1, overrides=None)
 
 
 def oracle_pool(o, steps, obs=(3.0, 3.0, 3.0, 0.0)):
-    """Closed loop (main.cpp:100-114): runMPC_ then simTimeStep.  Returns per-step controller inputs
-    (x0 before projection, u0, obs, warm start (guess, valid, fails) before the call)."""
+    """Closed loop (main.cpp:100-114): runMPC_ (which mutates x0's s, vs) then simTimeStep of the
+    mutated state.  Returns per-step controller inputs (x0 before projection, u0, obs, warm start
+    (guess, valid, fails) before the call)."""
     N = o.N
     x = np.zeros((1, 9)); x[0, :7] = Q0
     u = np.zeros((1, 8))
@@ -35,7 +36,7 @@ def oracle_pool(o, steps, obs=(3.0, 3.0, 3.0, 0.0)):
         out = o.run_mpc(xin, u, ob, guess, valid, fails)
         pool["status"].append(out["status"][0])
         u = out["u0"].copy()
-        x[0] = o.sim_time_step(x[0], u[0], o.params["Ts"])
+        x[0] = o.sim_time_step(xin[0], u[0], o.params["Ts"])
     return {k: np.array(v) for k, v in pool.items()}
 
 

@@ -202,8 +202,9 @@ def test_closed_loop_single(setup20):
         outo = o.run_mpc(xo, u, ob, go, vo, fo)
         assert outg["status"][0] == outo["status"][0], step
         assert np.abs(outg["u0"] - outo["u0"]).max() <= 1e-6, step
+        assert np.abs(xg - xo).max() <= 1e-9, step
         u = outo["u0"].copy()
-        x[0] = o.sim_time_step(x[0], u[0], o.params["Ts"])
+        x[0] = o.sim_time_step(xo[0], u[0], o.params["Ts"])  # the mutated state (main.cpp:103-105)
 
 
 @pytest.mark.parametrize("mask,B", [(2, 4096), (7, 1024)])
@@ -224,6 +225,42 @@ def test_benchmark_batch_parity(built_lib, oracle_lib, mask, B):
     assert np.abs(xg - xo).max() <= 1e-9
     assert np.array_equal(vg, vo) and np.array_equal(fg, fo)
     eng.close()
+
+
+# ---------------------------------------------------------------- the closed loop on the device
+def test_device_closed_loop(setup20):
+    """main.cpp:100-114 on the device for B instances (mpcc_closed_loop) against the oracle's loop:
+    runMPC_, then simTimeStep of the state runMPC_ updated, an instance stopping when runMPC_ returns
+    false.  Status at every step exact, inputs <= 1e-6, states <= 1e-8; the hipGraph replay is bitwise
+    the plain launch sequence."""
+    m, o, eng, pool = setup20
+    B, steps = 48, 25
+    rng = np.random.default_rng(SEED + 9)
+    z = rng.uniform(0.421, 0.621, B)
+    obs = np.column_stack([np.full(B, 0.48), np.full(B, 0.218), z, np.full(B, 5.0)])
+    x0, u0, obs, guess, valid, fails = batch_from_pool(pool, B, rng, obs=obs)
+    eng.set_warmstart(guess, valid, fails)
+    rg = eng.closed_loop(x0, u0, obs, steps, graph=True)
+    eng.set_warmstart(guess, valid, fails)
+    rp = eng.closed_loop(x0, u0, obs, steps, graph=False)
+    for key in ("x", "u", "status", "x_final", "u_final"):
+        assert np.array_equal(rg[key], rp[key]), key
+    x, u = x0.copy(), u0.copy()
+    g, v, f = guess.copy(), valid.copy(), fails.copy()
+    alive = np.ones(B, bool)
+    for k in range(steps):
+        assert np.abs(rg["x"][k] - x).max() <= 1e-8, k
+        xin = x.copy()
+        out = o.run_mpc(xin, u, obs, g, v, f)
+        assert np.array_equal(rg["status"][k], np.where(alive, out["status"], -1)), k
+        go = alive & (out["ok"] != 0)
+        u[go] = out["u0"][go]
+        for b in np.where(go)[0]:
+            x[b] = o.sim_time_step(xin[b], u[b], o.params["Ts"])
+        alive = go
+        assert np.abs(rg["u"][k] - u).max() <= 1e-6, k
+    assert np.abs(rg["x"][steps] - x).max() <= 1e-8
+    assert np.array_equal(rg["x_final"], rg["x"][steps])
 
 
 # ---------------------------------------------------------------- configs[2]: N = 40, both MLPs, obstacles

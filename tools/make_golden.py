@@ -33,7 +33,7 @@ def closed_loop(o, steps, obs):
         st.append(out["status"][0])
         u = out["u0"].copy()
         us.append(u[0].copy())
-        x[0] = o.sim_time_step(x[0], u[0], o.params["Ts"])
+        x[0] = o.sim_time_step(xin[0], u[0], o.params["Ts"])  # the state runMPC mutated (main.cpp:103-105)
     return np.array(xs), np.array(us), np.array(st, np.int32)
 
 
