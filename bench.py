@@ -98,7 +98,7 @@ def main():
     ap.add_argument("--N", type=int, default=None)
     ap.add_argument("--mask", type=int, default=None, help="polytopic rows: 1 self, 2 singularity, 4 env (configs[1] = 2)")
     ap.add_argument("--max-iter", type=int, default=2)
-    ap.add_argument("--pool-steps", type=int, default=400)
+    ap.add_argument("--pool-steps", type=int, default=1000)
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--cpu-sample", type=int, default=1024)
     ap.add_argument("--cpu-seconds", type=float, default=15.0, help="CPU-baseline budget (bounded sample)")
@@ -194,7 +194,11 @@ def main():
 
     # roofline of the dominant kernel (k_ipm: interior-point QP solve, one wave per instance)
     t_ipm = tm["solve_qp"] / max(1, nipm)
-    flops = B * algorithmic_qp_flops(N)
+    # QP solves per step: an instance solves min(sqp_iter + 1, max_iter) QPs (a SOLVED exit at SQP
+    # iteration i has solved i + 1); a launch is credited with the QPs it actually solved, on average
+    qps = int(np.minimum(stats["sqp_iter"] + 1, args.max_iter).sum())
+    launches_per_step = max(1, nipm) / max(1, ncalls)
+    flops = qps * algorithmic_qp_flops(N) / launches_per_step
     achieved = flops / t_ipm / 1e12
     traffic = None
     if os.path.exists(args.traffic):
@@ -204,7 +208,8 @@ def main():
             traffic = tr.get("hbm_bytes_per_launch")
     roof = {"kernel": "k_ipm", "bound": "mfma", "achieved": achieved, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
             "frac": achieved / FP64_PEAK_TFLOPS, "traffic": traffic,
-            "avg_launch_ms": t_ipm * 1e3, "launches_timed": nipm, "algorithmic_flops_per_launch": flops}
+            "avg_launch_ms": t_ipm * 1e3, "launches_timed": nipm, "algorithmic_flops_per_launch": flops,
+            "qp_solves_per_step": qps}
 
     # PCIe-inclusive rate (host buffers in and out through mpcc_solve): a diagnostic, never `value`
     pcie = None

@@ -148,6 +148,11 @@ int    mpcc_set_track(mpcc_engine* e, int n, const double* X, const double* Y, c
  * the reference's final fit (arc_length_spline.cpp:245-252).  Invalidates every warm start. */
 int    mpcc_set_track_path(mpcc_engine* e, int n, const double* s, const double* X, const double* Y, const double* Z,
                            const double* R9);
+/* Batched extension: one track per instance, instance b following way-points
+ * [b*n, (b+1)*n) of X, Y, Z (R9: 9 per point) — each built as MPC::setTrack would.  Later calls may use
+ * at most B instances; mpcc_set_track returns to one shared track.  mpcc_track_length / get_track_path
+ * report instance 0's track.  Invalidates every warm start. */
+int    mpcc_set_tracks(mpcc_engine* e, int B, int n, const double* X, const double* Y, const double* Z, const double* R9);
 double mpcc_track_length(mpcc_engine* e);
 /* final regular path data (getPathData): s, X, Y, Z [100], R9 [100*9] */
 /* host-only: build the arc-length spline from way-points without an engine (no GPU needed) and

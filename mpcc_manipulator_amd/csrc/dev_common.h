@@ -58,20 +58,33 @@ constexpr int MAX_FILT = 64;
 constexpr int SQ = SQ_FILT + 2 * MAX_FILT;
 
 // spline table (host-built, arc_length_spline.cpp:213-265): n points, regular grid
+// Track spline tables.  One track = 27 n + 2 doubles (n = NSPL): s[n] | a0 b0 c0 d0 | a1 .. | a2 .. |
+// R[9n] | cr[n] | dr[n] | logv[3n] | delta | L, padded to SPL_STRIDE.  Instance b uses the track at
+// base + b * stride: stride 0 = one shared track (MPC::setTrack), SPL_STRIDE = a track per instance.
+constexpr int SPL_A = NSPL, SPL_R = 13 * NSPL, SPL_CR = 22 * NSPL, SPL_DR = 23 * NSPL, SPL_LOGV = 24 * NSPL,
+              SPL_DELTA = 27 * NSPL, SPL_L = 27 * NSPL + 1, SPL_STRIDE = 27 * NSPL + 8;
 struct SplineDev {
-    const double* s;     // [n]
-    const double* a[3];  // x,y,z coefficients [n] (a = y data)
-    const double* b[3];  // [n-1]
-    const double* c[3];  // [n]
-    const double* d[3];  // [n-1]
-    const double* R;     // [n*9]
-    const double* cr;    // [n-1] 3/h^2
-    const double* dr;    // [n-1] -2/h^3
-    const double* logv;  // [(n-1)*3] invskew(LogMatrix(R_i^T R_{i+1}))
-    int n;
-    double delta;        // x_in(1) - x_in(0)
-    double L;            // s[n-1]
+    const double* base;
+    long stride;
 };
+// one track (cubic_spline.cpp / cubic_spline_rot.cpp tables of the final regular fit)
+struct SplineView {
+    const double* t;
+    double delta, L;
+    __device__ __forceinline__ double s(int i) const { return t[i]; }
+    __device__ __forceinline__ double a(int ax, int i) const { return t[SPL_A + 4 * NSPL * ax + i]; }
+    __device__ __forceinline__ double b(int ax, int i) const { return t[SPL_A + 4 * NSPL * ax + NSPL + i]; }
+    __device__ __forceinline__ double c(int ax, int i) const { return t[SPL_A + 4 * NSPL * ax + 2 * NSPL + i]; }
+    __device__ __forceinline__ double d(int ax, int i) const { return t[SPL_A + 4 * NSPL * ax + 3 * NSPL + i]; }
+    __device__ __forceinline__ const double* R(int i) const { return t + SPL_R + 9 * i; }
+    __device__ __forceinline__ double cr(int i) const { return t[SPL_CR + i]; }
+    __device__ __forceinline__ double dr(int i) const { return t[SPL_DR + i]; }
+    __device__ __forceinline__ const double* logv(int i) const { return t + SPL_LOGV + 3 * i; }
+};
+__device__ __forceinline__ SplineView spl_of(const SplineDev& sp, int b) {
+    const double* t = sp.base + (size_t)b * sp.stride;
+    return {t, t[SPL_DELTA], t[SPL_L]};
+}
 
 // Everything a kernel needs that is constant over a batch call (passed by value).
 struct DevConst {

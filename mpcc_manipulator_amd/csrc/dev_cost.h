@@ -24,7 +24,7 @@ struct RecView {  // strided view of one stage's robot record (SoA)
 
 // Stage cost.  want: 0 = objective only (line-search trials), 1 = objective + gradient + Hessian.
 // fx[9], fu[8], fxx[81] (row-major), fuu_diag[8]
-__device__ inline double stage_cost(const DevConst& c, const double* x, const double* u, const RecView& rec, int k,
+__device__ inline double stage_cost(const DevConst& c, const SplineView& sp, const double* x, const double* u, const RecView& rec, int k,
                                     bool want, double* fx, double* fu, double* fxx, double* fuu_diag) {
     const mpcc_params& p = c.p;
     const int N = c.N;
@@ -38,7 +38,7 @@ __device__ inline double stage_cost(const DevConst& c, const double* x, const do
     }
     const double s = x[7], vs = x[8];
     double pr[3], T[3], dd[3];
-    spline_pos3(c.spl, s, pr, T, dd);
+    spline_pos3(sp, s, pr, T, dd);
     const double ddr[3] = {dd[0], dd[1], dd[1]};  // Q2: ddz_ref = ddpos(1)
     double pos[3] = {rec[R_POS], rec[R_POS + 1], rec[R_POS + 2]};
     double et[3] = {pos[0] - pr[0], pos[1] - pr[1], pos[2] - pr[2]};
@@ -47,14 +47,14 @@ __device__ inline double stage_cost(const DevConst& c, const double* x, const do
     double ec[3] = {et[0] - el[0], et[1] - el[1], et[2] - el[2]};
     const double CC0 = (k < N) ? qc : p.q_c_N_mult * qc;
     const double CC1 = ql;
-    const double smax = c.spl.L;
+    const double smax = sp.L;
     const double des = (s < smax * p.deacc_ratio) ? p.desired_ee_velocity
                                                   : -p.desired_ee_velocity / (smax * p.deacc_ratio) * (s - smax);
     double obj_c = CC0 * (ec[0] * ec[0] + ec[1] * ec[1] + ec[2] * ec[2]) +
                    CC1 * (el[0] * el[0] + el[1] * el[1] + el[2] * el[2]) + p.q_vs * ((vs - des) * (vs - des));
     // heading (rotation error Log(R_ref^T R_ee))
     double Rref[9], dRref[3], Rcur[9], Rbar[9], w[3];
-    spline_rot(c.spl, s, Rref, want ? dRref : nullptr);
+    spline_rot(sp, s, Rref, want ? dRref : nullptr);
 #pragma unroll
     for (int a = 0; a < 9; a++) Rcur[a] = rec[R_ROT + a];
     m3mul_tn(Rref, Rcur, Rbar);

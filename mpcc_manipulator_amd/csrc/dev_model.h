@@ -248,52 +248,53 @@ __device__ inline void exp_skew(const double* v, double* E) {
 // unwrapInput (cubic_spline.cpp, arc_length_spline.cpp): std::max(0., std::min(x, L)) — comparison
 // semantics, so a NaN (0/0 Newton step at the track end, arc_length_spline.cpp:356-372) maps to 0,
 // where IEEE fmin/fmax would return L and end the projection there.
-__device__ __forceinline__ double spl_unwrap(const SplineDev& sp, double x) {
+__device__ __forceinline__ double spl_unwrap(const SplineView& sp, double x) {
     const double m = (sp.L < x) ? sp.L : x;
     return (0. < m) ? m : 0.;
 }
-__device__ __forceinline__ int spl_index(const SplineDev& sp, double x) {
-    if (x == sp.L) return sp.n - 1;
+__device__ __forceinline__ int spl_index(const SplineView& sp, double x) {
+    if (x == sp.L) return NSPL - 1;
     return (int)floor(x / sp.delta);
 }
 // position, first and second derivative of the x/y/z splines at arc length t
-__device__ inline void spline_pos3(const SplineDev& sp, double t, double* p, double* dp, double* ddp) {
+__device__ inline void spline_pos3(const SplineView& sp, double t, double* p, double* dp, double* ddp) {
     double x = spl_unwrap(sp, t);
     int i = spl_index(sp, x);
-    int n = sp.n;
-    double xi = sp.s[i];
+    const int n = NSPL;
+    double xi = sp.s(i);
     double d1 = x - xi, d2 = d1 * d1, d3 = d1 * d2;
 #pragma unroll
     for (int a = 0; a < 3; a++) {
         if (i == n - 1) {
-            if (p) p[a] = sp.a[a][n - 1];
+            if (p) p[a] = sp.a(a, n - 1);
             if (dp) dp[a] = 0.;
-            if (ddp) ddp[a] = 2.0 * sp.c[a][n - 1];
+            if (ddp) ddp[a] = 2.0 * sp.c(a, n - 1);
         } else {
-            double A = sp.a[a][i], B = sp.b[a][i], C = sp.c[a][i], D = sp.d[a][i];
+            double A = sp.a(a, i), B = sp.b(a, i), C = sp.c(a, i), D = sp.d(a, i);
             if (p) p[a] = A + B * d1 + C * d2 + D * d3;
             if (dp) dp[a] = B + 2.0 * C * d1 + 3.0 * D * d2;
             if (ddp) ddp[a] = 2.0 * C + 6.0 * D * d1;
         }
     }
 }
-__device__ inline void spline_rot(const SplineDev& sp, double t, double* R, double* dR) {
+__device__ inline void spline_rot(const SplineView& sp, double t, double* R, double* dR) {
     double x = spl_unwrap(sp, t);
     int i = spl_index(sp, x);
-    if (i == sp.n - 1) {
+    if (i == NSPL - 1) {
         if (R)
-            for (int a = 0; a < 9; a++) R[a] = sp.R[9 * (sp.n - 1) + a];
+            for (int a = 0; a < 9; a++) R[a] = sp.R(NSPL - 1)[a];
         if (dR) dR[0] = dR[1] = dR[2] = 0;
         return;
     }
-    double d1 = x - sp.s[i], d2 = d1 * d1, d3 = d1 * d2;
-    double lv[3] = {sp.logv[3 * i], sp.logv[3 * i + 1], sp.logv[3 * i + 2]};
-    double cr = sp.cr[i], dr = sp.dr[i];
+    double d1 = x - sp.s(i), d2 = d1 * d1, d3 = d1 * d2;
+    const double* lvp = sp.logv(i);
+    double lv[3] = {lvp[0], lvp[1], lvp[2]};
+    double cr = sp.cr(i), dr = sp.dr(i);
     if (R) {
         double f = cr * d2 + dr * d3;
         double v[3] = {lv[0] * f, lv[1] * f, lv[2] * f}, E[9];
         exp_skew(v, E);
-        m3mul(sp.R + 9 * i, E, R);
+        m3mul(sp.R(i), E, R);
     }
     if (dR) {
         double f = 2.0 * cr * d1 + 3.0 * dr * d2;
@@ -303,25 +304,25 @@ __device__ inline void spline_rot(const SplineDev& sp, double t, double* R, doub
 
 // projectOnSpline (arc_length_spline.cpp:318-379).  Far branch (quirk Q12) restated with Eigen's
 // scalar minCoeff semantics: NaN-masked valid entries never compare smaller, so index 0 wins.
-__device__ inline double project_on_spline(const SplineDev& sp, double proj_max_dist, double s_guess, const double* ee) {
+__device__ inline double project_on_spline(const SplineView& sp, double proj_max_dist, double s_guess, const double* ee) {
     double pp[3];
     spline_pos3(sp, s_guess, pp, nullptr, nullptr);
     double s_opt = s_guess;
     double dx = ee[0] - pp[0], dy = ee[1] - pp[1], dz = ee[2] - pp[2];
     double dist = sqrt(dx * dx + dy * dy + dz * dz);
     if (dist >= proj_max_dist) {
-        int n = sp.n;
+        const int n = NSPL;
         bool any = false;
         double best = 0;
         int bi = 0;
         for (int i = 0; i < n; i++) {
-            bool valid = fabs(sp.s[i] - s_guess) <= proj_max_dist;
+            bool valid = fabs(sp.s(i) - s_guess) <= proj_max_dist;
             any |= valid;
-            double ex = sp.a[0][i] - ee[0], ey = sp.a[1][i] - ee[1], ez = sp.a[2][i] - ee[2];
+            double ex = sp.a(0, i) - ee[0], ey = sp.a(1, i) - ee[1], ez = sp.a(2, i) - ee[2];
             double d2 = ex * ex + ey * ey + ez * ez;
             if (i == 0 || d2 < best) { best = d2; bi = i; }
         }
-        s_opt = any ? sp.s[0] : sp.s[bi];
+        s_opt = any ? sp.s(0) : sp.s(bi);
     }
     if (s_opt >= sp.L) return sp.L;
     double s_old = s_opt;

@@ -2,6 +2,7 @@
 // track upload and the batched runMPC_ launch sequence.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cmath>
 #include <cstdio>
 #include <cstring>
@@ -10,6 +11,7 @@
 #include <sstream>
 #include <stdexcept>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "host_json.h"
@@ -59,6 +61,7 @@ struct mpcc_engine {
     bool has_track = false;
     double* d_spl = nullptr;
     SplineDev spl{};
+    int n_tracks = 0;  // 1: shared track (stride 0); B: one per instance (mpcc_set_tracks)
     DevBuffers d{};
     // host-API staging
     double *s_x0 = nullptr, *s_u0 = nullptr, *s_obs = nullptr, *s_u0out = nullptr, *s_hor = nullptr;
@@ -231,31 +234,39 @@ void validate_params(const mpcc_params& p) {
         throw std::invalid_argument("do_SOC / use_BFGS (osqp_interface.cpp:658-757) are not supported by this engine");
 }
 
-void upload_track(mpcc_engine* e) {
-    const SplineTables& t = e->track;
+// one track's tables in the device layout (dev_common.h SplineDev): SPL_STRIDE doubles
+void pack_track(const SplineTables& t, double* out) {
     const int n = t.n;
-    // layout: s | a0 b0 c0 d0 | a1 .. | a2 .. | R (9n) | cr | dr | logv (3n)
-    std::vector<double> buf;
-    buf.reserve((size_t)n * 27);
-    auto push = [&](const std::vector<double>& v) { buf.insert(buf.end(), v.begin(), v.end()); };
-    push(t.s);
-    for (int a = 0; a < 3; a++) { push(t.a[a]); push(t.b[a]); push(t.c[a]); push(t.d[a]); }
-    push(t.R); push(t.cr); push(t.dr); push(t.logv);
+    if (n != NSPL) throw std::logic_error("spline tables must have N_SPLINE points");
+    size_t o = 0;
+    auto push = [&](const std::vector<double>& v, size_t len) {
+        if (v.size() != len) throw std::logic_error("spline table size");
+        std::memcpy(out + o, v.data(), len * sizeof(double));
+        o += len;
+    };
+    push(t.s, n);
+    for (int a = 0; a < 3; a++) { push(t.a[a], n); push(t.b[a], n); push(t.c[a], n); push(t.d[a], n); }
+    push(t.R, (size_t)9 * n); push(t.cr, n); push(t.dr, n); push(t.logv, (size_t)3 * n);
+    out[SPL_DELTA] = t.delta;
+    out[SPL_L] = t.length();
+    for (int i = SPL_L + 1; i < SPL_STRIDE; i++) out[i] = 0.0;
+}
+
+// tables of B tracks (B = 1 and stride 0: one track shared by every instance)
+void upload_tracks(mpcc_engine* e, const std::vector<SplineTables>& tracks, bool per_instance) {
+    std::vector<double> buf(tracks.size() * (size_t)SPL_STRIDE);
+    for (size_t i = 0; i < tracks.size(); i++) pack_track(tracks[i], buf.data() + i * SPL_STRIDE);
     if (e->d_spl) HIPCHK(hipFree(e->d_spl));
+    e->d_spl = nullptr;
     e->d_spl = dmalloc<double>(buf.size());
     HIPCHK(hipMemcpy(e->d_spl, buf.data(), buf.size() * sizeof(double), hipMemcpyHostToDevice));
-    SplineDev& s = e->spl;
-    const double* p = e->d_spl;
-    s.s = p; p += n;
-    for (int a = 0; a < 3; a++) { s.a[a] = p; p += n; s.b[a] = p; p += n; s.c[a] = p; p += n; s.d[a] = p; p += n; }
-    s.R = p; p += 9 * n;
-    s.cr = p; p += n;
-    s.dr = p; p += n;
-    s.logv = p;
-    s.n = n;
-    s.delta = t.delta;
-    s.L = t.length();
+    e->spl.base = e->d_spl;
+    e->spl.stride = per_instance ? SPL_STRIDE : 0;
+    e->track = tracks[0];
+    e->n_tracks = (int)tracks.size();
 }
+
+void upload_track(mpcc_engine* e) { upload_tracks(e, {e->track}, false); }
 
 void run_batch(mpcc_engine* e, int B, hipStream_t st, mpcc_timing* timing, bool ocp = false) {
     DevConst c = e->make_const(B);
@@ -458,6 +469,39 @@ int mpcc_set_track_path(mpcc_engine* e, int n, const double* s, const double* X,
     return MPCC_OK;
 }
 
+int mpcc_set_tracks(mpcc_engine* e, int B, int n, const double* X, const double* Y, const double* Z, const double* R9) {
+    if (!e || B < 1 || B > e->maxB || n < 3 || !X || !Y || !Z || !R9)
+        return fail(MPCC_E_INVALID, "mpcc_set_tracks: invalid argument");
+    try {
+        std::vector<SplineTables> tr(B);
+        const unsigned nt = std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
+        std::vector<std::thread> pool;
+        std::vector<std::string> err(nt);
+        for (unsigned w = 0; w < nt; w++)
+            pool.emplace_back([&, w]() {
+                try {
+                    for (int b = (int)w; b < B; b += (int)nt) {
+                        const size_t o = (size_t)b * n;
+                        tr[b] = build_track_spline(n, X + o, Y + o, Z + o, R9 + 9 * o);
+                    }
+                } catch (const std::exception& x) {
+                    err[w] = x.what();
+                }
+            });
+        for (auto& th : pool) th.join();
+        for (auto& m : err)
+            if (!m.empty()) throw std::invalid_argument(m);
+        upload_tracks(e, tr, true);
+        e->has_track = true;
+        HIPCHK(hipMemset(e->d.valid, 0, (size_t)e->maxB * sizeof(int32_t)));  // valid_initial_guess_ = false
+    } catch (const HipError& x) {
+        return fail(MPCC_E_HIP, std::string("mpcc_set_tracks: ") + x.what());
+    } catch (const std::exception& x) {
+        return fail(MPCC_E_INVALID, std::string("mpcc_set_tracks: ") + x.what());
+    }
+    return MPCC_OK;
+}
+
 int mpcc_track_build_host(int n, const double* X, const double* Y, const double* Z, const double* R9, double* s,
                           double* Xo, double* Yo, double* Zo, double* Ro9, double* length) {
     if (n < 3 || !X || !Y || !Z || !R9) return fail(MPCC_E_INVALID, "mpcc_track_build_host: invalid argument");
@@ -541,6 +585,7 @@ int mpcc_solve_device(mpcc_engine* e, int B, double* d_x0, const double* d_u0, c
     if (!e || B < 1 || B > e->maxB || !d_x0 || !d_u0 || !d_obs)
         return fail(MPCC_E_INVALID, "mpcc_solve_device: invalid argument");
     if (!e->has_track) return fail(MPCC_E_NOTRACK, "mpcc_solve_device: set_track first");
+    if (e->spl.stride && B > e->n_tracks) return fail(MPCC_E_INVALID, "mpcc_solve_device: more instances than per-instance tracks");
     try {
         hipStream_t st = stream ? (hipStream_t)stream : e->stream;
         e->d.x0 = d_x0; e->d.u0 = d_u0; e->d.obs = d_obs;
@@ -629,6 +674,7 @@ int mpcc_solve(mpcc_engine* e, int B, double* x0, const double* u0, const double
                int32_t* status, int32_t* ok, mpcc_timing* timing) {
     if (!e || B < 1 || B > e->maxB || !x0 || !u0 || !obs) return fail(MPCC_E_INVALID, "mpcc_solve: invalid argument");
     if (!e->has_track) return fail(MPCC_E_NOTRACK, "mpcc_solve: set_track first");
+    if (e->spl.stride && B > e->n_tracks) return fail(MPCC_E_INVALID, "mpcc_solve: more instances than per-instance tracks");
     try {
         hipStream_t st = e->stream;
         const size_t NS = e->N + 1;
@@ -656,6 +702,7 @@ int mpcc_solve_ocp(mpcc_engine* e, int B, const double* guess, const double* u_c
     if (!e || B < 1 || B > e->maxB || !guess || !u_cur || !obs || !opt_sol)
         return fail(MPCC_E_INVALID, "mpcc_solve_ocp: invalid argument");
     if (!e->has_track) return fail(MPCC_E_NOTRACK, "mpcc_solve_ocp: set_track first");
+    if (e->spl.stride && B > e->n_tracks) return fail(MPCC_E_INVALID, "mpcc_solve_ocp: more instances than per-instance tracks");
     try {
         hipStream_t st = e->stream;
         const size_t NS = e->N + 1;
@@ -680,6 +727,7 @@ int mpcc_closed_loop(mpcc_engine* e, int B, int steps, double* x0, double* u0, c
     if (!e || B < 1 || B > e->maxB || steps < 0 || !x0 || !u0 || !obs)
         return fail(MPCC_E_INVALID, "mpcc_closed_loop: invalid argument");
     if (!e->has_track) return fail(MPCC_E_NOTRACK, "mpcc_closed_loop: set_track first");
+    if (e->spl.stride && B > e->n_tracks) return fail(MPCC_E_INVALID, "mpcc_closed_loop: more instances than per-instance tracks");
     std::vector<void*> owned;
     auto dev = [&](size_t bytes) { void* p = dmalloc<char>(bytes ? bytes : 1); owned.push_back(p); return p; };
     hipGraph_t graph = nullptr;
@@ -884,6 +932,7 @@ int mpcc_debug_solve_qp(mpcc_engine* e, int B, const double* guess, const double
     if (!e || B < 1 || B > e->maxB || !guess || !rec || !u_cur)
         return fail(MPCC_E_INVALID, "mpcc_debug_solve_qp: invalid argument");
     if (!e->has_track) return fail(MPCC_E_NOTRACK, "mpcc_debug_solve_qp: no track");
+    if (e->spl.stride && B > e->n_tracks) return fail(MPCC_E_INVALID, "mpcc_debug_solve_qp: more instances than per-instance tracks");
     try {
         hipStream_t st = e->stream;
         const int N = e->N;

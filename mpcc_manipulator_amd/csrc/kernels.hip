@@ -30,7 +30,8 @@ __device__ inline void prepare_mpc(const DevConst& c, const DevBuffers& d, int b
     const double last_s = x[7];
     double ee[3], J[42];
     panda_fk(x, ee, nullptr, J, true);
-    x[7] = project_on_spline(c.spl, c.p.proj_max_dist, last_s, ee);
+    const SplineView sp = spl_of(c.spl, b);
+    x[7] = project_on_spline(sp, c.p.proj_max_dist, last_s, ee);
     double ev[3];
 #pragma unroll
     for (int i = 0; i < 3; i++) {
@@ -40,7 +41,7 @@ __device__ inline void prepare_mpc(const DevConst& c, const DevBuffers& d, int b
         ev[i] = s;
     }
     double dir[3];
-    spline_pos3(c.spl, x[7], nullptr, dir, nullptr);
+    spline_pos3(sp, x[7], nullptr, dir, nullptr);
     x[8] = ev[0] * dir[0] + ev[1] * dir[1] + ev[2] * dir[2];
     int valid = d.valid[b], fails = d.fails[b];
     if (fabs(last_s - x[7]) > c.p.guess_max_dist) { valid = 0; fails++; }
@@ -59,7 +60,7 @@ __device__ inline void prepare_mpc(const DevConst& c, const DevBuffers& d, int b
         }
         valid = 1;
     }
-    for (int i = 1; i <= N; i++) g[17 * i + 7] = fmin(g[17 * i + 7], c.spl.L);  // unwrapInitialGuess
+    for (int i = 1; i <= N; i++) g[17 * i + 7] = fmin(g[17 * i + 7], sp.L);  // unwrapInitialGuess
 #pragma unroll
     for (int i = 0; i < 9; i++) d.x0[9 * b + i] = x[i];
     d.valid[b] = valid;
@@ -130,7 +131,7 @@ __global__ void __launch_bounds__(64) k_records(DevConst c, DevBuffers d) {
 // k_setqp: stage QP record (setCost + setDynamics + setBounds + setPolytopicConstraints,
 // osqp_interface.cpp:129-344) in the stage-structured normalized form.
 // ------------------------------------------------------------------------------------------------
-__device__ inline void setqp_stage(const DevConst& c, const double* __restrict__ gb, const RecView& rv, int k,
+__device__ inline void setqp_stage(const DevConst& c, const SplineView& sp, const double* __restrict__ gb, const RecView& rv, int k,
                                    const double* __restrict__ ucur, double* __restrict__ q) {
     const mpcc_params& p = c.p;
     const int N = c.N;
@@ -139,7 +140,7 @@ __device__ inline void setqp_stage(const DevConst& c, const double* __restrict__
     const double* xk = gb + 17 * k;
     const double* uk = gb + 17 * k + 9;
     double fx[9], fu[8], fxx[81], fuu[8];
-    double obj = stage_cost(c, xk, uk, rv, k, true, fx, fu, fxx, fuu);
+    double obj = stage_cost(c, sp, xk, uk, rv, k, true, fx, fu, fxx, fuu);
     int flag = 0;
     for (int a = 0; a < 9; a++) {
         q[QS_q + a] = Tx[a] * fx[a];
@@ -238,7 +239,7 @@ __device__ inline void setqp_stage(const DevConst& c, const double* __restrict__
     }
     // box on y_k: state bounds (bounds.cpp:85-103, s trust region) intersected with the Q1 rows
     // (input bounds placed on stacked-state columns NU*i, osqp_interface.cpp:273)
-    const double L = c.spl.L;
+    const double L = sp.L;
     for (int m = 0; m < 9; m++) {
         double lo = p.lx[m], hi = p.ux[m];
         bool lo_inf = lo <= -BIG, hi_inf = hi >= BIG;
@@ -274,7 +275,7 @@ __global__ void __launch_bounds__(64) k_setqp(DevConst c, DevBuffers d, const do
     const double* gb = d.guess + (size_t)b * (N + 1) * 17;
     RecView rv{d.rec + t, c.S};
     double* q = d.qs + (size_t)t * QS;
-    setqp_stage(c, gb, rv, k, ucur_all + 8 * b, q);
+    setqp_stage(c, spl_of(c.spl, b), gb, rv, k, ucur_all + 8 * b, q);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -293,6 +294,7 @@ __global__ void __launch_bounds__(64) k_trial(DevConst c, DevBuffers d, const do
     if (!si[SQ_ACTIVE]) return;
     if (dead && !si[SQ_REJECT]) return;  // dead trials only follow a rejected alpha = 1
     const mpcc_params& p = c.p;
+    const SplineView sp = spl_of(c.spl, b);
     const double* gb = d.guess + (size_t)b * (N + 1) * 17;
     const double* sb = d.step + (size_t)b * (N + 1) * 17;
     auto tx = [&](int i, int a) { return gb[17 * i + a] + alpha * (p.Tx[a] * sb[17 * i + a]); };
@@ -302,7 +304,7 @@ __global__ void __launch_bounds__(64) k_trial(DevConst c, DevBuffers d, const do
     for (int a = 0; a < 8; a++) u[a] = tu(k, a);
     RecView rv{d.rec + t, c.S};
     double fdum[9], udum[8], hdum[81], rdum[8];
-    double obj = stage_cost(c, x, u, rv, k, false, fdum, udum, hdum, rdum);
+    double obj = stage_cost(c, sp, x, u, rv, k, false, fdum, udum, hdum, rdum);
     double objd = 0;
     if (k < N && k != N - 1) {
         double sq = 0;
@@ -327,7 +329,7 @@ __global__ void __launch_bounds__(64) k_trial(DevConst c, DevBuffers d, const do
     }
     for (int a = 0; a < 9; a++) {  // state bounds
         double l = p.lx[a], h = p.ux[a];
-        if (a == 7) { l = fmax(x[7] - p.s_trust_region, 0.); h = fmin(x[7] + p.s_trust_region, c.spl.L); }
+        if (a == 7) { l = fmax(x[7] - p.s_trust_region, 0.); h = fmin(x[7] + p.s_trust_region, sp.L); }
         lo += vfloor(fmax(l - x[a], 0.0), vf);
         up += vfloor(fmax(x[a] - h, 0.0), vf);
     }
@@ -584,15 +586,16 @@ __global__ void k_debug_spline(DevConst c, int M, const double* __restrict__ sv,
     const int t = blockIdx.x * blockDim.x + threadIdx.x;
     if (t >= M) return;
     double* o = out + (size_t)t * 21;
-    spline_pos3(c.spl, sv[t], o, o + 3, o + 6);
-    spline_rot(c.spl, sv[t], o + 9, o + 18);
+    const SplineView sp = spl_of(c.spl, 0);
+    spline_pos3(sp, sv[t], o, o + 3, o + 6);
+    spline_rot(sp, sv[t], o + 9, o + 18);
 }
 
 __global__ void k_debug_project(DevConst c, int M, const double* __restrict__ sg, const double* __restrict__ ee,
                                 double* __restrict__ out) {
     const int t = blockIdx.x * blockDim.x + threadIdx.x;
     if (t >= M) return;
-    out[t] = project_on_spline(c.spl, c.p.proj_max_dist, sg[t], ee + 3 * t);
+    out[t] = project_on_spline(spl_of(c.spl, 0), c.p.proj_max_dist, sg[t], ee + 3 * t);
 }
 
 __global__ void k_debug_cost(DevConst c, int M, const double* __restrict__ x, const double* __restrict__ u,
@@ -602,7 +605,7 @@ __global__ void k_debug_cost(DevConst c, int M, const double* __restrict__ x, co
     RecView rv{rec + t, M};
     double* o = out + (size_t)t * (1 + 9 + 8 + 81 + 64);
     double fuu[8];
-    o[0] = stage_cost(c, x + 9 * t, u + 8 * t, rv, kk[t], true, o + 1, o + 10, o + 18, fuu);
+    o[0] = stage_cost(c, spl_of(c.spl, 0), x + 9 * t, u + 8 * t, rv, kk[t], true, o + 1, o + 10, o + 18, fuu);
     for (int i = 0; i < 64; i++) o[99 + i] = 0.0;
     for (int i = 0; i < 8; i++) o[99 + 9 * i] = fuu[i];
 }

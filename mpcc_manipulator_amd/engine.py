@@ -110,6 +110,7 @@ def lib():
         "mpcc_solve": (C.c_int, [V, C.c_int, DP, DP, DP, DP, DP, IP, IP, C.POINTER(MpccTiming)]),
         "mpcc_solve_device": (C.c_int, [V, C.c_int, V, V, V, V, V, V, V, V]),
         "mpcc_closed_loop": (C.c_int, [V, C.c_int, C.c_int, DP, DP, DP, DP, DP, IP, C.c_int]),
+        "mpcc_set_tracks": (C.c_int, [V, C.c_int, C.c_int, DP, DP, DP, DP]),
         "mpcc_set_track_path": (C.c_int, [V, C.c_int, DP, DP, DP, DP, DP]),
         "mpcc_solve_ocp": (C.c_int, [V, C.c_int, DP, DP, DP, DP, IP, IP, C.POINTER(MpccTiming)]),
         "mpcc_sim_time_step": (C.c_int, [V, C.c_int, DP, DP, D, DP]),
@@ -292,6 +293,13 @@ class Engine:
         X, Y, Z = _f64(X), _f64(Y), _f64(Z)
         R = _f64(R).reshape(-1, 9)
         _check(self.L.mpcc_set_track(self.h, len(X), _dp(X), _dp(Y), _dp(Z), _dp(R)), "mpcc_set_track")
+
+    def set_tracks(self, X, Y, Z, R):
+        """One track per instance (mpcc_set_tracks): X, Y, Z [B, n], R [B, n, 3, 3]."""
+        X, Y, Z = _f64(X), _f64(Y), _f64(Z)
+        B, n = X.shape
+        R = _f64(R).reshape(B, n, 9)
+        _check(self.L.mpcc_set_tracks(self.h, B, n, _dp(X), _dp(Y), _dp(Z), _dp(R)), "mpcc_set_tracks")
 
     def set_track_path(self, s, X, Y, Z, R):
         """SolverInterface::setTrack(ArcLengthSpline): from getPathData() (100 regular points)."""

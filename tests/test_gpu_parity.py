@@ -263,6 +263,70 @@ def test_device_closed_loop(setup20):
     assert np.array_equal(rg["x_final"], rg["x"][steps])
 
 
+# ---------------------------------------------------------------- a track per instance
+def _track_variant(track, theta, scale):
+    """The default way-points rotated by theta about z through their start point and scaled about it
+    (rotations follow: R' = Rz R), as a different path for another controller of the batch."""
+    X, Y, Z, R = (np.asarray(a, float) for a in track)
+    c, sn = np.cos(theta), np.sin(theta)
+    Rz = np.array([[c, -sn, 0], [sn, c, 0], [0, 0, 1]])
+    P = np.stack([X - X[0], Y - Y[0], Z - Z[0]], 1) @ Rz.T * scale
+    return X[0] + P[:, 0], Y[0] + P[:, 1], Z[0] + P[:, 2], np.einsum("ij,njk->nik", Rz, R.reshape(-1, 3, 3))
+
+
+def test_per_instance_tracks(built_lib, oracle_lib):
+    """mpcc_set_tracks: instance b follows its own path.  Four track variants interleaved over 64
+    instances, each instance's state pool from the oracle's closed loop on its own track; every
+    instance matches the oracle holding that track (status, u <= 1e-6, x0 update, controller state).
+    Per-instance copies of one track are bitwise the shared track; a batch larger than the number of
+    tracks is refused."""
+    import mpcc_manipulator_amd as m
+    V, B, N = 4, 64, 20
+    base_o, P, track = make_oracle(N=N, max_iter=2, mask=7)
+    variants = [_track_variant(track, th, sc) for th, sc in [(0.0, 1.0), (-0.1, 1.05), (-0.2, 0.9), (0.1, 0.95)]]
+    orcs, pools = [], []
+    for X, Y, Z, R in variants:
+        o, _, _ = make_oracle(N=N, max_iter=2, mask=7)
+        o.set_track(X, Y, Z, R)
+        orcs.append(o)
+        pools.append(oracle_pool(o, 30))
+    rng = np.random.default_rng(SEED + 31)
+    inst = [batch_from_pool(pools[v], B // V, rng) for v in range(V)]
+    order = np.arange(B) % V                      # instance b -> variant b % V
+    pick = lambda j: np.stack([inst[order[b]][j][b // V] for b in range(B)])
+    x0, u0, obs, guess, valid, fails = (pick(j) for j in range(6))
+    n = len(variants[0][0])
+    TX = np.stack([variants[v][0] for v in order]); TY = np.stack([variants[v][1] for v in order])
+    TZ = np.stack([variants[v][2] for v in order]); TR = np.stack([variants[v][3] for v in order])
+    eng = m.Engine(m.load_params(N=N, overrides={"sqp": {"max_iter": 2}}), max_batch=2 * B, constraint_mask=7)
+    eng.set_tracks(TX, TY, TZ, TR)
+    eng.set_warmstart(guess, valid, fails)
+    xg = x0.copy()
+    outg = eng.solve(xg, u0, obs)
+    gg, vg, fg = eng.get_warmstart(B)
+    for v in range(V):
+        sel = np.where(order == v)[0]
+        xo = x0[sel].copy(); go = guess[sel].copy(); vo = valid[sel].copy(); fo = fails[sel].copy()
+        outo = orcs[v].run_mpc(xo, u0[sel], obs[sel], go, vo, fo)
+        assert np.array_equal(outg["status"][sel], outo["status"]), v
+        assert np.abs(outg["horizon"][sel] - outo["horizon"]).max() <= 1e-6, v
+        assert np.abs(xg[sel] - xo).max() <= 1e-9, v
+        assert np.array_equal(vg[sel], vo) and np.array_equal(fg[sel], fo), v
+    with pytest.raises(m.MpccError):
+        eng.solve(np.zeros((B + 1, 9)), np.zeros((B + 1, 8)), np.tile([3.0, 3.0, 3.0, 0.0], (B + 1, 1)))
+    # per-instance copies of one track == the shared track, bitwise
+    X, Y, Z, R = variants[1]
+    eng.set_tracks(np.tile(X, (B, 1)), np.tile(Y, (B, 1)), np.tile(Z, (B, 1)), np.tile(R, (B, 1, 1, 1)))
+    eng.set_warmstart(guess, valid, fails)
+    xa = x0.copy(); a = eng.solve(xa, u0, obs)
+    eng.set_track(X, Y, Z, R)
+    eng.set_warmstart(guess, valid, fails)
+    xb = x0.copy(); b2 = eng.solve(xb, u0, obs)
+    assert np.array_equal(a["horizon"], b2["horizon"]) and np.array_equal(xa, xb)
+    assert np.array_equal(a["status"], b2["status"])
+    eng.close()
+
+
 # ---------------------------------------------------------------- configs[2]: N = 40, both MLPs, obstacles
 def _obstacles(rng, B):
     """main_w_sim.py:42-45 scenario: xyz = (0.48, 0.218, z), z ~ U[0.421, 0.621], r = 5 cm."""

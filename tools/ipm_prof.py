@@ -31,7 +31,7 @@ def main():
     prof = getattr(L, "mpcc_debug_ipm_prof", None)
     params = m.load_params(args.N, overrides={"sqp": {"max_iter": 2}})
     params.constraint_mask = args.mask
-    pool, track = bench.make_pool(m, params, args.mask, 400, 0)
+    pool, track = bench.make_pool(m, params, args.mask, 1000, 0)
     for B in args.batch:
         eng = m.Engine(params, max_batch=B, device=0, constraint_mask=args.mask)
         eng.set_track(*track)

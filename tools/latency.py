@@ -16,7 +16,7 @@ import mpcc_manipulator_amd as m  # noqa: E402
 def main(steps=300):
     params = m.load_params(20, overrides={"sqp": {"max_iter": 2}})
     params.constraint_mask = 2
-    pool, track = bench.make_pool(m, params, 2, 400, 0)
+    pool, track = bench.make_pool(m, params, 2, 1000, 0)
     eng = m.Engine(params, max_batch=1, device=0, constraint_mask=2)
     eng.set_track(*track)
     x0 = np.zeros((1, 9)); x0[0, :7] = bench.Q0
