@@ -113,12 +113,21 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # MPCC_BENCH_REHEARSE=1: every rank on GPU 0 over gloo — rehearses the multi-rank path (sharding,
+    # u0 gather, max-over-ranks timing, aggregation) on a one-GPU box; real runs use one GPU per rank
+    # over RCCL ("nccl")
+    rehearse = os.environ.get("MPCC_BENCH_REHEARSE", "0") == "1"
+    if rehearse:
+        local = 0
     import torch
     torch.cuda.set_device(local)
     dist = None
     if world > 1:
         import torch.distributed as dist
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if rehearse:
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
 
     import mpcc_manipulator_amd as m
     from mpcc_manipulator_amd.distributed import gather_u0, max_over_ranks, shard_bounds
@@ -256,7 +265,8 @@ def main():
                                    (f"configs[2]: batch={B}/GPU Panda MPCC instances, N={N}, self+env collision NN "
                                     f"constraints (mask={args.mask}), per-instance obstacles, {args.max_iter} SQP iters"),
                        "batch_per_gpu": B, "global_batch": B * world, "horizon": N, "sqp_iters": args.max_iter,
-                       "parallelism": f"instance-sharded x{world}" + (", RCCL all_gather(u0)" if world > 1 else "")},
+                       "parallelism": f"instance-sharded x{world}" + ((", gloo rehearsal, all ranks on GPU 0" if rehearse else
+                                                                  ", RCCL all_gather(u0)") if world > 1 else "")},
             "roofline": roof,
             "cpu_baseline": cpu,
         }
