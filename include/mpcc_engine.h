@@ -159,6 +159,14 @@ double mpcc_track_length(mpcc_engine* e);
  * return its path data and total length (ArcLengthSpline::gen6DSpline + getPathData). */
 int    mpcc_track_build_host(int n, const double* X, const double* Y, const double* Z, const double* R9,
                              double* s, double* Xo, double* Yo, double* Zo, double* Ro9, double* length);
+/* host-only ArcLengthSpline queries on the spline of n way-points (built as mpcc_track_build_host):
+ * getPosition / getDerivative / getSecondDerivative / getOrientation / getOrientationDerivative at M
+ * arc lengths s (pos, d1, d2 [M*3], R [M*9], dR [M*3]; any may be NULL) and projectOnSpline(s_guess, ee)
+ * for M points (arc_length_spline.cpp:267-379) */
+int    mpcc_track_eval_host(int n, const double* X, const double* Y, const double* Z, const double* R9, int M,
+                            const double* s, double* pos, double* d1, double* d2, double* R, double* dR);
+int    mpcc_track_project_host(int n, const double* X, const double* Y, const double* Z, const double* R9, int M,
+                               double proj_max_dist, const double* s_guess, const double* ee, double* s_out);
 int    mpcc_get_track_path(mpcc_engine* e, double* s, double* X, double* Y, double* Z, double* R9);
 
 /* Per-instance controller state (mpc.h:119-127), device resident.  guess [B*(N+1)*17]. */

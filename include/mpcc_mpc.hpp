@@ -141,6 +141,8 @@ class MPC {
     void setParam(const ParamValue& param_value);
     Status lastStatus() const { return last_status_; }
     std::array<double, 3> eePosition(const std::array<double, 7>& q) { return impl_.eePosition(q); }
+    int horizon() const { return impl_.horizon(); }
+    mpcc_engine* engine() { return impl_.engine(); }
 
    private:
     BatchMPC impl_;

@@ -51,7 +51,29 @@ def build(verbose=False):
         if verbose:
             print("built", LIB)
     build_examples(verbose)
+    build_python_module(verbose)
     return LIB
+
+
+def build_python_module(verbose=False):
+    """MPCC_WRAPPER (csrc/wrapper_py.cpp, pybind11): the reference's Python module names over the
+    engine, written next to libmpcc_engine.so (rpath $ORIGIN)."""
+    import sysconfig
+    import pybind11
+    src = os.path.join(CSRC, "wrapper_py.cpp")
+    out = os.path.join(BUILD, "MPCC_WRAPPER" + sysconfig.get_config_var("EXT_SUFFIX"))
+    deps = [src, LIB] + [os.path.join(ROOT, "include", h) for h in os.listdir(os.path.join(ROOT, "include"))]
+    if os.path.exists(out) and os.path.getmtime(out) >= max(os.path.getmtime(d) for d in deps):
+        return out
+    cmd = ["g++", "-O2", "-std=c++17", "-shared", "-fPIC", "-fvisibility=hidden", "-I", os.path.join(ROOT, "include"),
+           "-I", pybind11.get_include(), "-I", sysconfig.get_paths()["include"], src, "-o", out,
+           "-L", BUILD, "-lmpcc_engine", "-Wl,-rpath,$ORIGIN", "-ldl"]
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if r.returncode != 0:
+        raise RuntimeError(f"MPCC_WRAPPER build failed: {' '.join(cmd)}\n{r.stdout}\n{r.stderr}")
+    if verbose:
+        print("built", out)
+    return out
 
 
 EXAMPLES = os.path.join(ROOT, "examples")

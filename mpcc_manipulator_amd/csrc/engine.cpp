@@ -502,6 +502,33 @@ int mpcc_set_tracks(mpcc_engine* e, int B, int n, const double* X, const double*
     return MPCC_OK;
 }
 
+int mpcc_track_eval_host(int n, const double* X, const double* Y, const double* Z, const double* R9, int M,
+                         const double* s, double* pos, double* d1, double* d2, double* R, double* dR) {
+    if (n < 3 || M < 0 || !X || !Y || !Z || !R9 || (M && !s)) return fail(MPCC_E_INVALID, "mpcc_track_eval_host: invalid argument");
+    try {
+        const SplineTables t = build_track_spline(n, X, Y, Z, R9);
+        for (int i = 0; i < M; i++)
+            eval_tables(t, s[i], pos ? pos + 3 * i : nullptr, d1 ? d1 + 3 * i : nullptr, d2 ? d2 + 3 * i : nullptr,
+                        R ? R + 9 * i : nullptr, dR ? dR + 3 * i : nullptr);
+    } catch (const std::exception& x) {
+        return fail(MPCC_E_INVALID, std::string("mpcc_track_eval_host: ") + x.what());
+    }
+    return MPCC_OK;
+}
+
+int mpcc_track_project_host(int n, const double* X, const double* Y, const double* Z, const double* R9, int M,
+                            double proj_max_dist, const double* s_guess, const double* ee, double* s_out) {
+    if (n < 3 || M < 0 || !X || !Y || !Z || !R9 || (M && (!s_guess || !ee || !s_out)))
+        return fail(MPCC_E_INVALID, "mpcc_track_project_host: invalid argument");
+    try {
+        const SplineTables t = build_track_spline(n, X, Y, Z, R9);
+        for (int i = 0; i < M; i++) s_out[i] = project_tables(t, proj_max_dist, s_guess[i], ee + 3 * i);
+    } catch (const std::exception& x) {
+        return fail(MPCC_E_INVALID, std::string("mpcc_track_project_host: ") + x.what());
+    }
+    return MPCC_OK;
+}
+
 int mpcc_track_build_host(int n, const double* X, const double* Y, const double* Z, const double* R9, double* s,
                           double* Xo, double* Yo, double* Zo, double* Ro9, double* length) {
     if (n < 3 || !X || !Y || !Z || !R9) return fail(MPCC_E_INVALID, "mpcc_track_build_host: invalid argument");

@@ -291,4 +291,94 @@ SplineTables build_track_from_path(int n, const double* s, const double* X, cons
     return t;
 }
 
+// ---- host evaluation of the final tables: the device's spline_pos3 / spline_rot / project_on_spline
+//      (dev_model.h), i.e. cubic_spline.cpp:126-246, cubic_spline_rot.cpp:216-259, arc_length_spline.cpp:318-379
+namespace {
+double tab_unwrap(const SplineTables& t, double x) {
+    const double L = t.length();
+    const double m = (L < x) ? L : x;
+    return (0. < m) ? m : 0.;
+}
+int tab_index(const SplineTables& t, double x) {
+    if (x == t.length()) return t.n - 1;
+    return (int)std::floor(x / t.delta);
+}
+}  // namespace
+
+void eval_tables(const SplineTables& t, double s, double* p, double* dp, double* ddp, double* R9, double* dR) {
+    const double x = tab_unwrap(t, s);
+    const int i = tab_index(t, x);
+    const int n = t.n;
+    const double d1 = x - t.s[i], d2 = d1 * d1, d3 = d1 * d2;
+    for (int a = 0; a < 3; a++) {
+        if (i == n - 1) {
+            if (p) p[a] = t.a[a][n - 1];
+            if (dp) dp[a] = 0.;
+            if (ddp) ddp[a] = 2.0 * t.c[a][n - 1];
+        } else {
+            const double A = t.a[a][i], B = t.b[a][i], C = t.c[a][i], D = t.d[a][i];
+            if (p) p[a] = A + B * d1 + C * d2 + D * d3;
+            if (dp) dp[a] = B + 2.0 * C * d1 + 3.0 * D * d2;
+            if (ddp) ddp[a] = 2.0 * C + 6.0 * D * d1;
+        }
+    }
+    if (i == n - 1) {
+        if (R9) for (int a = 0; a < 9; a++) R9[a] = t.R[(size_t)9 * (n - 1) + a];
+        if (dR) dR[0] = dR[1] = dR[2] = 0.;
+        return;
+    }
+    const double* lv = &t.logv[(size_t)3 * i];
+    const double cr = t.cr[i], dr = t.dr[i];
+    if (R9) {
+        const double f = cr * d2 + dr * d3;
+        double v[3] = {lv[0] * f, lv[1] * f, lv[2] * f}, E[9];
+        exp_skew(v, E);
+        const double* Ri = &t.R[(size_t)9 * i];
+        for (int r = 0; r < 3; r++)
+            for (int c = 0; c < 3; c++) {
+                double acc = 0;
+                for (int k = 0; k < 3; k++) acc += Ri[3 * r + k] * E[3 * k + c];
+                R9[3 * r + c] = acc;
+            }
+    }
+    if (dR) {
+        const double f = 2.0 * cr * d1 + 3.0 * dr * d2;
+        dR[0] = lv[0] * f; dR[1] = lv[1] * f; dR[2] = lv[2] * f;
+    }
+}
+
+double project_tables(const SplineTables& t, double proj_max_dist, double s_guess, const double* ee) {
+    double pp[3];
+    eval_tables(t, s_guess, pp, nullptr, nullptr, nullptr, nullptr);
+    double s_opt = s_guess;
+    const double dx = ee[0] - pp[0], dy = ee[1] - pp[1], dz = ee[2] - pp[2];
+    if (std::sqrt(dx * dx + dy * dy + dz * dz) >= proj_max_dist) {  // far branch (Q12), as the device
+        bool any = false;
+        double best = 0;
+        int bi = 0;
+        for (int i = 0; i < t.n; i++) {
+            any |= std::fabs(t.s[i] - s_guess) <= proj_max_dist;
+            const double ex = t.a[0][i] - ee[0], ey = t.a[1][i] - ee[1], ez = t.a[2][i] - ee[2];
+            const double d2 = ex * ex + ey * ey + ez * ez;
+            if (i == 0 || d2 < best) { best = d2; bi = i; }
+        }
+        s_opt = any ? t.s[0] : t.s[bi];
+    }
+    if (s_opt >= t.length()) return t.length();
+    double s_old = s_opt;
+    for (int it = 0; it < 20; it++) {
+        double p[3], dp[3], ddp[3];
+        eval_tables(t, s_opt, p, dp, ddp, nullptr, nullptr);
+        const double d0 = p[0] - ee[0], d1 = p[1] - ee[1], d2 = p[2] - ee[2];
+        const double jac = 2.0 * d0 * dp[0] + 2.0 * d1 * dp[1] + 2.0 * d2 * dp[2];
+        const double hes = 2.0 * dp[0] * dp[0] + 2.0 * d0 * ddp[0] + 2.0 * dp[1] * dp[1] + 2.0 * d1 * ddp[1] +
+                           2.0 * dp[2] * dp[2] + 2.0 * d2 * ddp[2];
+        s_opt -= jac / hes;
+        s_opt = tab_unwrap(t, s_opt);
+        if (std::fabs(s_old - s_opt) <= 1e-5) return s_opt;
+        s_old = s_opt;
+    }
+    return s_guess;
+}
+
 }  // namespace mpcc

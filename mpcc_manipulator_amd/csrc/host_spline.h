@@ -28,6 +28,11 @@ SplineTables build_track_spline(int n, const double* X, const double* Y, const d
 SplineTables build_track_from_path(int n, const double* s, const double* X, const double* Y, const double* Z,
                                    const double* R9);
 
+// evaluation of the final tables at arc length s (any output may be null): the device formulas
+void eval_tables(const SplineTables& t, double s, double* p, double* dp, double* ddp, double* R9, double* dR);
+// ArcLengthSpline::projectOnSpline(s_guess, ee) (arc_length_spline.cpp:318-379), as the device
+double project_tables(const SplineTables& t, double proj_max_dist, double s_guess, const double* ee);
+
 // quaternion (x, y, z, w) -> rotation as Eigen Quaterniond::normalized().toRotationMatrix() (track.cpp:45-53)
 void quat_to_rot(double qx, double qy, double qz, double qw, double* R9);
 
