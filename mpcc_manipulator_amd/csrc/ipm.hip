@@ -36,6 +36,7 @@ constexpr int IPM_MAX_IT = MPCC_IPM_MAXIT;  // 60 (oracle); a debug build may ca
 constexpr double IPM_TOL_MU = 1e-13, IPM_TOL_P = 1e-11, IPM_TOL_STEP = 1e-11;
 constexpr double IPM_TOL_FB = 1e-9;  // P2: a converged iterate is accepted when the Riccati factor breaks down
 constexpr double IPM_DIV = 1e6;      // P3: mu > IPM_DIV * mu_0 -> primal infeasible (divergent multipliers)
+constexpr double IPM_TAU = 0.995;    // fraction-to-boundary floor: tau = max(IPM_TAU, 1 - sqrt(mu))
 constexpr int IPW = 4;               // instances per wavefront (16 lanes each)
 
 // workspace fields, ws[(b*(N+1) + k)*IS + field*16 + lane]
@@ -815,7 +816,7 @@ __global__ void __launch_bounds__(64) k_ipm(DevConst c, DevBuffers d) {
             T0 = g_sum(T0); T1 = g_sum(T1); T2 = g_sum(T2);
             rpm = g_max(rpm);
             dzm = g_max(dzm);
-            alpha = fmin(1.0, 0.995 * amx);
+            alpha = fmin(1.0, fmax(IPM_TAU, 1.0 - sqrt(mu)) * amx);  // adaptive fraction to the boundary (oracle)
             sigma_mu = smu;
             pending = true;
             it++;

@@ -1094,6 +1094,7 @@ constexpr int IPM_MAX_IT = 60;
 constexpr double IPM_TOL_MU = 1e-13, IPM_TOL_P = 1e-11, IPM_TOL_STEP = 1e-11;
 constexpr double IPM_TOL_FB = 1e-9;  // P2: accept a converged iterate when the Riccati factor breaks down
 constexpr double IPM_DIV = 1e6;      // P3: mu > IPM_DIV * mu_0 -> primal infeasible (divergent multipliers)
+constexpr double IPM_TAU = 0.995;    // fraction-to-boundary floor
 constexpr double FEAS_TOL = 1e-9;
 
 // ---------------- stage-structured primal-dual IPM with a Riccati factorization ----------------
@@ -1515,7 +1516,11 @@ static int solve_struct_ipm(const StructQP& S, std::vector<double>& step, int* i
         gs = g0; add_rows(gs, coef);
         R.solve(S, gs, dz);
         recover(dz, ds, dl);
-        double a = std::min(1.0, 0.995 * max_step(ds, dl, 1e30));
+        // fraction to the boundary: tau = max(0.995, 1 - sqrt(mu)) lets the step approach the boundary as
+        // mu -> 0 (superlinear final phase; 10.4 -> 9.2 mean IPM iterations on the configs[1] workload,
+        // DESIGN.md §3.2); k_ipm applies the same rule
+        const double tau = std::max(IPM_TAU, 1.0 - std::sqrt(mu));
+        double a = std::min(1.0, tau * max_step(ds, dl, 1e30));
         double dzmax = 0;
         for (size_t i = 0; i < z.size(); i++) { z[i] += a * dz[i]; dzmax = std::max(dzmax, std::fabs(dz[i])); }
         for (int i = 0; i < m; i++) { sl[i] += a * ds[i]; lam[i] += a * dl[i]; }
@@ -1645,7 +1650,7 @@ static int solve_dense_ipm(const DenseQP& q, std::vector<double>& step, int* ite
         for (int i = 0; i < m; i++) rc[i] = s[i] * lam[i] + dsa[i] * dla[i] - sigma * mu;
         std::vector<double> dx, dnu, dS, dL;
         if (!do_solve(rc, dx, dnu, dS, dL)) break;
-        double a = std::min(1.0, 0.995 * max_step(dS, dL, 1e30));
+        double a = std::min(1.0, std::max(IPM_TAU, 1.0 - std::sqrt(mu)) * max_step(dS, dL, 1e30));
         double dxmax = 0;
         for (int j = 0; j < nv; j++) { x[j] += a * dx[j]; dxmax = std::max(dxmax, std::fabs(dx[j])); }
         last_dx = dxmax;
