@@ -103,7 +103,7 @@ def main():
     ap.add_argument("--cpu-sample", type=int, default=1024)
     ap.add_argument("--cpu-seconds", type=float, default=15.0, help="CPU-baseline budget (bounded sample)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "pmc_traffic_k_ipm.json"))
+    ap.add_argument("--traffic", default=None, help="PMC traffic summary (default profiles/pmc_traffic_<kernel>.json)")
     args = ap.parse_args()
     preset = {1: dict(batch=4096, N=20, mask=2), 2: dict(batch=65536, N=40, mask=7)}[args.config]
     for k, v in preset.items():
@@ -201,7 +201,9 @@ def main():
     value = B * world * args.steps / elapsed
     ms = elapsed / args.steps * 1e3
 
-    # roofline of the dominant kernel (k_ipm: interior-point QP solve, one wave per instance)
+    # roofline of the dominant kernel: k_sqp (the SQP loop with its interior-point QP solves, 16 lanes
+    # per instance), or k_ipm alone when the staged SQP loop is selected (MPCC_STAGED_SQP=1)
+    kname = "k_ipm" if os.environ.get("MPCC_STAGED_SQP", "0") == "1" else "k_sqp"
     t_ipm = tm["solve_qp"] / max(1, nipm)
     # QP solves per step: an instance solves min(sqp_iter + 1, max_iter) QPs (a SOLVED exit at SQP
     # iteration i has solved i + 1); a launch is credited with the QPs it actually solved, on average
@@ -210,12 +212,13 @@ def main():
     flops = qps * algorithmic_qp_flops(N) / launches_per_step
     achieved = flops / t_ipm / 1e12
     traffic = None
-    if os.path.exists(args.traffic):
-        with open(args.traffic) as f:
+    tpath = args.traffic or os.path.join(ROOT, "profiles", f"pmc_traffic_{kname}.json")
+    if os.path.exists(tpath):
+        with open(tpath) as f:
             tr = json.load(f)
-        if tr.get("batch") == B and tr.get("N") == N:
+        if tr.get("batch") == B and tr.get("N") == N and tr.get("kernel", "k_ipm") == kname:
             traffic = tr.get("hbm_bytes_per_launch")
-    roof = {"kernel": "k_ipm", "bound": "mfma", "achieved": achieved, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
+    roof = {"kernel": kname, "bound": "mfma", "achieved": achieved, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
             "frac": achieved / FP64_PEAK_TFLOPS, "traffic": traffic,
             "avg_launch_ms": t_ipm * 1e3, "launches_timed": nipm, "algorithmic_flops_per_launch": flops,
             "qp_solves_per_step": qps}

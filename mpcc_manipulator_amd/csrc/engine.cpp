@@ -5,6 +5,7 @@
 #include <algorithm>
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <fstream>
 #include <memory>
@@ -54,6 +55,9 @@ using namespace mpcc;
 
 struct mpcc_engine {
     mpcc_config cfg{};
+    // SQP loop: fused per-instance kernel k_sqp (default) or one launch per stage of each iteration
+    // (MPCC_STAGED_SQP=1; same arithmetic, kept for A/B timing and debugging)
+    bool staged_sqp = false;
     mpcc_params params{};
     int N = 0, maxB = 0;
     hipStream_t stream = nullptr;
@@ -296,6 +300,19 @@ void run_batch(mpcc_engine* e, int B, hipStream_t st, mpcc_timing* timing, bool 
         launch_nn(c, d, e->nn_env.desc, e->nn_env.d, 1, c.S, nullptr, nullptr, d.rec, c.S, st);
     if (tm) t_env1 = mark();
     const double* ucur = d.u0;
+    if (!e->staged_sqp) {
+        // first QP assembly lane-per-stage, then the whole SQP loop per instance in one kernel
+        int a0 = -1, a1 = -1, b1 = -1;
+        if (tm) a0 = mark();
+        launch_setqp(c, d, ucur, st);
+        if (tm) a1 = mark();
+        launch_sqp(c, d, ucur, poly_rows_max(c.p.constraint_mask), st);
+        if (tm) {
+            b1 = mark();
+            set_qp.push_back({a0, a1});
+            solve_qp.push_back({a1, b1});
+        }
+    } else {
     for (int it = 0; it < c.p.max_iter; it++) {
         int a0 = -1, a1 = -1, b1 = -1, c1 = -1;
         if (tm) a0 = mark();
@@ -319,6 +336,7 @@ void run_batch(mpcc_engine* e, int B, hipStream_t st, mpcc_timing* timing, bool 
             solve_qp.push_back({a1, b1});
             get_alpha.push_back({b1, c1});
         }
+    }
     }
     launch_finalize(c, d, st);
     HIPCHK(hipGetLastError());
@@ -356,6 +374,8 @@ int mpcc_create(const mpcc_config* cfg, const mpcc_params* params, const char* n
     std::unique_ptr<mpcc_engine> e(new mpcc_engine());
     try {
         e->cfg = *cfg;
+        const char* st = std::getenv("MPCC_STAGED_SQP");
+        e->staged_sqp = st && st[0] == '1';
         e->params = *params;
         e->params.N = cfg->N;
         e->params.Ts = cfg->Ts;

@@ -26,6 +26,10 @@
 #include "dev_common.h"
 #include "dev_dpp.h"
 #include "kernels.h"
+// QP assembly and line-search pieces of k_sqp: oracle operation order, no FP contraction
+#pragma clang fp contract(off)
+#include "dev_sqp.h"
+#pragma clang fp contract(fast)
 
 namespace mpcc {
 
@@ -206,11 +210,12 @@ __device__ __forceinline__ void sweep(int N, bool backward, In& b0, In& b1, Load
 
 }  // namespace
 
+// The QP solve of the 4 instances of this wavefront (16 lanes each); instances whose SQP is inactive
+// idle through it.  Writes the step (d.step), QP status and IPM iteration count (d.sqi).
 template <int NPM>
-__global__ void __launch_bounds__(64) k_ipm(DevConst c, DevBuffers d) {
+__device__ __forceinline__ void ipm_group(const DevConst& c, const DevBuffers& d, double* smem) {
     constexpr int NPE = NPM > 0 ? NPM : 1;
     using In = StageIn<NPE>;
-    extern __shared__ __attribute__((aligned(16))) double smem[];
     const int lane = threadIdx.x;
     const int grp = lane >> 4;
     const int t = lane & 15;
@@ -875,9 +880,98 @@ extern "C" int mpcc_debug_ipm_prof(unsigned long long* out, int reset) {
 }
 #endif
 
+// k_ipm: one QP solve per active instance (the staged SQP loop of run_batch and the debug QP entry)
+template <int NPM>
+__global__ void __launch_bounds__(64) k_ipm(DevConst c, DevBuffers d) {
+    extern __shared__ __attribute__((aligned(16))) double smem[];
+    ipm_group<NPM>(c, d, smem);
+}
+
+// ------------------------------------------------------------------------------------------------
+// k_sqp: the whole SQP loop of solveOCP (osqp_interface.cpp:431-574) per instance, one 16-lane group
+// per instance: QP solve, filter line-search trial (lane = stage), filter decision, step and
+// termination, then the next iteration's QP assembly (lane = stage) — without leaving the kernel.
+// An instance that needs another SQP iteration starts it as soon as its own line search is done, so
+// its second QP overlaps the first QPs of the rest of the batch instead of running as a separate,
+// nearly empty launch.  The first iteration's QP records come from k_setqp.  Arithmetic is that of
+// k_setqp / k_trial / k_accept / k_apply (dev_sqp.h, no FP contraction).
+// ------------------------------------------------------------------------------------------------
+// Phases of k_sqp as separate (non-inlined) functions: each has its own register allocation, so the
+// QP assembly and trial code does not add live ranges to the register-resident interior point.
+__device__ __attribute__((noinline)) void sqp_setqp_phase(const DevConst& c, const DevBuffers& d, int b, int t,
+                                                          const double* __restrict__ ucur) {
+    const int N = c.N, NS = N + 1;
+    const SplineView sp = spl_of(c.spl, b);
+    const double* gb = d.guess + (size_t)b * NS * 17;
+    for (int k = t; k <= N; k += 16)
+        setqp_stage(c, sp, gb, RecView{d.rec + (size_t)b * NS + k, c.S}, k, ucur, d.qs + ((size_t)b * NS + k) * QS);
+}
+__device__ __attribute__((noinline)) void sqp_trial_phase(const DevConst& c, const DevBuffers& d, int b, int t,
+                                                          const double* __restrict__ ucur, double alpha, bool keep) {
+    const int N = c.N, NS = N + 1;
+    for (int k = t; k <= N; k += 16) {
+        double out[4];
+        trial_stage(c, d, b, k, alpha, ucur, out);
+        if (keep) {
+            double* tr = d.trial + ((size_t)b * NS + k) * 4;
+            for (int i = 0; i < 4; i++) tr[i] = out[i];
+        }
+    }
+}
+template <int NPM>
+__device__ __attribute__((noinline)) void sqp_ipm_phase(const DevConst& c, const DevBuffers& d, double* smem) {
+    ipm_group<NPM>(c, d, smem);
+}
+
+template <int NPM>
+__global__ void __launch_bounds__(64) k_sqp(DevConst c, DevBuffers d, const double* __restrict__ ucur_all) {
+    extern __shared__ __attribute__((aligned(16))) double smem[];
+    const int t = threadIdx.x & 15;
+    const int b = blockIdx.x * IPW + (threadIdx.x >> 4);
+    const bool valid = b < c.Bn;
+    const int N = c.N, NS = N + 1;
+    const int bb = valid ? b : 0;
+    int32_t* si = d.sqi + (size_t)bb * SQI;
+    const double* ucur = ucur_all + 8 * bb;
+    for (int it = 0; it < c.p.max_iter; it++) {
+        bool act = valid && si[SQ_ACTIVE] != 0;
+        if (__ballot(act) == 0) break;
+        if (it > 0) {
+            if (act) sqp_setqp_phase(c, d, b, t, ucur);
+            __syncthreads();
+        }
+        sqp_ipm_phase<NPM>(c, d, smem);
+        __syncthreads();
+        act = valid && si[SQ_ACTIVE] != 0;
+        if (act) sqp_trial_phase(c, d, b, t, ucur, 1.0, true);
+        __syncthreads();
+        if (act && t == 0) accept_instance(c, d, b);
+        __syncthreads();
+        if (act && c.faithful_dead_trials && si[SQ_REJECT]) {  // discarded trials (Q5), evaluated for timing fidelity
+            double alpha = 1.0;
+            for (int l = 1; l < c.p.line_search_max_iter; l++) {
+                alpha *= c.p.line_search_tau;
+                sqp_trial_phase(c, d, b, t, ucur, alpha, false);
+            }
+        }
+        double nrm = 0.0;
+        if (act) {
+            const double alpha = d.sqd[(size_t)b * SQ + SQ_ALPHA];
+            for (int e = t; e < NS * 17; e += 16) nrm = fmax(nrm, apply_elem(c, d, b, e, alpha));
+        }
+        nrm = g_max(nrm);  // DPP: whole row active
+        if (act && t == 0) finish_iteration(c, d, b, nrm);
+        __syncthreads();
+    }
+}
+
 template <int NPM>
 static void launch_ipm_t(const DevConst& c, const DevBuffers& d, hipStream_t s) {
     hipLaunchKernelGGL(k_ipm<NPM>, dim3((c.Bn + IPW - 1) / IPW), dim3(64), ipm_lds_bytes(c.N, NPM), s, c, d);
+}
+template <int NPM>
+static void launch_sqp_t(const DevConst& c, const DevBuffers& d, const double* u_cur, hipStream_t s) {
+    hipLaunchKernelGGL(k_sqp<NPM>, dim3((c.Bn + IPW - 1) / IPW), dim3(64), ipm_lds_bytes(c.N, NPM), s, c, d, u_cur);
 }
 
 void launch_ipm(const DevConst& c, const DevBuffers& d, int npmax, hipStream_t s) {
@@ -888,6 +982,16 @@ void launch_ipm(const DevConst& c, const DevBuffers& d, int npmax, hipStream_t s
         case 9: launch_ipm_t<9>(c, d, s); break;
         case 10: launch_ipm_t<10>(c, d, s); break;
         default: launch_ipm_t<11>(c, d, s); break;
+    }
+}
+void launch_sqp(const DevConst& c, const DevBuffers& d, const double* u_cur, int npmax, hipStream_t s) {
+    switch (npmax) {
+        case 0: launch_sqp_t<0>(c, d, u_cur, s); break;
+        case 1: launch_sqp_t<1>(c, d, u_cur, s); break;
+        case 2: launch_sqp_t<2>(c, d, u_cur, s); break;
+        case 9: launch_sqp_t<9>(c, d, u_cur, s); break;
+        case 10: launch_sqp_t<10>(c, d, u_cur, s); break;
+        default: launch_sqp_t<11>(c, d, u_cur, s); break;
     }
 }
 

@@ -11,8 +11,7 @@
 //     k_trial      thread / (instance,stage) filter line-search trial at alpha = 1 (objective, violation)
 //     k_accept     thread / instance         filter, step, termination
 //   k_finalize     thread / instance         Status -> warm start / outputs (osqp_interface.cpp:575-589, mpc.cpp:140-189)
-#include "dev_cost.h"
-#include "kernels.h"
+#include "dev_sqp.h"
 
 namespace mpcc {
 
@@ -128,144 +127,8 @@ __global__ void __launch_bounds__(64) k_records(DevConst c, DevBuffers d) {
 }
 
 // ------------------------------------------------------------------------------------------------
-// k_setqp: stage QP record (setCost + setDynamics + setBounds + setPolytopicConstraints,
-// osqp_interface.cpp:129-344) in the stage-structured normalized form.
+// k_setqp: stage QP record (setqp_stage, dev_sqp.h), one lane per (instance, stage)
 // ------------------------------------------------------------------------------------------------
-__device__ inline void setqp_stage(const DevConst& c, const SplineView& sp, const double* __restrict__ gb, const RecView& rv, int k,
-                                   const double* __restrict__ ucur, double* __restrict__ q) {
-    const mpcc_params& p = c.p;
-    const int N = c.N;
-    const double* Tx = p.Tx;
-    const double* Tu = p.Tu;
-    const double* xk = gb + 17 * k;
-    const double* uk = gb + 17 * k + 9;
-    double fx[9], fu[8], fxx[81], fuu[8];
-    double obj = stage_cost(c, sp, xk, uk, rv, k, true, fx, fu, fxx, fuu);
-    int flag = 0;
-    for (int a = 0; a < 9; a++) {
-        q[QS_q + a] = Tx[a] * fx[a];
-        for (int bb = 0; bb < 9; bb++) {
-            double v = Tx[a] * fxx[a * 9 + bb] * Tx[bb];
-            q[QS_Q + a * 9 + bb] = v;
-            if (isnan(v)) flag |= 1;
-        }
-    }
-    // PD check of the state block (LLT pivots; NaN pivots pass as in Eigen)
-    {
-        double L[45];
-        int idx = 0;
-        for (int i = 0; i < 9; i++)
-            for (int j = 0; j <= i; j++) L[idx++] = q[QS_Q + i * 9 + j];
-        for (int j = 0; j < 9; j++) {
-            int jj = j * (j + 1) / 2;
-            double dgn = L[jj + j];
-            for (int m = 0; m < j; m++) dgn -= L[jj + m] * L[jj + m];
-            if (dgn <= 0) { flag |= 2; break; }
-            dgn = sqrt(dgn);
-            L[jj + j] = dgn;
-            for (int i = j + 1; i < 9; i++) {
-                int ii = i * (i + 1) / 2;
-                double s = L[ii + j];
-                for (int m = 0; m < j; m++) s -= L[ii + m] * L[jj + m];
-                L[ii + j] = s / dgn;
-            }
-        }
-    }
-    const double rddq = p.qp_r_ddq;
-    double objd = 0.0;
-    if (k < N) {
-        for (int j = 0; j < 8; j++) {
-            q[QS_r + j] = Tu[j] * fu[j];
-            q[QS_R + j] = Tu[j] * fuu[j] * Tu[j];
-        }
-        // ddq cost (osqp_interface.cpp:166-217)
-        if (k != N - 1) {
-            const double* un = gb + 17 * (k + 1) + 9;
-            double sq = 0;
-            for (int j = 0; j < DOF; j++) sq += (un[j] - uk[j]) * (un[j] - uk[j]);
-            objd = rddq * sq;
-        }
-        for (int j = 0; j < DOF; j++) {
-            double gg;
-            if (k == 0) gg = 2. * rddq * (uk[j] - gb[17 * (k + 1) + 9 + j]);
-            else if (k == N - 1) gg = 2. * rddq * (uk[j] - gb[17 * (k - 1) + 9 + j]);
-            else gg = 2. * rddq * (2. * uk[j] - gb[17 * (k + 1) + 9 + j] - gb[17 * (k - 1) + 9 + j]);
-            q[QS_r + j] += Tu[j] * gg;
-            double cii = (k == 0 || k == N - 1) ? 2. * rddq : 4. * rddq;
-            q[QS_R + j] += Tu[j] * cii * Tu[j];
-        }
-        for (int j = 0; j < 8; j++) if (isnan(q[QS_R + j])) flag |= 1;
-        // dynamics offset b_k = -c_{k+1} = -Tx^-1 (x_{k+1} - (A x_k + B u_k + g))   (:247)
-        const double* xn = gb + 17 * (k + 1);
-        for (int a = 0; a < 9; a++) {
-            double s1 = 0, s2 = 0;
-            for (int m = 0; m < 9; m++) s1 += c.A[a * 9 + m] * xk[m];
-            for (int m = 0; m < 8; m++) s2 += c.B[a * 8 + m] * uk[m];
-            double pred = s1 + s2 + 0.0;
-            q[QS_B + a] = -((1.0 / Tx[a]) * (xn[a] - pred));
-        }
-        // ddq rows (setBounds :279-297): v_0[j] (k=0) or v_k[j]-v_{k-1}[j] within (l - c) / coef
-        for (int j = 0; j < DOF; j++) {
-            double coef = 1. / p.Ts * Tu[j];
-            double cc, lo, hi;
-            if (k == 0) {
-                cc = 1. / p.Ts * uk[j];
-                lo = p.lddq[j] + 1. / p.Ts * ucur[j];
-                hi = p.uddq[j] + 1. / p.Ts * ucur[j];
-            } else {
-                cc = 1. / p.Ts * (uk[j] - gb[17 * (k - 1) + 9 + j]);
-                lo = p.lddq[j];
-                hi = p.uddq[j];
-            }
-            q[QS_DLB + j] = (lo - cc) / coef;
-            q[QS_DUB + j] = (hi - cc) / coef;
-        }
-        // polytopic rows (setPolytopicConstraints :302-344); upper bound 0 - c, lower -INF
-        int np = 0;
-        for (int r = 0; r < NPC; r++) {
-            double val, a[7], bv[7];
-            if (!poly_row(c, uk, rv, r, &val, true, a, bv)) continue;
-            double* row = q + QS_POLY + POLY_W * np;
-            for (int j = 0; j < 7; j++) { row[j] = a[j]; row[7 + j] = bv[j]; }
-            row[14] = 0.0 - val;
-            np++;
-        }
-        q[QS_NPOLY] = (double)np;
-    } else {
-        for (int j = 0; j < 8; j++) { q[QS_r + j] = 0.0; q[QS_R + j] = 0.0; }
-        for (int a = 0; a < 9; a++) q[QS_B + a] = 0.0;
-        for (int j = 0; j < 7; j++) { q[QS_DLB + j] = -INF; q[QS_DUB + j] = INF; }
-        q[QS_NPOLY] = 0.0;
-    }
-    // box on y_k: state bounds (bounds.cpp:85-103, s trust region) intersected with the Q1 rows
-    // (input bounds placed on stacked-state columns NU*i, osqp_interface.cpp:273)
-    const double L = sp.L;
-    for (int m = 0; m < 9; m++) {
-        double lo = p.lx[m], hi = p.ux[m];
-        bool lo_inf = lo <= -BIG, hi_inf = hi >= BIG;
-        if (m == 7) { lo = fmax(xk[7] - p.s_trust_region, 0.); hi = fmin(xk[7] + p.s_trust_region, L); lo_inf = hi_inf = false; }
-        double ylo = lo_inf ? -INF : (lo - xk[m]) / Tx[m];
-        double yhi = hi_inf ? INF : (hi - xk[m]) / Tx[m];
-        const int idx = 9 * k + m;
-        const int i = idx / 8, j = idx % 8;
-        if (i < N) {
-            const double ui = gb[17 * i + 9 + j];
-            if (p.lu[j] > -BIG) ylo = fmax(ylo, (p.lu[j] - ui) / Tu[j]);
-            if (p.uu[j] < BIG) yhi = fmin(yhi, (p.uu[j] - ui) / Tu[j]);
-        }
-        q[QS_YLB + m] = ylo;
-        q[QS_YUB + m] = yhi;
-        const double FEAS = 1e-9;
-        if (k == 0) {
-            if (ylo > FEAS || yhi < -FEAS) flag |= 4;  // constant rows on y_0 = 0
-        } else if (ylo > yhi) {
-            flag |= 4;
-        }
-    }
-    q[QS_FLAG] = (double)flag;
-    q[QS_OBJ] = obj + objd;
-}
-
 __global__ void __launch_bounds__(64) k_setqp(DevConst c, DevBuffers d, const double* __restrict__ ucur_all) {
     const int t = blockIdx.x * blockDim.x + threadIdx.x;
     if (t >= c.S) return;
@@ -279,10 +142,8 @@ __global__ void __launch_bounds__(64) k_setqp(DevConst c, DevBuffers d, const do
 }
 
 // ------------------------------------------------------------------------------------------------
-// k_trial: filterLineSearch trial (osqp_interface.cpp:759-808) — objective and l1 constraint
-// violation (:824-833) of setQP(obj, constr) at guess + alpha * T * step, one lane per stage.
-// Rows owned by stage k: dynamics block k, state bounds k, input bounds (Q1) k, ddq block k,
-// polytopic block k.
+// k_trial / k_accept / k_apply: filter line search and step (dev_sqp.h) as lane-per-stage and
+// lane-per-instance kernels; k_sqp (ipm.hip) runs the same pieces per instance inside the QP kernel.
 // ------------------------------------------------------------------------------------------------
 __global__ void __launch_bounds__(64) k_trial(DevConst c, DevBuffers d, const double* __restrict__ ucur_all,
                                              double alpha, int dead) {
@@ -293,166 +154,28 @@ __global__ void __launch_bounds__(64) k_trial(DevConst c, DevBuffers d, const do
     const int32_t* si = d.sqi + (size_t)b * SQI;
     if (!si[SQ_ACTIVE]) return;
     if (dead && !si[SQ_REJECT]) return;  // dead trials only follow a rejected alpha = 1
-    const mpcc_params& p = c.p;
-    const SplineView sp = spl_of(c.spl, b);
-    const double* gb = d.guess + (size_t)b * (N + 1) * 17;
-    const double* sb = d.step + (size_t)b * (N + 1) * 17;
-    auto tx = [&](int i, int a) { return gb[17 * i + a] + alpha * (p.Tx[a] * sb[17 * i + a]); };
-    auto tu = [&](int i, int a) { return (i < N) ? gb[17 * i + 9 + a] + alpha * (p.Tu[a] * sb[17 * i + 9 + a]) : gb[17 * i + 9 + a]; };
-    double x[9], u[8];
-    for (int a = 0; a < 9; a++) x[a] = tx(k, a);
-    for (int a = 0; a < 8; a++) u[a] = tu(k, a);
-    RecView rv{d.rec + t, c.S};
-    double fdum[9], udum[8], hdum[81], rdum[8];
-    double obj = stage_cost(c, sp, x, u, rv, k, false, fdum, udum, hdum, rdum);
-    double objd = 0;
-    if (k < N && k != N - 1) {
-        double sq = 0;
-        for (int j = 0; j < DOF; j++) { double dlt = tu(k + 1, j) - u[j]; sq += dlt * dlt; }
-        objd = p.qp_r_ddq * sq;
-    }
-    double lo = 0, up = 0;  // sum (l - c)^+ and sum (c - u)^+ (parity policy P1: noise floor per row)
-    const double vf = p.vio_floor;
-    auto vfloor = [](double v, double f) { return (v > f) ? v : 0.0; };
-    if (k >= 1) {  // dynamics rows, l = u = 0
-        double xp[9], up_[8];
-        for (int a = 0; a < 9; a++) xp[a] = tx(k - 1, a);
-        for (int a = 0; a < 8; a++) up_[a] = tu(k - 1, a);
-        for (int a = 0; a < 9; a++) {
-            double s1 = 0, s2 = 0;
-            for (int m = 0; m < 9; m++) s1 += c.A[a * 9 + m] * xp[m];
-            for (int m = 0; m < 8; m++) s2 += c.B[a * 8 + m] * up_[m];
-            double cv = (1.0 / p.Tx[a]) * (x[a] - (s1 + s2 + 0.0));
-            lo += vfloor(fmax(0.0 - cv, 0.0), vf);
-            up += vfloor(fmax(cv - 0.0, 0.0), vf);
-        }
-    }
-    for (int a = 0; a < 9; a++) {  // state bounds
-        double l = p.lx[a], h = p.ux[a];
-        if (a == 7) { l = fmax(x[7] - p.s_trust_region, 0.); h = fmin(x[7] + p.s_trust_region, sp.L); }
-        lo += vfloor(fmax(l - x[a], 0.0), vf);
-        up += vfloor(fmax(x[a] - h, 0.0), vf);
-    }
-    if (k < N) {
-        for (int a = 0; a < 8; a++) {  // input bounds (constr = u, :274)
-            lo += vfloor(fmax(p.lu[a] - u[a], 0.0), vf);
-            up += vfloor(fmax(u[a] - p.uu[a], 0.0), vf);
-        }
-        for (int j = 0; j < DOF; j++) {  // ddq rows
-            double cv, l, h;
-            if (k == 0) {
-                cv = 1. / p.Ts * u[j];
-                l = p.lddq[j] + 1. / p.Ts * ucur_all[8 * b + j];
-                h = p.uddq[j] + 1. / p.Ts * ucur_all[8 * b + j];
-            } else {
-                cv = 1. / p.Ts * (u[j] - tu(k - 1, j));
-                l = p.lddq[j];
-                h = p.uddq[j];
-            }
-            lo += vfloor(fmax(l - cv, 0.0), vf);
-            up += vfloor(fmax(cv - h, 0.0), vf);
-        }
-        for (int r = 0; r < NPC; r++) {  // polytopic: l = -INF, u = 0
-            double val;
-            if (!poly_row(c, u, rv, r, &val, false, nullptr, nullptr)) continue;
-            lo += vfloor(fmax(-INF - val, 0.0), vf);
-            up += vfloor(fmax(val - 0.0, 0.0), vf);
-        }
-    }
+    double out[4];
+    trial_stage(c, d, b, k, alpha, ucur_all + 8 * b, out);
     if (dead) return;  // faithful evaluation of a discarded trial: results are not used
     double* tr = d.trial + (size_t)t * 4;
-    tr[0] = obj;
-    tr[1] = objd;
-    tr[2] = lo;
-    tr[3] = up;
+    for (int i = 0; i < 4; i++) tr[i] = out[i];
 }
 
-// ------------------------------------------------------------------------------------------------
-// k_accept: filter decision, step, termination (osqp_interface.cpp:540-574, 759-808)
-// ------------------------------------------------------------------------------------------------
 __global__ void __launch_bounds__(64) k_accept(DevConst c, DevBuffers d) {
     const int b = blockIdx.x * blockDim.x + threadIdx.x;
     if (b >= c.Bn) return;
-    int32_t* si = d.sqi + (size_t)b * SQI;
-    if (!si[SQ_ACTIVE]) return;
-    const int N = c.N;
-    const mpcc_params& p = c.p;
-    const double* tr = d.trial + (size_t)b * (N + 1) * 4;
-    double obj = 0, lo = 0, up = 0;
-    for (int k = 0; k <= N; k++) {
-        obj += tr[4 * k];
-        obj += tr[4 * k + 1];
-        lo += tr[4 * k + 2];
-        up += tr[4 * k + 3];
-    }
-    const double vio = lo + up;
-    double* sd = d.sqd + (size_t)b * SQ;
-    int nf = si[SQ_NFILT];
-    bool accepted = true;
-    for (int j = 0; j < nf; j++)
-        if (obj >= sd[SQ_FILT + 2 * j] && vio >= sd[SQ_FILT + 2 * j + 1]) { accepted = false; break; }
-    double alpha = 1.0;
-    if (accepted) {
-        int m = 0;
-        for (int j = 0; j < nf; j++) {
-            double fo = sd[SQ_FILT + 2 * j], fv = sd[SQ_FILT + 2 * j + 1];
-            if (obj > fo || vio > fv) { sd[SQ_FILT + 2 * m] = fo; sd[SQ_FILT + 2 * m + 1] = fv; m++; }
-        }
-        if (m < MAX_FILT) { sd[SQ_FILT + 2 * m] = obj; sd[SQ_FILT + 2 * m + 1] = vio; m++; }
-        si[SQ_NFILT] = m;
-    } else {
-        for (int i = 0; i < p.line_search_max_iter; i++) alpha *= p.line_search_tau;
-    }
-    sd[SQ_ALPHA] = alpha;
-    si[SQ_REJECT] = accepted ? 0 : 1;
-    if (d.dbg_trace && si[SQ_ITER] < TRACE_IT) {
-        double* tr = d.dbg_trace + ((size_t)b * TRACE_IT + si[SQ_ITER]) * TRACE_W;
-        tr[0] = si[SQ_QPSTAT]; tr[1] = si[SQ_IPMIT]; tr[2] = obj; tr[3] = vio; tr[4] = accepted ? 1 : 0;
-    }
+    if (!d.sqi[(size_t)b * SQI + SQ_ACTIVE]) return;
+    accept_instance(c, d, b);
 }
 
-// take step (osqp_interface.cpp:549-573): guess += alpha * deNormalizeStep(step); termination test
 __global__ void __launch_bounds__(64) k_apply(DevConst c, DevBuffers d) {
     const int b = blockIdx.x * blockDim.x + threadIdx.x;
     if (b >= c.Bn) return;
-    int32_t* si = d.sqi + (size_t)b * SQI;
-    if (!si[SQ_ACTIVE]) return;
-    const int N = c.N;
-    const mpcc_params& p = c.p;
-    double* sd = d.sqd + (size_t)b * SQ;
-    const double alpha = sd[SQ_ALPHA];
-    double* g = d.guess + (size_t)b * (N + 1) * 17;
-    const double* st = d.step + (size_t)b * (N + 1) * 17;
+    if (!d.sqi[(size_t)b * SQI + SQ_ACTIVE]) return;
+    const double alpha = d.sqd[(size_t)b * SQ + SQ_ALPHA];
     double nrm = 0;
-    for (int k = 0; k <= N; k++) {
-        for (int a = 0; a < 9; a++) {
-            g[17 * k + a] = g[17 * k + a] + alpha * (p.Tx[a] * st[17 * k + a]);
-            nrm = fmax(nrm, fabs(st[17 * k + a]));
-        }
-        if (k < N)
-            for (int a = 0; a < 8; a++) {
-                g[17 * k + 9 + a] = g[17 * k + 9 + a] + alpha * (p.Tu[a] * st[17 * k + 9 + a]);
-                nrm = fmax(nrm, fabs(st[17 * k + 9 + a]));
-            }
-    }
-    const double pn = alpha * nrm;
-    int iter = si[SQ_ITER];
-    if (d.dbg_trace && iter < TRACE_IT) {
-        double* tr = d.dbg_trace + ((size_t)b * TRACE_IT + iter) * TRACE_W;
-        tr[5] = nrm; tr[6] = alpha; tr[7] = pn;
-    }
-    if (pn < p.eps_prim) {
-        si[SQ_STATUS] = MPCC_SOLVED;
-        si[SQ_ACTIVE] = 0;
-        si[SQ_ITER] = iter;
-        return;
-    }
-    iter++;
-    si[SQ_ITER] = iter;
-    if (iter >= p.max_iter) {
-        si[SQ_STATUS] = MPCC_MAX_ITER_EXCEEDED;
-        si[SQ_ACTIVE] = 0;
-    }
+    for (int e = 0; e < (c.N + 1) * 17; e++) nrm = fmax(nrm, apply_elem(c, d, b, e, alpha));
+    finish_iteration(c, d, b, nrm);
 }
 
 // ------------------------------------------------------------------------------------------------

@@ -1,11 +1,11 @@
 """Summarize a round profile (tools/profile_round.sh) into profiles/:
   <round>_kernel_stats.csv        rocprofv3 --stats of the bench command (per-kernel time)
-  <round>_k_ipm_pmc.json          k_ipm counters per benchmark-size launch (averaged)
-  pmc_traffic_k_ipm.json          HBM bytes per k_ipm launch (read by bench.py)
+  <round>_<kernel>_pmc.json       counters of the dominant kernel per benchmark-size launch (averaged)
+  pmc_traffic_<kernel>.json       HBM bytes per launch of that kernel (read by bench.py)
 FETCH_SIZE / WRITE_SIZE are kilobytes; on gfx950 FETCH_SIZE counts half of the bytes of wide
 coalesced reads, so it is doubled (MI355X_MICROARCH.md §HBM).
 
-    python tools/pmc_summary.py gpurun_out/prof r01 --batch 4096 --N 20
+    python tools/pmc_summary.py gpurun_out/prof r01 --batch 4096 --N 20 --kernel k_sqp
 """
 import argparse
 import collections
@@ -35,6 +35,7 @@ def main():
     ap.add_argument("round")
     ap.add_argument("--batch", type=int, default=4096)
     ap.add_argument("--N", type=int, default=20)
+    ap.add_argument("--kernel", default="k_sqp")
     args = ap.parse_args()
     prof = os.path.join(ROOT, "profiles")
     os.makedirs(prof, exist_ok=True)
@@ -45,7 +46,7 @@ def main():
     merged = collections.defaultdict(dict)
     for p in ("p1", "p2", "p3", "p4"):
         for k, v in load_pmc(args.dir, p).items():
-            if v["grid"] == grid:
+            if v["grid"] == grid and v["kernel"].startswith(f"void mpcc::{args.kernel}<"):
                 merged[p + ":" + str(k)] = v
     per = collections.defaultdict(list)
     for key, v in merged.items():
@@ -53,7 +54,7 @@ def main():
             if c not in ("grid", "kernel"):
                 per[c].append(x)
     avg = {c: sum(x) / len(x) for c, x in per.items()}
-    out = {"kernel": "k_ipm", "batch": args.batch, "N": args.N, "launches_averaged": len(per.get("FETCH_SIZE", [])),
+    out = {"kernel": args.kernel, "batch": args.batch, "N": args.N, "launches_averaged": len(per.get("FETCH_SIZE", [])),
            "counters_avg_per_launch": avg}
     if "FETCH_SIZE" in avg and "WRITE_SIZE" in avg:
         rd = 2.0 * avg["FETCH_SIZE"] * 1024.0
@@ -61,14 +62,14 @@ def main():
         out["hbm_read_bytes_per_launch"] = rd
         out["hbm_write_bytes_per_launch"] = wr
         out["hbm_bytes_per_launch"] = rd + wr
-        with open(os.path.join(prof, "pmc_traffic_k_ipm.json"), "w") as f:
-            json.dump({"batch": args.batch, "N": args.N, "hbm_bytes_per_launch": rd + wr,
+        with open(os.path.join(prof, f"pmc_traffic_{args.kernel}.json"), "w") as f:
+            json.dump({"kernel": args.kernel, "batch": args.batch, "N": args.N, "hbm_bytes_per_launch": rd + wr,
                        "hbm_read_bytes_per_launch": rd, "hbm_write_bytes_per_launch": wr,
-                       "source": f"profiles/{args.round}_k_ipm_pmc.json"}, f, indent=1)
+                       "source": f"profiles/{args.round}_{args.kernel}_pmc.json"}, f, indent=1)
     if "SQ_WAVE_CYCLES" in avg:
         wc = avg["SQ_WAVE_CYCLES"]
         out["wave_cycle_split"] = {k: avg.get(k, 0) / wc for k in ("SQ_ACTIVE_INST_ANY", "SQ_WAIT_ANY", "SQ_WAIT_INST_ANY")}
-    with open(os.path.join(prof, f"{args.round}_k_ipm_pmc.json"), "w") as f:
+    with open(os.path.join(prof, f"{args.round}_{args.kernel}_pmc.json"), "w") as f:
         json.dump(out, f, indent=1)
     print(json.dumps(out, indent=1))
 

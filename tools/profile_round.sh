@@ -1,6 +1,6 @@
 #!/bin/bash
 # Round profile of the benchmark command (GPU box): rocprofv3 kernel trace + stats of bench.py, then
-# separate PMC passes for k_ipm (never combined with trace domains).  Usage: bash tools/profile_round.sh OUT
+# separate PMC passes for the dominant kernel k_sqp (never combined with trace domains).  Usage: bash tools/profile_round.sh OUT
 set -e
 OUT=${1:-gpurun_out/prof}
 ROOT=$(pwd)
@@ -13,7 +13,7 @@ echo "trace done"
 PMCB="$ROOT/bench.py --steps 2 --warmup 1 --no-cpu-baseline"
 pmc() {
   local name=$1; shift
-  timeout -k 10 300 rocprofv3 --kernel-include-regex 'k_ipm' --pmc "$@" --output-format csv \
+  timeout -k 10 300 rocprofv3 --kernel-include-regex 'k_sqp' --pmc "$@" --output-format csv \
       -d "$ROOT/$OUT/$name" -o "$name" -- python3 $PMCB > "$ROOT/$OUT/$name.log" 2>&1
 }
 pmc p1 SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_INSTS_SALU
