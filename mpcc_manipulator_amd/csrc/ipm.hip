@@ -208,6 +208,28 @@ __device__ __forceinline__ void sweep(int N, bool backward, In& b0, In& b1, Load
     }
 }
 
+// Stage sweep with a ring of D stage buffers: stage s(i + D - 1) is loaded while stage s(i) is processed,
+// so D - 1 stages of loads are in flight.  Loads are unconditional (the stages past the end re-read
+// s(N)); the ring index is a constant after unrolling, so the buffers stay in registers.
+#ifndef MPCC_LIGHT_DEPTH
+#define MPCC_LIGHT_DEPTH 3
+#endif
+template <int D, class In, class LoadF, class BodyF>
+__device__ __forceinline__ void sweep_ring(int N, bool backward, In (&b)[D], LoadF load, BodyF body) {
+    auto s = [&](int i) { return backward ? N - i : i; };
+    auto cl = [&](int i) { return s(i <= N ? i : N); };
+#pragma unroll
+    for (int j = 0; j < D - 1; j++) load(cl(j), b[j]);
+    for (int i = 0; i <= N; i += D) {
+#pragma unroll
+        for (int j = 0; j < D; j++) {
+            load(cl(i + j + D - 1), b[(j + D - 1) % D]);
+            body(s(i + j), b[j]);
+            if (i + j + 1 > N) return;
+        }
+    }
+}
+
 }  // namespace
 
 // The QP solve of the 4 instances of this wavefront (16 lanes each); instances whose SQP is inactive
@@ -412,6 +434,13 @@ __device__ __forceinline__ void ipm_group(const DevConst& c, const DevBuffers& d
     // ---- start point: dynamics rollout with v = 0, s = max(-g, 1), lambda = 1
     double mcount = 0.0;
     In cur, nxt;
+    // the three sweeps without the factorization (predictor forward, corrector backward and forward)
+    // are short bodies that wait on their stage loads: they keep MPCC_LIGHT_DEPTH - 1 stages in flight
+    In ring[MPCC_LIGHT_DEPTH];
+    auto light_sweep = [&](bool backward, auto load, auto body) {
+        if constexpr (NPM <= 2) sweep_ring<MPCC_LIGHT_DEPTH>(N, backward, ring, load, body);
+        else sweep<false>(N, backward, cur, nxt, load, body);
+    };
     if (run) {
         double y = 0.0;  // lane a < 9: y_a of stage k
         double bk = 0, bkn = 0;
@@ -705,7 +734,7 @@ __device__ __forceinline__ void ipm_group(const DevConst& c, const DevBuffers& d
             double S0 = 0, S1 = 0, S2 = 0;
             MinRatio amr(1.0);
             double xt = 0.0;
-            sweep<(NPM <= 2)>(N, false, cur, nxt, [&](int k, In& o) { load_fwd(k, o, false); }, [&](int k, const In& cur) {
+            light_sweep(false, [&](int k, In& o) { load_fwd(k, o, false); }, [&](int k, const In& cur) {
                 const bool aL = row_active(k, cur.lb), aU = row_active(k, cur.ub), aP = poly_slot_active(cur, k);
                 double v = 0.0, xn = 0.0;
                 if (k < N) fwd_step(cur, xt, v, xn);
@@ -742,7 +771,7 @@ __device__ __forceinline__ void ipm_group(const DevConst& c, const DevBuffers& d
             // ---- corrector backward: coef with rc = s l + dsa dla - sigma mu; f = g_v + B~^T p;
             //      kff = -F^-1 f; p = g_x~ + A~^T p + K^T f
             double pv = 0.0;
-            sweep<(NPM <= 2)>(N, true, cur, nxt, [&](int k, In& o) { load_bwd(k, o); }, [&](int k, const In& cur) {
+            light_sweep(true, [&](int k, In& o) { load_bwd(k, o); }, [&](int k, const In& cur) {
                 const bool aL = row_active(k, cur.lb), aU = row_active(k, cur.ub), aP = poly_slot_active(cur, k);
                 const double cz = row_cz(k, cur.zx, cur.zv), ca = row_cz(k, cur.x0, cur.x1);
                 const double pcz = poly_cz(cur, k, cur.zx, cur.zv), pca = poly_cz(cur, k, cur.x0, cur.x1);
@@ -791,7 +820,7 @@ __device__ __forceinline__ void ipm_group(const DevConst& c, const DevBuffers& d
             double T0 = 0, T1 = 0, T2 = 0, rpm = 0, dzm = 0;
             MinRatio amc(1e30);
             xt = 0.0;
-            sweep<(NPM <= 2)>(N, false, cur, nxt, [&](int k, In& o) { load_fwd(k, o, true); }, [&](int k, const In& cur) {
+            light_sweep(false, [&](int k, In& o) { load_fwd(k, o, true); }, [&](int k, const In& cur) {
                 const bool aL = row_active(k, cur.lb), aU = row_active(k, cur.ub), aP = poly_slot_active(cur, k);
                 double v = 0.0, xn = 0.0;
                 if (k < N) fwd_step(cur, xt, v, xn);

@@ -182,23 +182,31 @@ __global__ void __launch_bounds__(64) k_apply(DevConst c, DevBuffers d) {
 // k_finalize: opt_sol / zero_guess, controller bookkeeping and outputs (osqp_interface.cpp:575-589,
 // mpc.cpp:136-189)
 // ------------------------------------------------------------------------------------------------
+// opt_sol / zero_guess element-wise (thread per horizon element, coalesced): a non-SOLVED instance gets
+// x_0 repeated with u = 0 (osqp_interface.cpp:422-428), a SOLVED one u_N = 0; the horizon output is the
+// result.  x_0 itself (k = 0, a < 9) is never rewritten, so the threads that read it do not race.
+__global__ void __launch_bounds__(256) k_finalize_horizon(DevConst c, DevBuffers d) {
+    const long e = (long)blockIdx.x * blockDim.x + threadIdx.x;
+    const int W = (c.N + 1) * 17;
+    if (e >= (long)c.Bn * W) return;
+    const int b = (int)(e / W), r = (int)(e - (long)b * W);
+    const int k = r / 17, a = r - 17 * k;
+    double* g = d.guess + (size_t)b * W;
+    const bool solved = d.sqi[(size_t)b * SQI + SQ_STATUS] == MPCC_SOLVED;
+    double v = g[r];
+    if (!solved) v = (a < 9) ? g[a] : 0.0;
+    else if (k == c.N && a >= 9) v = 0.0;
+    if (!(k == 0 && a < 9)) g[r] = v;
+    if (d.horizon) d.horizon[(size_t)b * W + r] = v;
+}
+
 __global__ void __launch_bounds__(64) k_finalize(DevConst c, DevBuffers d) {
     const int b = blockIdx.x * blockDim.x + threadIdx.x;
     if (b >= c.Bn) return;
     const int N = c.N;
     int32_t* si = d.sqi + (size_t)b * SQI;
     const int status = si[SQ_STATUS];
-    double* g = d.guess + (size_t)b * (N + 1) * 17;
-    if (status != MPCC_SOLVED) {  // zero_guess: x_0 repeated, u = 0
-        double x0[9];
-        for (int a = 0; a < 9; a++) x0[a] = g[a];
-        for (int k = 0; k <= N; k++) {
-            for (int a = 0; a < 9; a++) g[17 * k + a] = x0[a];
-            for (int a = 0; a < 8; a++) g[17 * k + 9 + a] = 0.0;
-        }
-    } else {
-        for (int a = 0; a < 8; a++) g[17 * N + 9 + a] = 0.0;
-    }
+    const double* g = d.guess + (size_t)b * (N + 1) * 17;  // already opt_sol / zero_guess (k_finalize_horizon)
     if (d.status) d.status[b] = status;
     if (c.ocp) {  // solveOCP's return value only; the MPC bookkeeping belongs to the caller
         if (d.ok) d.ok[b] = (status == MPCC_SOLVED) ? 1 : 0;
@@ -211,8 +219,6 @@ __global__ void __launch_bounds__(64) k_finalize(DevConst c, DevBuffers d) {
     }
     if (d.u0_out)
         for (int a = 0; a < 8; a++) d.u0_out[8 * b + a] = g[9 + a];
-    if (d.horizon)
-        for (int e = 0; e < (N + 1) * 17; e++) d.horizon[(size_t)b * (N + 1) * 17 + e] = g[e];
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -360,6 +366,7 @@ void launch_debug_records(const DevConst& c, int M, const double* q, const doubl
     hipLaunchKernelGGL(k_debug_records, dim3(nblk(M, 64)), dim3(64), 0, s, c, M, q, obs, rec);
 }
 void launch_finalize(const DevConst& c, const DevBuffers& d, hipStream_t s) {
+    hipLaunchKernelGGL(k_finalize_horizon, dim3(nblk((long)c.Bn * (c.N + 1) * 17, 256)), dim3(256), 0, s, c, d);
     hipLaunchKernelGGL(k_finalize, dim3(nblk(c.Bn, 64)), dim3(64), 0, s, c, d);
 }
 void launch_sim_step(int B, const double* x, const double* u, double ts, double* xn, hipStream_t s) {
