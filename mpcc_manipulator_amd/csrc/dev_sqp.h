@@ -152,6 +152,97 @@ __device__ inline void setqp_stage(const DevConst& c, const SplineView& sp, cons
 }
 
 // ------------------------------------------------------------------------------------------------
+// SecondOrderCorrection (osqp_interface.cpp:506-535, 658-681) of stage k: the QP is solved again with
+// the first QP's P, q and A, and the bounds l(x') - d, u(x') - d with d = c(x') - A step at
+// x' = OptvarToVector(initial_guess) + step — the normalized step added as is, before any
+// deNormalizeStep (:661).  Only the bound fields of the stage record change: dynamics offset, ddq box,
+// polytopic upper bounds and the y box with its feasibility flag.  Same formulas and order as the
+// oracle's build_struct_qp(zshift).
+// ------------------------------------------------------------------------------------------------
+__device__ inline void soc_stage(const DevConst& c, const SplineView& sp, const double* __restrict__ gb,
+                                 const double* __restrict__ sb, const RecView& rv, int k, const double* __restrict__ ucur,
+                                 double* __restrict__ q) {
+    const mpcc_params& p = c.p;
+    const int N = c.N;
+    const double* Tx = p.Tx;
+    const double* Tu = p.Tu;
+    auto X = [&](int i, int a) { return gb[17 * i + a] + sb[17 * i + a]; };
+    auto U = [&](int i, int a) { return gb[17 * i + 9 + a] + sb[17 * i + 9 + a]; };  // the step's u_N is 0
+    auto Y = [&](int i, int a) { return sb[17 * i + a]; };
+    auto V = [&](int i, int a) { return sb[17 * i + 9 + a]; };
+    double xk[9], uk[8];
+    for (int a = 0; a < 9; a++) xk[a] = X(k, a);
+    for (int a = 0; a < 8; a++) uk[a] = U(k, a);
+    int flag = ((int)q[QS_FLAG]) & 3;  // the Hessian bits of the first QP stay
+    if (k < N) {
+        for (int a = 0; a < 9; a++) {  // b' = -c_{k+1}(x') + (y_{k+1} - M y_k - G v_k)
+            double s1 = 0, s2 = 0;
+            for (int m = 0; m < 9; m++) s1 += c.A[a * 9 + m] * xk[m];
+            for (int m = 0; m < 8; m++) s2 += c.B[a * 8 + m] * uk[m];
+            double pred = s1 + s2 + 0.0;
+            const double bk = -((1.0 / Tx[a]) * (X(k + 1, a) - pred));
+            double ay = 0, gv = 0;
+            for (int m = 0; m < 9; m++) ay += c.M[a * 9 + m] * Y(k, m);
+            for (int m = 0; m < 8; m++) gv += c.G[a * 8 + m] * V(k, m);
+            q[QS_B + a] = bk + (Y(k + 1, a) - ay - gv);
+        }
+        for (int j = 0; j < DOF; j++) {  // ddq rows: + v_k[j] - v_{k-1}[j] (k = 0: v_0[j])
+            double coef = 1. / p.Ts * Tu[j];
+            double cc, lo, hi;
+            if (k == 0) {
+                cc = 1. / p.Ts * uk[j];
+                lo = p.lddq[j] + 1. / p.Ts * ucur[j];
+                hi = p.uddq[j] + 1. / p.Ts * ucur[j];
+            } else {
+                cc = 1. / p.Ts * (uk[j] - U(k - 1, j));
+                lo = p.lddq[j];
+                hi = p.uddq[j];
+            }
+            const double sh = (k == 0) ? V(0, j) : V(k, j) - V(k - 1, j);
+            q[QS_DLB + j] = (lo - cc) / coef + sh;
+            q[QS_DUB + j] = (hi - cc) / coef + sh;
+        }
+        int np = 0;  // polytopic rows: + a . y_k[0:7] + bv . v_k[0:7]
+        for (int r = 0; r < NPC; r++) {
+            double val;
+            if (!poly_row(c, uk, rv, r, &val, false, nullptr, nullptr)) continue;
+            double* row = q + QS_POLY + POLY_W * np;
+            double sh = 0;
+            for (int j = 0; j < 7; j++) sh += row[j] * Y(k, j);
+            for (int j = 0; j < 7; j++) sh += row[7 + j] * V(k, j);
+            row[14] = (0.0 - val) + sh;
+            np++;
+        }
+    }
+    const double L = sp.L;  // y box at x', + y_k[m] (finite bounds only)
+    for (int m = 0; m < 9; m++) {
+        double lo = p.lx[m], hi = p.ux[m];
+        bool lo_inf = lo <= -BIG, hi_inf = hi >= BIG;
+        if (m == 7) { lo = fmax(xk[7] - p.s_trust_region, 0.); hi = fmin(xk[7] + p.s_trust_region, L); lo_inf = hi_inf = false; }
+        double ylo = lo_inf ? -INF : (lo - xk[m]) / Tx[m];
+        double yhi = hi_inf ? INF : (hi - xk[m]) / Tx[m];
+        const int idx = 9 * k + m;
+        const int i = idx / 8, j = idx % 8;
+        if (i < N) {
+            const double ui = U(i, j);
+            if (p.lu[j] > -BIG) ylo = fmax(ylo, (p.lu[j] - ui) / Tu[j]);
+            if (p.uu[j] < BIG) yhi = fmin(yhi, (p.uu[j] - ui) / Tu[j]);
+        }
+        if (ylo > -BIG) ylo = ylo + Y(k, m);
+        if (yhi < BIG) yhi = yhi + Y(k, m);
+        q[QS_YLB + m] = ylo;
+        q[QS_YUB + m] = yhi;
+        const double FEAS = 1e-9;
+        if (k == 0) {
+            if (ylo > FEAS || yhi < -FEAS) flag |= 4;
+        } else if (ylo > yhi) {
+            flag |= 4;
+        }
+    }
+    q[QS_FLAG] = (double)flag;
+}
+
+// ------------------------------------------------------------------------------------------------
 // filterLineSearch trial (osqp_interface.cpp:759-808) of stage k of instance b: objective and l1
 // constraint violation (:824-833) of setQP(obj, constr) at guess + alpha * T * step, with the frozen
 // robot record (Q4).  Rows owned by stage k: dynamics block k, state bounds k, input bounds (Q1) k,

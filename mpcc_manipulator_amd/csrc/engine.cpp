@@ -234,8 +234,11 @@ void validate_params(const mpcc_params& p) {
     for (int i = 0; i < 9; i++) if (!(p.Tx[i] > 0)) throw std::invalid_argument("T_x must be > 0");
     for (int i = 0; i < 8; i++) if (!(p.Tu[i] > 0)) throw std::invalid_argument("T_u must be > 0");
     if (p.max_iter < 0 || p.line_search_max_iter < 0) throw std::invalid_argument("negative iteration limit");
-    if (p.do_SOC || p.use_BFGS)  // off in the reference's sqp.json and off the benchmark path
-        throw std::invalid_argument("do_SOC / use_BFGS (osqp_interface.cpp:658-757) are not supported by this engine");
+    // Damped BFGS (osqp_interface.cpp:683-715) replaces the Hessian by rank-2 updates that couple every
+    // stage with every other: the dense N_var x N_var matrix has no stage structure for the Riccati
+    // interior point to exploit.  Off in the reference's sqp.json and off the benchmark path.
+    if (p.use_BFGS)
+        throw std::invalid_argument("use_BFGS (osqp_interface.cpp:683-715) is not supported by this engine");
 }
 
 // one track's tables in the device layout (dev_common.h SplineDev): SPL_STRIDE doubles
@@ -319,6 +322,10 @@ void run_batch(mpcc_engine* e, int B, hipStream_t st, mpcc_timing* timing, bool 
         launch_setqp(c, d, ucur, st);
         if (tm) a1 = mark();
         launch_ipm(c, d, poly_rows_max(c.p.constraint_mask), st);
+        if (c.p.do_SOC) {  // SecondOrderCorrection (osqp_interface.cpp:506-535)
+            launch_soc(c, d, ucur, st);
+            launch_ipm(c, d, poly_rows_max(c.p.constraint_mask), st);
+        }
         if (tm) b1 = mark();
         launch_trial(c, d, ucur, 1.0, 0, st);
         launch_accept(c, d, st);

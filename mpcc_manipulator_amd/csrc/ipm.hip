@@ -947,6 +947,15 @@ __device__ __attribute__((noinline)) void sqp_trial_phase(const DevConst& c, con
         }
     }
 }
+__device__ __attribute__((noinline)) void sqp_soc_phase(const DevConst& c, const DevBuffers& d, int b, int t,
+                                                        const double* __restrict__ ucur) {
+    const int N = c.N, NS = N + 1;
+    const SplineView sp = spl_of(c.spl, b);
+    const size_t o = (size_t)b * NS * 17;
+    for (int k = t; k <= N; k += 16)
+        soc_stage(c, sp, d.guess + o, d.step + o, RecView{d.rec + (size_t)b * NS + k, c.S}, k, ucur,
+                  d.qs + ((size_t)b * NS + k) * QS);
+}
 template <int NPM>
 __device__ __attribute__((noinline)) void sqp_ipm_phase(const DevConst& c, const DevBuffers& d, double* smem) {
     ipm_group<NPM>(c, d, smem);
@@ -971,6 +980,13 @@ __global__ void __launch_bounds__(64) k_sqp(DevConst c, DevBuffers d, const doub
         }
         sqp_ipm_phase<NPM>(c, d, smem);
         __syncthreads();
+        if (c.p.do_SOC) {  // SecondOrderCorrection (osqp_interface.cpp:506-535): same P, q, A, shifted bounds
+            act = valid && si[SQ_ACTIVE] != 0;
+            if (act) sqp_soc_phase(c, d, b, t, ucur);
+            __syncthreads();
+            sqp_ipm_phase<NPM>(c, d, smem);  // a failed correction keeps the step (Q6)
+            __syncthreads();
+        }
         act = valid && si[SQ_ACTIVE] != 0;
         if (act) sqp_trial_phase(c, d, b, t, ucur, 1.0, true);
         __syncthreads();

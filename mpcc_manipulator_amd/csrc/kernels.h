@@ -51,6 +51,8 @@ void launch_nn(const DevConst& c, const DevBuffers& d, const NNDesc& nd, const d
                const double* q, const double* obs, double* rec, int rec_stride, hipStream_t s);
 void launch_setqp(const DevConst& c, const DevBuffers& d, const double* u_cur, hipStream_t s);
 void launch_ipm(const DevConst& c, const DevBuffers& d, int npmax, hipStream_t s);
+// SecondOrderCorrection bounds (osqp_interface.cpp:658-681) of the stage records, before a second k_ipm
+void launch_soc(const DevConst& c, const DevBuffers& d, const double* u_cur, hipStream_t s);
 // the fused SQP loop (QP solve, line search, step, next QP assembly) after the first k_setqp
 void launch_sqp(const DevConst& c, const DevBuffers& d, const double* u_cur, int npmax, hipStream_t s);
 size_t ipm_lds_bytes(int N, int npmax);

@@ -141,6 +141,18 @@ __global__ void __launch_bounds__(64) k_setqp(DevConst c, DevBuffers d, const do
     setqp_stage(c, spl_of(c.spl, b), gb, rv, k, ucur_all + 8 * b, q);
 }
 
+// k_soc: the SecondOrderCorrection bounds of each (instance, stage) record (soc_stage, dev_sqp.h)
+__global__ void __launch_bounds__(64) k_soc(DevConst c, DevBuffers d, const double* __restrict__ ucur_all) {
+    const int t = blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= c.S) return;
+    const int N = c.N;
+    const int b = t / (N + 1), k = t - b * (N + 1);
+    if (!d.sqi[(size_t)b * SQI + SQ_ACTIVE]) return;
+    const size_t o = (size_t)b * (N + 1) * 17;
+    soc_stage(c, spl_of(c.spl, b), d.guess + o, d.step + o, RecView{d.rec + t, c.S}, k, ucur_all + 8 * b,
+              d.qs + (size_t)t * QS);
+}
+
 // ------------------------------------------------------------------------------------------------
 // k_trial / k_accept / k_apply: filter line search and step (dev_sqp.h) as lane-per-stage and
 // lane-per-instance kernels; k_sqp (ipm.hip) runs the same pieces per instance inside the QP kernel.
@@ -352,6 +364,9 @@ void launch_stage_records(const DevConst& c, const DevBuffers& d, hipStream_t s)
 }
 void launch_setqp(const DevConst& c, const DevBuffers& d, const double* u_cur, hipStream_t s) {
     hipLaunchKernelGGL(k_setqp, dim3(nblk(c.S, 64)), dim3(64), 0, s, c, d, u_cur);
+}
+void launch_soc(const DevConst& c, const DevBuffers& d, const double* u_cur, hipStream_t s) {
+    hipLaunchKernelGGL(k_soc, dim3(nblk(c.S, 64)), dim3(64), 0, s, c, d, u_cur);
 }
 void launch_trial(const DevConst& c, const DevBuffers& d, const double* u_cur, double alpha, int dead, hipStream_t s) {
     hipLaunchKernelGGL(k_trial, dim3(nblk(c.S, 64)), dim3(64), 0, s, c, d, u_cur, alpha, dead);

@@ -1119,7 +1119,12 @@ struct StructQP {
 };
 
 // Build the stage-structured QP equivalent to the dense layout (same primal solution).
-static void build_struct_qp(const Oracle& o, const double* guess, const double* recs, const double* ucur, StructQP& S) {
+// zshift (SecondOrderCorrection, osqp_interface.cpp:658-681): a QP step in the reference layout
+// [x_0..x_N (9 each) | u_0..u_{N-1} (8 each)].  Each row's bounds then become l - d with d = c - A step,
+// i.e. the bounds at this guess shifted by the row's A step, written out per row kind below (the
+// engine's soc_stage, dev_sqp.h, uses the same formulas in the same order).
+static void build_struct_qp(const Oracle& o, const double* guess, const double* recs, const double* ucur, StructQP& S,
+                            const double* zshift = nullptr) {
     const OracleParams& p = o.p;
     const int N = p.N;
     const double* Tx = p.Tx; const double* Tu = p.Tu;
@@ -1132,6 +1137,8 @@ static void build_struct_qp(const Oracle& o, const double* guess, const double* 
     }
     const double rddq = p.qp_r_ddq;
     const double L = o.track.length();
+    auto ysh = [&](int k, int a) { return zshift[(size_t)NX * k + a]; };
+    auto vsh = [&](int k, int b) { return (k < N) ? zshift[(size_t)NX * (N + 1) + (size_t)NU * k + b] : 0.0; };
     // Box bounds on y (state bounds + Q1 rows), accumulated as intersections in y-units.
     std::vector<double> ylb((N + 1) * NX, -INF), yub((N + 1) * NX, INF);
     auto add_box = [&](int k, int m, double lo, double hi) {
@@ -1183,6 +1190,12 @@ static void build_struct_qp(const Oracle& o, const double* guess, const double* 
                 for (int b = 0; b < NU; b++) s2 += o.B[a * NU + b] * uk[b];
                 double pred = s1 + s2 + 0.0;
                 s.b[a] = -((1.0 / Tx[a]) * (xn[a] - pred));
+                if (zshift) {  // + (y_{k+1} - M y_k - G v_k) of the step
+                    double ay = 0, gv = 0;
+                    for (int m = 0; m < NX; m++) ay += S.M[a * NX + m] * ysh(k, m);
+                    for (int m = 0; m < NU; m++) gv += S.G[a * NU + m] * vsh(k, m);
+                    s.b[a] = s.b[a] + (ysh(k + 1, a) - ay - gv);
+                }
             }
         }
         // state bounds
@@ -1214,6 +1227,10 @@ static void build_struct_qp(const Oracle& o, const double* guess, const double* 
                     r.c[16 + j] = 1.0; r.c[9 + j] = -1.0;
                 }
                 r.lb = (lo - c) / coef; r.ub = (hi - c) / coef;
+                if (zshift) {  // + v_k[j] - v_{k-1}[j] (k = 0: v_0[j]) of the step
+                    const double sh = (k == 0) ? vsh(0, j) : vsh(k, j) - vsh(k - 1, j);
+                    r.lb = r.lb + sh; r.ub = r.ub + sh;
+                }
                 s.rows.push_back(r);
             }
             // polytopic rows
@@ -1228,10 +1245,24 @@ static void build_struct_qp(const Oracle& o, const double* guess, const double* 
                 for (int b = 0; b < NU; b++) row.c[16 + b] = cn.cu[r * NU + b] * Tu[b];
                 row.lb = lo_inf ? -INF : lo;
                 row.ub = hi_inf ? INF : hi;
+                if (zshift) {  // + a . y_k[0:7] + bv . v_k[0:7] of the step (the row's other entries are 0)
+                    double sh = 0;
+                    for (int a = 0; a < DOF; a++) sh += row.c[a] * ysh(k, a);
+                    for (int b = 0; b < DOF; b++) sh += row.c[16 + b] * vsh(k, b);
+                    if (!lo_inf) row.lb = lo + sh;
+                    if (!hi_inf) row.ub = hi + sh;
+                }
                 s.rows.push_back(row);
             }
         }
     }
+    // box rows: + y_k[m] of the step (state rows and Q1 rows alike; finite bounds only)
+    if (zshift)
+        for (int k = 0; k <= N; k++)
+            for (int m = 0; m < NX; m++) {
+                if (ylb[k * NX + m] > -BIG) ylb[k * NX + m] = ylb[k * NX + m] + ysh(k, m);
+                if (yub[k * NX + m] < BIG) yub[k * NX + m] = yub[k * NX + m] + ysh(k, m);
+            }
     // stage-0 y rows are constants (y_0 = 0): feasibility check only
     for (int m = 0; m < NX; m++) {
         if (ylb[m] > FEAS_TOL || yub[m] < -FEAS_TOL) S.infeasible = true;
@@ -1684,6 +1715,48 @@ static void denorm_add(const Oracle& o, const double* base, const std::vector<do
 // the engine's mpcc_debug_trace_get
 static thread_local double* g_trace = nullptr;
 
+// SecondOrderCorrection (osqp_interface.cpp:658-681).  The correction point is
+// vectorToOptvar(OptvarToVector(initial_guess) + step): the normalized QP step added as is, without
+// deNormalizeStep (:661).  The QP keeps the first QP's P, q and A; its bounds are l(x') - d and
+// u(x') - d with d = c(x') - A step (:676-678).  Returns the QP status; `out` is the new step on success.
+static void soc_point(const Oracle& o, const double* guess, const std::vector<double>& step, std::vector<double>& xs) {
+    const int N = o.p.N;
+    xs.assign(guess, guess + (size_t)(N + 1) * 17);
+    for (int k = 0; k <= N; k++) {
+        for (int a = 0; a < NX; a++) xs[17 * k + a] = guess[17 * k + a] + step[(size_t)NX * k + a];
+        if (k < N)
+            for (int b = 0; b < NU; b++) xs[17 * k + 9 + b] = guess[17 * k + 9 + b] + step[(size_t)NX * (N + 1) + NU * k + b];
+    }
+}
+static int soc_dense(const Oracle& o, const DenseQP& q, const double* guess, const double* recs, const double* ucur,
+                     const std::vector<double>& step, std::vector<double>& out, int* iters) {
+    std::vector<double> xs;
+    soc_point(o, guess, step, xs);
+    DenseQP q2;
+    set_qp(o, xs.data(), recs, ucur, false, q2);  // setConstraints(updates_initial_guess, NULL, ...) (:668)
+    DenseQP qc = q;
+    for (int r = 0; r < q.nc; r++) {
+        double as = 0;
+        for (int j = 0; j < q.nv; j++) as += q.A[(size_t)r * q.nv + j] * step[j];
+        qc.c[r] = q2.c[r] - as;  // d; the solver takes l - d <= A s <= u - d
+    }
+    qc.l = q2.l;
+    qc.u = q2.u;
+    return solve_dense_ipm(qc, out, iters);
+}
+static int soc_struct(const Oracle& o, const StructQP& S, const double* guess, const double* recs, const double* ucur,
+                      const std::vector<double>& step, std::vector<double>& out, int* iters) {
+    std::vector<double> xs;
+    soc_point(o, guess, step, xs);
+    StructQP S2;
+    build_struct_qp(o, xs.data(), recs, ucur, S2, step.data());
+    for (int k = 0; k <= S.N; k++) {  // objective of the first QP (P, q)
+        std::memcpy(S2.st[k].H, S.st[k].H, sizeof S.st[k].H);
+        std::memcpy(S2.st[k].h, S.st[k].h, sizeof S.st[k].h);
+    }
+    return solve_struct_ipm(S2, out, iters);
+}
+
 static int solve_ocp(const Oracle& o, double* guess, const double* recs, const double* ucur, double* opt_sol, int* iters_out) {
     const OracleParams& p = o.p;
     const int N = p.N;
@@ -1724,6 +1797,11 @@ static int solve_ocp(const Oracle& o, double* guess, const double* recs, const d
             int qs = solve_dense_ipm(q, st, &qit);
             if (g_trace && it < 4) { g_trace[8 * it] = qs; g_trace[8 * it + 1] = qit; }
             if (qs == 0) step = st; else { status = qs; status_set = true; }  // Q6: keep old step
+            if (p.do_SOC) {  // :506-535, on whatever step_ holds, even after a failed QP
+                int sit = 0;
+                const int ss = soc_dense(o, q, guess, recs, ucur, step, st, &sit);
+                if (ss == 0) step = st; else { status = ss; status_set = true; }
+            }
         } else {
             StructQP S;
             build_struct_qp(o, guess, recs, ucur, S);
@@ -1763,6 +1841,11 @@ static int solve_ocp(const Oracle& o, double* guess, const double* recs, const d
             int qs = solve_struct_ipm(S, st, &qit);
             if (g_trace && it < 4) { g_trace[8 * it] = qs; g_trace[8 * it + 1] = qit; }
             if (qs == 0) step = st; else { status = qs; status_set = true; }
+            if (p.do_SOC) {  // :506-535
+                int sit = 0;
+                const int ss = soc_struct(o, S, guess, recs, ucur, step, st, &sit);
+                if (ss == 0) step = st; else { status = ss; status_set = true; }
+            }
         }
         // filterLineSearch :759-808
         bool accepted = true;
@@ -1961,6 +2044,24 @@ int oracle_solve_qp(void* h, int mode, const double* guess, const double* recs, 
         rc = solve_struct_ipm(S, st, iters);
     }
     if (rc == 0) std::memcpy(step, st.data(), st.size() * 8);
+    return rc;
+}
+// SecondOrderCorrection QP (osqp_interface.cpp:658-681) after a first step step_in: mode 0 structured, 1 dense
+int oracle_solve_soc(void* h, int mode, const double* guess, const double* recs, const double* u_current,
+                     const double* step_in, double* step_out, int* iters) {
+    Oracle* o = (Oracle*)h;
+    std::vector<double> step(step_in, step_in + o->nvar()), st;
+    int rc;
+    if (mode == 1) {
+        DenseQP q;
+        set_qp(*o, guess, recs, u_current, true, q);
+        rc = soc_dense(*o, q, guess, recs, u_current, step, st, iters);
+    } else {
+        StructQP S;
+        build_struct_qp(*o, guess, recs, u_current, S);
+        rc = soc_struct(*o, S, guess, recs, u_current, step, st, iters);
+    }
+    if (rc == 0) std::memcpy(step_out, st.data(), st.size() * 8);
     return rc;
 }
 void oracle_rk4(const double* x9, const double* u8, double ts, double* out9) { rk4(x9, u8, ts, out9); }

@@ -91,6 +91,10 @@ double oracle_dense_qp(void* h, const double* guess, const double* recs, const d
  * (0 ok, else Status code).  iters = IPM iterations used. */
 int    oracle_solve_qp(void* h, int mode, const double* guess, const double* recs, const double* u_current,
                        double* step, int* iters);
+/* SecondOrderCorrection QP (osqp_interface.cpp:658-681) after the first step step_in [nv]: same P, q, A,
+ * bounds at guess + step_in shifted by A step_in; step_out [nv]; returns status. */
+int    oracle_solve_soc(void* h, int mode, const double* guess, const double* recs, const double* u_current,
+                        const double* step_in, double* step_out, int* iters);
 /* Integrator (integrator.cpp:29-68) */
 void   oracle_rk4(const double* x9, const double* u8, double ts, double* out9);
 void   oracle_sim_time_step(const double* x9, const double* u8, double ts, double* out9);

@@ -84,6 +84,8 @@ def lib():
         L.oracle_dense_qp.argtypes = [C.c_void_p, DP, DP, DP, DP, DP, DP, DP, DP, DP]
         L.oracle_solve_qp.restype = C.c_int
         L.oracle_solve_qp.argtypes = [C.c_void_p, C.c_int, DP, DP, DP, DP, IP]
+        L.oracle_solve_soc.restype = C.c_int
+        L.oracle_solve_soc.argtypes = [C.c_void_p, C.c_int, DP, DP, DP, DP, DP, IP]
         L.oracle_rk4.argtypes = [DP, DP, D, DP]
         L.oracle_sim_time_step.argtypes = [DP, DP, D, DP]
         L.oracle_run_mpc.restype = C.c_int
@@ -240,6 +242,14 @@ class Oracle:
         rc = self.L.oracle_solve_qp(self.h, int(mode), _dp(_f64(guess)), _dp(_f64(recs)),
                                     _dp(_f64(u_current)), _dp(step), _ip(it))
         return rc, step, int(it[0])
+
+    def solve_soc(self, guess, recs, u_current, step, mode=0):
+        """SecondOrderCorrection QP (osqp_interface.cpp:658-681) after the first QP's step."""
+        out = np.zeros(self.nvar())
+        it = np.zeros(1, dtype=np.int32)
+        rc = self.L.oracle_solve_soc(self.h, int(mode), _dp(_f64(guess)), _dp(_f64(recs)), _dp(_f64(u_current)),
+                                     _dp(_f64(step)), _dp(out), _ip(it))
+        return rc, out, int(it[0])
 
     def rk4(self, x, u, ts):
         out = np.zeros(9)

@@ -227,6 +227,38 @@ def test_benchmark_batch_parity(built_lib, oracle_lib, mask, B):
     eng.close()
 
 
+# ---------------------------------------------------------------- second-order correction
+@pytest.mark.parametrize("mask,B,staged", [(2, 1024, False), (7, 256, False), (7, 256, True)])
+def test_soc_batch_parity(built_lib, oracle_lib, monkeypatch, mask, B, staged):
+    """do_SOC = 1 (SecondOrderCorrection, osqp_interface.cpp:506-535, 658-681): a second QP with the first
+    QP's P, q, A and the bounds at x + step shifted by A step, in the fused k_sqp and in the staged
+    loop (k_soc + k_ipm), against the oracle (status exact, inputs 1e-6)."""
+    import mpcc_manipulator_amd as m
+    if staged:
+        monkeypatch.setenv("MPCC_STAGED_SQP", "1")
+    ov = {"sqp": {"max_iter": 2, "do_SOC": 1}}
+    o, P, track = make_oracle(N=20, max_iter=2, mask=mask, nthreads=16, overrides=ov)
+    assert P["do_SOC"] == 1
+    params = m.load_params(N=20, overrides=ov)
+    eng = m.Engine(params, max_batch=B, constraint_mask=mask)
+    eng.set_track(*track)
+    pool = oracle_pool(o, 200, obs=(0.48, 0.218, 0.521, 5.0) if mask == 7 else (3.0, 3.0, 3.0, 0.0))
+    rng = np.random.default_rng(SEED + 17)
+    obs = None
+    if mask == 7:
+        obs = np.column_stack([np.full(B, 0.48), np.full(B, 0.218), rng.uniform(0.421, 0.621, B), np.full(B, 5.0)])
+    x0, u0, obs, guess, valid, fails = batch_from_pool(pool, B, rng, qnoise=0.005, obs=obs)
+    (xg, outg, gg, vg, fg), (xo, outo, go, vo, fo) = _run_both(eng, o, x0, u0, obs, guess, valid, fails)
+    assert np.array_equal(outg["status"], outo["status"])
+    assert np.abs(outg["horizon"][:, :-1, 9:] - outo["horizon"][:, :-1, 9:]).max() <= 1e-6
+    assert np.array_equal(vg, vo) and np.array_equal(fg, fo)
+    # the correction is live: the same batch without it gives different inputs
+    o2, _, _ = make_oracle(N=20, max_iter=2, mask=mask, nthreads=16)
+    out2 = o2.run_mpc(x0.copy(), u0, obs, guess.copy(), valid.copy(), fails.copy())
+    assert np.abs(out2["horizon"][:, :-1, 9:] - outo["horizon"][:, :-1, 9:]).max() > 1e-6
+    eng.close()
+
+
 # ---------------------------------------------------------------- SURVEY §8(f)1: the closed loop on the device
 def test_device_closed_loop(setup20):
     """main.cpp:100-114 on the device for B instances (mpcc_closed_loop) against the oracle's loop:

@@ -126,14 +126,26 @@ def test_engine_fails_loudly_without_gpu(built_lib):
         m.Engine(params, max_batch=4, constraint_mask=2)
 
 
-@pytest.mark.parametrize("key", ["do_SOC", "use_BFGS"])
-def test_unsupported_sqp_variants_rejected(built_lib, key):
-    """SOC / BFGS (osqp_interface.cpp:658-757) are off the path; enabling them is an error raised before
-    any device work, never a silent fallback to plain SQP."""
+def test_bfgs_rejected(built_lib):
+    """Damped BFGS (osqp_interface.cpp:683-715) makes the Hessian dense across stages, outside the
+    stage-structured interior point: enabling it is an error raised before any device work, never a
+    silent fallback to plain SQP."""
     import mpcc_manipulator_amd as m
-    params = m.load_params(N=20, overrides={"sqp": {key: 1.0}})
+    params = m.load_params(N=20, overrides={"sqp": {"use_BFGS": 1.0}})
     with pytest.raises(m.MpccError, match="not supported"):
         m.Engine(params, max_batch=4, constraint_mask=2)
+
+
+@pytest.mark.skipif(torch.cuda.is_available(), reason="checks the no-GPU failure path")
+def test_soc_passes_validation(built_lib):
+    """do_SOC (SecondOrderCorrection, osqp_interface.cpp:506-535, 658-681) is supported: parameter
+    validation accepts it, and without a GPU creation fails only at the device."""
+    import mpcc_manipulator_amd as m
+    params = m.load_params(N=20, overrides={"sqp": {"do_SOC": 1.0}})
+    assert params.do_SOC == 1
+    with pytest.raises(m.MpccError) as e:
+        m.Engine(params, max_batch=4, constraint_mask=2)
+    assert "not supported" not in str(e.value)
 
 
 def test_host_integrator_matches_oracle(built_lib, oracle_lib):

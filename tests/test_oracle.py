@@ -261,6 +261,55 @@ def test_qp_layouts_agree(oracle_lib):
         assert np.abs(s0 - s1).max() < 1e-8
 
 
+def test_soc_layouts_agree(oracle_lib):
+    """SecondOrderCorrection (osqp_interface.cpp:658-681): the structured restatement (the bounds at
+    x + step shifted per row kind by A step) equals the verbatim dense formula l(x') - (c(x') - A step)
+    on closed-loop QPs with the collision rows."""
+    from helpers import oracle_pool
+    o, P, track = make_oracle(N=20, max_iter=2, mask=7)
+    pool = oracle_pool(o, 30)
+    rng = np.random.default_rng(SEED + 5)
+    N = 20
+    solved = 0
+    for t in range(5, 25, 4):
+        g = pool["guess"][t + 1].copy()
+        g[:, :7] += rng.normal(0, 0.01, (N + 1, 7))
+        recs = np.stack([o.robot_record(g[k, :7]) for k in range(N + 1)])
+        u = pool["u0"][t + 1]
+        rc, s, _ = o.solve_qp(g, recs, u, mode=0)
+        assert rc == 0
+        rc0, s0, _ = o.solve_soc(g, recs, u, s, mode=0)
+        rc1, s1, _ = o.solve_soc(g, recs, u, s, mode=1)
+        assert rc0 == rc1
+        if rc0 == 0:
+            solved += 1
+            assert np.abs(s0 - s1).max() < 1e-8
+            assert np.abs(s0 - s).max() > 0  # the correction moved the step
+    assert solved >= 3
+
+
+def test_soc_closed_loop_layouts_agree(oracle_lib):
+    """do_SOC = 1 through the whole runMPC_ closed loop (main.cpp:100-114): structured and dense-layout
+    oracles take the same statuses and inputs."""
+    ov = {"sqp": {"do_SOC": True}}
+    (o0, P, track), (o1, _, _) = (make_oracle(N=10, max_iter=2, mask=7, qp_mode=m, overrides=ov) for m in (0, 1))
+    assert P["do_SOC"] == 1
+    N = 10
+    x = np.zeros((1, 9)); x[0, :7] = Q0
+    u = np.zeros((1, 8)); ob = np.array([[0.48, 0.218, 0.521, 5.0]])
+    st = [(np.zeros((1, N + 1, 17)), np.zeros(1, np.int32), np.zeros(1, np.int32)) for _ in range(2)]
+    for step in range(25):
+        outs, xs = [], []
+        for o, (g, v, f) in zip((o0, o1), st):
+            xi = x.copy()
+            outs.append(o.run_mpc(xi, u, ob, g, v, f))
+            xs.append(xi)
+        assert outs[0]["status"][0] == outs[1]["status"][0], step
+        assert np.abs(outs[0]["u0"] - outs[1]["u0"]).max() <= 1e-6, step
+        u = outs[0]["u0"].copy()
+        x[0] = o0.sim_time_step(xs[0][0], u[0], P["Ts"])
+
+
 def test_params_resolution(oracle_lib):
     """Params/*.json with the reference's override semantics: T_x/T_u (normalization.json:3-20)."""
     P = rp.resolve(N=20)

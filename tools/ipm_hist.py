@@ -21,11 +21,19 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--batch", type=int, default=4096)
     ap.add_argument("--threads", type=int, default=8)
+    ap.add_argument("--N", type=int, default=20)
+    ap.add_argument("--mask", type=int, default=2)
+    ap.add_argument("--pool", type=int, default=400, help="closed-loop pool steps when no committed pool exists")
+    ap.add_argument("--obstacles", action="store_true", help="configs[2] obstacles (main_w_sim.py:42-45)")
     args = ap.parse_args()
-    from helpers import make_oracle
-    o, P, track = make_oracle(N=20, max_iter=2, mask=2, nthreads=args.threads)
-    f = np.load(os.path.join(ROOT, "mpcc_manipulator_amd", "data", "bench_pool_n20_mask2.npz"), allow_pickle=False)
-    pool = {k: f[k] for k in f.files}
+    from helpers import make_oracle, oracle_pool
+    o, P, track = make_oracle(N=args.N, max_iter=2, mask=args.mask, nthreads=args.threads)
+    path = os.path.join(ROOT, "mpcc_manipulator_amd", "data", f"bench_pool_n{args.N}_mask{args.mask}.npz")
+    if os.path.exists(path):
+        f = np.load(path, allow_pickle=False)
+        pool = {k: f[k] for k in f.files}
+    else:
+        pool = oracle_pool(o, args.pool, obs=(0.48, 0.218, 0.521, 5.0) if args.obstacles else (3.0, 3.0, 3.0, 0.0))
     B = args.batch
     rng = np.random.default_rng(0x4D504343)
     idx = np.arange(B) % len(pool["x0"])
@@ -36,6 +44,8 @@ def main():
     valid = pool["valid"][idx].astype(np.int32)
     fails = pool["fails"][idx].astype(np.int32)
     obs = np.tile(np.array([3.0, 3.0, 3.0, 0.0]), (B, 1))
+    if args.obstacles:
+        obs = np.column_stack([np.full(B, 0.48), np.full(B, 0.218), rng.uniform(0.421, 0.621, B), np.full(B, 5.0)])
     out = o.run_mpc(x0, u0, obs, guess, valid, fails, trace=True)
     tr = out["trace"]
     it1 = tr[:, 0, 1].astype(int)
