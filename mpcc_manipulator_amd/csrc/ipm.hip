@@ -478,6 +478,7 @@ __device__ __forceinline__ void ipm_group(const DevConst& c, const DevBuffers& d
     int it = 0;
     bool conv = false, diverged = false;
     double mu0 = 0.0;                    // mu of the starting point (P3)
+    double dz_prev = 1e30;               // max |dz| of the previous iteration (step test)
     double alpha = 0.0, sigma_mu = 0.0;  // previous iteration's step length and sigma*mu (lazy update)
     double mu_cur = 1e30, rp_cur = 1e30; // mu and max |rp| of the current iterate (known for it > 0)
     bool pending = false;
@@ -862,7 +863,11 @@ __device__ __forceinline__ void ipm_group(const DevConst& c, const DevBuffers& d
                 const double rpn = (1.0 - alpha) * rpm;
                 mu_cur = mun;
                 rp_cur = rpn;
-                if (mun < IPM_TOL_MU && rpn < IPM_TOL_P && dzm < IPM_TOL_STEP) {
+                // step test: |dz| below tolerance, or quadratic contraction dz^2 / dz_prev below it
+                // (the oracle's step_converged, mpcc_oracle.cpp)
+                const bool step_ok = dzm < IPM_TOL_STEP || dzm * dzm < IPM_TOL_STEP * dz_prev;
+                dz_prev = dzm;
+                if (mun < IPM_TOL_MU && rpn < IPM_TOL_P && step_ok) {
                     conv = true;
                     run = false;
                 } else if (mun > IPM_DIV * mu0) {  // P3: divergent multipliers, primal infeasible
