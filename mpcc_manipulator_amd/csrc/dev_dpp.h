@@ -7,15 +7,14 @@ namespace dpp {
 
 template <int CTRL>
 __device__ __forceinline__ double dpp_d(double v) {
-    const unsigned long long x = (unsigned long long)__double_as_longlong(v);
-    int lo = (int)(unsigned)(x & 0xffffffffull), hi = (int)(unsigned)(x >> 32);
-    lo = __builtin_amdgcn_update_dpp(0, lo, CTRL, 0xF, 0xF, true);
-    hi = __builtin_amdgcn_update_dpp(0, hi, CTRL, 0xF, 0xF, true);
+    // One 64-bit DPP move: gfx950 executes row_newbcast on 64-bit operands as a single v_mov_b64_dpp
+    // (the DP-ALU DPP form); the other row controls are split into two v_mov_b32_dpp by the backend.
+    long long x = __builtin_amdgcn_update_dpp(0LL, (long long)__double_as_longlong(v), CTRL, 0xF, 0xF, true);
     // Pin the DPP where it is written: the optimizer may otherwise sink it into a lane-divergent branch
     // of its only consumer (e.g. the t >= 9 side of a select), where the source lanes are masked off
     // and read as 0.  An empty volatile asm on the result cannot be moved across control flow.
-    asm volatile("" : "+v"(lo), "+v"(hi));
-    return __longlong_as_double((long long)(((unsigned long long)(unsigned)hi << 32) | (unsigned)lo));
+    asm volatile("" : "+v"(x));
+    return __longlong_as_double(x);
 }
 template <int n> __device__ __forceinline__ double from_up(double v) { return dpp_d<0x100 + n>(v); }    // row_shl: lane t <- t+n
 template <int n> __device__ __forceinline__ double from_down(double v) { return dpp_d<0x110 + n>(v); } // row_shr: lane t <- t-n

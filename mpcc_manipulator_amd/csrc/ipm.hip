@@ -41,6 +41,7 @@ constexpr double IPM_TOL_MU = 1e-13, IPM_TOL_P = 1e-11, IPM_TOL_STEP = 1e-11;
 constexpr double IPM_TOL_FB = 1e-9;  // P2: a converged iterate is accepted when the Riccati factor breaks down
 constexpr double IPM_DIV = 1e6;      // P3: mu > IPM_DIV * mu_0 -> primal infeasible (divergent multipliers)
 constexpr double IPM_TAU = 0.995;    // fraction-to-boundary floor: tau = max(IPM_TAU, 1 - sqrt(mu))
+typedef __attribute__((address_space(1))) double gdouble;  // global-memory double (global_* loads/stores)
 constexpr int IPW = 4;               // instances per wavefront (16 lanes each)
 
 // workspace fields, ws[(b*(N+1) + k)*IS + field*16 + lane]
@@ -255,9 +256,13 @@ __device__ __forceinline__ void ipm_group(const DevConst& c, const DevBuffers& d
     bool run = valid && si[SQ_ACTIVE] != 0;
     if (__ballot(run) == 0) return;
 
-    const double* QSb = d.qs + (size_t)(valid ? b : 0) * NS * QS;
-    double* WSb = d.is + (size_t)(valid ? b : 0) * NS * IS;
-    auto ws = [&](int k, int f) -> double* { return WSb + (size_t)k * IS + f * 16 + t; };
+    // QP records and the workspace through global-address-space pointers: their loads and stores compile
+    // to global_* instructions, which count only in vmcnt.  Through the generic pointers of DevBuffers they
+    // were flat_*, which also count in lgkmcnt, so every LDS wait (lgkmcnt(0), the U/K reads of the factor
+    // sweep) drained the in-flight stage prefetch as well.
+    const gdouble* QSb = (const gdouble*)(d.qs + (size_t)(valid ? b : 0) * NS * QS);
+    gdouble* WSb = (gdouble*)(d.is + (size_t)(valid ? b : 0) * NS * IS);
+    auto ws = [&](int k, int f) -> gdouble* { return WSb + (size_t)k * IS + f * 16 + t; };
 
     // ---- model constants of this lane (sparse M, G; selects keep the kernel-argument reads scalar)
     const double m78 = c.M[7 * 9 + 8], m77 = c.M[7 * 10], m88 = c.M[8 * 10];
@@ -314,7 +319,7 @@ __device__ __forceinline__ void ipm_group(const DevConst& c, const DevBuffers& d
     // ---- stage loaders: every load unconditional (addresses clamped inside the stage record), the
     //      lane/stage conditions applied as selects afterwards (see sweep())
     auto load_common = [&](int k, In& o) {
-        const double* q = QSb + (size_t)k * QS;
+        const gdouble* q = QSb + (size_t)k * QS;
         o.lb = q[rowY ? QS_YLB + t : QS_DLB + j9];
         o.ub = q[rowY ? QS_YUB + t : QS_DUB + j9];
         o.np = q[QS_NPOLY];
@@ -333,7 +338,7 @@ __device__ __forceinline__ void ipm_group(const DevConst& c, const DevBuffers& d
     };
     auto load_factor = [&](int k, In& o, bool upd) {
         load_common(k, o);
-        const double* q = QSb + (size_t)k * QS;
+        const gdouble* q = QSb + (size_t)k * QS;
 #pragma unroll
         for (int m = 0; m < 9; m++) {
             const double v = q[QS_Q + t * 9 + m];
@@ -894,7 +899,7 @@ __device__ __forceinline__ void ipm_group(const DevConst& c, const DevBuffers& d
         return;
     }
     if (t == 0) si[SQ_QPSTAT] = 0;
-    double* stp = d.step + (size_t)b * NS * 17;
+    gdouble* stp = (gdouble*)(d.step + (size_t)b * NS * 17);
     for (int k = 0; k <= N; k++) {
         const double zx = *ws(k, WF_ZX) + alpha * *ws(k, WF_DX);
         const double zv = *ws(k, WF_ZV) + alpha * *ws(k, WF_DV);
