@@ -10,7 +10,9 @@
 //    the same sample broadcast over the 16-lane row by DPP) are applied in place between layers.
 //  * W is packed on the host in fragment order ([row tile][k-step][lane]), zero-padded to 16-row /
 //    4-column multiples: every A fragment is one coalesced 512-byte line.  Both networks' weights
-//    (1.84 MB) stay L2-resident; a weight element feeds 16 columns = 2 samples per load.
+//    (1.84 MB) stay L2-resident.  The env network's 256x256 layers stage each k-tile of W through LDS for the
+//    block's 4 waves (mfma_layer_lds), so a weight element loaded from L2 feeds 4 x 16 columns =
+//    8 samples: k_mlp_env 51.5 -> 24.8 ms on 335,872 samples, 27% -> 55% of the FP64 roof.
 //  * v_mfma_f64_16x16x4f64 accumulates as an ascending fma chain over k (bitwise,
 //    tools/probes/mfma_f64_probe.hip); the oracle's MLP uses the same chain.
 #include "dev_common.h"
@@ -40,6 +42,52 @@ __device__ __forceinline__ void mfma_layer(const double* __restrict__ Wp, const 
                 out[t] = __builtin_amdgcn_mfma_f64_16x16x4f64(Wp[((size_t)t * KS + s) * 64 + lane], in[kt][r], out[t], 0,
                                                               0, 0);
         }
+}
+
+// The same layer with the weights staged through LDS for the block's 4 waves: k-tile kt of every row
+// tile (RT x 4 k-steps x 64 lanes = RT x 2 KB) is loaded once per block, cooperatively and coalesced,
+// into one of two LDS buffers while the MFMAs of k-tile kt - 1 run from the other.  Every A fragment
+// then comes from L2 once per 4 waves (8 samples) instead of once per wave, and the per-MFMA operand
+// latency is an LDS read.  Same fragments, same ascending k order per row tile: bitwise the result
+// of mfma_layer.  All 256 threads of the block must call it (it contains barriers).
+template <int KT, int RT>
+__device__ __forceinline__ void mfma_layer_lds(const double* __restrict__ Wp, const d4 (&in)[KT], d4 (&out)[RT],
+                                               int lane, double* __restrict__ lds /* 2 x RT*256 */) {
+    constexpr int KS = 4 * KT;
+    constexpr int CH = RT * 256;       // doubles per k-tile chunk
+    constexpr int PT = CH / 256 / 2;   // double2 per thread per chunk
+    static_assert(RT % 2 == 0, "mfma_layer_lds: RT must be even");
+    const int tid = threadIdx.x;
+    double2 st[PT];
+    auto fetch = [&](int kt) {
+#pragma unroll
+        for (int j = 0; j < PT; j++) {
+            const int idx = 2 * (tid + 256 * j);           // chunk element: [t][r][lane]
+            const int t = idx >> 8, w = idx & 255;
+            st[j] = *reinterpret_cast<const double2*>(Wp + ((size_t)t * KS + 4 * kt) * 64 + w);
+        }
+    };
+    auto stash = [&](int buf) {
+#pragma unroll
+        for (int j = 0; j < PT; j++) reinterpret_cast<double2*>(lds + buf * CH)[tid + 256 * j] = st[j];
+    };
+#pragma unroll
+    for (int t = 0; t < RT; t++) out[t] = d4{0.0, 0.0, 0.0, 0.0};
+    fetch(0);
+    stash(0);
+    __syncthreads();
+#pragma unroll
+    for (int kt = 0; kt < KT; kt++) {
+        if (kt + 1 < KT) fetch(kt + 1);
+        const double* L = lds + (kt & 1) * CH;
+#pragma unroll
+        for (int r = 0; r < 4; r++)
+#pragma unroll
+            for (int t = 0; t < RT; t++)
+                out[t] = __builtin_amdgcn_mfma_f64_16x16x4f64(L[(t * 4 + r) * 64 + lane], in[kt][r], out[t], 0, 0, 0);
+        if (kt + 1 < KT) stash((kt + 1) & 1);
+        __syncthreads();
+    }
 }
 
 // hidden-layer epilogue: value columns h = relu(z + b); tangent columns dh = (z + b > 0) ? dz : 0
@@ -145,7 +193,7 @@ __global__ void __launch_bounds__(256) k_mlp_self(DevConst c, DevBuffers d, NNDe
     nerf_input<7>(x, a0, lane);
     mfma_layer<2, 16>(W + nd.offW[0], a0, a1, lane);
     relu_gate<16>(a1, W + nd.offb[0], lane);
-    mfma_layer<16, 4>(W + nd.offW[1], a1, a2, lane);
+    mfma_layer<16, 4>(W + nd.offW[1], a1, a2, lane);  // LDS staging measured 6% slower at RT = 4
     relu_gate<4>(a2, W + nd.offb[1], lane);
     mfma_layer<4, 1>(W + nd.offW[2], a2, o, lane);
     write_out<1>(o[0], W + nd.offb[2], lane, m, M, rec, S, R_SEL, R_DSEL);
@@ -158,7 +206,9 @@ __global__ void __launch_bounds__(256) k_mlp_env(DevConst c, DevBuffers d, NNDes
     const int lane = threadIdx.x & 63;
     const int wave = blockIdx.x * 4 + (threadIdx.x >> 6);
     const int m = 2 * wave + ((lane >> 3) & 1);
-    if (2 * wave >= M) return;
+    // no early exit: the hidden layers synchronize the block (a wave past M computes on a clamped
+    // sample and write_out drops its result)
+    __shared__ __attribute__((aligned(16))) double wl[2 * 16 * 256];
     double x[10];
     sample_input(c, d, m, M, qin, obsin, x);
     d4 a0[2], a[16], h[16], o[1];
@@ -166,7 +216,7 @@ __global__ void __launch_bounds__(256) k_mlp_env(DevConst c, DevBuffers d, NNDes
     mfma_layer<2, 16>(W + nd.offW[0], a0, a, lane);
     relu_gate<16>(a, W + nd.offb[0], lane);
     for (int l = 1; l <= 3; l++) {  // three 256 x 256 hidden layers share one unrolled body
-        mfma_layer<16, 16>(W + nd.offW[l], a, h, lane);
+        mfma_layer_lds<16, 16>(W + nd.offW[l], a, h, lane, wl);
         relu_gate<16>(h, W + nd.offb[l], lane);
 #pragma unroll
         for (int t = 0; t < 16; t++) a[t] = h[t];
