@@ -40,6 +40,8 @@ constexpr int IPM_MAX_IT = MPCC_IPM_MAXIT;  // 60 (oracle); a debug build may ca
 constexpr double IPM_TOL_MU = 1e-13, IPM_TOL_P = 1e-11, IPM_TOL_STEP = 1e-11;
 constexpr double IPM_TOL_FB = 1e-9;  // P2: a converged iterate is accepted when the Riccati factor breaks down
 constexpr double IPM_DIV = 1e6;      // P3: mu > IPM_DIV * mu_0 -> primal infeasible (divergent multipliers)
+constexpr double IPM_S0 = 0.02, IPM_L0 = 0.002;  // scaled start point (oracle: solve_struct_ipm)
+constexpr int IPM_MAX_IT_SCALED = 30;
 constexpr double IPM_TAU = 0.995;    // fraction-to-boundary floor: tau = max(IPM_TAU, 1 - sqrt(mu))
 typedef __attribute__((address_space(1))) double gdouble;  // global-memory double (global_* loads/stores)
 constexpr int IPW = 4;               // instances per wavefront (16 lanes each)
@@ -436,8 +438,9 @@ __device__ __forceinline__ void ipm_group(const DevConst& c, const DevBuffers& d
         else xn = vj;
     };
 
-    // ---- start point: dynamics rollout with v = 0, s = max(-g, 1), lambda = 1
-    double mcount = 0.0;
+    // ---- start point: dynamics rollout with v = 0; slacks s = max(-g, IPM_S0), lambda = IPM_L0 / s, at most
+    //      IPM_MAX_IT_SCALED iterations; a solve that does not converge from there restarts from
+    //      s = max(-g, 1), lambda = 1 with IPM_MAX_IT (the oracle's solve_struct_ipm)
     In cur, nxt;
     // the three sweeps without the factorization (predictor forward, corrector backward and forward)
     // are short bodies that wait on their stage loads: they keep MPCC_LIGHT_DEPTH - 1 stages in flight
@@ -446,6 +449,20 @@ __device__ __forceinline__ void ipm_group(const DevConst& c, const DevBuffers& d
         if constexpr (NPM <= 2) sweep_ring<MPCC_LIGHT_DEPTH>(N, backward, ring, load, body);
         else sweep<false>(N, backward, cur, nxt, load, body);
     };
+    int it = 0, it_total = 0;
+    bool conv = false, diverged = false;
+    double alpha = 0.0;  // step length of the last iteration (the final iterate is z + alpha dz)
+#pragma unroll 1
+    for (int attempt = 0; attempt < 2; attempt++) {
+    const double s_floor = (attempt == 0) ? IPM_S0 : 1.0;
+    const double lam_scale = (attempt == 0) ? IPM_L0 : 0.0;
+    const int max_it = (attempt == 0) ? IPM_MAX_IT_SCALED : IPM_MAX_IT;
+    if (attempt == 1) {
+        run = entered && !conv;  // restart only the solves that did not converge from the scaled start
+        if (__ballot(run) == 0) break;
+        if (run) diverged = false;
+    }
+    double mcount = 0.0;
     if (run) {
         double y = 0.0;  // lane a < 9: y_a of stage k
         double bk = 0, bkn = 0;
@@ -461,9 +478,9 @@ __device__ __forceinline__ void ipm_group(const DevConst& c, const DevBuffers& d
             const double pcz = poly_cz(cur, k, yx, 0.0);
             const bool aL = row_active(k, cur.lb), aU = row_active(k, cur.ub), aP = poly_slot_active(cur, k);
             double sL = 1, lL = 0, sU = 1, lU = 0, sP = 1, lP = 0;
-            if (aL) { sL = fmax(-(sgnL * cz - sgnL * cur.lb), 1.0); lL = 1.0; }
-            if (aU) { sU = fmax(-(sgnU * cz - sgnU * cur.ub), 1.0); lU = 1.0; }
-            if (aP) { sP = fmax(-(sgnU * pcz - sgnU * cur.pub), 1.0); lP = 1.0; }
+            if (aL) { sL = fmax(-(sgnL * cz - sgnL * cur.lb), s_floor); lL = (lam_scale > 0) ? lam_scale / sL : 1.0; }
+            if (aU) { sU = fmax(-(sgnU * cz - sgnU * cur.ub), s_floor); lU = (lam_scale > 0) ? lam_scale / sU : 1.0; }
+            if (aP) { sP = fmax(-(sgnU * pcz - sgnU * cur.pub), s_floor); lP = (lam_scale > 0) ? lam_scale / sP : 1.0; }
             mcount += (aL ? 1.0 : 0.0) + (aU ? 1.0 : 0.0) + (aP ? 1.0 : 0.0);
             *ws(k, WF_SL) = sL; *ws(k, WF_LL) = lL; *ws(k, WF_SU) = sU; *ws(k, WF_LU) = lU;
             *ws(k, WF_SP) = sP; *ws(k, WF_LP) = lP;
@@ -480,13 +497,13 @@ __device__ __forceinline__ void ipm_group(const DevConst& c, const DevBuffers& d
     mcount = g_sum(mcount);
     PMARK(0);
 
-    int it = 0;
-    bool conv = false, diverged = false;
+    it = 0;
     double mu0 = 0.0;                    // mu of the starting point (P3)
     double dz_prev = 1e30;               // max |dz| of the previous iteration (step test)
-    double alpha = 0.0, sigma_mu = 0.0;  // previous iteration's step length and sigma*mu (lazy update)
+    double sigma_mu = 0.0;               // previous iteration's sigma*mu (lazy update)
     double mu_cur = 1e30, rp_cur = 1e30; // mu and max |rp| of the current iterate (known for it > 0)
     bool pending = false;
+    if (run) alpha = 0.0;
     while (true) {
         if (__ballot(run) == 0) break;
         if (run) {
@@ -861,8 +878,8 @@ __device__ __forceinline__ void ipm_group(const DevConst& c, const DevBuffers& d
             pending = true;
             it++;
             PMARK(5);
-            // convergence test at the start of the next iteration (oracle: only while it < IPM_MAX_IT)
-            if (it < IPM_MAX_IT) {
+            // convergence test at the start of the next iteration (oracle: only while it < max_it)
+            if (it < max_it) {
                 double mun = T0 + alpha * T1 + alpha * alpha * T2;
                 mun = (mcount > 0) ? mun / mcount : 0.0;
                 const double rpn = (1.0 - alpha) * rpm;
@@ -884,16 +901,18 @@ __device__ __forceinline__ void ipm_group(const DevConst& c, const DevBuffers& d
             }
         }
     }
+    it_total += it;
+    }  // attempt
 
 #ifdef MPCC_IPM_PROF
     if (entered && t == 0) {
         for (int i = 0; i < 16; i++) if (i != 6 && i != 7) atomicAdd(&g_ipm_prof[i], (unsigned long long)prof_acc[i]);
-        atomicAdd(&g_ipm_prof[6], (unsigned long long)it);
+        atomicAdd(&g_ipm_prof[6], (unsigned long long)it_total);
         atomicAdd(&g_ipm_prof[7], 1ull);
     }
 #endif
     if (!entered) return;
-    if (t == 0) si[SQ_IPMIT] = it;
+    if (t == 0) si[SQ_IPMIT] = it_total;
     if (!conv) {  // keep the previous step (Q6)
         if (t == 0) si[SQ_QPSTAT] = diverged ? MPCC_QP_PrimalInfeasible : MPCC_QP_MaxIterReached;
         return;

@@ -1429,7 +1429,8 @@ struct Riccati {
 // Returns 0 on success (step filled in reference layout: [y_0..y_N | v_0..v_{N-1}]), else Status.
 static const bool g_ipm_debug = std::getenv("MPCC_ORACLE_IPM_DEBUG") != nullptr;  // per-iteration log (debug)
 
-static int solve_struct_ipm(const StructQP& S, std::vector<double>& step, int* iters_out) {
+static int solve_struct_ipm_from(const StructQP& S, std::vector<double>& step, int* iters_out, double s_floor,
+                                 double lam_scale, int max_it) {
     const int N = S.N;
     if (S.infeasible) return QP_PrimalInfeasible;
     std::vector<Ineq> I;
@@ -1459,14 +1460,15 @@ static int solve_struct_ipm(const StructQP& S, std::vector<double>& step, int* i
     std::vector<double> sl(m), lam(m, 1.0), rp(m), W(m), dsa(m), dla(m), ds(m), dl(m), rc(m);
     for (int i = 0; i < m; i++) {
         double g = I[i].sgn * rowdot(I[i], z) - I[i].sgn * I[i].bnd;
-        sl[i] = std::max(-g, 1.0);
+        sl[i] = std::max(-g, s_floor);
+        if (lam_scale > 0) lam[i] = lam_scale / sl[i];
     }
     std::vector<double> Hs((size_t)(N + 1) * NZ * NZ), gs((size_t)(N + 1) * NZ), dz, dza;
     Riccati R;
     int it;
     bool conv = false, diverged = false;
     double last_dz = 1e30, prev_dz = 1e30, mu0 = 0.0;
-    for (it = 0; it < IPM_MAX_IT; it++) {
+    for (it = 0; it < max_it; it++) {
         double mu = 0, rpmax = 0;
         for (int i = 0; i < m; i++) {
             rp[i] = I[i].sgn * rowdot(I[i], z) - I[i].sgn * I[i].bnd + sl[i];
@@ -1579,6 +1581,22 @@ static int solve_struct_ipm(const StructQP& S, std::vector<double>& step, int* i
             for (int b = 0; b < NU; b++) step[(size_t)NX * (N + 1) + NU * k + b] = z[(size_t)k * NZ + 16 + b];
     }
     return 0;
+}
+
+// Start point: first from slacks floored at IPM_S0 with complementary multipliers
+// lambda = IPM_L0 / s (mu_0 = IPM_L0: close to the central path and scaled to the bounds), at most
+// IPM_MAX_IT_SCALED iterations; a solve that does not converge from there (max iterations, P3) restarts
+// from the unit start point s = max(-g, 1), lambda = 1 with the full IPM_MAX_IT.  The restart is
+// exactly the solve without the scaled attempt, so the scaled start can only change which iterate a
+// converging QP ends on (~1e-12), never a failure into a different failure.
+constexpr double IPM_S0 = 0.02, IPM_L0 = 0.002;
+constexpr int IPM_MAX_IT_SCALED = 30;
+static int solve_struct_ipm(const StructQP& S, std::vector<double>& step, int* iters_out) {
+    int it1 = 0, it2 = 0;
+    int rc = solve_struct_ipm_from(S, step, &it1, IPM_S0, IPM_L0, IPM_MAX_IT_SCALED);
+    if (rc != 0) rc = solve_struct_ipm_from(S, step, &it2, 1.0, 0.0, IPM_MAX_IT);
+    if (iters_out) *iters_out = it1 + it2;
+    return rc;
 }
 
 // ---------------- dense-layout primal-dual IPM (validation; solves the reference QP verbatim) ---
