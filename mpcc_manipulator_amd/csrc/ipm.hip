@@ -264,7 +264,21 @@ __device__ __forceinline__ void ipm_group(const DevConst& c, const DevBuffers& d
     // sweep) drained the in-flight stage prefetch as well.
     const gdouble* QSb = (const gdouble*)(d.qs + (size_t)(valid ? b : 0) * NS * QS);
     gdouble* WSb = (gdouble*)(d.is + (size_t)(valid ? b : 0) * NS * IS);
-    auto ws = [&](int k, int f) -> gdouble* { return WSb + (size_t)k * IS + f * 16 + t; };
+    // Stage base addresses pass through an empty asm: the optimizer cannot strength-reduce every
+    // (field, stage) address into its own 64-bit induction variable.  It did, ran out of registers,
+    // spilled the addresses to scratch, and each scratch reload (s_waitcnt vmcnt(0)) drained the stage
+    // prefetch.  Fields are then immediate offsets from one stage pointer.
+    gdouble* const WSt = WSb + t;
+    auto ws = [&](int k, int f) -> gdouble* {
+        gdouble* wk = WSt + (size_t)k * IS;
+        asm("" : "+v"(wk));
+        return wk + f * 16;
+    };
+    auto qs_stage = [&](int k) -> const gdouble* {
+        const gdouble* qk = QSb + (size_t)k * QS;
+        asm("" : "+v"(qk));
+        return qk;
+    };
 
     // ---- model constants of this lane (sparse M, G; selects keep the kernel-argument reads scalar)
     const double m78 = c.M[7 * 9 + 8], m77 = c.M[7 * 10], m88 = c.M[8 * 10];
@@ -321,7 +335,7 @@ __device__ __forceinline__ void ipm_group(const DevConst& c, const DevBuffers& d
     // ---- stage loaders: every load unconditional (addresses clamped inside the stage record), the
     //      lane/stage conditions applied as selects afterwards (see sweep())
     auto load_common = [&](int k, In& o) {
-        const gdouble* q = QSb + (size_t)k * QS;
+        const gdouble* q = qs_stage(k);
         o.lb = q[rowY ? QS_YLB + t : QS_DLB + j9];
         o.ub = q[rowY ? QS_YUB + t : QS_DUB + j9];
         o.np = q[QS_NPOLY];
@@ -340,7 +354,7 @@ __device__ __forceinline__ void ipm_group(const DevConst& c, const DevBuffers& d
     };
     auto load_factor = [&](int k, In& o, bool upd) {
         load_common(k, o);
-        const gdouble* q = QSb + (size_t)k * QS;
+        const gdouble* q = qs_stage(k);
 #pragma unroll
         for (int m = 0; m < 9; m++) {
             const double v = q[QS_Q + t * 9 + m];
