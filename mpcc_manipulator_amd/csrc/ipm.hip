@@ -214,8 +214,10 @@ __device__ __forceinline__ void sweep(int N, bool backward, In& b0, In& b1, Load
 // Stage sweep with a ring of D stage buffers: stage s(i + D - 1) is loaded while stage s(i) is processed,
 // so D - 1 stages of loads are in flight.  Loads are unconditional (the stages past the end re-read
 // s(N)); the ring index is a constant after unrolling, so the buffers stay in registers.
+// D = 2 since the stage addresses stopped spilling: same box, configs[1], k_sqp
+// 3.83 ms at D = 2, 3.88 ms at D = 3, 4.14 ms at D = 4 (tools/bench_variants.sh).
 #ifndef MPCC_LIGHT_DEPTH
-#define MPCC_LIGHT_DEPTH 3
+#define MPCC_LIGHT_DEPTH 2
 #endif
 template <int D, class In, class LoadF, class BodyF>
 __device__ __forceinline__ void sweep_ring(int N, bool backward, In (&b)[D], LoadF load, BodyF body) {
