@@ -213,7 +213,7 @@ __global__ void __launch_bounds__(256) k_mlp_env(DevConst c, DevBuffers d, NNDes
     sample_input(c, d, m, M, qin, obsin, x);
     d4 a0[2], a[16], h[16], o[1];
     nerf_input<10>(x, a0, lane);
-    mfma_layer<2, 16>(W + nd.offW[0], a0, a, lane);
+    mfma_layer_lds<2, 16>(W + nd.offW[0], a0, a, lane, wl);
     relu_gate<16>(a, W + nd.offb[0], lane);
     for (int l = 1; l <= 3; l++) {  // three 256 x 256 hidden layers share one unrolled body
         mfma_layer_lds<16, 16>(W + nd.offW[l], a, h, lane, wl);
