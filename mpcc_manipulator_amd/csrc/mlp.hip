@@ -10,7 +10,7 @@
 //    the same sample broadcast over the 16-lane row by DPP) are applied in place between layers.
 //  * W is packed on the host in fragment order ([row tile][k-step][lane]), zero-padded to 16-row /
 //    4-column multiples: every A fragment is one coalesced 512-byte line.  Both networks' weights
-//    (1.84 MB) stay L2-resident.  The env network's 256x256 layers stage each k-tile of W through LDS for the
+//    (1.84 MB) stay L2-resident.  The 256-row layers (both input layers, the env hidden layers) stage each k-tile of W through LDS for the
 //    block's 4 waves (mfma_layer_lds), so a weight element loaded from L2 feeds 4 x 16 columns =
 //    8 samples: k_mlp_env 51.5 -> 24.8 ms on 335,872 samples, 27% -> 55% of the FP64 roof.
 //  * v_mfma_f64_16x16x4f64 accumulates as an ascending fma chain over k (bitwise,
@@ -183,7 +183,8 @@ __global__ void __launch_bounds__(256) k_mlp_self(DevConst c, DevBuffers d, NNDe
     const int lane = threadIdx.x & 63;
     const int wave = blockIdx.x * 4 + (threadIdx.x >> 6);
     const int m = 2 * wave + ((lane >> 3) & 1);
-    if (2 * wave >= M) return;  // wave-uniform
+    // no early exit: the input layer synchronizes the block (see k_mlp_env)
+    __shared__ __attribute__((aligned(16))) double wl[2 * 16 * 256];
     double xin[10];
     sample_input(c, d, m, M, qin, obsin, xin);
     double x[7];
@@ -191,7 +192,7 @@ __global__ void __launch_bounds__(256) k_mlp_self(DevConst c, DevBuffers d, NNDe
     for (int i = 0; i < 7; i++) x[i] = xin[i];
     d4 a0[2], a1[16], a2[4], o[1];
     nerf_input<7>(x, a0, lane);
-    mfma_layer<2, 16>(W + nd.offW[0], a0, a1, lane);
+    mfma_layer_lds<2, 16>(W + nd.offW[0], a0, a1, lane, wl);
     relu_gate<16>(a1, W + nd.offb[0], lane);
     mfma_layer<16, 4>(W + nd.offW[1], a1, a2, lane);  // LDS staging measured 6% slower at RT = 4
     relu_gate<4>(a2, W + nd.offb[1], lane);
