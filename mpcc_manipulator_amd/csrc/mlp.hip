@@ -10,9 +10,10 @@
 //    the same sample broadcast over the 16-lane row by DPP) are applied in place between layers.
 //  * W is packed on the host in fragment order ([row tile][k-step][lane]), zero-padded to 16-row /
 //    4-column multiples: every A fragment is one coalesced 512-byte line.  Both networks' weights
-//    (1.84 MB) stay L2-resident.  The 256-row layers (both input layers, the env hidden layers) stage each k-tile of W through LDS for the
-//    block's 4 waves (mfma_layer_lds), so a weight element loaded from L2 feeds 4 x 16 columns =
-//    8 samples: k_mlp_env 51.5 -> 24.8 ms on 335,872 samples, 27% -> 55% of the FP64 roof.
+//    (1.84 MB) stay L2-resident.  The 256-row layers (both input layers, the env hidden layers)
+//    stage each k-tile of W through LDS for the block's 4 waves (mfma_layer_lds), so a weight element
+//    loaded from L2 feeds 4 x 16 columns = 8 samples: k_mlp_env 51.5 -> 23.7 ms on 335,872 samples,
+//    27% -> 58% of the FP64 roof; k_mlp_self 5.9 -> 4.8 ms.
 //  * v_mfma_f64_16x16x4f64 accumulates as an ascending fma chain over k (bitwise,
 //    tools/probes/mfma_f64_probe.hip); the oracle's MLP uses the same chain.
 #include "dev_common.h"
