@@ -10,6 +10,8 @@ over RCCL each step.  Prints one JSON line (rank 0).
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -86,6 +88,47 @@ def cpu_baseline(params_dict, track, x0, u0, obs, guess, valid, fails, threads, 
     return done / dt, n, passes, dt
 
 
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def launch_ranks(n):
+    """`python bench.py --gpus N` outside a launcher: start N ranks (one process per GPU) as child
+    processes before this process touches the GPU, with the env torch.distributed.run would set, and
+    exit with the worst child exit code.  Rank 0 writes the JSON line to our stdout."""
+    import torch
+    rehearse = os.environ.get("MPCC_BENCH_REHEARSE", "0") == "1"
+    ndev = torch.cuda.device_count()  # counts devices without initialising the GPU
+    if not rehearse and ndev < n:
+        print(f"bench.py: --gpus {n} requested but {ndev} GPU(s) visible", file=sys.stderr)
+        sys.exit(2)
+    port = _free_port()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env,
+                                      stdout=None if r == 0 else subprocess.DEVNULL))
+    codes = [None] * n
+    while any(c is None for c in codes):
+        for i, p in enumerate(procs):
+            if codes[i] is None:
+                codes[i] = p.poll()
+        if any(c not in (None, 0) for c in codes):  # one rank failed: stop the others (exact PIDs)
+            for i, p in enumerate(procs):
+                if codes[i] is None:
+                    p.kill()
+                    codes[i] = p.wait()
+            break
+        time.sleep(0.05)
+    bad = [c for c in codes if c != 0]
+    sys.exit(bad[0] if bad else 0)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -104,7 +147,12 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=15.0, help="CPU-baseline budget (bounded sample)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--traffic", default=None, help="PMC traffic summary (default profiles/pmc_traffic_<kernel>.json)")
+    ap.add_argument("--dump-u0", default=None, help="rank 0 writes the last step's gathered u0 [world*B, 8] (.npy)")
     args = ap.parse_args()
+    if args.gpus < 1:
+        ap.error("--gpus must be >= 1")
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        launch_ranks(args.gpus)
     preset = {1: dict(batch=4096, N=20, mask=2), 2: dict(batch=65536, N=40, mask=7)}[args.config]
     for k, v in preset.items():
         if getattr(args, k) is None:
@@ -113,6 +161,9 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        print(f"bench.py: WORLD_SIZE={world} but --gpus {args.gpus}", file=sys.stderr)
+        sys.exit(2)
     # MPCC_BENCH_REHEARSE=1: every rank on GPU 0 over gloo — rehearses the multi-rank path (sharding,
     # u0 gather, max-over-ranks timing, aggregation) on a one-GPU box; real runs use one GPU per rank
     # over RCCL ("nccl")
@@ -120,6 +171,9 @@ def main():
     if rehearse:
         local = 0
     import torch
+    if torch.cuda.device_count() <= local:
+        print(f"bench.py: rank {rank} needs GPU {local} but {torch.cuda.device_count()} GPU(s) visible", file=sys.stderr)
+        sys.exit(2)
     torch.cuda.set_device(local)
     dist = None
     if world > 1:
@@ -130,7 +184,7 @@ def main():
             dist.init_process_group("nccl", device_id=torch.device("cuda", local))
 
     import mpcc_manipulator_amd as m
-    from mpcc_manipulator_amd.distributed import gather_u0, max_over_ranks, shard_bounds
+    from mpcc_manipulator_amd.distributed import check_equal_shards, gather_u0, max_over_ranks, shard_bounds
 
     N, B = args.N, args.batch
     params = m.load_params(N, overrides={"sqp": {"max_iter": args.max_iter}})
@@ -140,19 +194,20 @@ def main():
     eng = m.Engine(params, max_batch=B, device=local, constraint_mask=args.mask)
     eng.set_track(*track)
 
-    # instances: pool step t = (global index) mod T, q += N(0, 0.005)
-    rng = np.random.default_rng(SEED + rank)
+    # instances: pool step t = (global index) mod T, q += N(0, 0.005); the noise is
+    # drawn for the global batch, so instance i gets the same input whatever the number of ranks
+    rng = np.random.default_rng(SEED)
     T = len(pool["x0"])
     start, _ = shard_bounds(B * world, rank, world)  # contiguous instance block of this rank
     idx = (np.arange(B) + start) % T
     x0 = pool["x0"][idx].copy()
-    x0[:, :7] += rng.normal(0.0, 0.005, size=(B, 7))
+    x0[:, :7] += rng.normal(0.0, 0.005, size=(B * world, 7))[start:start + B]
     u0 = pool["u0"][idx].copy()
     guess = pool["guess"][idx].copy()
     valid = pool["valid"][idx].astype(np.int32)
     fails = pool["fails"][idx].astype(np.int32)
     if args.config == 2:  # main_w_sim.py:42-45 scenario: xyz = (0.48, 0.218, z), z ~ U[0.421, 0.621], r = 5 cm
-        z = rng.uniform(0.421, 0.621, B)
+        z = rng.uniform(0.421, 0.621, B * world)[start:start + B]
         obs = np.column_stack([np.full(B, 0.48), np.full(B, 0.218), z, np.full(B, 5.0)])
     else:  # dummy obstacle of MPC::runMPC (mpc.cpp:97-100)
         obs = np.tile(np.array([3.0, 3.0, 3.0, 0.0]), (B, 1))
@@ -176,6 +231,8 @@ def main():
         if world > 1:
             gather_u0(u_out, world, out=u_all)  # RCCL all-gather of u0 over xGMI
 
+    if world > 1:
+        check_equal_shards(B, device=dev)
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize()
@@ -274,6 +331,8 @@ def main():
             "cpu_baseline": cpu,
         }
         print(json.dumps(line))
+    if args.dump_u0 and rank == 0:
+        np.save(args.dump_u0, (u_all if world > 1 else u_out).cpu().numpy())
     if dist is not None:
         dist.destroy_process_group()
 

@@ -66,6 +66,7 @@ struct mpcc_engine {
     double* d_spl = nullptr;
     SplineDev spl{};
     int n_tracks = 0;  // 1: shared track (stride 0); B: one per instance (mpcc_set_tracks)
+    bool ext_async = false;  // a device call was queued on a caller stream since the last quiesce()
     DevBuffers d{};
     // host-API staging
     double *s_x0 = nullptr, *s_u0 = nullptr, *s_obs = nullptr, *s_u0out = nullptr, *s_hor = nullptr;
@@ -275,6 +276,31 @@ void upload_tracks(mpcc_engine* e, const std::vector<SplineTables>& tracks, bool
 
 void upload_track(mpcc_engine* e) { upload_tracks(e, {e->track}, false); }
 
+// Every entry point runs on the engine's device, whatever device the calling thread has current
+// (a process may hold engines on several GPUs); the caller's current device is restored on return.
+struct DevGuard {
+    int prev = -1, dev = -1;
+    explicit DevGuard(const mpcc_engine* e) : dev(e->cfg.device) {
+        if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+        if (prev != dev) (void)hipSetDevice(dev);
+    }
+    ~DevGuard() {
+        if (prev >= 0 && prev != dev) (void)hipSetDevice(prev);
+    }
+};
+
+// Host-side accessors of engine state (warm start, tracks, params, debug entries) first wait for every
+// asynchronous call that may still use that state: the engine stream, and — when a device call ran
+// on a caller stream (mpcc_solve_device / mpcc_set_warmstart_device with stream != NULL, which the
+// engine's non-blocking stream does not order against) — the whole device.
+void quiesce(mpcc_engine* e) {
+    HIPCHK(hipStreamSynchronize(e->stream));
+    if (e->ext_async) {
+        HIPCHK(hipDeviceSynchronize());
+        e->ext_async = false;
+    }
+}
+
 void run_batch(mpcc_engine* e, int B, hipStream_t st, mpcc_timing* timing, bool ocp = false) {
     DevConst c = e->make_const(B);
     c.ocp = ocp ? 1 : 0;
@@ -437,10 +463,16 @@ int mpcc_create(const mpcc_config* cfg, const mpcc_params* params, const char* n
     return MPCC_OK;
 }
 
-void mpcc_destroy(mpcc_engine* e) { delete e; }
+void mpcc_destroy(mpcc_engine* e) {
+    if (!e) return;
+    DevGuard dg_(e);
+    (void)hipDeviceSynchronize();  // no kernel may still use the buffers being freed
+    delete e;
+}
 
 int mpcc_set_params(mpcc_engine* e, const mpcc_params* p) {
     if (!e || !p) return fail(MPCC_E_INVALID, "mpcc_set_params: null argument");
+    DevGuard dg_(e);
     mpcc_params np = *p;
     np.N = e->N;  // horizon and Ts are fixed at creation (device buffers, model)
     np.Ts = e->params.Ts;
@@ -448,6 +480,7 @@ int mpcc_set_params(mpcc_engine* e, const mpcc_params* p) {
         return fail(MPCC_E_INVALID, "mpcc_set_params: collision rows need NN weights loaded at create");
     const mpcc_params old = e->params;
     try {
+        quiesce(e);
         validate_params(np);
         e->params = np;
         e->set_model();
@@ -461,13 +494,16 @@ int mpcc_set_params(mpcc_engine* e, const mpcc_params* p) {
 
 int mpcc_get_params(mpcc_engine* e, mpcc_params* out) {
     if (!e || !out) return fail(MPCC_E_INVALID, "mpcc_get_params: null argument");
+    DevGuard dg_(e);
     *out = e->params;
     return MPCC_OK;
 }
 
 int mpcc_set_track(mpcc_engine* e, int n, const double* X, const double* Y, const double* Z, const double* R9) {
     if (!e || n < 3 || !X || !Y || !Z || !R9) return fail(MPCC_E_INVALID, "mpcc_set_track: invalid argument");
+    DevGuard dg_(e);
     try {
+        quiesce(e);
         e->track = build_track_spline(n, X, Y, Z, R9);
         upload_track(e);
         e->has_track = true;
@@ -483,7 +519,9 @@ int mpcc_set_track(mpcc_engine* e, int n, const double* X, const double* Y, cons
 int mpcc_set_track_path(mpcc_engine* e, int n, const double* s, const double* X, const double* Y, const double* Z,
                         const double* R9) {
     if (!e || !s || !X || !Y || !Z || !R9) return fail(MPCC_E_INVALID, "mpcc_set_track_path: invalid argument");
+    DevGuard dg_(e);
     try {
+        quiesce(e);
         e->track = build_track_from_path(n, s, X, Y, Z, R9);
         upload_track(e);
         e->has_track = true;
@@ -499,7 +537,9 @@ int mpcc_set_track_path(mpcc_engine* e, int n, const double* s, const double* X,
 int mpcc_set_tracks(mpcc_engine* e, int B, int n, const double* X, const double* Y, const double* Z, const double* R9) {
     if (!e || B < 1 || B > e->maxB || n < 3 || !X || !Y || !Z || !R9)
         return fail(MPCC_E_INVALID, "mpcc_set_tracks: invalid argument");
+    DevGuard dg_(e);
     try {
+        quiesce(e);
         std::vector<SplineTables> tr(B);
         const unsigned nt = std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
         std::vector<std::thread> pool;
@@ -577,6 +617,7 @@ double mpcc_track_length(mpcc_engine* e) { return (e && e->has_track) ? e->track
 
 int mpcc_get_track_path(mpcc_engine* e, double* s, double* X, double* Y, double* Z, double* R9) {
     if (!e || !e->has_track) return fail(MPCC_E_NOTRACK, "mpcc_get_track_path: no track");
+    DevGuard dg_(e);
     const SplineTables& t = e->track;
     if (s) std::memcpy(s, t.s.data(), t.n * sizeof(double));
     if (X) std::memcpy(X, t.X.data(), t.n * sizeof(double));
@@ -588,7 +629,9 @@ int mpcc_get_track_path(mpcc_engine* e, double* s, double* X, double* Y, double*
 
 int mpcc_set_warmstart(mpcc_engine* e, int B, const double* guess, const int32_t* valid, const int32_t* fails) {
     if (!e || B < 0 || B > e->maxB) return fail(MPCC_E_INVALID, "mpcc_set_warmstart: invalid argument");
+    DevGuard dg_(e);
     try {
+        quiesce(e);
         const size_t NS = e->N + 1;
         if (guess) HIPCHK(hipMemcpy(e->d.guess, guess, (size_t)B * NS * 17 * sizeof(double), hipMemcpyHostToDevice));
         if (valid) HIPCHK(hipMemcpy(e->d.valid, valid, (size_t)B * sizeof(int32_t), hipMemcpyHostToDevice));
@@ -601,9 +644,10 @@ int mpcc_set_warmstart(mpcc_engine* e, int B, const double* guess, const int32_t
 
 int mpcc_get_warmstart(mpcc_engine* e, int B, double* guess, int32_t* valid, int32_t* fails) {
     if (!e || B < 0 || B > e->maxB) return fail(MPCC_E_INVALID, "mpcc_get_warmstart: invalid argument");
+    DevGuard dg_(e);
     try {
+        quiesce(e);
         const size_t NS = e->N + 1;
-        HIPCHK(hipStreamSynchronize(e->stream));
         if (guess) HIPCHK(hipMemcpy(guess, e->d.guess, (size_t)B * NS * 17 * sizeof(double), hipMemcpyDeviceToHost));
         if (valid) HIPCHK(hipMemcpy(valid, e->d.valid, (size_t)B * sizeof(int32_t), hipMemcpyDeviceToHost));
         if (fails) HIPCHK(hipMemcpy(fails, e->d.fails, (size_t)B * sizeof(int32_t), hipMemcpyDeviceToHost));
@@ -615,8 +659,9 @@ int mpcc_get_warmstart(mpcc_engine* e, int B, double* guess, int32_t* valid, int
 
 int mpcc_reset_warmstart(mpcc_engine* e, int B, const uint8_t* mask) {
     if (!e || B < 0 || B > e->maxB) return fail(MPCC_E_INVALID, "mpcc_reset_warmstart: invalid argument");
+    DevGuard dg_(e);
     try {
-        HIPCHK(hipStreamSynchronize(e->stream));
+        quiesce(e);
         if (!mask) {
             HIPCHK(hipMemset(e->d.valid, 0, (size_t)B * sizeof(int32_t)));
             HIPCHK(hipMemset(e->d.fails, 0, (size_t)B * sizeof(int32_t)));
@@ -639,9 +684,11 @@ int mpcc_solve_device(mpcc_engine* e, int B, double* d_x0, const double* d_u0, c
     if (!e || B < 1 || B > e->maxB || !d_x0 || !d_u0 || !d_obs)
         return fail(MPCC_E_INVALID, "mpcc_solve_device: invalid argument");
     if (!e->has_track) return fail(MPCC_E_NOTRACK, "mpcc_solve_device: set_track first");
+    DevGuard dg_(e);
     if (e->spl.stride && B > e->n_tracks) return fail(MPCC_E_INVALID, "mpcc_solve_device: more instances than per-instance tracks");
     try {
         hipStream_t st = stream ? (hipStream_t)stream : e->stream;
+        if (st != e->stream) e->ext_async = true;
         e->d.x0 = d_x0; e->d.u0 = d_u0; e->d.obs = d_obs;
         e->d.u0_out = d_u0_out; e->d.horizon = d_horizon; e->d.status = d_status; e->d.ok = d_ok;
         run_batch(e, B, st, nullptr);
@@ -654,8 +701,10 @@ int mpcc_solve_device(mpcc_engine* e, int B, double* d_x0, const double* d_u0, c
 int mpcc_set_warmstart_device(mpcc_engine* e, int B, const double* d_guess, const int32_t* d_valid,
                               const int32_t* d_fails, void* stream) {
     if (!e || B < 0 || B > e->maxB) return fail(MPCC_E_INVALID, "mpcc_set_warmstart_device: invalid argument");
+    DevGuard dg_(e);
     try {
         hipStream_t st = stream ? (hipStream_t)stream : e->stream;
+        if (st != e->stream) e->ext_async = true;
         const size_t NS = e->N + 1;
         if (d_guess)
             HIPCHK(hipMemcpyAsync(e->d.guess, d_guess, (size_t)B * NS * 17 * sizeof(double), hipMemcpyDeviceToDevice, st));
@@ -669,6 +718,7 @@ int mpcc_set_warmstart_device(mpcc_engine* e, int B, const double* d_guess, cons
 
 int mpcc_timing_begin(mpcc_engine* e) {
     if (!e) return fail(MPCC_E_INVALID, "mpcc_timing_begin: null engine");
+    DevGuard dg_(e);
     e->live = true;
     e->live_used = 0;
     e->live_calls = 0;
@@ -678,6 +728,7 @@ int mpcc_timing_begin(mpcc_engine* e) {
 
 int mpcc_timing_end(mpcc_engine* e, mpcc_timing* sum, int32_t* n_calls, int32_t* n_ipm) {
     if (!e || !e->live) return fail(MPCC_E_INVALID, "mpcc_timing_end: timing not active");
+    DevGuard dg_(e);
     try {
         mpcc_timing t{};
         auto acc = [&](const std::vector<std::pair<hipEvent_t, hipEvent_t>>& v) {
@@ -708,9 +759,10 @@ int mpcc_timing_end(mpcc_engine* e, mpcc_timing* sum, int32_t* n_calls, int32_t*
 
 int mpcc_get_solve_stats(mpcc_engine* e, int B, int32_t* sqp_iter, int32_t* ipm_iters, int32_t* qp_status) {
     if (!e || B < 1 || B > e->maxB) return fail(MPCC_E_INVALID, "mpcc_get_solve_stats: invalid argument");
+    DevGuard dg_(e);
     try {
-        HIPCHK(hipStreamSynchronize(e->stream));
-        HIPCHK(hipDeviceSynchronize());
+        quiesce(e);
+        HIPCHK(hipDeviceSynchronize());  // the stats of the last solve, whichever stream it ran on
         std::vector<int32_t> sqi((size_t)B * SQI);
         HIPCHK(hipMemcpy(sqi.data(), e->d.sqi, sqi.size() * sizeof(int32_t), hipMemcpyDeviceToHost));
         for (int b = 0; b < B; b++) {
@@ -727,9 +779,11 @@ int mpcc_get_solve_stats(mpcc_engine* e, int B, int32_t* sqp_iter, int32_t* ipm_
 int mpcc_solve(mpcc_engine* e, int B, double* x0, const double* u0, const double* obs, double* u0_out, double* horizon_out,
                int32_t* status, int32_t* ok, mpcc_timing* timing) {
     if (!e || B < 1 || B > e->maxB || !x0 || !u0 || !obs) return fail(MPCC_E_INVALID, "mpcc_solve: invalid argument");
+    DevGuard dg_(e);
     if (!e->has_track) return fail(MPCC_E_NOTRACK, "mpcc_solve: set_track first");
     if (e->spl.stride && B > e->n_tracks) return fail(MPCC_E_INVALID, "mpcc_solve: more instances than per-instance tracks");
     try {
+        quiesce(e);
         hipStream_t st = e->stream;
         const size_t NS = e->N + 1;
         HIPCHK(hipMemcpyAsync(e->s_x0, x0, B * 9 * sizeof(double), hipMemcpyHostToDevice, st));
@@ -756,8 +810,10 @@ int mpcc_solve_ocp(mpcc_engine* e, int B, const double* guess, const double* u_c
     if (!e || B < 1 || B > e->maxB || !guess || !u_cur || !obs || !opt_sol)
         return fail(MPCC_E_INVALID, "mpcc_solve_ocp: invalid argument");
     if (!e->has_track) return fail(MPCC_E_NOTRACK, "mpcc_solve_ocp: set_track first");
+    DevGuard dg_(e);
     if (e->spl.stride && B > e->n_tracks) return fail(MPCC_E_INVALID, "mpcc_solve_ocp: more instances than per-instance tracks");
     try {
+        quiesce(e);
         hipStream_t st = e->stream;
         const size_t NS = e->N + 1;
         HIPCHK(hipMemcpyAsync(e->d.guess, guess, B * NS * 17 * sizeof(double), hipMemcpyHostToDevice, st));
@@ -781,6 +837,7 @@ int mpcc_closed_loop(mpcc_engine* e, int B, int steps, double* x0, double* u0, c
     if (!e || B < 1 || B > e->maxB || steps < 0 || !x0 || !u0 || !obs)
         return fail(MPCC_E_INVALID, "mpcc_closed_loop: invalid argument");
     if (!e->has_track) return fail(MPCC_E_NOTRACK, "mpcc_closed_loop: set_track first");
+    DevGuard dg_(e);
     if (e->spl.stride && B > e->n_tracks) return fail(MPCC_E_INVALID, "mpcc_closed_loop: more instances than per-instance tracks");
     std::vector<void*> owned;
     auto dev = [&](size_t bytes) { void* p = dmalloc<char>(bytes ? bytes : 1); owned.push_back(p); return p; };
@@ -788,6 +845,7 @@ int mpcc_closed_loop(mpcc_engine* e, int B, int steps, double* x0, double* u0, c
     hipGraphExec_t exec = nullptr;
     int rc = MPCC_OK;
     try {
+        quiesce(e);
         hipStream_t st = e->stream;
         double* dx = (double*)dev((size_t)B * 9 * 8);
         double* du = (double*)dev((size_t)B * 8 * 8);
@@ -842,7 +900,9 @@ int mpcc_closed_loop(mpcc_engine* e, int B, int steps, double* x0, double* u0, c
 
 int mpcc_sim_time_step(mpcc_engine* e, int B, const double* x, const double* u, double ts, double* x_next) {
     if (!e || B < 1 || !x || !u || !x_next) return fail(MPCC_E_INVALID, "mpcc_sim_time_step: invalid argument");
+    DevGuard dg_(e);
     try {
+        quiesce(e);
         double* dx = dmalloc<double>((size_t)B * 9);
         double* du = dmalloc<double>((size_t)B * 8);
         double* dn = dmalloc<double>((size_t)B * 9);
@@ -862,7 +922,9 @@ int mpcc_sim_time_step(mpcc_engine* e, int B, const double* x, const double* u, 
 
 int mpcc_debug_robot_records(mpcc_engine* e, int M, const double* q, const double* obs, double* rec) {
     if (!e || M < 1 || !q || !obs || !rec) return fail(MPCC_E_INVALID, "mpcc_debug_robot_records: invalid argument");
+    DevGuard dg_(e);
     try {
+        quiesce(e);
         double* dq = dmalloc<double>((size_t)M * 7);
         double* dob = dmalloc<double>((size_t)M * 4);
         double* drec = dmalloc<double>((size_t)M * REC);
@@ -890,9 +952,11 @@ int mpcc_debug_robot_records(mpcc_engine* e, int M, const double* q, const doubl
 
 int mpcc_debug_project(mpcc_engine* e, int M, const double* s_guess, const double* ee, double* s_out) {
     if (!e || M < 1 || !s_guess || !ee || !s_out) return fail(MPCC_E_INVALID, "mpcc_debug_project: invalid argument");
+    DevGuard dg_(e);
     if (!e->has_track) return fail(MPCC_E_NOTRACK, "mpcc_debug_project: no track");
     double *dg = nullptr, *de = nullptr, *dout = nullptr;
     try {
+        quiesce(e);
         dg = dmalloc<double>(M);
         de = dmalloc<double>((size_t)M * 3);
         dout = dmalloc<double>(M);
@@ -912,8 +976,10 @@ int mpcc_debug_project(mpcc_engine* e, int M, const double* s_guess, const doubl
 
 int mpcc_debug_spline(mpcc_engine* e, int M, const double* s, double* pos, double* dd1, double* dd2, double* R, double* dR) {
     if (!e || M < 1 || !s) return fail(MPCC_E_INVALID, "mpcc_debug_spline: invalid argument");
+    DevGuard dg_(e);
     if (!e->has_track) return fail(MPCC_E_NOTRACK, "mpcc_debug_spline: no track");
     try {
+        quiesce(e);
         double* ds = dmalloc<double>(M);
         double* dout = dmalloc<double>((size_t)M * 21);
         HIPCHK(hipMemcpy(ds, s, M * sizeof(double), hipMemcpyHostToDevice));
@@ -944,8 +1010,10 @@ int mpcc_debug_spline(mpcc_engine* e, int M, const double* s, double* pos, doubl
 int mpcc_debug_stage_cost(mpcc_engine* e, int M, const double* x, const double* u, const double* rec, const int32_t* k,
                           double* obj, double* fx, double* fu, double* fxx, double* fuu) {
     if (!e || M < 1 || !x || !u || !rec || !k) return fail(MPCC_E_INVALID, "mpcc_debug_stage_cost: invalid argument");
+    DevGuard dg_(e);
     if (!e->has_track) return fail(MPCC_E_NOTRACK, "mpcc_debug_stage_cost: no track");
     try {
+        quiesce(e);
         const int W = 1 + 9 + 8 + 81 + 64;
         double* dx = dmalloc<double>((size_t)M * 9);
         double* du = dmalloc<double>((size_t)M * 8);
@@ -986,8 +1054,10 @@ int mpcc_debug_solve_qp(mpcc_engine* e, int B, const double* guess, const double
     if (!e || B < 1 || B > e->maxB || !guess || !rec || !u_cur)
         return fail(MPCC_E_INVALID, "mpcc_debug_solve_qp: invalid argument");
     if (!e->has_track) return fail(MPCC_E_NOTRACK, "mpcc_debug_solve_qp: no track");
+    DevGuard dg_(e);
     if (e->spl.stride && B > e->n_tracks) return fail(MPCC_E_INVALID, "mpcc_debug_solve_qp: more instances than per-instance tracks");
     try {
+        quiesce(e);
         hipStream_t st = e->stream;
         const int N = e->N;
         const size_t NS = N + 1, S = (size_t)B * NS;
@@ -1030,7 +1100,9 @@ int mpcc_debug_solve_qp(mpcc_engine* e, int B, const double* guess, const double
 
 int mpcc_debug_trace_enable(mpcc_engine* e, int enable) {
     if (!e) return fail(MPCC_E_INVALID, "mpcc_debug_trace_enable: null engine");
+    DevGuard dg_(e);
     try {
+        quiesce(e);
         if (enable && !e->d.dbg_trace) e->d.dbg_trace = dmalloc<double>((size_t)e->cfg.max_batch * TRACE_IT * TRACE_W);
         if (!enable && e->d.dbg_trace) { HIPCHK(hipFree(e->d.dbg_trace)); e->d.dbg_trace = nullptr; }
     } catch (const std::exception& x) {
@@ -1042,6 +1114,7 @@ int mpcc_debug_trace_enable(mpcc_engine* e, int enable) {
 int mpcc_debug_trace_get(mpcc_engine* e, int B, double* out) {
     if (!e || !out || B < 1 || B > e->cfg.max_batch || !e->d.dbg_trace)
         return fail(MPCC_E_INVALID, "mpcc_debug_trace_get: invalid argument or trace disabled");
+    DevGuard dg_(e);
     try {
         HIPCHK(hipDeviceSynchronize());
         HIPCHK(hipMemcpy(out, e->d.dbg_trace, sizeof(double) * B * TRACE_IT * TRACE_W, hipMemcpyDeviceToHost));
@@ -1053,6 +1126,7 @@ int mpcc_debug_trace_get(mpcc_engine* e, int B, double* out) {
 
 int mpcc_debug_workspace(mpcc_engine* e, int B, double* out) {
     if (!e || !out || B < 1 || B > e->cfg.max_batch) return fail(MPCC_E_INVALID, "mpcc_debug_workspace: invalid argument");
+    DevGuard dg_(e);
     try {
         HIPCHK(hipDeviceSynchronize());
         HIPCHK(hipMemcpy(out, e->d.is, sizeof(double) * (size_t)B * (e->N + 1) * IS, hipMemcpyDeviceToHost));

@@ -19,10 +19,22 @@ def shard_bounds(n_total: int, rank: int, world: int):
     return start, count
 
 
+def check_equal_shards(n_local: int, device=None, group=None) -> None:
+    """gather_u0 concatenates equal blocks: raise on every rank unless all ranks hold n_local instances
+    (shard_bounds gives unequal blocks when the total is not a multiple of the world size)."""
+    t = torch.tensor([n_local, -n_local], dtype=torch.int64, device=device)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX, group=group)
+    if int(t[0]) != n_local or int(-t[1]) != n_local:
+        raise ValueError(f"unequal shards: instances per rank range over [{int(-t[1])}, {int(t[0])}]")
+
+
 def gather_u0(u_local: torch.Tensor, world: int, out: torch.Tensor = None, group=None) -> torch.Tensor:
-    """All-gather equal-size per-rank u0 blocks [B_local, 8] -> [world * B_local, 8] on every rank."""
+    """All-gather equal-size per-rank u0 blocks [B_local, 8] -> [world * B_local, 8] on every rank
+    (check the sizes once with check_equal_shards)."""
     if world == 1:
         return u_local
+    if out is not None and out.shape[0] != world * u_local.shape[0]:
+        raise ValueError(f"gather_u0: out has {out.shape[0]} rows, expected {world} x {u_local.shape[0]}")
     if out is None:
         out = torch.empty((world * u_local.shape[0],) + tuple(u_local.shape[1:]), dtype=u_local.dtype,
                           device=u_local.device)

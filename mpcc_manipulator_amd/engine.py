@@ -268,6 +268,7 @@ class Engine:
         self.h = h
         self.N = int(params.N)
         self.max_batch = int(max_batch)
+        self.device = int(device)
 
     def close(self):
         if getattr(self, "h", None):
@@ -382,18 +383,51 @@ class Engine:
                "mpcc_solve_ocp")
         return dict(opt_sol=sol, status=st, solved=ok)
 
+    def _dev_ptr(self, t, name, dtype, shape, required=False):
+        """data_ptr() of a device tensor after checking what the kernels assume of it: dtype, this
+        engine's device, contiguity and (leading) shape.  A wrong tensor would otherwise make the
+        kernels read or write out of bounds in HBM."""
+        import torch
+        if t is None:
+            if required:
+                raise MpccError(f"{name} is required")
+            return None
+        if not isinstance(t, torch.Tensor):
+            raise MpccError(f"{name}: expected a torch tensor on the device, got {type(t).__name__}")
+        if t.dtype != dtype:
+            raise MpccError(f"{name}: dtype {t.dtype}, expected {dtype}")
+        if t.device.type != "cuda" or t.device.index != self.device:
+            raise MpccError(f"{name}: on {t.device}, the engine is on cuda:{self.device}")
+        if not t.is_contiguous():
+            raise MpccError(f"{name}: not contiguous")
+        if tuple(t.shape[:len(shape)]) != tuple(shape) or t.numel() != int(np.prod(shape)):
+            raise MpccError(f"{name}: shape {tuple(t.shape)}, expected {tuple(shape)}")
+        return C.c_void_p(t.data_ptr())
+
     def solve_device(self, B, x0, u0, obs, u_out=None, horizon=None, status=None, ok=None, stream=None):
         """Batched runMPC_ on device-resident torch tensors (float64 / int32), asynchronous on 'stream'."""
-        ptr = lambda t: C.c_void_p(t.data_ptr()) if t is not None else None
+        import torch
+        B = int(B)
+        if not 1 <= B <= self.max_batch:
+            raise MpccError(f"B = {B} outside [1, {self.max_batch}]")
+        f64, i32 = torch.float64, torch.int32
+        a = [self._dev_ptr(x0, "x0", f64, (B, 9), True), self._dev_ptr(u0, "u0", f64, (B, 8), True),
+             self._dev_ptr(obs, "obs", f64, (B, 4), True), self._dev_ptr(u_out, "u_out", f64, (B, 8)),
+             self._dev_ptr(horizon, "horizon", f64, (B, self.N + 1, 17)), self._dev_ptr(status, "status", i32, (B,)),
+             self._dev_ptr(ok, "ok", i32, (B,))]
         s = C.c_void_p(stream.cuda_stream) if stream is not None else None
-        _check(self.L.mpcc_solve_device(self.h, int(B), ptr(x0), ptr(u0), ptr(obs), ptr(u_out), ptr(horizon),
-                                        ptr(status), ptr(ok), s), "mpcc_solve_device")
+        _check(self.L.mpcc_solve_device(self.h, B, *a, s), "mpcc_solve_device")
 
     def set_warmstart_device(self, B, guess, valid, fails, stream=None):
-        ptr = lambda t: C.c_void_p(t.data_ptr()) if t is not None else None
+        """Device-to-device warm start of instances [0, B) (float64 guess [B, N+1, 17], int32 valid/fails)."""
+        import torch
+        B = int(B)
+        if not 0 <= B <= self.max_batch:
+            raise MpccError(f"B = {B} outside [0, {self.max_batch}]")
+        a = [self._dev_ptr(guess, "guess", torch.float64, (B, self.N + 1, 17)),
+             self._dev_ptr(valid, "valid", torch.int32, (B,)), self._dev_ptr(fails, "fails", torch.int32, (B,))]
         s = C.c_void_p(stream.cuda_stream) if stream is not None else None
-        _check(self.L.mpcc_set_warmstart_device(self.h, int(B), ptr(guess), ptr(valid), ptr(fails), s),
-               "mpcc_set_warmstart_device")
+        _check(self.L.mpcc_set_warmstart_device(self.h, B, *a, s), "mpcc_set_warmstart_device")
 
     def timing_begin(self):
         _check(self.L.mpcc_timing_begin(self.h), "mpcc_timing_begin")

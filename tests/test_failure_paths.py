@@ -1,0 +1,181 @@
+"""Failure paths of solveOCP / runMPC_ driven on purpose, engine (through the C ABI) vs the oracle.
+
+Reference behaviour under test:
+  * isPosdef before isNan on the (normalized) Hessian: NON_PD_HESSIAN / NAN_HESSIAN end the SQP at
+    once (osqp_interface.cpp:454-473, Eigen LLT: a NaN pivot is not <= 0, so a NaN Hessian passes
+    isPosdef and is caught by isNan);
+  * a QP that fails keeps the old step and the loop goes on (Q6, :479-505, 540-551);
+  * any non-SOLVED exit returns the zero guess — x0 repeated, u = 0 (Q7, :422-428, 585-589);
+  * runMPC_'s bookkeeping: valid = false and fails + 1 on a failure, fails = 0 on success, and the
+    return value SOLVED || (MAX_ITER_EXCEEDED && fails < 5) (mpc.cpp:140-189) — it turns false at the
+    5th consecutive MAX_ITER_EXCEEDED.
+Each case is a parameter set a user can load (a cost weight ParamValue, an SQP setting, a bounds
+file), applied identically to the engine and the oracle.
+"""
+import numpy as np
+import pytest
+
+from helpers import SEED, batch_from_pool, make_oracle, oracle_pool
+
+pytestmark = pytest.mark.gpu
+
+NAN_HESSIAN, NON_PD_HESSIAN, MAX_ITER_EXCEEDED, QP_PRIMAL_INFEASIBLE = 10, 11, 1, 6
+
+
+@pytest.fixture(scope="module")
+def base(built_lib, oracle_lib):
+    o, P, track = make_oracle(N=20, max_iter=2, mask=2)
+    pool = oracle_pool(o, 60)
+    return o, P, track, pool
+
+
+def _pair(base, overrides=None, bounds=None, B=48, seed=0):
+    """Engine + oracle with the same effective parameters and the same batch."""
+    import mpcc_manipulator_amd as m
+    o0, P0, track, pool = base
+    ov = {"sqp": {"max_iter": 2}}
+    for k, v in (overrides or {}).items():
+        ov.setdefault(k, {}).update(v)
+    o, P, _ = make_oracle(N=20, max_iter=None, mask=2, overrides=ov)
+    params = m.load_params(N=20, overrides=ov)
+    if bounds:  # a bounds file with other values (BoundsParam is read from the file, osqp_interface.cpp:54)
+        for key, idx, val in bounds:
+            getattr(params, key)[idx] = val
+            P[key][idx] = val
+        o.set_params(P)
+    eng = m.Engine(params, max_batch=B, constraint_mask=2)
+    eng.set_track(*track)
+    rng = np.random.default_rng(SEED + 900 + seed)
+    x0, u0, obs, guess, valid, fails = batch_from_pool(pool, B, rng)
+    return eng, o, (x0, u0, obs, guess, valid, fails)
+
+
+def _step(eng, o, x0, u0, obs, go, vo, fo, trace=False):
+    """One runMPC_ on both sides from the same controller state; returns both outputs + states."""
+    B = x0.shape[0]
+    if trace:
+        eng.trace_enable(True)
+    eng.set_warmstart(go, vo, fo)
+    xg = x0.copy()
+    outg = eng.solve(xg, u0, obs)
+    gg, vg, fg = eng.get_warmstart(B)
+    trg = eng.trace_get(B) if trace else None
+    xo, g2, v2, f2 = x0.copy(), go.copy(), vo.copy(), fo.copy()
+    outo = o.run_mpc(xo, u0, obs, g2, v2, f2, trace=trace)
+    return (xg, outg, gg, vg, fg, trg), (xo, outo, g2, v2, f2)
+
+
+def _assert_same(g, r, zero_guess_status):
+    xg, outg, gg, vg, fg, _ = g
+    xo, outo, go, vo, fo = r
+    assert np.array_equal(outg["status"], outo["status"]), (outg["status"], outo["status"])
+    assert np.array_equal(outg["ok"], outo["ok"])
+    assert np.array_equal(vg, vo) and np.array_equal(fg, fo)
+    assert np.abs(xg - xo).max() <= 1e-9
+    bad = np.isin(outg["status"], zero_guess_status)
+    assert bad.any()
+    # Q7: the zero guess — x0 (as runMPC_ updated it) on every stage, u = 0
+    hb = outg["horizon"][bad]
+    assert np.array_equal(hb[:, :, 9:], np.zeros_like(hb[:, :, 9:]))
+    assert np.array_equal(hb[:, :, :9], np.repeat(xg[bad][:, None, :], hb.shape[1], axis=1))
+    assert np.array_equal(outg["u0"][bad], np.zeros_like(outg["u0"][bad]))
+    assert np.abs(outg["horizon"] - outo["horizon"]).max() <= 1e-6
+
+
+def test_nan_hessian(base):
+    """A NaN cost weight (ParamValue cost qC = NaN) makes every stage Hessian NaN: NAN_HESSIAN at the
+    first SQP iteration, zero guess, runMPC_ false, valid = false, fails + 1."""
+    eng, o, (x0, u0, obs, guess, valid, fails) = _pair(base, overrides={"cost": {"qC": float("nan")}})
+    g, r = _step(eng, o, x0, u0, obs, guess, valid, fails)
+    _assert_same(g, r, [NAN_HESSIAN])
+    assert np.all(g[1]["status"] == NAN_HESSIAN)
+    assert np.all(g[1]["ok"] == 0) and np.all(g[3] == 0) and np.array_equal(g[4], fails + 1)
+    eng.close()
+
+
+def test_non_pd_hessian(base):
+    """A negative input weight (ParamValue cost rdq < 0 beyond the ddq-rate term) makes the input block
+    of the Hessian indefinite: NON_PD_HESSIAN, zero guess, runMPC_ false."""
+    eng, o, (x0, u0, obs, guess, valid, fails) = _pair(base, overrides={"cost": {"rdq": -50.0}})
+    g, r = _step(eng, o, x0, u0, obs, guess, valid, fails)
+    _assert_same(g, r, [NON_PD_HESSIAN])
+    assert np.all(g[1]["status"] == NON_PD_HESSIAN)
+    assert np.all(g[1]["ok"] == 0) and np.array_equal(g[4], fails + 1)
+    eng.close()
+
+
+def test_infeasible_bounds_keep_old_step(base):
+    """A bounds file whose joint-1 interval is empty (q1 lower > upper) makes every QP primal
+    infeasible.  The reference keeps the old (zero) step (Q6), the filter accepts it and the
+    zero step norm ends the SQP as SOLVED with the warm start unchanged; the QP status of each SQP
+    iteration is QP_PrimalInfeasible on both sides."""
+    eng, o, (x0, u0, obs, guess, valid, fails) = _pair(base, bounds=[("lx", 0, 1.0), ("ux", 0, -1.0)])
+    g, r = _step(eng, o, x0, u0, obs, guess, valid, fails, trace=True)
+    xg, outg, gg, vg, fg, trg = g
+    xo, outo, go, vo, fo = r
+    assert np.array_equal(outg["status"], outo["status"])
+    assert np.array_equal(outg["ok"], outo["ok"]) and np.array_equal(vg, vo) and np.array_equal(fg, fo)
+    assert np.abs(outg["horizon"] - outo["horizon"]).max() <= 1e-6
+    # first SQP iteration's QP status (trace column 0) on both sides
+    assert np.array_equal(trg[:, 0, 0], outo["trace"][:, 0, 0])
+    assert np.all(trg[:, 0, 0] == QP_PRIMAL_INFEASIBLE)
+    eng.close()
+
+
+def test_max_iter_fail_counter_and_return_rule(base):
+    """eps_prim = 0 (no step norm is < 0) makes every solve end MAX_ITER_EXCEEDED.  Six consecutive
+    runMPC_ calls on the same controllers: zero guess every time, fails 1..6, and the return value true
+    while fails < 5, false from the 5th consecutive failure on (mpc.cpp:188)."""
+    eng, o, (x0, u0, obs, guess, valid, fails) = _pair(base, overrides={"sqp": {"eps_prim": 0.0}}, B=32, seed=1)
+    fails = np.zeros_like(fails)
+    go, vo, fo = guess.copy(), valid.copy(), fails.copy()
+    x, u = x0.copy(), u0.copy()
+    oks = []
+    for step in range(6):
+        g, r = _step(eng, o, x, u, obs, go, vo, fo)
+        _assert_same(g, r, [MAX_ITER_EXCEEDED])
+        assert np.all(g[1]["status"] == MAX_ITER_EXCEEDED)
+        assert np.all(g[4] == step + 1), (step, g[4])
+        oks.append(g[1]["ok"].copy())
+        # carry the controller state, as the closed loop does
+        xo, outo, go, vo, fo = r
+        x, u = xo, outo["u0"]
+    oks = np.array(oks)
+    assert np.all(oks[:4] == 1) and np.all(oks[4:] == 0), oks[:, 0]
+    eng.close()
+
+
+def test_scaled_start_restart_matches_oracle(base):
+    """The IPM restart from the unit start point: QPs of an instance set whose scaled
+    attempt fails (IPM iteration cap at the scaled start) are solved again from s = 1, lambda = 1.  The
+    engine's QP status, IPM iteration count (both attempts) and step match the oracle's
+    solve_struct_ipm on heavily perturbed linearization points."""
+    import mpcc_manipulator_amd as m
+    o, P, track, pool = base
+    eng = m.Engine(m.load_params(N=20, overrides={"sqp": {"max_iter": 2}}), max_batch=64, constraint_mask=2)
+    eng.set_track(*track)
+    rng = np.random.default_rng(SEED + 77)
+    N = o.N
+    B = 64
+    T = len(pool["x0"])
+    guess = np.zeros((B, N + 1, 17)); recs = np.zeros((B, N + 1, 143)); ucur = np.zeros((B, 8))
+    for b in range(B):
+        t = 3 + (b * 5) % (T - 4)
+        gs = pool["guess"][t + 1].copy()
+        gs[:, :7] += rng.normal(0, 0.4, (N + 1, 7))  # oracle: 45 of 64 QPs converge only after the restart
+        gs[:N, 9:] += rng.normal(0, 0.2, (N, 8))
+        guess[b] = gs
+        ucur[b] = pool["u0"][t + 1]
+        for k in range(N + 1):
+            recs[b, k] = o.robot_record(gs[k, :7])
+    step, st, it = eng.solve_qp(guess, recs, ucur)
+    restarted = 0
+    for b in range(B):
+        rc, so, ito = o.solve_qp(guess[b], recs[b], ucur[b], mode=0)
+        assert st[b] == rc, (b, st[b], rc)
+        assert it[b] == ito, (b, it[b], ito)
+        restarted += int(ito > 30 and rc == 0)
+        if rc == 0:
+            assert np.max(np.abs(step[b] - so)) < 1e-8, b
+    assert restarted > 0, "no QP took the restart; perturb harder"
+    eng.close()

@@ -154,6 +154,7 @@ def test_qp_step(setup20, scale):
     for b in range(B):
         rc, so, ito = o.solve_qp(guess[b], recs[b], ucur[b], mode=0)
         assert st[b] == rc, (b, st[b], rc)
+        assert it[b] == ito, (b, it[b], ito)  # IPM iterations of both attempts (scaled start + restart)
         if rc == 0:
             assert np.max(np.abs(step[b] - so)) < 1e-8, (b, np.max(np.abs(step[b] - so)))
 
