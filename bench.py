@@ -222,14 +222,17 @@ def main():
     status = torch.empty(B, dtype=torch.int32, device=dev)
     ok = torch.empty(B, dtype=torch.int32, device=dev)
     u_all = torch.empty((world * B, 8), dtype=torch.float64, device=dev) if world > 1 else None
-    stream = torch.cuda.current_stream(dev)
+    # One dedicated stream carries the whole step: the x0 restore, the engine's kernels and the u0
+    # gather (RCCL waits on the current stream), so every step reads the inputs it restored.
+    stream = torch.cuda.Stream(dev)
 
     def step():
-        x0_d.copy_(x0_p)
-        eng.set_warmstart_device(B, g_p, v_p, f_p, stream=stream)
-        eng.solve_device(B, x0_d, u0_d, obs_d, u_out, hor, status, ok, stream=stream)
-        if world > 1:
-            gather_u0(u_out, world, out=u_all)  # RCCL all-gather of u0 over xGMI
+        with torch.cuda.stream(stream):
+            x0_d.copy_(x0_p)
+            eng.set_warmstart_device(B, g_p, v_p, f_p, stream=stream)
+            eng.solve_device(B, x0_d, u0_d, obs_d, u_out, hor, status, ok, stream=stream)
+            if world > 1:
+                gather_u0(u_out, world, out=u_all)  # RCCL all-gather of u0 over xGMI
 
     if world > 1:
         check_equal_shards(B, device=dev)

@@ -418,7 +418,10 @@ int mpcc_create(const mpcc_config* cfg, const mpcc_params* params, const char* n
         e->N = cfg->N;
         e->maxB = cfg->max_batch;
         HIPCHK(hipSetDevice(cfg->device));
-        HIPCHK(hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking));
+        // A blocking stream: work a caller queues on the legacy default stream (torch's default
+        // stream, or any NULL-stream copy of the inputs) is ordered before and after the engine's
+        // kernels, as the ABI's "NULL = engine stream" would otherwise race with it.
+        HIPCHK(hipStreamCreateWithFlags(&e->stream, hipStreamDefault));
         const size_t B = (size_t)e->maxB, NS = (size_t)e->N + 1;
         DevBuffers& d = e->d;
         d.guess = dmalloc<double>(B * NS * 17);

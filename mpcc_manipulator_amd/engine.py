@@ -89,6 +89,14 @@ def lib():
         return _lib
     if not os.path.exists(LIB_PATH):
         raise MpccError(f"libmpcc_engine.so not built ({LIB_PATH}); run python -m mpcc_manipulator_amd._build")
+    # One HIP runtime per process.  torch ships its own libamdhip64 (SONAME libamdhip64.so.7, loaded by
+    # the unversioned name libamdhip64.so).  Loaded first, it satisfies the engine's libamdhip64.so.7
+    # dependency; loaded after the engine had pulled in /opt/rocm's copy, it would be a second runtime
+    # in the process and torch.cuda fails to initialise ("No HIP GPUs are available").
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
     L = C.CDLL(LIB_PATH)
     V = C.c_void_p
     sig = {
@@ -404,8 +412,19 @@ class Engine:
             raise MpccError(f"{name}: shape {tuple(t.shape)}, expected {tuple(shape)}")
         return C.c_void_p(t.data_ptr())
 
+    def _stream_handle(self, stream):
+        """The torch stream the call is ordered on: 'stream', else torch's current stream on the engine's
+        device.  torch's default stream has handle 0, which the ABI reads as the engine's stream; that
+        stream is a blocking stream, so it is ordered with the default stream's work."""
+        import torch
+        if stream is None:
+            stream = torch.cuda.current_stream(self.device)
+        h = stream.cuda_stream
+        return C.c_void_p(h) if h else None
+
     def solve_device(self, B, x0, u0, obs, u_out=None, horizon=None, status=None, ok=None, stream=None):
-        """Batched runMPC_ on device-resident torch tensors (float64 / int32), asynchronous on 'stream'."""
+        """Batched runMPC_ on device-resident torch tensors (float64 / int32), asynchronous on 'stream'
+        (default: torch's current stream)."""
         import torch
         B = int(B)
         if not 1 <= B <= self.max_batch:
@@ -415,7 +434,7 @@ class Engine:
              self._dev_ptr(obs, "obs", f64, (B, 4), True), self._dev_ptr(u_out, "u_out", f64, (B, 8)),
              self._dev_ptr(horizon, "horizon", f64, (B, self.N + 1, 17)), self._dev_ptr(status, "status", i32, (B,)),
              self._dev_ptr(ok, "ok", i32, (B,))]
-        s = C.c_void_p(stream.cuda_stream) if stream is not None else None
+        s = self._stream_handle(stream)
         _check(self.L.mpcc_solve_device(self.h, B, *a, s), "mpcc_solve_device")
 
     def set_warmstart_device(self, B, guess, valid, fails, stream=None):
@@ -426,7 +445,7 @@ class Engine:
             raise MpccError(f"B = {B} outside [0, {self.max_batch}]")
         a = [self._dev_ptr(guess, "guess", torch.float64, (B, self.N + 1, 17)),
              self._dev_ptr(valid, "valid", torch.int32, (B,)), self._dev_ptr(fails, "fails", torch.int32, (B,))]
-        s = C.c_void_p(stream.cuda_stream) if stream is not None else None
+        s = self._stream_handle(stream)
         _check(self.L.mpcc_set_warmstart_device(self.h, B, *a, s), "mpcc_set_warmstart_device")
 
     def timing_begin(self):
