@@ -219,6 +219,26 @@ int mpcc_closed_loop(mpcc_engine* e, int B, int steps, double* x0, double* u0, c
 /* Integrator::simTimeStep (integrator.cpp:55-68) for B states, host arrays (closed-loop driver). */
 int mpcc_sim_time_step(mpcc_engine* e, int B, const double* x, const double* u, double ts, double* x_next);
 
+/* ---- stand-alone objects of the reference's Python surface (MPCC_wrapper.cpp:254-347) ---- */
+/* SelCollNNmodel / EnvCollNNmodel (SelfCollisionModel.cpp / EnvCollisionModel.cpp:75-250): setNeuralNetwork(
+ * n_input, n_output, n_hidden, is_nerf) with the weights of dir (weight_l / bias_l as this repo's .f64 or the
+ * reference's .txt), and calculateMlpOutput for M inputs on the GPU: out [M*n_output] and the full Jacobian
+ * jac [M*n_output*n_input] (row-major; may be NULL).  At most 16 inputs and 7 hidden layers. */
+typedef struct mpcc_mlp mpcc_mlp;
+int  mpcc_mlp_create(int device, const char* dir, int n_input, int n_output, const int32_t* n_hidden, int n_layers_hidden,
+                     int is_nerf, mpcc_mlp** out);
+int  mpcc_mlp_eval(mpcc_mlp* m, int M, const double* in, double* out, double* jac);
+int  mpcc_mlp_dims(mpcc_mlp* m, int32_t* n_input, int32_t* n_output);
+void mpcc_mlp_destroy(mpcc_mlp* m);
+/* RobotModel::getPosition / getOrientation / getJacobian / getManipulability / getDManipulability with a frame_id
+ * (robot_model.cpp:354-450; frame 1 = panda_link0, 2..8 = panda_link1..7, 9 = panda_hand_tcp) for M joint vectors
+ * q [M*7] on GPU 'device': pos [M*3], R [M*9], J [M*42] (rows Jv; Jw), mani [M], dmani [M*7]; any may be NULL. */
+int  mpcc_robot_frames(int device, int M, const double* q, int frame_id, double* pos, double* R, double* J, double* mani,
+                       double* dmani);
+/* LogMatrix / ExpMatrix (cubic_spline_rot.cpp:44-95, quirks Q10/Q11), host only: 3x3 row-major */
+int  mpcc_so3_log(const double* R9, double* S9);
+int  mpcc_so3_exp(const double* S9, double* R9);
+
 /* ---- stage-level entry points for parity tests (host arrays) ---- */
 #define MPCC_REC_SIZE 143
 /* RobotData::update + updateEnv (robot_data.h:55-88) for M joint vectors q[M*7], obs[M*4] */

@@ -12,13 +12,13 @@ CSRC = os.path.join(PKG, "csrc")
 PROF = os.environ.get("MPCC_PROF_BUILD", "0") == "1"  # cycle-accounting variant (tools/ipm_prof.py)
 BUILD = os.path.join(PKG, "_build_prof" if PROF else "_build")
 LIB = os.path.join(BUILD, "libmpcc_engine.so")
-SOURCES = ["kernels.hip", "ipm.hip", "mlp.hip", "engine.cpp", "host_params.cpp", "host_spline.cpp", "mpc.cpp"]
+SOURCES = ["kernels.hip", "ipm.hip", "mlp.hip", "nn_generic.hip", "engine.cpp", "host_params.cpp", "host_spline.cpp", "mpc.cpp"]
 ARCH = os.environ.get("MPCC_OFFLOAD_ARCH", "gfx950")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 # The stage kernels (projection, kinematics, records, QP assembly, line-search trials) follow the
 # oracle's operation order without FMA contraction, so their discrete decisions (projection Newton,
 # warm-start validity, filter comparisons) see the same values as the reference CPU arithmetic.
-FILE_FLAGS = {"kernels.hip": ["-ffp-contract=off"], "mlp.hip": ["-ffp-contract=off"]}
+FILE_FLAGS = {"kernels.hip": ["-ffp-contract=off"], "mlp.hip": ["-ffp-contract=off"], "nn_generic.hip": ["-ffp-contract=off"]}
 CFLAGS = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-I", os.path.join(ROOT, "include"),
           "-I", CSRC, "-Wno-unused-result"] + (["-DMPCC_IPM_PROF"] if PROF else [])
 

@@ -92,6 +92,60 @@ __device__ inline void panda_fk(const double* q, double* pos, double* Rout, doub
     }
 }
 
+// Frame of RobotModel::getPosition/getOrientation/getJacobian(frame_id) (robot_model.cpp:354-398,
+// body_id_ at :310-319): 1 = panda_link0 (the base), 2..8 = panda_link1..7 (origin after joint f-1),
+// 9 = panda_hand_tcp (= panda_fk).  J is the 6x7 point Jacobian at the frame origin, zero columns for
+// the joints after the frame.  Any output may be null.
+__device__ inline void panda_frame(const double* q, int frame, double* pos, double* Rout, double* J) {
+    if (frame >= 9) {
+        double Jt[42];
+        panda_fk(q, pos, Rout, Jt, J != nullptr);
+        if (J)
+            for (int a = 0; a < 42; a++) J[a] = Jt[a];
+        return;
+    }
+    double Rc[9] = {1, 0, 0, 0, 1, 0, 0, 0, 1};
+    double pc[3] = {0, 0, 0};
+    double z[7][3], o[7][3];
+    const int nj = frame - 1;  // joints that move the frame
+    for (int i = 1; i <= nj; i++) {
+        double r[3], E[9], Rt[9];
+        joint_offset(i, r);
+        pc[0] += Rc[0] * r[0] + Rc[1] * r[1] + Rc[2] * r[2];
+        pc[1] += Rc[3] * r[0] + Rc[4] * r[1] + Rc[5] * r[2];
+        pc[2] += Rc[6] * r[0] + Rc[7] * r[1] + Rc[8] * r[2];
+        joint_fixed_rot(i, E);
+        m3mul(Rc, E, Rt);
+        z[i - 1][0] = Rt[2]; z[i - 1][1] = Rt[5]; z[i - 1][2] = Rt[8];
+        o[i - 1][0] = pc[0]; o[i - 1][1] = pc[1]; o[i - 1][2] = pc[2];
+        double s, c;
+        sincos(q[i - 1], &s, &c);
+        for (int a = 0; a < 3; a++) {
+            const double r0 = Rt[3 * a], r1 = Rt[3 * a + 1];
+            Rc[3 * a] = r0 * c + r1 * s;
+            Rc[3 * a + 1] = -r0 * s + r1 * c;
+            Rc[3 * a + 2] = Rt[3 * a + 2];
+        }
+    }
+    if (pos) { pos[0] = pc[0]; pos[1] = pc[1]; pos[2] = pc[2]; }
+    if (Rout)
+        for (int a = 0; a < 9; a++) Rout[a] = Rc[a];
+    if (J)
+        for (int i = 0; i < 7; i++) {
+            if (i < nj) {
+                const double r0 = pc[0] - o[i][0], r1 = pc[1] - o[i][1], r2 = pc[2] - o[i][2];
+                J[0 * 7 + i] = z[i][1] * r2 - z[i][2] * r1;
+                J[1 * 7 + i] = z[i][2] * r0 - z[i][0] * r2;
+                J[2 * 7 + i] = z[i][0] * r1 - z[i][1] * r0;
+                J[3 * 7 + i] = z[i][0];
+                J[4 * 7 + i] = z[i][1];
+                J[5 * 7 + i] = z[i][2];
+            } else {
+                for (int a = 0; a < 6; a++) J[a * 7 + i] = 0.0;
+            }
+        }
+}
+
 // sqrt(det(J J^T)) with a partial-pivot LU of the 6x6 Gram matrix (robot_model.cpp:431-435;
 // Eigen's MatrixXd::determinant for n > 4 is PartialPivLU).
 __device__ inline double manip_from_J(const double* J) {

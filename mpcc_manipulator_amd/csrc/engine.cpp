@@ -156,8 +156,9 @@ namespace {
 
 // ---- NN weights: binary (manifest.json + *.f64, this repo's data/nn) or the reference's text files
 bool read_doubles_bin(const std::string& path, std::vector<double>& out, size_t n) {
-    std::ifstream f(path, std::ios::binary);
-    if (!f) return false;
+    std::ifstream f(path, std::ios::binary | std::ios::ate);
+    if (!f || (size_t)f.tellg() != n * sizeof(double)) return false;  // exactly rows x cols values
+    f.seekg(0);
     out.resize(n);
     f.read((char*)out.data(), (std::streamsize)(n * sizeof(double)));
     return (bool)f;
@@ -170,6 +171,23 @@ bool read_doubles_txt(const std::string& path, std::vector<double>& out, size_t 
         if (!(f >> out[i])) return false;  // operator>> as SelfCollisionModel.cpp:29
     return true;
 }
+
+}  // namespace
+
+// Layer l (R x C row-major W, b[R]) of a network under dir: <dir>/weight_l.f64 (this repo's binary
+// form), else the reference's text files <dir>/parameter/weight_l.txt or <dir>/weight_l.txt
+// (SelfCollisionModel.cpp:19-73).
+bool mpcc::nn_read_layer(const std::string& dir, int l, int R, int C, std::vector<double>& W, std::vector<double>& b) {
+    const std::string base = dir + "/", tb = base + "parameter/", ls = std::to_string(l);
+    return (read_doubles_bin(base + "weight_" + ls + ".f64", W, (size_t)R * C) &&
+            read_doubles_bin(base + "bias_" + ls + ".f64", b, R)) ||
+           (read_doubles_txt(tb + "weight_" + ls + ".txt", W, (size_t)R * C) &&
+            read_doubles_txt(tb + "bias_" + ls + ".txt", b, R)) ||
+           (read_doubles_txt(base + "weight_" + ls + ".txt", W, (size_t)R * C) &&
+            read_doubles_txt(base + "bias_" + ls + ".txt", b, R));
+}
+
+namespace {
 
 void load_nn(mpcc_engine* e, const std::string& dir, int nin, int nout, std::vector<int> hidden, NNWeights& w) {
     // k_mlp_self / k_mlp_env are specialized for the reference architectures (osqp_interface.cpp:35-43)
@@ -189,18 +207,7 @@ void load_nn(mpcc_engine* e, const std::string& dir, int nin, int nout, std::vec
     for (int l = 0; l < L; l++) {
         const int R = dims[l + 1], C = dims[l];
         std::vector<double> W, b;
-        std::string base = dir + "/";
-        bool ok = read_doubles_bin(base + "weight_" + std::to_string(l) + ".f64", W, (size_t)R * C) &&
-                  read_doubles_bin(base + "bias_" + std::to_string(l) + ".f64", b, R);
-        if (!ok) {  // reference layout: <dir>/parameter/weight_l.txt or <dir>/weight_l.txt
-            std::string tb = base + "parameter/";
-            ok = read_doubles_txt(tb + "weight_" + std::to_string(l) + ".txt", W, (size_t)R * C) &&
-                 read_doubles_txt(tb + "bias_" + std::to_string(l) + ".txt", b, R);
-            if (!ok)
-                ok = read_doubles_txt(base + "weight_" + std::to_string(l) + ".txt", W, (size_t)R * C) &&
-                     read_doubles_txt(base + "bias_" + std::to_string(l) + ".txt", b, R);
-        }
-        if (!ok) throw std::runtime_error("cannot read MLP layer " + std::to_string(l) + " under " + dir);
+        if (!nn_read_layer(dir, l, R, C, W, b)) throw std::runtime_error("cannot read MLP layer " + std::to_string(l) + " under " + dir);
         // MFMA fragment order (mlp.hip): [row tile t][k-step s][lane l] = W[16t + (l & 15)][4s + (l >> 4)],
         // zero-padded to 16-row tiles and 16-deep k-tiles; bias zero-padded to the row tiles
         const int RT = (R + 15) / 16, KS = 4 * ((C + 15) / 16);
@@ -400,6 +407,21 @@ void run_batch(mpcc_engine* e, int B, hipStream_t st, mpcc_timing* timing, bool 
 extern "C" {
 
 int mpcc_abi_version(void) { return MPCC_ABI_VERSION; }
+
+int mpcc_so3_log(const double* R9, double* S9) {
+    if (!R9 || !S9) return fail(MPCC_E_INVALID, "mpcc_so3_log: null argument");
+    double v[3];
+    host_log_vec(R9, v);
+    const double S[9] = {0, -v[2], v[1], v[2], 0, -v[0], -v[1], v[0], 0};
+    std::memcpy(S9, S, sizeof S);
+    return MPCC_OK;
+}
+
+int mpcc_so3_exp(const double* S9, double* R9) {
+    if (!S9 || !R9) return fail(MPCC_E_INVALID, "mpcc_so3_exp: null argument");
+    host_exp_matrix(S9, R9);
+    return MPCC_OK;
+}
 const char* mpcc_last_error(void) { return g_last_error.c_str(); }
 
 int mpcc_create(const mpcc_config* cfg, const mpcc_params* params, const char* nn_dir, mpcc_engine** out) {

@@ -381,4 +381,23 @@ double project_tables(const SplineTables& t, double proj_max_dist, double s_gues
     return s_guess;
 }
 
+// ExpMatrix(sk) (cubic_spline_rot.cpp:81-95): a zero matrix when sk is not skew-symmetric (the reference
+// prints an error and returns Zero), else Exp of invskew(sk) with quirk Q11
+void host_exp_matrix(const double* sk, double* E) {
+    double n1 = 0, n2 = 0;
+    for (int i = 0; i < 3; i++) {
+        for (int j = 0; j < 3; j++) {
+            const double a = sk[3 * j + i] + sk[3 * i + j];
+            n1 += a * a;
+        }
+        n2 += sk[4 * i] * sk[4 * i];
+    }
+    if (std::sqrt(n1) >= 1e-8 || std::sqrt(n2) >= 1e-8) {
+        for (int i = 0; i < 9; i++) E[i] = 0.0;
+        return;
+    }
+    const double v[3] = {sk[7], sk[2], sk[3]};  // getInverseSkewVector: (R21, R02, R10)
+    exp_skew(v, E);
+}
+
 }  // namespace mpcc

@@ -38,5 +38,6 @@ void quat_to_rot(double qx, double qy, double qz, double qw, double* R9);
 
 // host LogMatrix / ExpMatrix (cubic_spline_rot.cpp:44-95), exposed for tests
 void host_log_vec(const double* R, double* v);
+void host_exp_matrix(const double* sk, double* E);
 
 }  // namespace mpcc

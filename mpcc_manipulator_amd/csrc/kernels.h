@@ -2,9 +2,16 @@
 #pragma once
 #include <hip/hip_runtime.h>
 
+#include <string>
+#include <vector>
+
 #include "dev_common.h"
 
 namespace mpcc {
+
+// host: one layer of a collision network from disk (engine.cpp), and the thread's last-error message
+bool nn_read_layer(const std::string& dir, int l, int R, int C, std::vector<double>& W, std::vector<double>& b);
+void set_last_error(const std::string& m);
 
 struct DevBuffers {
     // per-call I/O (device)

@@ -195,28 +195,78 @@ struct PyMPC {
     }
 };
 
-// RobotModel (robot_model.cpp:366-450): kinematics records from the engine (one small engine)
+// RobotModel (robot_model.h:27-141, robot_model.cpp:354-450): frame kinematics on the GPU
+// (mpcc_robot_frames).  Like the reference object it keeps the joint vector of the last
+// getUpdateKinematics for the frame_id-only getters.
+constexpr int EE_FRAME = 9;  // PANDA_NUM_LINKS: panda_hand_tcp
 struct PyRobot {
-    std::unique_ptr<BatchMPC> eng;
-    PyRobot() {
-        PathToJson p;
-        p.merged_path = g_data + "/params/default_params.json";
-        eng.reset(new BatchMPC(1, 0.01, 1, p, ParamValue{}, 0, MPCC_CON_SING));
+    std::vector<double> q = std::vector<double>(7, 0.0), qdot = std::vector<double>(7, 0.0);
+    struct Frame {
+        double pos[3], R[9], J[42], mani, dmani[7];
+    };
+    Frame frame(const std::vector<double>& qv, int f) const {
+        Frame o;
+        check(mpcc_robot_frames(0, 1, qv.data(), f, o.pos, o.R, o.J, &o.mani, o.dmani), "RobotModel");
+        return o;
     }
-    std::vector<double> rec(const py::handle& q) {
-        const auto v = values(q, 7, "joint angles");
-        const double obs[4] = {3.0, 3.0, 3.0, 0.0};
-        std::vector<double> r(MPCC_REC_SIZE);
-        check(mpcc_debug_robot_records(eng->engine(), 1, v.data(), obs, r.data()), "RobotModel");
-        return r;
-    }
-    Arr jac(const py::handle& q, int row0, int rows) {
-        const auto r = rec(q);
+    Frame at(const py::handle& qh, int f) const { return frame(values(qh, 7, "joint angles"), f); }
+    static Arr jac(const Frame& fr, int row0, int rows) {
         Arr a({rows, 7});
         for (int i = 0; i < rows; i++)
-            for (int j = 0; j < 7; j++) a.mutable_data()[7 * i + j] = r[12 + 7 * (row0 + i) + j];
+            for (int j = 0; j < 7; j++) a.mutable_data()[7 * i + j] = fr.J[7 * (row0 + i) + j];
         return a;
     }
+    static Arr trans(const Frame& fr) {  // Affine3d as a 4x4 homogeneous matrix
+        Arr a({4, 4});
+        double* d = a.mutable_data();
+        for (int i = 0; i < 16; i++) d[i] = 0.0;
+        for (int i = 0; i < 3; i++) {
+            for (int j = 0; j < 3; j++) d[4 * i + j] = fr.R[3 * i + j];
+            d[4 * i + 3] = fr.pos[i];
+        }
+        d[15] = 1.0;
+        return a;
+    }
+    // getX(q) / getX(frame_id) / getX(q, frame_id) of the reference overload sets
+    Frame resolve(const py::object& a, const py::object& b) const {
+        if (a.is_none()) return frame(q, EE_FRAME);
+        const bool scalar = !py::isinstance<py::array>(a) && !py::isinstance<py::sequence>(a);  // int / numpy int
+        if (scalar && b.is_none()) return frame(q, a.cast<int>());
+        return at(a, b.is_none() ? EE_FRAME : b.cast<int>());
+    }
+};
+
+// SelCollNNmodel / EnvCollNNmodel (SelfCollisionModel.cpp / EnvCollisionModel.cpp): setNeuralNetwork loads a
+// network of any shape from the model path; calculateMlpOutput -> (output, Jacobian wrt every input)
+struct PyNN {
+    std::string path;
+    std::shared_ptr<mpcc_mlp> net;
+    int nin = 0, nout = 0;
+    explicit PyNN(std::string p) : path(std::move(p)) {}
+    void setNeuralNetwork(int n_input, int n_output, const py::handle& hidden, bool is_nerf) {
+        const auto h = values(hidden, "n_hidden");
+        std::vector<int32_t> hs(h.size());
+        for (size_t i = 0; i < h.size(); i++) hs[i] = (int32_t)h[i];
+        mpcc_mlp* m = nullptr;
+        check(mpcc_mlp_create(0, path.c_str(), n_input, n_output, hs.data(), (int)hs.size(), is_nerf ? 1 : 0, &m),
+              "setNeuralNetwork");
+        net.reset(m, mpcc_mlp_destroy);
+        nin = n_input;
+        nout = n_output;
+    }
+    py::tuple calculateMlpOutput(const py::handle& input, bool /*time_verbose*/) {
+        if (!net) throw std::runtime_error("calculateMlpOutput: setNeuralNetwork first");
+        const auto x = values(input, (size_t)nin, "input");
+        Arr out(nout), jac({nout, nin});
+        check(mpcc_mlp_eval(net.get(), 1, x.data(), out.mutable_data(), jac.mutable_data()), "calculateMlpOutput");
+        return py::make_tuple(out, jac);
+    }
+};
+struct PySelfNN : PyNN {
+    using PyNN::PyNN;
+};
+struct PyEnvNN : PyNN {
+    using PyNN::PyNN;
 };
 
 // Integrator (integrator.cpp:29-68) of the kinematic model (model.cpp:31-45)
@@ -372,16 +422,85 @@ PYBIND11_MODULE(MPCC_WRAPPER, m) {
         .def("getTrackLength", &PyMPC::getTrackLength)
         .def("setParam", &PyMPC::setParam);
 
+    using PR = PyRobot;
+    const auto none = py::none();
     py::class_<PyRobot>(m, "RobotModel")
         .def(py::init<>())
-        .def("getNumq", [](PyRobot&) { return 7; })
-        .def("getEEPosition", [](PyRobot& r, const py::handle& q) { auto v = r.rec(q); return vec(v.data(), 3); })
-        .def("getEEOrientation", [](PyRobot& r, const py::handle& q) { auto v = r.rec(q); return mat3(v.data() + 3); })
-        .def("getJacobian", [](PyRobot& r, const py::handle& q) { return r.jac(q, 0, 6); })
-        .def("getJacobianv", [](PyRobot& r, const py::handle& q) { return r.jac(q, 0, 3); })
-        .def("getJacobianw", [](PyRobot& r, const py::handle& q) { return r.jac(q, 3, 3); })
-        .def("getManipulability", [](PyRobot& r, const py::handle& q) { return r.rec(q)[54]; })
-        .def("getDManipulability", [](PyRobot& r, const py::handle& q) { auto v = r.rec(q); return vec(v.data() + 55, 7); });
+        .def("getNumq", [](PR&) { return 7; })
+        .def("getNumv", [](PR&) { return 7; })
+        .def("getNumu", [](PR&) { return 7; })
+        .def("getUpdateKinematics", [](PR& r, const py::handle& q, const py::handle& qd) {
+            r.q = values(q, 7, "q");
+            r.qdot = values(qd, 7, "qdot");
+        })
+        .def("getJointPosition", [](PR& r) { return vec(r.q.data(), 7); })
+        .def("getJacobian", [](PR& r, py::object a, py::object b) { return PR::jac(r.resolve(a, b), 0, 6); },
+             py::arg("q_or_frame"), py::arg("frame_id") = none)
+        .def("getJacobianv", [](PR& r, py::object a, py::object b) { return PR::jac(r.resolve(a, b), 0, 3); },
+             py::arg("q"), py::arg("frame_id") = none)
+        .def("getJacobianw", [](PR& r, py::object a, py::object b) { return PR::jac(r.resolve(a, b), 3, 3); },
+             py::arg("q"), py::arg("frame_id") = none)
+        .def("getPosition", [](PR& r, int f) { return vec(r.frame(r.q, f).pos, 3); })
+        .def("getEEPosition", [](PR& r, py::object q) { return vec(r.resolve(q, py::none()).pos, 3); },
+             py::arg("q") = none)
+        .def("getOrientation", [](PR& r, int f) { return mat3(r.frame(r.q, f).R); })
+        .def("getEEOrientation", [](PR& r, py::object q) { return mat3(r.resolve(q, py::none()).R); },
+             py::arg("q") = none)
+        .def("getTransformation", [](PR& r, int f) { return PR::trans(r.frame(r.q, f)); })
+        .def("getEETransformation", [](PR& r, py::object q) { return PR::trans(r.resolve(q, py::none())); },
+             py::arg("q") = none)
+        .def("getManipulability", [](PR& r, const py::handle& q, int f) { return r.at(q, f).mani; },
+             py::arg("q"), py::arg("frame_id") = EE_FRAME)
+        .def("getDManipulability", [](PR& r, const py::handle& q, int f) { return vec(r.at(q, f).dmani, 7); },
+             py::arg("q"), py::arg("frame_id") = EE_FRAME);
+
+    py::class_<PySelfNN>(m, "SelCollNNmodel")
+        .def(py::init([]() { return PySelfNN(g_data + "/nn/self"); }))
+        .def(py::init<std::string>())
+        .def("setNeuralNetwork", &PyNN::setNeuralNetwork)
+        .def("calculateMlpOutput", &PyNN::calculateMlpOutput, py::arg("input"), py::arg("time_verbose") = false);
+    py::class_<PyEnvNN>(m, "EnvCollNNmodel")
+        .def(py::init([]() { return PyEnvNN(g_data + "/nn/env"); }))
+        .def(py::init<std::string>())
+        .def("setNeuralNetwork", &PyNN::setNeuralNetwork)
+        .def("calculateMlpOutput", &PyNN::calculateMlpOutput, py::arg("input"), py::arg("time_verbose") = false);
+
+    // cubic_spline_rot.h utilities (cubic_spline_rot.cpp:25-95)
+    m.def("getSkewMatrix", [](const py::handle& v) {
+        const auto a = values(v, 3, "getSkewMatrix");
+        const double S[9] = {0, -a[2], a[1], a[2], 0, -a[0], -a[1], a[0], 0};
+        return mat3(S);
+    });
+    m.def("getInverseSkewVector", [](const py::handle& R) {
+        const auto a = values(R, 9, "getInverseSkewVector");
+        const double v[3] = {a[7], a[2], a[3]};
+        return vec(v, 3);
+    });
+    m.def("LogMatrix", [](const py::handle& R) {
+        const auto a = values(R, 9, "LogMatrix");
+        double S[9];
+        check(mpcc_so3_log(a.data(), S), "LogMatrix");
+        return mat3(S);
+    });
+    m.def("ExpMatrix", [](const py::handle& S) {
+        const auto a = values(S, 9, "ExpMatrix");
+        double R[9];
+        check(mpcc_so3_exp(a.data(), R), "ExpMatrix");
+        return mat3(R);
+    });
+
+    // StateInputIndex (config.h:40-76)
+    struct SII {};
+    auto sii = py::class_<SII>(m, "StateInputIndex").def(py::init<>());
+    const char* qn[] = {"q1", "q2", "q3", "q4", "q5", "q6", "q7", "s", "vs"};
+    for (int i = 0; i < 9; i++) sii.def_property_readonly(qn[i], [i](const SII&) { return i; });
+    const char* un[] = {"dq1", "dq2", "dq3", "dq4", "dq5", "dq6", "dq7", "dVs"};
+    for (int i = 0; i < 8; i++) sii.def_property_readonly(un[i], [i](const SII&) { return i; });
+    sii.def_property_readonly("con_selcol", [](const SII&) { return 0; });
+    sii.def_property_readonly("con_sing", [](const SII&) { return 1; });
+    for (int i = 1; i <= 9; i++)
+        sii.def_property_readonly(("con_envcol" + std::to_string(i)).c_str(), [i](const SII&) { return i + 1; });
+    m.attr("si_index") = SII{};
 
     py::class_<PyIntegrator>(m, "Integrator")
         .def(py::init<>())

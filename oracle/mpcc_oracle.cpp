@@ -473,6 +473,47 @@ static void fk(const double* q, double* pos, double* Rout, double* J) {
     }
 }
 
+// Frame f of RobotModel::getPosition/getOrientation/getJacobian(frame_id) (robot_model.cpp:354-398; body_id_
+// :310-319): 1 = panda_link0, 2..8 = panda_link1..7 (RBDL body origin after joint f-1), 9 = panda_hand_tcp.
+// CalcPointJacobian6D at the body origin: joints after the frame give zero columns.
+static void fk_frame(const double* q, int frame, double* pos, double* Rout, double* J) {
+    if (frame >= 9) { fk(q, pos, Rout, J); return; }
+    double Rc[9] = {1, 0, 0, 0, 1, 0, 0, 0, 1}, pc[3] = {0, 0, 0};
+    double z[7][3], o[7][3];
+    const int nj = frame - 1;
+    for (int i = 1; i <= nj; i++) {
+        double t[3];
+        mat3_vec(Rc, JOINT_R[i], t);
+        pc[0] += t[0]; pc[1] += t[1]; pc[2] += t[2];
+        double Et[9], Rt[9];
+        for (int a = 0; a < 3; a++)
+            for (int b = 0; b < 3; b++) Et[3 * a + b] = JOINT_E[i][3 * b + a];
+        mat3_mul(Rc, Et, Rt);
+        z[i - 1][0] = Rt[2]; z[i - 1][1] = Rt[5]; z[i - 1][2] = Rt[8];
+        o[i - 1][0] = pc[0]; o[i - 1][1] = pc[1]; o[i - 1][2] = pc[2];
+        double c = std::cos(q[i - 1]), s = std::sin(q[i - 1]);
+        double Rz[9] = {c, -s, 0, s, c, 0, 0, 0, 1};
+        mat3_mul(Rt, Rz, Rc);
+    }
+    if (pos) { pos[0] = pc[0]; pos[1] = pc[1]; pos[2] = pc[2]; }
+    if (Rout) std::memcpy(Rout, Rc, 72);
+    if (J) {
+        for (int i = 0; i < 7; i++) {
+            if (i >= nj) {
+                for (int a = 0; a < 6; a++) J[a * 7 + i] = 0.0;
+                continue;
+            }
+            double r[3] = {pc[0] - o[i][0], pc[1] - o[i][1], pc[2] - o[i][2]};
+            J[0 * 7 + i] = z[i][1] * r[2] - z[i][2] * r[1];
+            J[1 * 7 + i] = z[i][2] * r[0] - z[i][0] * r[2];
+            J[2 * 7 + i] = z[i][0] * r[1] - z[i][1] * r[0];
+            J[3 * 7 + i] = z[i][0];
+            J[4 * 7 + i] = z[i][1];
+            J[5 * 7 + i] = z[i][2];
+        }
+    }
+}
+
 // det via partial-pivot LU (Eigen MatrixXd::determinant for n>4 -> PartialPivLU)
 static double det_lu(double* A, int n) {
     double det = 1.0;
@@ -2022,6 +2063,17 @@ void oracle_track_path(void* h, double* s, double* X, double* Y, double* Z, doub
 }
 void oracle_fk(const double* q, double* pos3, double* R9, double* J42) { fk(q, pos3, R9, J42); }
 double oracle_manipulability(const double* q) { return manipulability(q); }
+void oracle_fk_frame(const double* q, int frame, double* pos3, double* R9, double* J42) { fk_frame(q, frame, pos3, R9, J42); }
+double oracle_manip_from_J(const double* J42) {  // robot_model.cpp:431-435 on a given Jacobian
+    double A[36];
+    for (int i = 0; i < 6; i++)
+        for (int j = 0; j < 6; j++) {
+            double s = 0;
+            for (int k = 0; k < 7; k++) s += J42[7 * i + k] * J42[7 * j + k];
+            A[6 * i + j] = s;
+        }
+    return std::sqrt(det_lu(A, 6));
+}
 void oracle_dmanipulability(const double* q, double* d7) { dmanipulability(q, d7); }
 void oracle_self_mlp(void* h, const double* q7, double* d, double* grad7) { ((Oracle*)h)->self_nn.eval(q7, d, grad7); }
 void oracle_env_mlp(void* h, const double* in10, double* d9, double* jac90) { ((Oracle*)h)->env_nn.eval(in10, d9, jac90); }

@@ -67,6 +67,9 @@ void   oracle_track_path(void* h, double* s, double* X, double* Y, double* Z, do
 /* RobotModel (robot_model.cpp:366-450) */
 void   oracle_fk(const double* q, double* pos3, double* R9, double* J42);
 double oracle_manipulability(const double* q);
+/* RobotModel frame 1..9 (panda_link0..7, panda_hand_tcp): robot_model.cpp:354-398 */
+void   oracle_fk_frame(const double* q, int frame, double* pos3, double* R9, double* J42);
+double oracle_manip_from_J(const double* J42);
 void   oracle_dmanipulability(const double* q, double* d7);
 /* NN models (SelfCollisionModel.cpp:140-250, EnvCollisionModel.cpp:137-247) */
 void   oracle_self_mlp(void* h, const double* q7, double* d, double* grad7);

@@ -97,6 +97,9 @@ def lib():
         L.oracle_run_mpc_trace.restype = C.c_int
         L.oracle_run_mpc_trace.argtypes = [C.c_void_p, C.c_int, DP, DP, DP, DP, IP, IP, DP, DP, IP, IP, IP, DP]
         L.oracle_rec_size.restype = C.c_int
+        L.oracle_fk_frame.argtypes = [DP, C.c_int, DP, DP, DP]
+        L.oracle_manip_from_J.restype = D
+        L.oracle_manip_from_J.argtypes = [DP]
         assert L.oracle_rec_size() == REC_SIZE
         _lib = L
     return _lib
@@ -176,6 +179,16 @@ class Oracle:
         p, R, J = np.zeros(3), np.zeros(9), np.zeros(42)
         self.L.oracle_fk(_dp(q), _dp(p), _dp(R), _dp(J))
         return p, R.reshape(3, 3), J.reshape(6, 7)
+
+    def fk_frame(self, q, frame):
+        """RobotModel frame 1..9 (panda_link0..7, panda_hand_tcp): position, rotation, 6x7 Jacobian."""
+        q = _f64(q)
+        p, R, J = np.zeros(3), np.zeros(9), np.zeros(42)
+        self.L.oracle_fk_frame(_dp(q), int(frame), _dp(p), _dp(R), _dp(J))
+        return p, R.reshape(3, 3), J.reshape(6, 7)
+
+    def manip_from_J(self, J):
+        return self.L.oracle_manip_from_J(_dp(_f64(J).reshape(42)))
 
     def manipulability(self, q):
         return self.L.oracle_manipulability(_dp(_f64(q)))

@@ -161,3 +161,131 @@ def test_robot_model_gpu(W, oracle_lib):
         assert np.allclose(robot.getJacobianw(q), Jo[3:], rtol=1e-12, atol=1e-14)
         assert abs(robot.getManipulability(q) - o.manipulability(q)) <= 1e-12
         assert np.allclose(robot.getDManipulability(q), o.dmanipulability(q), rtol=1e-9, atol=1e-9)
+
+
+# ---------------------------------------------------------------- the rest of the reference's module surface
+# every name python/MPCC/*.py imports from MPCC_WRAPPER (MPCC.py:7, robot_model.py:5, self_collision_nn.py:5,
+# env_collision_nn.py:5, integrator.py:7-9, utils.py:6-9) and the bound classes of MPCC_wrapper.cpp:139,254-347
+REFERENCE_NAMES = ["RobotModel", "SelCollNNmodel", "EnvCollNNmodel", "Integrator", "NX", "NU", "vectorToState",
+                   "vectorToInput", "stateToVector", "pkg_path", "PathToJson", "getSkewMatrix", "getInverseSkewVector",
+                   "LogMatrix", "ExpMatrix", "StateInputIndex", "MPC", "MPCReturn", "ComputeTime", "OptVariables",
+                   "Track", "TrackPos", "ArcLengthSpline", "PathData", "ParamValue", "State", "Input"]
+
+
+def test_reference_module_surface(W):
+    for name in REFERENCE_NAMES:
+        assert hasattr(W, name), name
+    si = W.StateInputIndex()  # config.h:40-76
+    assert [getattr(si, n) for n in ["q1", "q7", "s", "vs", "dq1", "dq7", "dVs"]] == [0, 6, 7, 8, 0, 6, 7]
+    assert [si.con_selcol, si.con_sing, si.con_envcol1, si.con_envcol9] == [0, 1, 2, 10]
+    for meth in ["getNumq", "getNumv", "getNumu", "getUpdateKinematics", "getJacobian", "getJacobianv", "getJacobianw",
+                 "getPosition", "getEEPosition", "getOrientation", "getEEOrientation", "getTransformation",
+                 "getEETransformation", "getJointPosition", "getManipulability", "getDManipulability"]:
+        assert hasattr(W.RobotModel, meth), meth
+    for cls in (W.SelCollNNmodel, W.EnvCollNNmodel):
+        assert hasattr(cls, "setNeuralNetwork") and hasattr(cls, "calculateMlpOutput")
+
+
+def test_so3_utilities(W):
+    """getSkewMatrix / getInverseSkewVector / LogMatrix / ExpMatrix (cubic_spline_rot.cpp:25-95) against an
+    independent rotation-vector formula (scipy), plus the reference's special branches: |tr - 3| < 1e-6 -> 0
+    (Q10), the small-angle branch I + cos(|v|) sk (Q11: integer 1/2 == 0) and a non-skew input -> zero matrix."""
+    from scipy.spatial.transform import Rotation
+    rng = np.random.default_rng(SEED + 31)
+    for _ in range(20):
+        v = rng.normal(size=3)
+        v *= rng.uniform(0.01, 3.0) / np.linalg.norm(v)  # angle < pi: Log is the inverse of Exp
+        S = W.getSkewMatrix(v)
+        assert np.array_equal(S, -S.T) and np.array_equal(W.getInverseSkewVector(S), v)
+        R = W.ExpMatrix(S)
+        assert np.abs(R - Rotation.from_rotvec(v).as_matrix()).max() <= 1e-14
+        assert np.abs(W.getInverseSkewVector(W.LogMatrix(R)) - v).max() <= 1e-12 * max(1.0, np.linalg.norm(v))
+    assert np.array_equal(W.LogMatrix(Rotation.from_rotvec([1e-4, 0, 0]).as_matrix()), np.zeros((3, 3)))
+    small = np.array([1e-9, -2e-9, 3e-9])
+    Ssm = W.getSkewMatrix(small)
+    assert np.array_equal(W.ExpMatrix(Ssm), np.eye(3) + np.cos(np.linalg.norm(small)) * Ssm)
+    assert np.array_equal(W.ExpMatrix(np.eye(3)), np.zeros((3, 3)))
+    # theta = pi: the eigen-solver branch returns -skew(u) pi for the unit eigenvector u of eigenvalue 1
+    Rpi = Rotation.from_rotvec(np.pi * np.array([0.0, 0.6, 0.8])).as_matrix()
+    L = W.getInverseSkewVector(W.LogMatrix(Rpi))
+    assert abs(np.linalg.norm(L) - np.pi) <= 1e-9 and abs(abs(L @ np.array([0.0, 0.6, 0.8])) - np.pi) <= 1e-9
+
+
+REF_PY = "/root/reference/python"
+
+
+@pytest.mark.skipif(not os.path.isdir(os.path.join(REF_PY, "MPCC")), reason="reference python package not present")
+def test_reference_python_package_imports(W):
+    """The reference's own package (python/MPCC/__init__.py:1-6) imports against this MPCC_WRAPPER, and its
+    host-side pieces run: utils (getSkewMatrix / LogMatrix / Log / Exp), Integrator.simTimeStep."""
+    sys.path.insert(0, REF_PY)
+    try:
+        import MPCC as ref
+        from MPCC import utils
+        x = np.array([0.3, -0.2, 0.1])
+        assert np.array_equal(ref.getSkewMatrix(x), W.getSkewMatrix(x))
+        R = W.ExpMatrix(W.getSkewMatrix(x))
+        assert np.abs(utils.Log(R) - x).max() <= 1e-12
+        xn = ref.Integrator().simTimeStep(np.zeros(9), np.full(8, 0.5))
+        assert np.allclose(xn[:7], 0.005) and abs(xn[8] - 0.005) <= 1e-15
+        for cls in ["RobotModel", "SelfCollisionNN", "EnvCollisionNN", "MPCC"]:
+            assert hasattr(ref, cls)
+    finally:
+        sys.path.remove(REF_PY)
+        for k in [k for k in sys.modules if k == "MPCC" or k.startswith("MPCC.")]:
+            del sys.modules[k]
+
+
+@pytest.mark.gpu
+def test_collision_nn_models_gpu(W, oracle_lib):
+    """SelCollNNmodel / EnvCollNNmodel with the calls of self_collision_nn.py / env_collision_nn.py:
+    setNeuralNetwork(7, 1, [256, 64], True) and (10, 9, [256]*4, True) on the default model paths, then
+    calculateMlpOutput(input) -> (output, Jacobian wrt every input) against the oracle's MLPs (value and
+    the full 9x10 env Jacobian, Q17) to 1e-10 relative."""
+    o, P, track = make_oracle(N=20, max_iter=2, mask=7)
+    sc = W.SelCollNNmodel()
+    sc.setNeuralNetwork(7, 1, np.array([256, 64]), True)
+    ec = W.EnvCollNNmodel()
+    ec.setNeuralNetwork(10, 9, np.array([256, 256, 256, 256]), True)
+    rng = np.random.default_rng(SEED + 32)
+    for _ in range(6):
+        q = Q0 + rng.normal(0, 0.4, 7)
+        d, J = sc.calculateMlpOutput(q, False)
+        do, go = o.self_mlp(q)
+        assert d.shape == (1,) and J.shape == (1, 7)
+        assert abs(d[0] - do) <= 1e-10 * max(1.0, abs(do))
+        assert np.allclose(J[0], go, rtol=1e-10, atol=1e-10)
+        inp = np.concatenate([q, [0.48, 0.218, rng.uniform(0.42, 0.62)]])
+        de, Je = ec.calculateMlpOutput(inp, False)
+        deo, Jeo = o.env_mlp(inp)
+        assert de.shape == (9,) and Je.shape == (9, 10)
+        assert np.allclose(de, deo, rtol=1e-10, atol=1e-10)
+        assert np.allclose(Je, np.asarray(Jeo).reshape(9, 10), rtol=1e-10, atol=1e-10)
+    with pytest.raises(Exception):
+        W.SelCollNNmodel("/nonexistent").setNeuralNetwork(7, 1, np.array([256, 64]), True)
+
+
+@pytest.mark.gpu
+def test_robot_model_frames_gpu(W, oracle_lib):
+    """RobotModel frame getters (robot_model.h:27-141): getUpdateKinematics(q, qdot) then getPosition /
+    getOrientation / getTransformation / getJacobian(frame_id) for frames 1..9, getJacobian(q, frame_id),
+    getManipulability(q, frame_id) against the oracle's frame kinematics."""
+    o, P, track = make_oracle(N=20, max_iter=2, mask=7)
+    robot = W.RobotModel()
+    rng = np.random.default_rng(SEED + 33)
+    for _ in range(4):
+        q = Q0 + rng.normal(0, 0.3, 7)
+        robot.getUpdateKinematics(q, np.zeros(7))
+        assert np.array_equal(robot.getJointPosition(), q)
+        for f in range(1, 10):
+            p, R, J = o.fk_frame(q, f)
+            assert np.allclose(robot.getPosition(f), p, rtol=1e-12, atol=1e-14), f
+            assert np.allclose(robot.getOrientation(f), R, rtol=1e-12, atol=1e-14), f
+            T = robot.getTransformation(f)
+            assert np.allclose(T[:3, :3], R, atol=1e-14) and np.allclose(T[:3, 3], p, atol=1e-14) and T[3, 3] == 1
+            assert np.allclose(robot.getJacobian(f), J, rtol=1e-12, atol=1e-14), f
+            assert np.allclose(robot.getJacobian(q, f), J, rtol=1e-12, atol=1e-14), f
+            if f >= 8:
+                assert abs(robot.getManipulability(q, f) - o.manip_from_J(J)) <= 1e-12
+        assert np.allclose(robot.getEETransformation()[:3, 3], o.fk(q)[0], atol=1e-14)
+        assert np.allclose(robot.getDManipulability(q, 9), o.dmanipulability(q), rtol=1e-9, atol=1e-9)
