@@ -66,11 +66,31 @@ def make_pool(m, params, mask, steps, device, pool_obs=(3.0, 3.0, 3.0, 0.0)):
     return {k: np.array(v) for k, v in pool.items()}, track
 
 
-def cpu_baseline(params_dict, track, x0, u0, obs, guess, valid, fails, threads, sample, budget_s):
+def cpu_info():
+    """Host CPU of this run: logical CPUs of the machine (nproc), the CPUs this process may use (its
+    affinity mask / the box's share), the OpenMP thread cap of the environment and the lscpu model name."""
+    model = None
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    usable = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else os.cpu_count()
+    omp = os.environ.get("OMP_NUM_THREADS")
+    return {"nproc": os.cpu_count(), "usable": usable, "omp_num_threads": int(omp) if omp and omp.isdigit() else None,
+            "model": model}
+
+
+def cpu_baseline(params_dict, track, x0, u0, obs, guess, valid, fails, threads, sample, budget_s, latency_n=200):
     """The oracle (CPU restatement of the reference algorithm, oracle/) on a bounded sample of the same
     workload: repeated passes over the first `sample` instances (each pass from the same inputs, so
     every pass is one full runMPC_ per instance), OpenMP over instances, until `budget_s` seconds of
-    CPU work.  Test infrastructure used only as the reported baseline."""
+    CPU work.  Then the single-controller latency BASELINE.md §2 asks for: `latency_n` solves one at a
+    time on one thread (ms per runMPC_, against the Ts = 10 ms real-time budget of config.json:4).
+    Test infrastructure used only as the reported baseline."""
     from oracle.pyoracle import Oracle
     o = Oracle(params_dict, os.path.join(ROOT, "mpcc_manipulator_amd", "data", "nn"), qp_mode=0, nthreads=threads)
     o.set_track(*track)
@@ -85,7 +105,18 @@ def cpu_baseline(params_dict, track, x0, u0, obs, guess, valid, fails, threads, 
         done += n
         passes += 1
     o.close()
-    return done / dt, n, passes, dt
+    o1 = Oracle(params_dict, os.path.join(ROOT, "mpcc_manipulator_amd", "data", "nn"), qp_mode=0, nthreads=1)
+    o1.set_track(*track)
+    lat = []
+    for i in range(min(latency_n, x0.shape[0])):
+        xs, gs, vs, fs = x0[i:i + 1].copy(), guess[i:i + 1].copy(), valid[i:i + 1].copy(), fails[i:i + 1].copy()
+        t0 = time.perf_counter()
+        o1.run_mpc(xs, u0[i:i + 1], obs[i:i + 1], gs, vs, fs)
+        lat.append(time.perf_counter() - t0)
+    o1.close()
+    lat = np.array(lat) * 1e3
+    return done / dt, n, passes, dt, {"mean_ms": float(lat.mean()), "p99_ms": float(np.percentile(lat, 99)),
+                                      "max_ms": float(lat.max()), "solves": int(lat.size), "budget_ms": 10.0}
 
 
 def _free_port():
@@ -142,7 +173,8 @@ def main():
     ap.add_argument("--mask", type=int, default=None, help="polytopic rows: 1 self, 2 singularity, 4 env (configs[1] = 2)")
     ap.add_argument("--max-iter", type=int, default=2)
     ap.add_argument("--pool-steps", type=int, default=1000)
-    ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--cpu-threads", type=int, default=None,
+                    help="OpenMP threads of the CPU baseline (default: the CPUs this process may use, capped by OMP_NUM_THREADS)")
     ap.add_argument("--cpu-sample", type=int, default=1024)
     ap.add_argument("--cpu-seconds", type=float, default=15.0, help="CPU-baseline budget (bounded sample)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -303,9 +335,13 @@ def main():
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         try:
             pd = params.as_dict()
-            v, n, passes, dt = cpu_baseline(pd, track, x0, u0, obs, guess, valid, fails, args.cpu_threads,
-                                            args.cpu_sample, args.cpu_seconds)
-            cpu = {"value": v, "unit": "solves/s", "cores": args.cpu_threads, "kind": "port",
+            ci = cpu_info()
+            threads = args.cpu_threads or min(ci["usable"], ci["omp_num_threads"] or ci["usable"])
+            args.cpu_threads = threads
+            v, n, passes, dt, lat = cpu_baseline(pd, track, x0, u0, obs, guess, valid, fails, threads,
+                                                 args.cpu_sample, args.cpu_seconds)
+            cpu = {"value": v, "unit": "solves/s", "cores": threads, "kind": "port", "host": ci,
+                   "latency_1thread": lat,
                    "sample": f"{passes} passes over the first {n} instances of the same workload "
                              f"({passes * n} runMPC_ solves, {dt:.1f} s; oracle = CPU restatement of the "
                              f"reference algorithm with OSQP replaced by an exact IPM, OpenMP {args.cpu_threads} threads)"}

@@ -235,6 +235,13 @@ void mpcc_mlp_destroy(mpcc_mlp* m);
  * q [M*7] on GPU 'device': pos [M*3], R [M*9], J [M*42] (rows Jv; Jw), mani [M], dmani [M*7]; any may be NULL. */
 int  mpcc_robot_frames(int device, int M, const double* q, int frame_id, double* pos, double* R, double* J, double* mani,
                        double* dmani);
+/* CubicSpline::genSpline + getPoint/getDerivative/getSecondDerivative (cubic_spline.cpp:65-246) of n points at m
+ * abscissas, host only: out3 [m*3] = value, d1, d2.  regular = 1: regular grid (index by floor(x/dx)). */
+int  mpcc_cubic_spline_host(int n, const double* x, const double* y, int regular, int m, const double* xq, double* out3);
+/* CubicSplineRot::genSpline + getPoint/getDerivative (cubic_spline_rot.cpp:142-259), host only: R9 [n*9] in,
+ * Rq [m*9], dRq [m*3] out (either may be NULL). */
+int  mpcc_rot_spline_host(int n, const double* x, const double* R9, int regular, int m, const double* xq, double* Rq,
+                          double* dRq);
 /* LogMatrix / ExpMatrix (cubic_spline_rot.cpp:44-95, quirks Q10/Q11), host only: 3x3 row-major */
 int  mpcc_so3_log(const double* R9, double* S9);
 int  mpcc_so3_exp(const double* S9, double* R9);

@@ -408,6 +408,19 @@ extern "C" {
 
 int mpcc_abi_version(void) { return MPCC_ABI_VERSION; }
 
+int mpcc_cubic_spline_host(int n, const double* x, const double* y, int regular, int m, const double* xq, double* out3) {
+    if (n < 2 || m < 0 || !x || !y || (m && (!xq || !out3))) return fail(MPCC_E_INVALID, "mpcc_cubic_spline_host: invalid argument");
+    host_cubic_spline(n, x, y, regular != 0, m, xq, out3);
+    return MPCC_OK;
+}
+
+int mpcc_rot_spline_host(int n, const double* x, const double* R9, int regular, int m, const double* xq, double* Rq,
+                         double* dRq) {
+    if (n < 2 || m < 0 || !x || !R9 || (m && !xq)) return fail(MPCC_E_INVALID, "mpcc_rot_spline_host: invalid argument");
+    host_rot_spline(n, x, R9, regular != 0, m, xq, Rq, dRq);
+    return MPCC_OK;
+}
+
 int mpcc_so3_log(const double* R9, double* S9) {
     if (!R9 || !S9) return fail(MPCC_E_INVALID, "mpcc_so3_log: null argument");
     double v[3];

@@ -122,6 +122,20 @@ struct Cubic {  // CubicSpline (cubic_spline.cpp)
         if (i == (int)x.size() - 1) return y.back();
         return a[i] + b[i] * d1 + c[i] * d2 + d[i] * d3;
     }
+    double deriv(double xx) const {  // getDerivative (cubic_spline.cpp)
+        xx = std::max(0., std::min(xx, x.back()));
+        int i = index(xx);
+        double d1 = xx - x[i], d2 = d1 * d1;
+        if (i == (int)x.size() - 1) return 0.;
+        return b[i] + 2.0 * c[i] * d1 + 3.0 * d[i] * d2;
+    }
+    double deriv2(double xx) const {  // getSecondDerivative
+        xx = std::max(0., std::min(xx, x.back()));
+        int i = index(xx);
+        double d1 = xx - x[i];
+        if (i == (int)x.size() - 1) return 2.0 * c[i];
+        return 2.0 * c[i] + 6.0 * d[i] * d1;
+    }
 };
 
 struct CubicRot {  // CubicSplineRot (cubic_spline_rot.cpp)
@@ -160,6 +174,14 @@ struct CubicRot {  // CubicSplineRot (cubic_spline_rot.cpp)
         Mat3 E;
         exp_skew(v, E.data());
         return mul(R[i], E);
+    }
+    std::array<double, 3> deriv(double xx) const {  // getDerivative (cubic_spline_rot.cpp:239-259)
+        xx = std::max(0., std::min(xx, x.back()));
+        int i = index(xx);
+        if (i == (int)x.size() - 1) return {0, 0, 0};
+        double d1 = xx - x[i], d2 = d1 * d1;
+        double f = 2.0 * c[i] * d1 + 3.0 * d[i] * d2;
+        return {lv[i][0] * f, lv[i][1] * f, lv[i][2] * f};
     }
 };
 
@@ -379,6 +401,34 @@ double project_tables(const SplineTables& t, double proj_max_dist, double s_gues
         s_old = s_opt;
     }
     return s_guess;
+}
+
+// CubicSpline / CubicSplineRot fitted to n points and evaluated at m abscissas (host, for tests and the
+// C ABI): value, first and second derivative; rotation and its derivative vector
+void host_cubic_spline(int n, const double* x, const double* y, bool regular, int m, const double* xq, double* out3) {
+    Cubic c;
+    c.gen(std::vector<double>(x, x + n), std::vector<double>(y, y + n), regular);
+    for (int i = 0; i < m; i++) {
+        out3[3 * i] = c.point(xq[i]);
+        out3[3 * i + 1] = c.deriv(xq[i]);
+        out3[3 * i + 2] = c.deriv2(xq[i]);
+    }
+}
+void host_rot_spline(int n, const double* x, const double* R9, bool regular, int m, const double* xq, double* Rq, double* dRq) {
+    std::vector<Mat3> R(n);
+    for (int i = 0; i < n; i++) std::copy(R9 + 9 * i, R9 + 9 * i + 9, R[i].begin());
+    CubicRot c;
+    c.gen(std::vector<double>(x, x + n), R, regular);
+    for (int i = 0; i < m; i++) {
+        if (Rq) {
+            const Mat3 r = c.point(xq[i]);
+            std::copy(r.begin(), r.end(), Rq + 9 * i);
+        }
+        if (dRq) {
+            const auto d = c.deriv(xq[i]);
+            std::copy(d.begin(), d.end(), dRq + 3 * i);
+        }
+    }
 }
 
 // ExpMatrix(sk) (cubic_spline_rot.cpp:81-95): a zero matrix when sk is not skew-symmetric (the reference

@@ -39,5 +39,7 @@ void quat_to_rot(double qx, double qy, double qz, double qw, double* R9);
 // host LogMatrix / ExpMatrix (cubic_spline_rot.cpp:44-95), exposed for tests
 void host_log_vec(const double* R, double* v);
 void host_exp_matrix(const double* sk, double* E);
+void host_cubic_spline(int n, const double* x, const double* y, bool regular, int m, const double* xq, double* out3);
+void host_rot_spline(int n, const double* x, const double* R9, bool regular, int m, const double* xq, double* Rq, double* dRq);
 
 }  // namespace mpcc

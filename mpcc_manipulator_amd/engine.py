@@ -134,6 +134,17 @@ def lib():
         "mpcc_debug_workspace": (C.c_int, [V, C.c_int, DP]),
         "mpcc_debug_project": (C.c_int, [V, C.c_int, DP, DP, DP]),
         "mpcc_debug_trace_get": (C.c_int, [V, C.c_int, DP]),
+        "mpcc_track_eval_host": (C.c_int, [C.c_int, DP, DP, DP, DP, C.c_int, DP, DP, DP, DP, DP, DP]),
+        "mpcc_track_project_host": (C.c_int, [C.c_int, DP, DP, DP, DP, C.c_int, D, DP, DP, DP]),
+        "mpcc_cubic_spline_host": (C.c_int, [C.c_int, DP, DP, C.c_int, C.c_int, DP, DP]),
+        "mpcc_rot_spline_host": (C.c_int, [C.c_int, DP, DP, C.c_int, C.c_int, DP, DP, DP]),
+        "mpcc_so3_log": (C.c_int, [DP, DP]),
+        "mpcc_so3_exp": (C.c_int, [DP, DP]),
+        "mpcc_mlp_create": (C.c_int, [C.c_int, C.c_char_p, C.c_int, C.c_int, IP, C.c_int, C.c_int, C.POINTER(V)]),
+        "mpcc_mlp_eval": (C.c_int, [V, C.c_int, DP, DP, DP]),
+        "mpcc_mlp_dims": (C.c_int, [V, IP, IP]),
+        "mpcc_mlp_destroy": (None, [V]),
+        "mpcc_robot_frames": (C.c_int, [C.c_int, C.c_int, DP, C.c_int, DP, DP, DP, DP, DP]),
     }
     for name, (res, args) in sig.items():
         f = getattr(L, name)
@@ -257,6 +268,37 @@ def build_track_host(X, Y, Z, R):
            "mpcc_track_build_host")
     s, Xo, Yo, Zo, Ro, L = out
     return s, Xo, Yo, Zo, Ro.reshape(100, 3, 3), float(L[0])
+
+
+def eval_track_host(X, Y, Z, R, s):
+    """ArcLengthSpline queries on the host spline of the way-points (mpcc_track_eval_host): pos, d1, d2
+    [M, 3], R [M, 3, 3], dR [M, 3] at the arc lengths s."""
+    X, Y, Z = _f64(X), _f64(Y), _f64(Z)
+    R = _f64(R).reshape(-1, 9)
+    s = _f64(s).reshape(-1)
+    M = len(s)
+    pos, d1, d2, Rq, dR = np.zeros((M, 3)), np.zeros((M, 3)), np.zeros((M, 3)), np.zeros((M, 9)), np.zeros((M, 3))
+    _check(lib().mpcc_track_eval_host(len(X), _dp(X), _dp(Y), _dp(Z), _dp(R), M, _dp(s), _dp(pos), _dp(d1), _dp(d2),
+                                      _dp(Rq), _dp(dR)), "mpcc_track_eval_host")
+    return pos, d1, d2, Rq.reshape(M, 3, 3), dR
+
+
+def cubic_spline_host(x, y, xq, regular):
+    """CubicSpline fit + (value, d1, d2) at xq [M] -> [M, 3] (mpcc_cubic_spline_host)."""
+    x, y, xq = _f64(x), _f64(y), _f64(xq).reshape(-1)
+    out = np.zeros((len(xq), 3))
+    _check(lib().mpcc_cubic_spline_host(len(x), _dp(x), _dp(y), int(bool(regular)), len(xq), _dp(xq), _dp(out)),
+           "mpcc_cubic_spline_host")
+    return out
+
+
+def rot_spline_host(x, R, xq, regular):
+    """CubicSplineRot fit + (R [M, 3, 3], dR [M, 3]) at xq (mpcc_rot_spline_host)."""
+    x, R, xq = _f64(x), _f64(R).reshape(-1, 9), _f64(xq).reshape(-1)
+    Rq, dR = np.zeros((len(xq), 9)), np.zeros((len(xq), 3))
+    _check(lib().mpcc_rot_spline_host(len(x), _dp(x), _dp(R), int(bool(regular)), len(xq), _dp(xq), _dp(Rq), _dp(dR)),
+           "mpcc_rot_spline_host")
+    return Rq.reshape(-1, 3, 3), dR
 
 
 # ------------------------------------------------------------------------------------------------
