@@ -165,9 +165,11 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--config", type=int, default=1, choices=[1, 2],
+    ap.add_argument("--config", default="1", choices=["1", "2", "1-all-rows"],
                     help="BASELINE configs[i] preset: 1 = B 4096, N 20, mask 2 (the metric); "
-                         "2 = B 65536, N 40, mask 7, per-instance obstacles (parity case, timing only)")
+                         "2 = B 65536, N 40, mask 7, per-instance obstacles (parity case, timing only); "
+                         "1-all-rows = configs[1]'s B 4096, N 20 with the reference's default rows (all 11: self + "
+                         "singularity + 9 env collision, config.h:34) and the main_w_sim.py:42-45 obstacles")
     ap.add_argument("--batch", type=int, default=None, help="instances per GPU")
     ap.add_argument("--N", type=int, default=None)
     ap.add_argument("--mask", type=int, default=None, help="polytopic rows: 1 self, 2 singularity, 4 env (configs[1] = 2)")
@@ -185,7 +187,9 @@ def main():
         ap.error("--gpus must be >= 1")
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
         launch_ranks(args.gpus)
-    preset = {1: dict(batch=4096, N=20, mask=2), 2: dict(batch=65536, N=40, mask=7)}[args.config]
+    preset = {"1": dict(batch=4096, N=20, mask=2), "2": dict(batch=65536, N=40, mask=7),
+              "1-all-rows": dict(batch=4096, N=20, mask=7)}[args.config]
+    obstacles = args.config in ("2", "1-all-rows")
     for k, v in preset.items():
         if getattr(args, k) is None:
             setattr(args, k, v)
@@ -221,7 +225,7 @@ def main():
     N, B = args.N, args.batch
     params = m.load_params(N, overrides={"sqp": {"max_iter": args.max_iter}})
     params.constraint_mask = args.mask
-    pool_obs = (0.48, 0.218, 0.521, 5.0) if args.config == 2 else (3.0, 3.0, 3.0, 0.0)
+    pool_obs = (0.48, 0.218, 0.521, 5.0) if obstacles else (3.0, 3.0, 3.0, 0.0)
     pool, track = make_pool(m, params, args.mask, args.pool_steps, local, pool_obs)
     eng = m.Engine(params, max_batch=B, device=local, constraint_mask=args.mask)
     eng.set_track(*track)
@@ -238,7 +242,7 @@ def main():
     guess = pool["guess"][idx].copy()
     valid = pool["valid"][idx].astype(np.int32)
     fails = pool["fails"][idx].astype(np.int32)
-    if args.config == 2:  # main_w_sim.py:42-45 scenario: xyz = (0.48, 0.218, z), z ~ U[0.421, 0.621], r = 5 cm
+    if obstacles:  # main_w_sim.py:42-45 scenario: xyz = (0.48, 0.218, z), z ~ U[0.421, 0.621], r = 5 cm
         z = rng.uniform(0.421, 0.621, B * world)[start:start + B]
         obs = np.column_stack([np.full(B, 0.48), np.full(B, 0.218), z, np.full(B, 5.0)])
     else:  # dummy obstacle of MPC::runMPC (mpc.cpp:97-100)
@@ -359,10 +363,14 @@ def main():
             "value": value, "unit": "solves/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
             "ms_per_step": ms, "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f64",
             "data": "synthetic (closed-loop state pool on the default track, q + N(0, 0.005 rad))",
-            "config": {"workload": (f"configs[1]: batch={B}/GPU Panda MPCC instances, N={N}, bounds+singularity "
-                                    f"constraints (mask={args.mask}), {args.max_iter} SQP iters") if args.config == 1 else
-                                   (f"configs[2]: batch={B}/GPU Panda MPCC instances, N={N}, self+env collision NN "
-                                    f"constraints (mask={args.mask}), per-instance obstacles, {args.max_iter} SQP iters"),
+            "config": {"workload": {
+                "1": f"configs[1]: batch={B}/GPU Panda MPCC instances, N={N}, bounds+singularity constraints "
+                     f"(mask={args.mask}), {args.max_iter} SQP iters",
+                "2": f"configs[2]: batch={B}/GPU Panda MPCC instances, N={N}, self+env collision NN constraints "
+                     f"(mask={args.mask}), per-instance obstacles, {args.max_iter} SQP iters",
+                "1-all-rows": f"configs[1] shape with the reference's default rows: batch={B}/GPU Panda MPCC instances, "
+                              f"N={N}, all 11 polytopic rows incl. both collision NNs (mask={args.mask}), per-instance "
+                              f"obstacles, {args.max_iter} SQP iters"}[args.config],
                        "batch_per_gpu": B, "global_batch": B * world, "horizon": N, "sqp_iters": args.max_iter,
                        "parallelism": f"instance-sharded x{world}" + ((", gloo rehearsal, all ranks on GPU 0" if rehearse else
                                                                   ", RCCL all_gather(u0)") if world > 1 else "")},

@@ -9,6 +9,6 @@ mkdir -p "$V"
 /opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC --offload-arch=gfx950 -I "$ROOT/include" -I "$ROOT/mpcc_manipulator_amd/csrc" \
     -Wno-unused-result $2 -c "$ROOT/mpcc_manipulator_amd/csrc/ipm.hip" -o "$V/ipm.o"
 objs=""
-for o in kernels mlp engine host_params host_spline mpc; do objs="$objs $B/$o.o"; done
+for o in kernels mlp nn_generic engine host_params host_spline mpc; do objs="$objs $B/$o.o"; done
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o "$V/libmpcc_engine.so" "$V/ipm.o" $objs
 echo "built $V"
