@@ -24,13 +24,19 @@
 
 namespace orc {
 
-constexpr int NX = 9, NU = 8, NPC = 11, DOF = 7, NLINK = 9;
+// Robot dimensions: ORC_DOF = 7 is the reference's Franka Panda (config.h:29-38); ORC_DOF = 10 builds the
+// same restatement for the Husky+Panda mobile manipulator (BASELINE configs[3]): planar base
+// joints (x, y, theta) followed by the seven Panda joints.  State [q(DOF), s, vs], input [dq(DOF), dVs].
+constexpr int DOF = ORC_DOF, NX = DOF + 2, NU = DOF + 1, NXU = NX + NU, NPC = 11, NLINK = 9;
+constexpr int IS = DOF, IVS = DOF + 1, IDVS = DOF;  // indices of s, vs in the state and of dVs in the input
+constexpr int NARM = 7, NBASE = DOF - NARM;       // the Panda joints follow the base joints
 constexpr double INF = 1e30;                 // config.h:37
 constexpr int N_SPLINE = 100;                // config.h:38
-constexpr int REC = 143;                     // robot record size (see rec_* offsets)
-// RobotData layout (robot_data.h:13-31)
-constexpr int R_POS = 0, R_ROT = 3, R_J = 12, R_MU = 54, R_DMU = 55, R_SEL = 62, R_DSEL = 63,
-              R_OBSR = 70, R_ENV = 71, R_DENV = 80;
+// RobotData layout (robot_data.h:13-31): pos 3, R 9, J 6 x DOF, mu, dmu DOF, d_self, dd_self DOF, obs_r,
+// d_env 9, dd_env 9 x DOF (143 doubles for the Panda)
+constexpr int R_POS = 0, R_ROT = 3, R_J = 12, R_MU = R_J + 6 * DOF, R_DMU = R_MU + 1, R_SEL = R_DMU + DOF,
+              R_DSEL = R_SEL + 1, R_OBSR = R_DSEL + DOF, R_ENV = R_OBSR + 1, R_DENV = R_ENV + 9;
+constexpr int REC = R_DENV + 9 * DOF;
 
 enum Status {  // solver_interface.h:28-42
     SOLVED, MAX_ITER_EXCEEDED, QP_DualInfeasibleInaccurate, QP_PrimalInfeasibleInaccurate,
@@ -428,8 +434,9 @@ static const double JOINT_R[9][3] = {
     {-0.0825, 0.384, 0}, {0, 0, 0}, {0.088, 0, 0}, {0, 0, 0.107}};  // :171-179
 static const double TCP_R[3] = {0, 0, 0.1034};                      // :182
 
-// FK + geometric Jacobian of panda_hand_tcp.  J rows 0-2 = Jv, 3-5 = Jw (robot_model.cpp:372-375)
-static void fk(const double* q, double* pos, double* Rout, double* J) {
+// FK + geometric Jacobian of panda_hand_tcp for the 7 Panda joints.  J 6x7: rows 0-2 = Jv, 3-5 = Jw
+// (robot_model.cpp:372-375)
+static void fk_arm(const double* q, double* pos, double* Rout, double* J) {
     double Rc[9] = {1, 0, 0, 0, 1, 0, 0, 0, 1}, pc[3] = {0, 0, 0};
     double z[7][3], o[7][3];
     for (int i = 1; i <= 7; i++) {
@@ -477,7 +484,7 @@ static void fk(const double* q, double* pos, double* Rout, double* J) {
 // :310-319): 1 = panda_link0, 2..8 = panda_link1..7 (RBDL body origin after joint f-1), 9 = panda_hand_tcp.
 // CalcPointJacobian6D at the body origin: joints after the frame give zero columns.
 static void fk_frame(const double* q, int frame, double* pos, double* Rout, double* J) {
-    if (frame >= 9) { fk(q, pos, Rout, J); return; }
+    if (frame >= 9) { fk_arm(q, pos, Rout, J); return; }
     double Rc[9] = {1, 0, 0, 0, 1, 0, 0, 0, 1}, pc[3] = {0, 0, 0};
     double z[7][3], o[7][3];
     const int nj = frame - 1;
@@ -537,24 +544,67 @@ static double det_lu(double* A, int n) {
     return det;
 }
 
-// Manipulability — robot_model.cpp:431-435
-static double manipulability(const double* q) {
-    double J[42], JJ[36];
-    fk(q, nullptr, nullptr, J);
+// Mobile base of the Husky+Panda (ORC_DOF = 10; robot_model.cpp:321-352 setHusky: prismatic x, prismatic y,
+// revolute theta about z, then the fixed husky_base).  The reference never mounts the Panda on it
+// (setRobot appends only setPanda, :58-66); this build mounts panda_link0 at MOBILE_MOUNT in the base
+// frame with identity rotation (setPanda(base_id, base_position, I), :68) — our definition, DESIGN.md §11.
+static const double MOBILE_MOUNT[3] = {0.0, 0.0, 0.35};
+
+// FK + geometric Jacobian of panda_hand_tcp for the robot of this build: J 6 x DOF, rows Jv; Jw.  With the
+// base: p = [x, y, 0] + Rz(th) (mount + p_arm), R = Rz(th) R_arm; base columns e_x, e_y and
+// (e_z x (p - [x, y, 0]), e_z); arm columns rotated by Rz(th) — CalcPointJacobian6D of that chain.
+static void fk(const double* q, double* pos, double* Rout, double* J) {
+    if (NBASE == 0) { fk_arm(q, pos, Rout, J); return; }
+    double pa[3], Ra[9], Ja[42];
+    fk_arm(q + NBASE, pa, Ra, J ? Ja : nullptr);
+    const double c = std::cos(q[2]), sn = std::sin(q[2]);
+    const double Rz[9] = {c, -sn, 0, sn, c, 0, 0, 0, 1};
+    const double pl[3] = {MOBILE_MOUNT[0] + pa[0], MOBILE_MOUNT[1] + pa[1], MOBILE_MOUNT[2] + pa[2]};
+    double pw[3];
+    mat3_vec(Rz, pl, pw);
+    const double p3[3] = {q[0] + pw[0], q[1] + pw[1], 0.0 + pw[2]};
+    if (pos) { pos[0] = p3[0]; pos[1] = p3[1]; pos[2] = p3[2]; }
+    if (Rout) mat3_mul(Rz, Ra, Rout);
+    if (J) {
+        for (int i = 0; i < 6 * DOF; i++) J[i] = 0.0;
+        J[0 * DOF + 0] = 1.0;                      // x
+        J[1 * DOF + 1] = 1.0;                      // y
+        J[0 * DOF + 2] = -(p3[1] - q[1]);          // theta: e_z x (p - base)
+        J[1 * DOF + 2] = p3[0] - q[0];
+        J[5 * DOF + 2] = 1.0;
+        for (int j = 0; j < NARM; j++) {
+            const double v[3] = {Ja[0 * 7 + j], Ja[1 * 7 + j], Ja[2 * 7 + j]}, w[3] = {Ja[3 * 7 + j], Ja[4 * 7 + j], Ja[5 * 7 + j]};
+            double rv[3], rw[3];
+            mat3_vec(Rz, v, rv);
+            mat3_vec(Rz, w, rw);
+            for (int a = 0; a < 3; a++) { J[a * DOF + NBASE + j] = rv[a]; J[(3 + a) * DOF + NBASE + j] = rw[a]; }
+        }
+    }
+}
+
+// sqrt(det(J J^T)) of a 6 x DOF Jacobian — robot_model.cpp:431-435
+static double manip_of_J(const double* J) {
+    double JJ[36];
     for (int i = 0; i < 6; i++)
         for (int j = 0; j < 6; j++) {
             double s = 0;
-            for (int k = 0; k < 7; k++) s += J[7 * i + k] * J[7 * j + k];
+            for (int k = 0; k < DOF; k++) s += J[DOF * i + k] * J[DOF * j + k];
             JJ[6 * i + j] = s;
         }
     return std::sqrt(det_lu(JJ, 6));
 }
+// Manipulability — robot_model.cpp:431-435
+static double manipulability(const double* q) {
+    double J[6 * DOF];
+    fk(q, nullptr, nullptr, J);
+    return manip_of_J(J);
+}
 // dManipulability — robot_model.cpp:437-450 (central FD, delta = 1e-4)
 static void dmanipulability(const double* q, double* d) {
     const double delta = 1e-4;
-    for (int i = 0; i < 7; i++) {
-        double qp[7], qm[7];
-        for (int k = 0; k < 7; k++) { qp[k] = q[k] + (k == i ? delta : 0.0); qm[k] = q[k] - (k == i ? delta : 0.0); }
+    for (int i = 0; i < DOF; i++) {
+        double qp[DOF], qm[DOF];
+        for (int k = 0; k < DOF; k++) { qp[k] = q[k] + (k == i ? delta : 0.0); qm[k] = q[k] - (k == i ? delta : 0.0); }
         double m1 = manipulability(qp), m2 = manipulability(qm);
         d[i] = (m1 - m2) / (2 * delta);
     }
@@ -670,10 +720,10 @@ struct Oracle {
         track.proj_max_dist = p.proj_max_dist;
         for (int i = 0; i < NX * NX; i++) A[i] = (i % (NX + 1) == 0) ? 1.0 : 0.0;
         for (int i = 0; i < NX * NU; i++) B[i] = 0.0;
-        A[7 * NX + 8] = p.Ts;                          // s <- vs
+        A[IS * NX + IVS] = p.Ts;                       // s <- vs
         for (int j = 0; j < DOF; j++) B[j * NU + j] = p.Ts;  // q <- dq
-        B[7 * NU + 7] = p.Ts * p.Ts / 2.0;             // s <- dVs
-        B[8 * NU + 7] = p.Ts;                          // vs <- dVs
+        B[IS * NU + IDVS] = p.Ts * p.Ts / 2.0;         // s <- dVs
+        B[IVS * NU + IDVS] = p.Ts;                     // vs <- dVs
     }
     int N() const { return p.N; }
     int nvar() const { return (N() + 1) * NX + N() * NU; }
@@ -686,20 +736,37 @@ static void robot_record(const Oracle& o, const double* q, const double* obs, do
     fk(q, rec + R_POS, rec + R_ROT, rec + R_J);
     rec[R_MU] = manipulability(q);
     dmanipulability(q, rec + R_DMU);
+    // The Panda-trained networks see the arm: joints q[NBASE..] (self: the base moves no arm link relative to
+    // another, so its columns are zero) and the obstacle in the panda_link0 frame (env, below).
+    const double* qa = q + NBASE;
     if ((o.p.constraint_mask & 1) && o.self_nn.ok) {
-        o.self_nn.eval(q, rec + R_SEL, rec + R_DSEL);
+        o.self_nn.eval(qa, rec + R_SEL, rec + R_DSEL + NBASE);
     } else {
         rec[R_SEL] = std::numeric_limits<double>::infinity();  // masked: no self-collision data
     }
     // RobotData::updateEnv (robot_data.h:74-88)
     rec[R_OBSR] = obs_r;
     if ((o.p.constraint_mask & 4) && o.env_nn.ok) {
-        double in[10] = {q[0], q[1], q[2], q[3], q[4], q[5], q[6], obs[0], obs[1], obs[2]};
+        double oa[3] = {obs[0], obs[1], obs[2]};
+        double dO[3][3] = {};  // d o_arm / d (x, y, theta)
+        if (NBASE > 0) {       // o_arm = Rz(th)^T (obs - [x, y, 0]) - mount
+            const double c = std::cos(q[2]), sn = std::sin(q[2]);
+            const double dx = obs[0] - q[0], dy = obs[1] - q[1], dz = obs[2];
+            oa[0] = (c * dx + sn * dy) - MOBILE_MOUNT[0];
+            oa[1] = (-sn * dx + c * dy) - MOBILE_MOUNT[1];
+            oa[2] = dz - MOBILE_MOUNT[2];
+            dO[0][0] = -c;  dO[1][0] = sn;  dO[2][0] = 0.0;   // d/dx
+            dO[0][1] = -sn; dO[1][1] = -c;  dO[2][1] = 0.0;   // d/dy
+            dO[0][2] = -sn * dx + c * dy; dO[1][2] = -c * dx - sn * dy; dO[2][2] = 0.0;  // d/dtheta
+        }
+        double in[10] = {qa[0], qa[1], qa[2], qa[3], qa[4], qa[5], qa[6], oa[0], oa[1], oa[2]};
         double out[9], jac[90];
         o.env_nn.eval(in, out, jac);
         for (int i = 0; i < 9; i++) {
             rec[R_ENV + i] = out[i];
-            for (int j = 0; j < 7; j++) rec[R_DENV + 7 * i + j] = jac[10 * i + j];  // 9x7 block (Q17)
+            for (int j = 0; j < 7; j++) rec[R_DENV + DOF * i + NBASE + j] = jac[10 * i + j];  // 9x7 arm block (Q17)
+            for (int b = 0; b < NBASE; b++)
+                rec[R_DENV + DOF * i + b] = jac[10 * i + 7] * dO[0][b] + jac[10 * i + 8] * dO[1][b] + jac[10 * i + 9] * dO[2][b];
         }
     } else {
         for (int i = 0; i < 9; i++) rec[R_ENV + i] = std::numeric_limits<double>::infinity();
@@ -734,7 +801,7 @@ static void stage_cost(const Oracle& o, const double* x, const double* u, const 
     } else {
         qc = p.q_c; ql = p.q_l; qo = p.q_ori;
     }
-    const double s = x[7], vs = x[8];
+    const double s = x[IS], vs = x[IVS];
     // getRefPoint :46-68 (Q2: ddz_ref = ddpos(1))
     double pr[3], dpr[3], ddp[3];
     o.track.pos(s, pr);
@@ -752,8 +819,8 @@ static void stage_cost(const Oracle& o, const double* x, const double* u, const 
     // d_total (3x9): q cols = Jv, s col = -T
     double dt[3][NX] = {};
     for (int i = 0; i < 3; i++) {
-        for (int j = 0; j < DOF; j++) dt[i][j] = rec[R_J + 7 * i + j];
-        dt[i][7] = -T[i];
+        for (int j = 0; j < DOF; j++) dt[i][j] = rec[R_J + DOF * i + j];
+        dt[i][IS] = -T[i];
     }
     double nel = std::sqrt(el[0] * el[0] + el[1] * el[1] + el[2] * el[2]);
     // d_lag = (T T^T) d_total + (T e^T + |e_l| I) d_T, d_T only in s col = ddr  (Q3)
@@ -762,7 +829,7 @@ static void stage_cost(const Oracle& o, const double* x, const double* u, const 
         for (int j = 0; j < NX; j++) {
             double a = T[i] * T[0] * dt[0][j] + T[i] * T[1] * dt[1][j] + T[i] * T[2] * dt[2][j];
             double b = 0;
-            if (j == 7) {
+            if (j == IS) {
                 for (int m = 0; m < 3; m++) b += (T[i] * et[m] + (i == m ? nel : 0.0)) * ddr[m];
             }
             dl[i][j] = a + b;
@@ -793,7 +860,7 @@ static void stage_cost(const Oracle& o, const double* x, const double* u, const 
     if (k != N) {
         double dq2 = 0;
         for (int j = 0; j < DOF; j++) dq2 += u[j] * u[j];
-        obj_i = p.r_dq * dq2 + p.r_dVs * std::pow(u[7], 2);
+        obj_i = p.r_dq * dq2 + p.r_dVs * std::pow(u[IDVS], 2);
     }
     // ---- singularity (:272-288)
     double obj_s = -p.q_sing * rec[R_MU];
@@ -807,14 +874,14 @@ static void stage_cost(const Oracle& o, const double* x, const double* u, const 
         for (int i = 0; i < 3; i++) { s1 += dc[i][j] * ec[i]; s2 += dl[i][j] * el[i]; }
         gxc[j] = 2.0 * CC0 * s1 + 2.0 * CC1 * s2;
     }
-    gxc[8] += 2.0 * p.q_vs * (vs - des);
+    gxc[IVS] += 2.0 * p.q_vs * (vs - des);
     for (int a = 0; a < NX; a++)
         for (int b = 0; b < NX; b++) {
             double s1 = 0, s2 = 0;
             for (int i = 0; i < 3; i++) { s1 += dc[i][a] * dc[i][b]; s2 += dl[i][a] * dl[i][b]; }
             hxc[a * NX + b] = 2.0 * CC0 * s1 + 2.0 * CC1 * s2;
         }
-    hxc[8 * NX + 8] += 2.0 * p.q_vs;
+    hxc[IVS * NX + IVS] += 2.0 * p.q_vs;
 
     // heading linearization :183-205 (Q23: '+' sign in the J_r^{-1} coefficient, as written)
     double Jri[9];
@@ -839,12 +906,12 @@ static void stage_cost(const Oracle& o, const double* x, const double* u, const 
     for (int i = 0; i < 3; i++) {
         for (int j = 0; j < DOF; j++) {
             double sacc = 0;
-            for (int m = 0; m < 3; m++) sacc += JRt[3 * i + m] * rec[R_J + 7 * (3 + m) + j];
+            for (int m = 0; m < 3; m++) sacc += JRt[3 * i + m] * rec[R_J + DOF * (3 + m) + j];
             dL[i][j] = sacc;
         }
         double sacc = 0;
         for (int m = 0; m < 3; m++) sacc += JRt[3 * i + m] * dRref[m];
-        dL[i][7] = -sacc;
+        dL[i][IS] = -sacc;
     }
     double gxh[NX], hxh[NX * NX];
     for (int j = 0; j < NX; j++) {
@@ -862,9 +929,9 @@ static void stage_cost(const Oracle& o, const double* x, const double* u, const 
     double gui[NU] = {}, huu[NU * NU] = {};
     if (k != N) {
         for (int j = 0; j < DOF; j++) gui[j] = 2.0 * p.r_dq * u[j];
-        gui[7] = 2.0 * p.r_dVs * u[7];
+        gui[IDVS] = 2.0 * p.r_dVs * u[IDVS];
         for (int j = 0; j < DOF; j++) huu[j * NU + j] = 2.0 * p.r_dq;
-        huu[7 * NU + 7] = 2.0 * p.r_dVs;
+        huu[IDVS * NU + IDVS] = 2.0 * p.r_dVs;
     }
     double gxs[NX] = {};
     for (int j = 0; j < DOF; j++) gxs[j] = -p.q_sing * rec[R_DMU + j];
@@ -942,12 +1009,12 @@ static void stage_constraints(const Oracle& o, const double* x, const double* u,
             double R = rbf(delta, md - r);
             if (k != N) {
                 double dot = 0;
-                for (int j = 0; j < DOF; j++) dot += (0.01 * rec[R_DENV + 7 * m + j]) * u[j];
+                for (int j = 0; j < DOF; j++) dot += (0.01 * rec[R_DENV + DOF * m + j]) * u[j];
                 out.l[2 + m] = -INF; out.u[2 + m] = 0.0; out.c[2 + m] = -dot + R;
                 if (want_jac) {
                     double dR = drbf(delta, md - r);
                     for (int j = 0; j < DOF; j++) {
-                        double g = 0.01 * rec[R_DENV + 7 * m + j];
+                        double g = 0.01 * rec[R_DENV + DOF * m + j];
                         out.cx[(2 + m) * NX + j] = dR * g;
                         out.cu[(2 + m) * NU + j] = -g;
                     }
@@ -967,8 +1034,8 @@ struct DenseQP {
     std::vector<double> P, g, A, c, l, u;
 };
 
-static inline const double* gx(const double* guess, int i) { return guess + 17 * i; }
-static inline const double* gu(const double* guess, int i) { return guess + 17 * i + 9; }
+static inline const double* gx(const double* guess, int i) { return guess + NXU * i; }
+static inline const double* gu(const double* guess, int i) { return guess + NXU * i + NX; }
 
 // setCost (:129-219) + setConstraints (:221-389).  want: 0 = obj/constr/l/u only, 1 = full.
 static void set_qp(const Oracle& o, const double* guess, const double* recs, const double* ucur, bool full, DenseQP& q) {
@@ -1072,8 +1139,8 @@ static void set_qp(const Oracle& o, const double* guess, const double* recs, con
             q.l[r0 + a] = p.lx[a];
             q.u[r0 + a] = p.ux[a];
         }
-        q.l[r0 + 7] = std::max(xi[7] - p.s_trust_region, 0.);
-        q.u[r0 + 7] = std::min(xi[7] + p.s_trust_region, L);
+        q.l[r0 + IS] = std::max(xi[IS] - p.s_trust_region, 0.);
+        q.u[r0 + IS] = std::min(xi[IS] + p.s_trust_region, L);
         if (i != N) {
             const double* ui = gu(guess, i);
             int r1 = Neq + NX * (N + 1) + NU * i;  // input bounds, Q1: columns NU*i (state columns)
@@ -1151,7 +1218,7 @@ constexpr double FEAS_TOL = 1e-9;
 // Stage vector z_k = [y(9) | w(7) | v(8)] (normalized step of x_k; w_k = previous joint-input step
 // v_{k-1}[0:7]; v_k = normalized step of u_k).  Dynamics: y_{k+1} = M y_k + G v_k, w_{k+1} = E v_k
 // with M = Tx^-1 A Tx, G = Tx^-1 B Tu.  y_0 = 0, w_0 = 0 (dynamics row block 0, osqp_interface.cpp:231-237).
-constexpr int NZ = 24, NXA = 16;
+constexpr int NXA = NX + DOF, NZ = NXA + NU;  // y | w | v
 
 struct SRow { double c[NZ]; double lb, ub; };
 struct SStage {
@@ -1207,11 +1274,11 @@ static void build_struct_qp(const Oracle& o, const double* guess, const double* 
         }
         if (k != N) {
             for (int a = 0; a < NU; a++) {
-                s.h[16 + a] = Tu[a] * co.fu[a];
-                for (int b = 0; b < NU; b++) s.H[(16 + a) * NZ + 16 + b] = Tu[a] * co.fuu[a * NU + b] * Tu[b];
+                s.h[NXA + a] = Tu[a] * co.fu[a];
+                for (int b = 0; b < NU; b++) s.H[(NXA + a) * NZ + NXA + b] = Tu[a] * co.fuu[a * NU + b] * Tu[b];
                 for (int b = 0; b < NX; b++) {
                     double v = Tx[b] * co.fxu[b * NU + a] * Tu[a];
-                    s.H[(16 + a) * NZ + b] = v; s.H[b * NZ + 16 + a] = v;
+                    s.H[(NXA + a) * NZ + b] = v; s.H[b * NZ + NXA + a] = v;
                 }
             }
             // ddq cost gradient + diagonal, coupling to v_{k-1} via w_k
@@ -1220,14 +1287,14 @@ static void build_struct_qp(const Oracle& o, const double* guess, const double* 
                 if (k == 0) gg = 2. * rddq * (uk[j] - gu(guess, k + 1)[j]);
                 else if (k == N - 1) gg = 2. * rddq * (uk[j] - gu(guess, k - 1)[j]);
                 else gg = 2. * rddq * (2. * uk[j] - gu(guess, k + 1)[j] - gu(guess, k - 1)[j]);
-                s.h[16 + j] += Tu[j] * gg;
+                s.h[NXA + j] += Tu[j] * gg;
                 double cii = (k == 0 || k == N - 1) ? 2. * rddq : 4. * rddq;
-                s.H[(16 + j) * NZ + 16 + j] += Tu[j] * cii * Tu[j];
+                s.H[(NXA + j) * NZ + NXA + j] += Tu[j] * cii * Tu[j];
                 if (k >= 1) {  // coupling between v_{k-1} (= w_k) and v_k, present when k-1 != N-1
                     double cij = -2. * rddq;
                     double v = Tu[j] * cij * Tu[j];
-                    s.H[(16 + j) * NZ + 9 + j] += v;
-                    s.H[(9 + j) * NZ + 16 + j] += v;
+                    s.H[(NXA + j) * NZ + NX + j] += v;
+                    s.H[(NX + j) * NZ + NXA + j] += v;
                 }
             }
         }
@@ -1251,7 +1318,7 @@ static void build_struct_qp(const Oracle& o, const double* guess, const double* 
         // state bounds
         for (int a = 0; a < NX; a++) {
             double lo = p.lx[a], hi = p.ux[a];
-            if (a == 7) { lo = std::max(xk[7] - p.s_trust_region, 0.); hi = std::min(xk[7] + p.s_trust_region, L); }
+            if (a == IS) { lo = std::max(xk[IS] - p.s_trust_region, 0.); hi = std::min(xk[IS] + p.s_trust_region, L); }
             add_box(k, a, (lo - xk[a]) / Tx[a], (hi - xk[a]) / Tx[a]);
         }
         if (k != N) {
@@ -1270,11 +1337,11 @@ static void build_struct_qp(const Oracle& o, const double* guess, const double* 
                     c = 1. / p.Ts * uk[j];
                     lo = p.lddq[j] + 1. / p.Ts * ucur[j];
                     hi = p.uddq[j] + 1. / p.Ts * ucur[j];
-                    r.c[16 + j] = 1.0;
+                    r.c[NXA + j] = 1.0;
                 } else {
                     c = 1. / p.Ts * (uk[j] - gu(guess, k - 1)[j]);
                     lo = p.lddq[j]; hi = p.uddq[j];
-                    r.c[16 + j] = 1.0; r.c[9 + j] = -1.0;
+                    r.c[NXA + j] = 1.0; r.c[NX + j] = -1.0;
                 }
                 r.lb = (lo - c) / coef; r.ub = (hi - c) / coef;
                 if (zshift) {  // + v_k[j] - v_{k-1}[j] (k = 0: v_0[j]) of the step
@@ -1292,13 +1359,13 @@ static void build_struct_qp(const Oracle& o, const double* guess, const double* 
                 if (lo_inf && hi_inf) continue;
                 SRow row; std::memset(row.c, 0, sizeof row.c);
                 for (int a = 0; a < NX; a++) row.c[a] = cn.cx[r * NX + a] * Tx[a];
-                for (int b = 0; b < NU; b++) row.c[16 + b] = cn.cu[r * NU + b] * Tu[b];
+                for (int b = 0; b < NU; b++) row.c[NXA + b] = cn.cu[r * NU + b] * Tu[b];
                 row.lb = lo_inf ? -INF : lo;
                 row.ub = hi_inf ? INF : hi;
                 if (zshift) {  // + a . y_k[0:7] + bv . v_k[0:7] of the step (the row's other entries are 0)
                     double sh = 0;
                     for (int a = 0; a < DOF; a++) sh += row.c[a] * ysh(k, a);
-                    for (int b = 0; b < DOF; b++) sh += row.c[16 + b] * vsh(k, b);
+                    for (int b = 0; b < DOF; b++) sh += row.c[NXA + b] * vsh(k, b);
                     if (!lo_inf) row.lb = lo + sh;
                     if (!hi_inf) row.ub = hi + sh;
                 }
@@ -1374,7 +1441,7 @@ struct Riccati {
             for (int b = 0; b < NX; b++) At[a * NXA + b] = S.M[a * NX + b];
             for (int b = 0; b < NU; b++) Bt[a * NU + b] = S.G[a * NU + b];
         }
-        for (int j = 0; j < DOF; j++) Bt[(9 + j) * NU + j] = 1.0;
+        for (int j = 0; j < DOF; j++) Bt[(NX + j) * NU + j] = 1.0;
         double P[NXA * NXA];
         const double* HN = &Hs[(size_t)N * NZ * NZ];
         for (int a = 0; a < NXA; a++)
@@ -1390,12 +1457,12 @@ struct Riccati {
             for (int i = 0; i < NU; i++)
                 for (int j = 0; j < NU; j++) {
                     double s = 0; for (int m = 0; m < NXA; m++) s += Bt[m * NU + i] * PB[m * NU + j];
-                    F[i * NU + j] = H[(16 + i) * NZ + 16 + j] + s;
+                    F[i * NU + j] = H[(NXA + i) * NZ + NXA + j] + s;
                 }
             for (int i = 0; i < NU; i++)
                 for (int j = 0; j < NXA; j++) {
                     double s = 0; for (int m = 0; m < NXA; m++) s += Bt[m * NU + i] * PA[m * NXA + j];
-                    Gk[i * NXA + j] = H[(16 + i) * NZ + j] + s;
+                    Gk[i * NXA + j] = H[(NXA + i) * NZ + j] + s;
                 }
             for (int i = 0; i < NXA; i++)
                 for (int j = 0; j < NXA; j++) {
@@ -1429,14 +1496,14 @@ struct Riccati {
             for (int b = 0; b < NX; b++) At[a * NXA + b] = S.M[a * NX + b];
             for (int b = 0; b < NU; b++) Bt[a * NU + b] = S.G[a * NU + b];
         }
-        for (int j = 0; j < DOF; j++) Bt[(9 + j) * NU + j] = 1.0;
+        for (int j = 0; j < DOF; j++) Bt[(NX + j) * NU + j] = 1.0;
         std::vector<double> kf((size_t)N * NU);
         double pv[NXA];
         for (int a = 0; a < NXA; a++) pv[a] = gs[(size_t)N * NZ + a];
         for (int k = N - 1; k >= 0; k--) {
             const double* g = &gs[(size_t)k * NZ];
             double f[NU];
-            for (int i = 0; i < NU; i++) { double s = 0; for (int m = 0; m < NXA; m++) s += Bt[m * NU + i] * pv[m]; f[i] = g[16 + i] + s; }
+            for (int i = 0; i < NU; i++) { double s = 0; for (int m = 0; m < NXA; m++) s += Bt[m * NU + i] * pv[m]; f[i] = g[NXA + i] + s; }
             chol_solve(&LF[(size_t)k * NU * NU], NU, f);
             for (int i = 0; i < NU; i++) kf[(size_t)k * NU + i] = -f[i];
             const double* Gk = &Gm[(size_t)k * NU * NXA];
@@ -1454,11 +1521,11 @@ struct Riccati {
             double* z = &dz[(size_t)k * NZ];
             for (int a = 0; a < NXA; a++) z[a] = x[a];
             const double* Kk = &K[(size_t)k * NU * NXA];
-            for (int i = 0; i < NU; i++) { double s = 0; for (int m = 0; m < NXA; m++) s += Kk[i * NXA + m] * x[m]; z[16 + i] = s + kf[(size_t)k * NU + i]; }
+            for (int i = 0; i < NU; i++) { double s = 0; for (int m = 0; m < NXA; m++) s += Kk[i * NXA + m] * x[m]; z[NXA + i] = s + kf[(size_t)k * NU + i]; }
             double xn[NXA];
             for (int a = 0; a < NXA; a++) {
                 double s = 0; for (int m = 0; m < NXA; m++) s += At[a * NXA + m] * x[m];
-                for (int m = 0; m < NU; m++) s += Bt[a * NU + m] * z[16 + m];
+                for (int m = 0; m < NU; m++) s += Bt[a * NU + m] * z[NXA + m];
                 xn[a] = s;
             }
             std::memcpy(x, xn, sizeof xn);
@@ -1619,7 +1686,7 @@ static int solve_struct_ipm_from(const StructQP& S, std::vector<double>& step, i
     for (int k = 0; k <= N; k++) {
         for (int a = 0; a < NX; a++) step[(size_t)NX * k + a] = z[(size_t)k * NZ + a];
         if (k < N)
-            for (int b = 0; b < NU; b++) step[(size_t)NX * (N + 1) + NU * k + b] = z[(size_t)k * NZ + 16 + b];
+            for (int b = 0; b < NU; b++) step[(size_t)NX * (N + 1) + NU * k + b] = z[(size_t)k * NZ + NXA + b];
     }
     return 0;
 }
@@ -1775,9 +1842,9 @@ static void denorm_add(const Oracle& o, const double* base, const std::vector<do
     // out = base + alpha * deNormalizeStep(step)  (:859-869), base/out in (N+1)x17 layout
     const int N = o.p.N;
     for (int i = 0; i <= N; i++) {
-        for (int a = 0; a < NX; a++) out[17 * i + a] = base[17 * i + a] + alpha * (o.p.Tx[a] * step[(size_t)NX * i + a]);
+        for (int a = 0; a < NX; a++) out[NXU * i + a] = base[NXU * i + a] + alpha * (o.p.Tx[a] * step[(size_t)NX * i + a]);
         for (int b = 0; b < NU; b++)
-            out[17 * i + 9 + b] = (i != N) ? base[17 * i + 9 + b] + alpha * (o.p.Tu[b] * step[(size_t)NX * (N + 1) + NU * i + b]) : base[17 * i + 9 + b];
+            out[NXU * i + NX + b] = (i != N) ? base[NXU * i + NX + b] + alpha * (o.p.Tu[b] * step[(size_t)NX * (N + 1) + NU * i + b]) : base[NXU * i + NX + b];
     }
 }
 
@@ -1791,11 +1858,11 @@ static thread_local double* g_trace = nullptr;
 // u(x') - d with d = c(x') - A step (:676-678).  Returns the QP status; `out` is the new step on success.
 static void soc_point(const Oracle& o, const double* guess, const std::vector<double>& step, std::vector<double>& xs) {
     const int N = o.p.N;
-    xs.assign(guess, guess + (size_t)(N + 1) * 17);
+    xs.assign(guess, guess + (size_t)(N + 1) * NXU);
     for (int k = 0; k <= N; k++) {
-        for (int a = 0; a < NX; a++) xs[17 * k + a] = guess[17 * k + a] + step[(size_t)NX * k + a];
+        for (int a = 0; a < NX; a++) xs[NXU * k + a] = guess[NXU * k + a] + step[(size_t)NX * k + a];
         if (k < N)
-            for (int b = 0; b < NU; b++) xs[17 * k + 9 + b] = guess[17 * k + 9 + b] + step[(size_t)NX * (N + 1) + NU * k + b];
+            for (int b = 0; b < NU; b++) xs[NXU * k + NX + b] = guess[NXU * k + NX + b] + step[(size_t)NX * (N + 1) + NU * k + b];
     }
 }
 static int soc_dense(const Oracle& o, const DenseQP& q, const double* guess, const double* recs, const double* ucur,
@@ -1833,12 +1900,12 @@ static int solve_ocp(const Oracle& o, double* guess, const double* recs, const d
     const int nv = o.nvar();
     std::vector<double> step(nv, 0.0);
     std::vector<Filter> filter;
-    std::vector<double> zero((size_t)(N + 1) * 17, 0.0);
-    for (int i = 0; i <= N; i++) for (int a = 0; a < NX; a++) zero[17 * i + a] = guess[a];
+    std::vector<double> zero((size_t)(N + 1) * NXU, 0.0);
+    for (int i = 0; i <= N; i++) for (int a = 0; a < NX; a++) zero[NXU * i + a] = guess[a];
     int status = MAX_ITER_EXCEEDED;
     bool status_set = false;
     int it;
-    std::vector<double> trial((size_t)(N + 1) * 17);
+    std::vector<double> trial((size_t)(N + 1) * NXU);
     for (it = 0; it < p.max_iter; it++) {
         // setQP + PD / NaN checks of the normalized Hessian (:445-473)
         bool nan = false, pd = true;
@@ -1893,9 +1960,9 @@ static int solve_ocp(const Oracle& o, double* guess, const double* recs, const d
                 double prev_l = 0;  // L_{k,k-1}
                 double prev_d = 0;
                 for (int k = 0; k < N; k++) {
-                    double dk = S.st[k].H[(16 + b) * NZ + 16 + b];
+                    double dk = S.st[k].H[(NXA + b) * NZ + NXA + b];
                     if (std::isnan(dk)) nan = true;
-                    double off = (k >= 1 && b < DOF) ? S.st[k].H[(16 + b) * NZ + 9 + b] : 0.0;
+                    double off = (k >= 1 && b < DOF) ? S.st[k].H[(NXA + b) * NZ + NX + b] : 0.0;
                     double l = (k >= 1) ? off / prev_d : 0.0;
                     double d = dk - l * l;
                     if (d <= 0) { pd = false; break; }
@@ -1942,7 +2009,7 @@ static int solve_ocp(const Oracle& o, double* guess, const double* recs, const d
         }
         // take step :549-551
         denorm_add(o, guess, step, alpha, trial.data());
-        std::memcpy(guess, trial.data(), sizeof(double) * (N + 1) * 17);
+        std::memcpy(guess, trial.data(), sizeof(double) * (N + 1) * NXU);
         double nrm = 0;
         for (int i = 0; i < nv; i++) nrm = std::max(nrm, std::fabs(step[i]));
         double pn = alpha * nrm;
@@ -1952,8 +2019,8 @@ static int solve_ocp(const Oracle& o, double* guess, const double* recs, const d
     if (it == p.max_iter) status = MAX_ITER_EXCEEDED;
     (void)status_set;
     if (iters_out) *iters_out = it;
-    if (status == SOLVED) std::memcpy(opt_sol, guess, sizeof(double) * (N + 1) * 17);
-    else std::memcpy(opt_sol, zero.data(), sizeof(double) * (N + 1) * 17);
+    if (status == SOLVED) std::memcpy(opt_sol, guess, sizeof(double) * (N + 1) * NXU);
+    else std::memcpy(opt_sol, zero.data(), sizeof(double) * (N + 1) * NXU);
     return status;
 }
 
@@ -1961,17 +2028,17 @@ static int solve_ocp(const Oracle& o, double* guess, const double* recs, const d
 static void rk4(const double* x, const double* u, double ts, double* out) {
     auto f = [&](const double* xx, double* o) {
         for (int j = 0; j < DOF; j++) o[j] = u[j];
-        o[7] = xx[8]; o[8] = u[7];
+        o[IS] = xx[IVS]; o[IVS] = u[IDVS];
     };
-    double k1[9], k2[9], k3[9], k4[9], t[9];
+    double k1[NX], k2[NX], k3[NX], k4[NX], t[NX];
     f(x, k1);
-    for (int i = 0; i < 9; i++) t[i] = x[i] + ts / 2. * k1[i];
+    for (int i = 0; i < NX; i++) t[i] = x[i] + ts / 2. * k1[i];
     f(t, k2);
-    for (int i = 0; i < 9; i++) t[i] = x[i] + ts / 2. * k2[i];
+    for (int i = 0; i < NX; i++) t[i] = x[i] + ts / 2. * k2[i];
     f(t, k3);
-    for (int i = 0; i < 9; i++) t[i] = x[i] + ts * k3[i];
+    for (int i = 0; i < NX; i++) t[i] = x[i] + ts * k3[i];
     f(t, k4);
-    for (int i = 0; i < 9; i++) out[i] = x[i] + ts * (k1[i] / 6. + k2[i] / 3. + k3[i] / 3. + k4[i] / 6.);
+    for (int i = 0; i < NX; i++) out[i] = x[i] + ts * (k1[i] / 6. + k2[i] / 3. + k3[i] / 3. + k4[i] / 6.);
 }
 
 // MPC::runMPC_ — mpc.cpp:104-190 for one instance
@@ -1980,34 +2047,34 @@ static void prepare_one(const Oracle& o, double* x0, const double* u0, const dou
                         int* fails, double* recs) {
     const OracleParams& p = o.p;
     const int N = p.N;
-    double last_s = x0[7];
-    double ee[3], J[42];
+    double last_s = x0[IS];
+    double ee[3], J[6 * DOF];
     fk(x0, ee, nullptr, nullptr);
-    x0[7] = o.track.project(last_s, ee);
+    x0[IS] = o.track.project(last_s, ee);
     fk(x0, nullptr, nullptr, J);
     double ev[3] = {0, 0, 0};
-    for (int i = 0; i < 3; i++) { double s = 0; for (int j = 0; j < DOF; j++) s += J[7 * i + j] * u0[j]; ev[i] = s; }
+    for (int i = 0; i < 3; i++) { double s = 0; for (int j = 0; j < DOF; j++) s += J[DOF * i + j] * u0[j]; ev[i] = s; }
     double dir[3];
-    o.track.dpos(x0[7], dir);
-    x0[8] = ev[0] * dir[0] + ev[1] * dir[1] + ev[2] * dir[2];
-    if (std::fabs(last_s - x0[7]) > p.guess_max_dist) { *valid = 0; (*fails)++; }
+    o.track.dpos(x0[IS], dir);
+    x0[IVS] = ev[0] * dir[0] + ev[1] * dir[1] + ev[2] * dir[2];
+    if (std::fabs(last_s - x0[IS]) > p.guess_max_dist) { *valid = 0; (*fails)++; }
     const double L = o.track.length();
     if (*valid) {  // updateInitialGuess :54-68
-        for (int i = 1; i < N; i++) std::memcpy(guess + 17 * (i - 1), guess + 17 * i, sizeof(double) * 17);
-        std::memcpy(guess, x0, sizeof(double) * 9);
-        std::memcpy(guess + 17 * (N - 1), guess + 17 * (N - 2), sizeof(double) * 17);
-        rk4(guess + 17 * (N - 1), guess + 17 * (N - 1) + 9, p.Ts, guess + 17 * N);
-        for (int b = 0; b < NU; b++) guess[17 * N + 9 + b] = 0.0;
+        for (int i = 1; i < N; i++) std::memcpy(guess + NXU * (i - 1), guess + NXU * i, sizeof(double) * NXU);
+        std::memcpy(guess, x0, sizeof(double) * NX);
+        std::memcpy(guess + NXU * (N - 1), guess + NXU * (N - 2), sizeof(double) * NXU);
+        rk4(guess + NXU * (N - 1), guess + NXU * (N - 1) + NX, p.Ts, guess + NXU * N);
+        for (int b = 0; b < NU; b++) guess[NXU * N + NX + b] = 0.0;
     } else {  // generateNewInitialGuess :79-89
         for (int i = 0; i <= N; i++) {
-            std::memcpy(guess + 17 * i, x0, sizeof(double) * 9);
-            for (int b = 0; b < NU; b++) guess[17 * i + 9 + b] = 0.0;
+            std::memcpy(guess + NXU * i, x0, sizeof(double) * NX);
+            for (int b = 0; b < NU; b++) guess[NXU * i + NX + b] = 0.0;
         }
         *valid = 1;
     }
-    for (int i = 1; i <= N; i++) guess[17 * i + 7] = std::min(guess[17 * i + 7], L);  // unwrapInitialGuess
+    for (int i = 1; i <= N; i++) guess[NXU * i + IS] = std::min(guess[NXU * i + IS], L);  // unwrapInitialGuess
     // setInitialGuess + setEnvData: robot records at the warm start (Q4)
-    for (int i = 0; i <= N; i++) robot_record(o, guess + 17 * i, obs, obs[3], &recs[(size_t)REC * i]);
+    for (int i = 0; i <= N; i++) robot_record(o, guess + NXU * i, obs, obs[3], &recs[(size_t)REC * i]);
 }
 
 static int run_mpc_one(const Oracle& o, double* x0, const double* u0, const double* obs, double* guess, int* valid,
@@ -2016,13 +2083,13 @@ static int run_mpc_one(const Oracle& o, double* x0, const double* u0, const doub
     const int N = p.N;
     std::vector<double> recs((size_t)REC * (N + 1));
     prepare_one(o, x0, u0, obs, guess, valid, fails, recs.data());
-    std::vector<double> sol((size_t)(N + 1) * 17);
+    std::vector<double> sol((size_t)(N + 1) * NXU);
     int status = solve_ocp(o, guess, recs.data(), u0, sol.data(), iters);
-    std::memcpy(guess, sol.data(), sizeof(double) * 17 * (N + 1));  // initial_guess_ = opt_sol
+    std::memcpy(guess, sol.data(), sizeof(double) * NXU * (N + 1));  // initial_guess_ = opt_sol
     if (status == SOLVED) { *valid = 1; *fails = 0; }
     else { *valid = 0; (*fails)++; }
-    std::memcpy(u0_out, guess + 9, sizeof(double) * 8);
-    std::memcpy(horizon, guess, sizeof(double) * 17 * (N + 1));
+    std::memcpy(u0_out, guess + NX, sizeof(double) * NU);
+    std::memcpy(horizon, guess, sizeof(double) * NXU * (N + 1));
     *ok = (status == SOLVED || (status == MAX_ITER_EXCEEDED && *fails < 5)) ? 1 : 0;
     return status;
 }
@@ -2064,16 +2131,7 @@ void oracle_track_path(void* h, double* s, double* X, double* Y, double* Z, doub
 void oracle_fk(const double* q, double* pos3, double* R9, double* J42) { fk(q, pos3, R9, J42); }
 double oracle_manipulability(const double* q) { return manipulability(q); }
 void oracle_fk_frame(const double* q, int frame, double* pos3, double* R9, double* J42) { fk_frame(q, frame, pos3, R9, J42); }
-double oracle_manip_from_J(const double* J42) {  // robot_model.cpp:431-435 on a given Jacobian
-    double A[36];
-    for (int i = 0; i < 6; i++)
-        for (int j = 0; j < 6; j++) {
-            double s = 0;
-            for (int k = 0; k < 7; k++) s += J42[7 * i + k] * J42[7 * j + k];
-            A[6 * i + j] = s;
-        }
-    return std::sqrt(det_lu(A, 6));
-}
+double oracle_manip_from_J(const double* J) { return manip_of_J(J); }  // robot_model.cpp:431-435, J 6 x DOF
 void oracle_dmanipulability(const double* q, double* d7) { dmanipulability(q, d7); }
 void oracle_self_mlp(void* h, const double* q7, double* d, double* grad7) { ((Oracle*)h)->self_nn.eval(q7, d, grad7); }
 void oracle_env_mlp(void* h, const double* in10, double* d9, double* jac90) { ((Oracle*)h)->env_nn.eval(in10, d9, jac90); }
@@ -2149,10 +2207,10 @@ void oracle_rk4(const double* x9, const double* u8, double ts, double* out9) { r
 void oracle_sim_time_step(const double* x9, const double* u8, double ts, double* out9) {  // integrator.cpp:55-68
     const double fine = 0.001;
     int steps = (int)(ts / fine);
-    double x[9];
-    std::memcpy(x, x9, 72);
-    for (int i = 0; i < steps; i++) { double t[9]; rk4(x, u8, fine, t); std::memcpy(x, t, 72); }
-    std::memcpy(out9, x, 72);
+    double x[NX];
+    std::memcpy(x, x9, sizeof(double) * NX);
+    for (int i = 0; i < steps; i++) { double t[NX]; rk4(x, u8, fine, t); std::memcpy(x, t, sizeof(double) * NX); }
+    std::memcpy(out9, x, sizeof(double) * NX);
 }
 int oracle_run_mpc_trace(void* h, int B, double* x0, const double* u0, const double* obs, double* guess, int* valid,
                          int* fails, double* u0_out, double* horizon, int* status, int* ok, int* sqp_iters, double* trace) {
@@ -2166,8 +2224,8 @@ int oracle_run_mpc_trace(void* h, int B, double* x0, const double* u0, const dou
         int it = 0;
         g_trace = trace ? trace + (size_t)32 * b : nullptr;
         if (g_trace) for (int i = 0; i < 32; i++) g_trace[i] = 0.0;
-        status[b] = run_mpc_one(*o, x0 + 9 * b, u0 + 8 * b, obs + 4 * b, guess + (size_t)17 * (N + 1) * b, valid + b,
-                                fails + b, u0_out + 8 * b, horizon + (size_t)17 * (N + 1) * b, ok + b, &it);
+        status[b] = run_mpc_one(*o, x0 + NX * b, u0 + NU * b, obs + 4 * b, guess + (size_t)NXU * (N + 1) * b, valid + b,
+                                fails + b, u0_out + NU * b, horizon + (size_t)NXU * (N + 1) * b, ok + b, &it);
         if (sqp_iters) sqp_iters[b] = it;
         g_trace = nullptr;
     }
@@ -2178,6 +2236,7 @@ int oracle_run_mpc(void* h, int B, double* x0, const double* u0, const double* o
     return oracle_run_mpc_trace(h, B, x0, u0, obs, guess, valid, fails, u0_out, horizon, status, ok, sqp_iters, nullptr);
 }
 int oracle_rec_size(void) { return REC; }
+int oracle_dof(void) { return DOF; }
 // CubicSpline (cubic_spline.cpp:126-246) on (x, y): value, first and second derivative at xq
 void oracle_cubic_spline(int n, const double* x, const double* y, int regular, int m, const double* xq, double* out3) {
     CubicSpline sp;
@@ -2193,7 +2252,7 @@ int oracle_prepare(void* h, int B, double* x0, const double* u0, const double* o
     Oracle* o = (Oracle*)h;
     const int N = o->p.N;
     for (int b = 0; b < B; b++)
-        prepare_one(*o, x0 + 9 * b, u0 + 8 * b, obs + 4 * b, guess + (size_t)17 * (N + 1) * b, valid + b, fails + b,
+        prepare_one(*o, x0 + NX * b, u0 + NU * b, obs + 4 * b, guess + (size_t)NXU * (N + 1) * b, valid + b, fails + b,
                     recs + (size_t)REC * (N + 1) * b);
     return 0;
 }

@@ -16,6 +16,13 @@
  */
 #ifndef MPCC_ORACLE_API_H
 #define MPCC_ORACLE_API_H
+/* Robot: ORC_DOF 7 = Franka Panda (liboracle.so), 10 = Husky+Panda mobile manipulator
+ * (liboracle_mobile.so, BASELINE configs[3]); arrays below are sized by it. */
+#ifndef ORC_DOF
+#define ORC_DOF 7
+#endif
+#define ORC_NX (ORC_DOF + 2)
+#define ORC_NU (ORC_DOF + 1)
 #ifdef __cplusplus
 extern "C" {
 #endif
@@ -39,9 +46,9 @@ typedef struct {
     double con_tol_selcol, con_tol_sing, con_tol_envcol;
     /* Bounds (bounds.cpp) */
     double s_trust_region;
-    double lx[9], ux[9], lu[8], uu[8], lddq[7], uddq[7];
+    double lx[ORC_NX], ux[ORC_NX], lu[ORC_NU], uu[ORC_NU], lddq[ORC_DOF], uddq[ORC_DOF];
     /* NormalizationParam diag(T_x), diag(T_u) */
-    double Tx[9], Tu[8];
+    double Tx[ORC_NX], Tu[ORC_NU];
     /* SQPParam */
     double eps_prim, eps_dual, line_search_tau, line_search_eta, line_search_rho;
     int    max_iter, line_search_max_iter, do_SOC, use_BFGS;
@@ -56,6 +63,7 @@ typedef struct {
 } OracleOptions;
 
 void*  oracle_create(const OracleParams* p, const char* nn_dir, OracleOptions opt);
+int    oracle_dof(void);  /* ORC_DOF of this build */
 void   oracle_destroy(void* h);
 void   oracle_set_params(void* h, const OracleParams* p);
 /* MPC::setTrack(X,Y,Z,R) -> ArcLengthSpline::gen6DSpline (arc_length_spline.cpp:213-265) */

@@ -18,23 +18,34 @@ DP = C.POINTER(C.c_double)
 IP = C.POINTER(C.c_int)
 
 
-class OracleParams(C.Structure):
-    _fields_ = [
-        ("N", C.c_int), ("Ts", D), ("constraint_mask", C.c_int),
-        ("proj_max_dist", D), ("guess_max_dist", D),
-        ("desired_ee_velocity", D), ("deacc_ratio", D), ("cost_tol_selcol", D), ("cost_tol_sing", D),
-        ("q_c", D), ("q_c_N_mult", D), ("q_l", D), ("q_vs", D), ("q_ori", D), ("q_sing", D),
-        ("r_dq", D), ("r_dVs", D), ("q_c_red_ratio", D), ("q_l_inc_ratio", D), ("q_ori_red_ratio", D),
-        ("qp_r_ddq", D),
-        ("con_tol_selcol", D), ("con_tol_sing", D), ("con_tol_envcol", D),
-        ("s_trust_region", D),
-        ("lx", D * 9), ("ux", D * 9), ("lu", D * 8), ("uu", D * 8), ("lddq", D * 7), ("uddq", D * 7),
-        ("Tx", D * 9), ("Tu", D * 8),
-        ("eps_prim", D), ("eps_dual", D), ("line_search_tau", D), ("line_search_eta", D),
-        ("line_search_rho", D),
-        ("max_iter", C.c_int), ("line_search_max_iter", C.c_int), ("do_SOC", C.c_int), ("use_BFGS", C.c_int),
-        ("vio_floor", D),
-    ]
+def _params_struct(dof):
+    nx, nu = dof + 2, dof + 1
+
+    class _P(C.Structure):
+        _fields_ = [
+            ("N", C.c_int), ("Ts", D), ("constraint_mask", C.c_int),
+            ("proj_max_dist", D), ("guess_max_dist", D),
+            ("desired_ee_velocity", D), ("deacc_ratio", D), ("cost_tol_selcol", D), ("cost_tol_sing", D),
+            ("q_c", D), ("q_c_N_mult", D), ("q_l", D), ("q_vs", D), ("q_ori", D), ("q_sing", D),
+            ("r_dq", D), ("r_dVs", D), ("q_c_red_ratio", D), ("q_l_inc_ratio", D), ("q_ori_red_ratio", D),
+            ("qp_r_ddq", D),
+            ("con_tol_selcol", D), ("con_tol_sing", D), ("con_tol_envcol", D),
+            ("s_trust_region", D),
+            ("lx", D * nx), ("ux", D * nx), ("lu", D * nu), ("uu", D * nu), ("lddq", D * dof), ("uddq", D * dof),
+            ("Tx", D * nx), ("Tu", D * nu),
+            ("eps_prim", D), ("eps_dual", D), ("line_search_tau", D), ("line_search_eta", D),
+            ("line_search_rho", D),
+            ("max_iter", C.c_int), ("line_search_max_iter", C.c_int), ("do_SOC", C.c_int), ("use_BFGS", C.c_int),
+            ("vio_floor", D),
+        ]
+    _P.__name__ = f"OracleParams{dof}"
+    return _P
+
+
+OracleParams = _params_struct(7)
+OracleParamsMobile = _params_struct(10)
+PARAMS = {7: OracleParams, 10: OracleParamsMobile}
+LIBS = {7: "liboracle.so", 10: "liboracle_mobile.so"}
 
 
 class OracleOptions(C.Structure):
@@ -51,19 +62,21 @@ def build(quiet=True):
     return LIB_PATH
 
 
-_lib = None
+_libs = {}
 
 
-def lib():
-    global _lib
-    if _lib is None:
-        if not os.path.exists(LIB_PATH):
+def lib(dof=7):
+    """The oracle build for a robot: dof 7 = Panda (liboracle.so), 10 = Husky+Panda (liboracle_mobile.so)."""
+    if dof not in _libs:
+        path = os.path.join(HERE, "_build", LIBS[dof])
+        if not os.path.exists(path):
             build()
-        L = C.CDLL(LIB_PATH)
+        L = C.CDLL(path)
+        OP = PARAMS[dof]
         L.oracle_create.restype = C.c_void_p
-        L.oracle_create.argtypes = [C.POINTER(OracleParams), C.c_char_p, OracleOptions]
+        L.oracle_create.argtypes = [C.POINTER(OP), C.c_char_p, OracleOptions]
         L.oracle_destroy.argtypes = [C.c_void_p]
-        L.oracle_set_params.argtypes = [C.c_void_p, C.POINTER(OracleParams)]
+        L.oracle_set_params.argtypes = [C.c_void_p, C.POINTER(OP)]
         L.oracle_set_track.argtypes = [C.c_void_p, C.c_int, DP, DP, DP, DP]
         L.oracle_track_length.restype = D
         L.oracle_track_length.argtypes = [C.c_void_p]
@@ -100,9 +113,10 @@ def lib():
         L.oracle_fk_frame.argtypes = [DP, C.c_int, DP, DP, DP]
         L.oracle_manip_from_J.restype = D
         L.oracle_manip_from_J.argtypes = [DP]
-        assert L.oracle_rec_size() == REC_SIZE
-        _lib = L
-    return _lib
+        L.oracle_dof.restype = C.c_int
+        assert L.oracle_dof() == dof and L.oracle_rec_size() == 24 + 17 * dof
+        _libs[dof] = L
+    return _libs[dof]
 
 
 def _dp(a):
@@ -120,9 +134,9 @@ def _f64(a, shape=None):
     return a
 
 
-def make_params(d):
+def make_params(d, dof=7):
     """OracleParams from a dict of resolved values (see tests/refparams.py)."""
-    p = OracleParams()
+    p = PARAMS[dof]()
     for name, _ in OracleParams._fields_:
         v = d[name]
         f = getattr(p, name)
@@ -135,10 +149,14 @@ def make_params(d):
 
 
 class Oracle:
-    def __init__(self, params: dict, nn_dir: str, qp_mode=0, nthreads=1):
-        self.L = lib()
+    def __init__(self, params: dict, nn_dir: str, qp_mode=0, nthreads=1, dof=7):
+        self.dof = dof
+        self.NX, self.NU = dof + 2, dof + 1
+        self.NXU = self.NX + self.NU
+        self.REC = 24 + 17 * dof
+        self.L = lib(dof)
         self.params = dict(params)
-        self._p = make_params(params)
+        self._p = make_params(params, dof)
         opt = OracleOptions(qp_mode, nthreads)
         self.h = self.L.oracle_create(C.byref(self._p), nn_dir.encode() if nn_dir else None, opt)
         self.N = params["N"]
@@ -156,7 +174,7 @@ class Oracle:
 
     def set_params(self, params: dict):
         self.params = dict(params)
-        self._p = make_params(params)
+        self._p = make_params(params, self.dof)
         self.L.oracle_set_params(self.h, C.byref(self._p))
 
     def set_track(self, X, Y, Z, R):
@@ -176,9 +194,9 @@ class Oracle:
     # ---- kinematics
     def fk(self, q):
         q = _f64(q)
-        p, R, J = np.zeros(3), np.zeros(9), np.zeros(42)
+        p, R, J = np.zeros(3), np.zeros(9), np.zeros(6 * self.dof)
         self.L.oracle_fk(_dp(q), _dp(p), _dp(R), _dp(J))
-        return p, R.reshape(3, 3), J.reshape(6, 7)
+        return p, R.reshape(3, 3), J.reshape(6, self.dof)
 
     def fk_frame(self, q, frame):
         """RobotModel frame 1..9 (panda_link0..7, panda_hand_tcp): position, rotation, 6x7 Jacobian."""
@@ -188,13 +206,13 @@ class Oracle:
         return p, R.reshape(3, 3), J.reshape(6, 7)
 
     def manip_from_J(self, J):
-        return self.L.oracle_manip_from_J(_dp(_f64(J).reshape(42)))
+        return self.L.oracle_manip_from_J(_dp(_f64(J).reshape(6 * self.dof)))
 
     def manipulability(self, q):
         return self.L.oracle_manipulability(_dp(_f64(q)))
 
     def dmanipulability(self, q):
-        d = np.zeros(7)
+        d = np.zeros(self.dof)
         self.L.oracle_dmanipulability(_dp(_f64(q)), _dp(d))
         return d
 
@@ -218,28 +236,31 @@ class Oracle:
         return self.L.oracle_project(self.h, float(s), _dp(_f64(ee)))
 
     def robot_record(self, q, obs=(3.0, 3.0, 3.0), obs_r=0.0):
-        rec = np.zeros(REC_SIZE)
-        self.L.oracle_robot_record(self.h, _dp(_f64(q)[:7].copy()), _dp(_f64(obs)), float(obs_r), _dp(rec))
+        rec = np.zeros(self.REC)
+        self.L.oracle_robot_record(self.h, _dp(_f64(q)[:self.dof].copy()), _dp(_f64(obs)), float(obs_r), _dp(rec))
         return rec
 
     def stage_cost(self, x, u, rec, k):
         obj = np.zeros(1)
-        fx, fu, fxx, fuu, fxu = np.zeros(9), np.zeros(8), np.zeros(81), np.zeros(64), np.zeros(72)
+        nx, nu = self.NX, self.NU
+        fx, fu, fxx, fuu, fxu = np.zeros(nx), np.zeros(nu), np.zeros(nx * nx), np.zeros(nu * nu), np.zeros(nx * nu)
         self.L.oracle_stage_cost(self.h, _dp(_f64(x)), _dp(_f64(u)), _dp(_f64(rec)), int(k), _dp(obj),
                                  _dp(fx), _dp(fu), _dp(fxx), _dp(fuu), _dp(fxu))
-        return obj[0], fx, fu, fxx.reshape(9, 9), fuu.reshape(8, 8), fxu.reshape(9, 8)
+        return obj[0], fx, fu, fxx.reshape(nx, nx), fuu.reshape(nu, nu), fxu.reshape(nx, nu)
 
     def stage_constraints(self, x, u, rec, k):
-        c, l, u_, cx, cu = np.zeros(11), np.zeros(11), np.zeros(11), np.zeros(99), np.zeros(88)
+        nx, nu = self.NX, self.NU
+        c, l, u_, cx, cu = np.zeros(11), np.zeros(11), np.zeros(11), np.zeros(11 * nx), np.zeros(11 * nu)
         self.L.oracle_stage_constraints(self.h, _dp(_f64(x)), _dp(_f64(u)), _dp(_f64(rec)), int(k),
                                         _dp(c), _dp(l), _dp(u_), _dp(cx), _dp(cu))
-        return c, l, u_, cx.reshape(11, 9), cu.reshape(11, 8)
+        return c, l, u_, cx.reshape(11, nx), cu.reshape(11, nu)
 
     def nvar(self):
-        return 17 * self.N + 9
+        return self.NXU * self.N + self.NX
 
     def nconstr(self):
-        return 45 * self.N + 29
+        nx, nu, N = self.NX, self.NU, self.N
+        return (N + 1) * nx + ((N + 1) * nx + 2 * N * nu) + (N + 1) * 11
 
     def dense_qp(self, guess, recs, u_current):
         nv, nc = self.nvar(), self.nconstr()
@@ -265,12 +286,12 @@ class Oracle:
         return rc, out, int(it[0])
 
     def rk4(self, x, u, ts):
-        out = np.zeros(9)
+        out = np.zeros(self.NX)
         self.L.oracle_rk4(_dp(_f64(x)), _dp(_f64(u)), float(ts), _dp(out))
         return out
 
     def sim_time_step(self, x, u, ts):
-        out = np.zeros(9)
+        out = np.zeros(self.NX)
         self.L.oracle_sim_time_step(_dp(_f64(x)), _dp(_f64(u)), float(ts), _dp(out))
         return out
 
@@ -286,7 +307,7 @@ class Oracle:
         """runMPC_ up to the SQP (in place on x0, guess, valid, fails); returns the frozen records."""
         B = x0.shape[0]
         recs = np.zeros((B, self.N + 1, self.L.oracle_rec_size()))
-        self.L.oracle_prepare(self.h, B, _dp(x0), _dp(_f64(u0, (B, 8))), _dp(_f64(obs, (B, 4))), _dp(guess),
+        self.L.oracle_prepare(self.h, B, _dp(x0), _dp(_f64(u0, (B, self.NU))), _dp(_f64(obs, (B, 4))), _dp(guess),
                               _ip(valid), _ip(fails), _dp(recs))
         return recs
 
@@ -295,13 +316,14 @@ class Oracle:
         (x0, guess, valid, fails).  Returns dict of outputs."""
         B = x0.shape[0]
         N = self.N
-        assert x0.dtype == np.float64 and x0.flags.c_contiguous and x0.shape == (B, 9)
-        assert guess.dtype == np.float64 and guess.flags.c_contiguous and guess.shape == (B, N + 1, 17)
+        nx, nu, nxu = self.NX, self.NU, self.NXU
+        assert x0.dtype == np.float64 and x0.flags.c_contiguous and x0.shape == (B, nx)
+        assert guess.dtype == np.float64 and guess.flags.c_contiguous and guess.shape == (B, N + 1, nxu)
         assert valid.dtype == np.int32 and fails.dtype == np.int32
-        u0 = _f64(u0, (B, 8))
+        u0 = _f64(u0, (B, nu))
         obs = _f64(obs, (B, 4))
-        u0_out = np.zeros((B, 8))
-        hor = np.zeros((B, N + 1, 17))
+        u0_out = np.zeros((B, nu))
+        hor = np.zeros((B, N + 1, nxu))
         status = np.zeros(B, dtype=np.int32)
         ok = np.zeros(B, dtype=np.int32)
         iters = np.zeros(B, dtype=np.int32)

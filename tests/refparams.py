@@ -57,9 +57,15 @@ def default_track_xyzr(init_position):
     return X, Y, Z, R
 
 
-def resolve(sections=None, overrides=None, N=20, Ts=None, constraint_mask=7, ctor_overrides=True):
-    """Effective per-consumer parameter values (dict keyed like OracleParams)."""
-    s = sections or load_default_sections()
+def load_mobile_sections():
+    with open(os.path.join(DATA, "params", "mobile_params.json")) as f:
+        return json.load(f)
+
+
+def resolve(sections=None, overrides=None, N=20, Ts=None, constraint_mask=7, ctor_overrides=True, dof=7):
+    """Effective per-consumer parameter values (dict keyed like OracleParams).  dof = 10: the Husky+Panda
+    (base joints xb, yb, thb before the Panda joints; data/params/mobile_params.json)."""
+    s = sections or (load_mobile_sections() if dof == 10 else load_default_sections())
     ov = overrides or {}
     m = dict(s["model"]); c = dict(s["cost"]); b = dict(s["bounds"])
     nrm = dict(s["normalization"]); q = dict(s["sqp"])
@@ -68,8 +74,9 @@ def resolve(sections=None, overrides=None, N=20, Ts=None, constraint_mask=7, cto
     nrm_o = {**nrm, **ov.get("normalization", {})} if ctor_overrides else nrm
     q_o = {**q, **ov.get("sqp", {})} if ctor_overrides else q
     ts = Ts if Ts is not None else s["config"]["Ts"]
-    qn = ["q1", "q2", "q3", "q4", "q5", "q6", "q7"]
-    un = ["dq1", "dq2", "dq3", "dq4", "dq5", "dq6", "dq7"]
+    base = ["xb", "yb", "thb"] if dof == 10 else []
+    qn = base + ["q1", "q2", "q3", "q4", "q5", "q6", "q7"]
+    un = ["d" + b for b in base] + ["dq1", "dq2", "dq3", "dq4", "dq5", "dq6", "dq7"]
     return dict(
         N=N, Ts=ts, constraint_mask=constraint_mask,
         proj_max_dist=m_o["max_dist_proj"], guess_max_dist=m_o["max_dist_proj"],
