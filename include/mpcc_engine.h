@@ -21,11 +21,17 @@
  * handle must be serialized by the caller (as the reference's RobotModel is not reentrant);
  * engines on different devices are independent.
  *
+ * Robot dimensions are compile-time, as the reference's NX/NU (config.h:29-38): MPCC_DOF = 7 is the
+ * Franka Panda (libmpcc_engine.so), MPCC_DOF = 10 the Husky+Panda mobile manipulator of BASELINE
+ * configs[3] (libmpcc_engine_mobile.so: planar base joints xb, yb, thb before q1..q7).  A client of
+ * the mobile library compiles with -DMPCC_DOF=10; mpcc_robot_dof() reports the library's value.
+ * NX = DOF + 2, NU = DOF + 1 below (9 / 8 for the Panda).
+ *
  * Layouts (per instance b):
- *   x0     [9]            q1..q7, s, vs         (types.h:33-57)       in/out: s, vs are overwritten
- *   u0     [8]            dq1..dq7, dVs         (types.h:59-76)       current input (setCurrentInput)
+ *   x0     [NX]           q1..q7, s, vs         (types.h:33-57)       in/out: s, vs are overwritten
+ *   u0     [NU]           dq1..dq7, dVs         (types.h:59-76)       current input (setCurrentInput)
  *   obs    [4]            obstacle x, y, z [m], radius [cm]  (runMPC_ obs_position, obs_radius)
- *   guess  [(N+1)*17]     per stage [x_k(9), u_k(8)] (OptVariables, osqp_interface.h:48-62)
+ *   guess  [(N+1)*NXU]    per stage [x_k(NX), u_k(NU)] (OptVariables, osqp_interface.h:48-62)
  *   status                Status enum values (solver_interface.h:28-42)
  *   ok                    runMPC_ return value (mpc.cpp:188-189)
  */
@@ -37,6 +43,13 @@ extern "C" {
 #endif
 
 #define MPCC_ABI_VERSION 1
+
+#ifndef MPCC_DOF
+#define MPCC_DOF 7                       /* joints: 7 = Panda, 10 = Husky base (x, y, theta) + Panda */
+#endif
+#define MPCC_NX (MPCC_DOF + 2)           /* state  [q, s, vs]   (config.h:29 NX = 9)  */
+#define MPCC_NU (MPCC_DOF + 1)           /* input  [dq, dVs]    (config.h:30 NU = 8)  */
+#define MPCC_NXU (MPCC_NX + MPCC_NU)     /* one horizon stage of OptVariables         */
 
 enum {
     MPCC_OK = 0,
@@ -76,8 +89,9 @@ typedef struct {
     double qp_r_ddq;           /* OsqpInterface::cost_param_.r_ddq (file value only, Q8) */
     double con_tol_selcol, con_tol_sing, con_tol_envcol;                        /* Constraints::param_ */
     double s_trust_region;                                                      /* Bounds::param_ */
-    double lx[9], ux[9], lu[8], uu[8], lddq[7], uddq[7];                        /* BoundsParam (file) */
-    double Tx[9], Tu[8];                                                        /* NormalizationParam */
+    double lx[MPCC_NX], ux[MPCC_NX], lu[MPCC_NU], uu[MPCC_NU];                  /* BoundsParam (file) */
+    double lddq[MPCC_DOF], uddq[MPCC_DOF];
+    double Tx[MPCC_NX], Tu[MPCC_NU];                                            /* NormalizationParam */
     double eps_prim, eps_dual, line_search_tau, line_search_eta, line_search_rho; /* SQPParam */
     int32_t max_iter, line_search_max_iter, do_SOC, use_BFGS;
     /* Parity policy P1: per-row constraint violations <= vio_floor count as zero in
@@ -126,6 +140,7 @@ typedef struct {
 typedef struct mpcc_engine mpcc_engine;
 
 int         mpcc_abi_version(void);
+int         mpcc_robot_dof(void);   /* MPCC_DOF this library was built with (7 or 10) */
 const char* mpcc_last_error(void);
 
 /* Params JSON files + ParamValue -> effective values.  ctor_semantics=1 resolves as the
@@ -169,7 +184,7 @@ int    mpcc_track_project_host(int n, const double* X, const double* Y, const do
                                double proj_max_dist, const double* s_guess, const double* ee, double* s_out);
 int    mpcc_get_track_path(mpcc_engine* e, double* s, double* X, double* Y, double* Z, double* R9);
 
-/* Per-instance controller state (mpc.h:119-127), device resident.  guess [B*(N+1)*17]. */
+/* Per-instance controller state (mpc.h:119-127), device resident.  guess [B*(N+1)*NXU]. */
 int mpcc_set_warmstart(mpcc_engine* e, int B, const double* guess, const int32_t* valid, const int32_t* fails);
 int mpcc_get_warmstart(mpcc_engine* e, int B, double* guess, int32_t* valid, int32_t* fails);
 int mpcc_reset_warmstart(mpcc_engine* e, int B, const uint8_t* mask /* NULL = all */);
@@ -201,7 +216,7 @@ int mpcc_solve_device(mpcc_engine* e, int B, double* d_x0, const double* d_u0, c
  * setCurrentInput(u_cur) + setEnvData(obs) + solveOCP(opt_sol, status, time)
  * (osqp_interface.cpp:102-127, 398-590).  No projection, warm-start shift or valid/fail bookkeeping:
  * that stays with the caller's MPC (mpc.cpp:104-189), as in the reference.  guess, opt_sol
- * [B*(N+1)*17]; u_cur [B*8]; obs [B*4]; status [B]; solved [B] = solveOCP's bool (may be NULL).
+ * [B*(N+1)*NXU]; u_cur [B*NU]; obs [B*4]; status [B]; solved [B] = solveOCP's bool (may be NULL).
  * Uses the engine's warm-start slots [0, B) as the iterate (they are overwritten). */
 int mpcc_solve_ocp(mpcc_engine* e, int B, const double* guess, const double* u_cur, const double* obs,
                    double* opt_sol, int32_t* status, int32_t* solved, mpcc_timing* timing);
@@ -210,8 +225,8 @@ int mpcc_solve_ocp(mpcc_engine* e, int B, const double* guess, const double* u_c
  * runMPC_ (the engine's warm-start state carries over; x's s and vs are updated as mpc.cpp:107-115), takes
  * u0 and integrates the updated state with simTimeStep (integrator.cpp:55-68).  An instance whose runMPC_
  * returns false stops (main.cpp:108-112): its state stays the one that entered that step and later steps
- * report status -1.  x0 [B*9] / u0 [B*8] in, out: final state / input; obs [B*4] constant;
- * x_traj [(steps+1)*B*9], u_traj [steps*B*8], status_traj [steps*B] (any may be NULL).
+ * report status -1.  x0 [B*NX] / u0 [B*NU] in, out: final state / input; obs [B*4] constant;
+ * x_traj [(steps+1)*B*NX], u_traj [steps*B*NU], status_traj [steps*B] (any may be NULL).
  * use_graph = 1 captures one control step in a hipGraph and replays it (same results, fewer launches). */
 int mpcc_closed_loop(mpcc_engine* e, int B, int steps, double* x0, double* u0, const double* obs, double* x_traj,
                      double* u_traj, int32_t* status_traj, int use_graph);
@@ -232,7 +247,7 @@ int  mpcc_mlp_dims(mpcc_mlp* m, int32_t* n_input, int32_t* n_output);
 void mpcc_mlp_destroy(mpcc_mlp* m);
 /* RobotModel::getPosition / getOrientation / getJacobian / getManipulability / getDManipulability with a frame_id
  * (robot_model.cpp:354-450; frame 1 = panda_link0, 2..8 = panda_link1..7, 9 = panda_hand_tcp) for M joint vectors
- * q [M*7] on GPU 'device': pos [M*3], R [M*9], J [M*42] (rows Jv; Jw), mani [M], dmani [M*7]; any may be NULL. */
+ * q [M*7] (Panda library only) on GPU 'device': pos [M*3], R [M*9], J [M*42] (rows Jv; Jw), mani [M], dmani [M*7]; any may be NULL. */
 int  mpcc_robot_frames(int device, int M, const double* q, int frame_id, double* pos, double* R, double* J, double* mani,
                        double* dmani);
 /* CubicSpline::genSpline + getPoint/getDerivative/getSecondDerivative (cubic_spline.cpp:65-246) of n points at m
@@ -247,19 +262,19 @@ int  mpcc_so3_log(const double* R9, double* S9);
 int  mpcc_so3_exp(const double* S9, double* R9);
 
 /* ---- stage-level entry points for parity tests (host arrays) ---- */
-#define MPCC_REC_SIZE 143
-/* RobotData::update + updateEnv (robot_data.h:55-88) for M joint vectors q[M*7], obs[M*4] */
+#define MPCC_REC_SIZE (24 + 17 * MPCC_DOF)   /* 143 for the Panda: robot_data.h:13-31 */
+/* RobotData::update + updateEnv (robot_data.h:55-88) for M joint vectors q[M*DOF], obs[M*4] */
 int mpcc_debug_robot_records(mpcc_engine* e, int M, const double* q, const double* obs, double* rec);
 /* ArcLengthSpline evals at M arc lengths: pos,d,dd [M*3], R [M*9], dR [M*3] */
 int mpcc_debug_spline(mpcc_engine* e, int M, const double* s, double* pos, double* d, double* dd, double* R, double* dR);
-/* Cost::getCost for M (x,u,rec,k) tuples: obj [M], fx [M*9], fu [M*8], fxx [M*81], fuu [M*64] */
+/* Cost::getCost for M (x,u,rec,k) tuples: obj [M], fx [M*NX], fu [M*NU], fxx [M*NX*NX], fuu [M*NU*NU] */
 int mpcc_debug_stage_cost(mpcc_engine* e, int M, const double* x, const double* u, const double* rec, const int32_t* k,
                           double* obj, double* fx, double* fu, double* fxx, double* fuu);
 /* ArcLengthSpline::projectOnSpline (arc_length_spline.cpp:318-379) for M (s_guess, ee[3]) pairs */
 int mpcc_debug_project(mpcc_engine* e, int M, const double* s_guess, const double* ee, double* s_out);
 
-/* one QP of the SQP for B instances: guess [B*(N+1)*17], rec [B*(N+1)*143], u_cur [B*8]
- * -> step [B*(17N+9)] in the reference's stacked layout, qp_status [B], ipm_iters [B] */
+/* one QP of the SQP for B instances: guess [B*(N+1)*NXU], rec [B*(N+1)*MPCC_REC_SIZE], u_cur [B*NU]
+ * -> step [B*(NXU*N+NX)] in the reference's stacked layout, qp_status [B], ipm_iters [B] */
 int mpcc_debug_solve_qp(mpcc_engine* e, int B, const double* guess, const double* rec, const double* u_cur,
                         double* step, int32_t* qp_status, int32_t* ipm_iters);
 
@@ -267,7 +282,13 @@ int mpcc_debug_solve_qp(mpcc_engine* e, int B, const double* guess, const double
  * (at most 4) 8 doubles: qp status, ipm iterations, trial objective and violation at alpha = 1,
  * accepted, |step|_inf, alpha, alpha*|step|_inf (osqp_interface.cpp:540-574, 759-808). */
 int mpcc_debug_trace_enable(mpcc_engine* e, int enable);
-/* raw interior-point workspace of the last solve [B*(N+1)*816] (layout: csrc/ipm.hip WF_*) */
+/* raw interior-point workspace of the last solve [B*(N+1)*MPCC_IPM_WS] (layout: csrc/ipm.hip WF_*,
+ * csrc/ipm_wide.hip for the mobile library) */
+#if MPCC_DOF == 7
+#define MPCC_IPM_WS 816
+#else
+#define MPCC_IPM_WS 1280
+#endif
 int mpcc_debug_workspace(mpcc_engine* e, int B, double* out);
 int mpcc_debug_trace_get(mpcc_engine* e, int B, double* out /* [B*4*8] */);
 

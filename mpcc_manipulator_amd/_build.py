@@ -13,6 +13,13 @@ PROF = os.environ.get("MPCC_PROF_BUILD", "0") == "1"  # cycle-accounting variant
 BUILD = os.path.join(PKG, "_build_prof" if PROF else "_build")
 LIB = os.path.join(BUILD, "libmpcc_engine.so")
 SOURCES = ["kernels.hip", "ipm.hip", "mlp.hip", "nn_generic.hip", "engine.cpp", "host_params.cpp", "host_spline.cpp", "mpc.cpp"]
+# The Husky+Panda mobile manipulator (BASELINE configs[3]): the same sources built with the
+# robot's compile-time dimensions (as the reference's config.h NX/NU), its own 32-lane interior point and
+# namespace, into a second library with the same C ABI.
+MOBILE_LIB = os.path.join(BUILD, "libmpcc_engine_mobile.so")
+MOBILE_SOURCES = ["kernels.hip", "ipm_wide.hip", "mlp.hip", "nn_generic.hip", "engine.cpp", "host_params.cpp",
+                  "host_spline.cpp"]
+MOBILE_FLAGS = ["-DMPCC_DOF=10", "-Dmpcc=mpcc_m10"]
 ARCH = os.environ.get("MPCC_OFFLOAD_ARCH", "gfx950")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 # The stage kernels (projection, kinematics, records, QP assembly, line-search trials) follow the
@@ -23,33 +30,41 @@ CFLAGS = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-I", os.path.
           "-I", CSRC, "-Wno-unused-result"] + (["-DMPCC_IPM_PROF"] if PROF else [])
 
 
-def _compile(src):
+def _compile(src, variant=""):
     path = os.path.join(CSRC, src)
-    obj = os.path.join(BUILD, os.path.splitext(src)[0] + ".o")
+    obj = os.path.join(BUILD, os.path.splitext(src)[0] + variant + ".o")
     deps = [path] + [os.path.join(CSRC, h) for h in os.listdir(CSRC) if h.endswith(".h")]
     inc = os.path.join(ROOT, "include")
     deps += [os.path.join(inc, h) for h in os.listdir(inc)]
     if os.path.exists(obj) and os.path.getmtime(obj) >= max(os.path.getmtime(d) for d in deps):
         return obj
     lang = ["-x", "hip"] if src.endswith(".cpp") else []
-    cmd = [HIPCC] + CFLAGS + lang + FILE_FLAGS.get(src, []) + ["-c", path, "-o", obj]
+    extra = MOBILE_FLAGS if variant == "_mobile" else []
+    cmd = [HIPCC] + CFLAGS + extra + lang + FILE_FLAGS.get(src, []) + ["-c", path, "-o", obj]
     r = subprocess.run(cmd, capture_output=True, text=True)
     if r.returncode != 0:
         raise RuntimeError(f"compile failed: {' '.join(cmd)}\n{r.stdout}\n{r.stderr}")
     return obj
 
 
-def build(verbose=False):
-    os.makedirs(BUILD, exist_ok=True)
-    with cf.ThreadPoolExecutor(max_workers=min(8, len(SOURCES))) as ex:
-        objs = list(ex.map(_compile, SOURCES))
-    if not (os.path.exists(LIB) and os.path.getmtime(LIB) >= max(os.path.getmtime(o) for o in objs)):
-        cmd = [HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", LIB] + objs
+def _link(lib, objs, verbose):
+    if not (os.path.exists(lib) and os.path.getmtime(lib) >= max(os.path.getmtime(o) for o in objs)):
+        cmd = [HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", lib] + objs
         r = subprocess.run(cmd, capture_output=True, text=True)
         if r.returncode != 0:
             raise RuntimeError(f"link failed: {' '.join(cmd)}\n{r.stdout}\n{r.stderr}")
         if verbose:
-            print("built", LIB)
+            print("built", lib)
+
+
+def build(verbose=False):
+    os.makedirs(BUILD, exist_ok=True)
+    jobs = [(s, "") for s in SOURCES] + ([] if PROF else [(s, "_mobile") for s in MOBILE_SOURCES])
+    with cf.ThreadPoolExecutor(max_workers=8) as ex:
+        objs = list(ex.map(lambda j: _compile(*j), jobs))
+    _link(LIB, objs[:len(SOURCES)], verbose)
+    if not PROF:
+        _link(MOBILE_LIB, objs[len(SOURCES):], verbose)
     build_examples(verbose)
     build_python_module(verbose)
     return LIB

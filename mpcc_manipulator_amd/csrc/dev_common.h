@@ -7,48 +7,48 @@
 
 namespace mpcc {
 
-constexpr int NX = 9, NU = 8, NPC = 11, DOF = 7, NLINK = 9;   // config.h:29-38
+// Robot dimensions (config.h:29-38) are compile-time, as in the reference: MPCC_DOF = 7 builds the Panda
+// engine, MPCC_DOF = 10 the Husky+Panda mobile manipulator (libmpcc_engine_mobile.so):
+// state [q(DOF), s, vs], input [dq(DOF), dVs]; the base joints (x, y, theta) precede the Panda joints.
+constexpr int DOF = MPCC_DOF, NX = MPCC_NX, NU = MPCC_NU, NXU = MPCC_NXU, NPC = 11, NLINK = 9;
+constexpr int XS = DOF, XVS = DOF + 1, UVS = DOF;  // s and vs in the state, dVs in the input
+constexpr int NARM = 7, NBASE = DOF - NARM;        // Panda joints follow the base joints
+static_assert(DOF == 7 || DOF == 10, "MPCC_DOF: 7 (Panda) or 10 (Husky+Panda)");
 constexpr int NSPL = 100;                                      // N_SPLINE, config.h:38
 constexpr double INF = 1e30;                                   // config.h:37
 constexpr double BIG = 1e20;   // |bound| >= BIG is an infinite bound (OSQP_INFTY semantics)
 constexpr int NMAX = 64;       // largest supported horizon (one lane per stage in the record kernels)
 
 // ---- robot record (RobotData, robot_data.h:13-31) — SoA: rec[field * S + b*(N+1) + k] ----
+//      pos 3 | R 9 | J 6 x DOF (rows Jv; Jw) | mu | dmu DOF | d_self | dd_self DOF | obs_r | d_env 9 | dd_env 9 x DOF
 constexpr int REC = MPCC_REC_SIZE;
-constexpr int R_POS = 0, R_ROT = 3, R_J = 12, R_MU = 54, R_DMU = 55, R_SEL = 62, R_DSEL = 63,
-              R_OBSR = 70, R_ENV = 71, R_DENV = 80;
+constexpr int R_POS = 0, R_ROT = 3, R_J = 12, R_MU = R_J + 6 * DOF, R_DMU = R_MU + 1, R_SEL = R_DMU + DOF,
+              R_DSEL = R_SEL + 1, R_OBSR = R_DSEL + DOF, R_ENV = R_OBSR + 1, R_DENV = R_ENV + 9;
+static_assert(R_DENV + 9 * DOF == REC, "robot record layout");
 
 // ---- per (instance, stage) QP record, AoS per instance: qs[(b*(N+1)+k)*QS + field] ----
-// Stage-structured normalized QP: y = Tx^-1 dx, v = Tu^-1 du.
-constexpr int QS_Q = 0;        // 81  Tx f_xx Tx               (osqp_interface.cpp:158)
-constexpr int QS_q = 81;       // 9   Tx f_x                   (:157)
-constexpr int QS_R = 90;       // 8   diag(Tu f_uu Tu) + ddq diag (:162, :210)
-constexpr int QS_r = 98;       // 8   Tu f_u + Tu ddq_grad     (:161, :191)
-constexpr int QS_B = 106;      // 9   y_{k+1} = M y_k + G v_k + b_k, b_k = -c_{k+1} (:247)
-constexpr int QS_YLB = 115;    // 9   box on y_k (state bounds ∩ Q1 rows)
-constexpr int QS_YUB = 124;    // 9
-constexpr int QS_DLB = 133;    // 7   ddq rows: v_0[j] (k=0) or v_k[j]-v_{k-1}[j] in [lb, ub]
-constexpr int QS_DUB = 140;    // 7
-constexpr int QS_NPOLY = 147;  // 1   number of live polytopic rows
-constexpr int QS_POLY = 148;   // 11 x 15: a[7] (on y[0:7]), bv[7] (on v[0:7]), ub
-constexpr int QS_FLAG = 313;   // 1   bit0: NaN in stage Hessian, bit1: non-PD state block, bit2: infeasible constant rows
-constexpr int QS_OBJ = 314;    // 1   stage objective (cost + ddq term)
-constexpr int QS = 320;
-constexpr int POLY_W = 15;
+// Stage-structured normalized QP: y = Tx^-1 dx, v = Tu^-1 du.  Offsets for the Panda in
+// brackets.
+constexpr int POLY_W = 2 * DOF + 1;         // polytopic row: a[DOF] (on y[0:DOF]), bv[DOF] (on v[0:DOF]), ub
+constexpr int QS_Q = 0;                     // NX x NX  Tx f_xx Tx            (osqp_interface.cpp:158)  [0]
+constexpr int QS_q = QS_Q + NX * NX;        // NX   Tx f_x                   (:157)                    [81]
+constexpr int QS_R = QS_q + NX;             // NU   diag(Tu f_uu Tu) + ddq diag (:162, :210)           [90]
+constexpr int QS_r = QS_R + NU;             // NU   Tu f_u + Tu ddq_grad     (:161, :191)              [98]
+constexpr int QS_B = QS_r + NU;             // NX   y_{k+1} = M y_k + G v_k + b_k, b_k = -c_{k+1} (:247) [106]
+constexpr int QS_YLB = QS_B + NX;           // NX   box on y_k (state bounds ∩ Q1 rows)                 [115]
+constexpr int QS_YUB = QS_YLB + NX;         // NX                                                        [124]
+constexpr int QS_DLB = QS_YUB + NX;         // DOF  ddq rows: v_0[j] (k=0) or v_k[j]-v_{k-1}[j] in [lb, ub] [133]
+constexpr int QS_DUB = QS_DLB + DOF;        // DOF                                                       [140]
+constexpr int QS_NPOLY = QS_DUB + DOF;      // 1    number of live polytopic rows                        [147]
+constexpr int QS_POLY = QS_NPOLY + 1;       // NPC x POLY_W                                              [148]
+constexpr int QS_FLAG = QS_POLY + NPC * POLY_W;  // bit0: NaN in stage Hessian, bit1: non-PD state block,
+                                                 // bit2: infeasible constant rows                      [313]
+constexpr int QS_OBJ = QS_FLAG + 1;         // stage objective (cost + ddq term)                         [314]
+constexpr int QS = (QS_OBJ + 1 + 7) / 8 * 8;  // 64-byte records                                         [320]
+static_assert(DOF != 7 || (QS_POLY == 148 && QS == 320), "Panda QP record layout");
 
-// ---- IPM state per (instance, stage), AoS: is[(b*(N+1)+k)*IS + field] ----
-constexpr int NSLOT = 43;      // 9 y-lower, 9 y-upper, 7 ddq-lower, 7 ddq-upper, 11 poly
-constexpr int SL_YL = 0, SL_YU = 9, SL_DL = 18, SL_DU = 25, SL_P = 32;
-constexpr int IS_S = 0, IS_L = 43, IS_W = 86, IS_RP = 129, IS_DSA = 172, IS_DLA = 215, IS_COEF = 258,
-              IS_RC = 301, IS_DS = 344, IS_DL = 387, IS_BND = 430, IS_ACT = 473;
-constexpr int IS_Z = 516;      // 24: y(9) w(7) v(8)
-constexpr int IS_DZ = 540;     // 24
-constexpr int IS_G0 = 564;     // 24 objective gradient H z + h
-constexpr int IS_G = 588;      // 24 step-system gradient
-constexpr int IS_U = 612;      // 8x16  U = LF^-1 Gm
-constexpr int IS_LF = 740;     // 8x8   chol(F)
-constexpr int IS_T = 804;      // 8     LF^-1 f
-constexpr int IS = 816;
+// ---- IPM workspace per (instance, stage): ipm.hip (Panda, 16 lanes x 35 fields) / ipm_wide.hip (mobile)
+constexpr int IS = MPCC_IPM_WS;
 
 // ---- per-instance SQP bookkeeping (sqp[b*SQ + field]) ----
 constexpr int SQ_STATUS = 0, SQ_ACTIVE = 1, SQ_ITER = 2, SQ_NFILT = 3, SQ_QPSTAT = 4, SQ_IPMIT = 5;

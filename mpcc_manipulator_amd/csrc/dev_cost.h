@@ -23,7 +23,7 @@ struct RecView {  // strided view of one stage's robot record (SoA)
 };
 
 // Stage cost.  want: 0 = objective only (line-search trials), 1 = objective + gradient + Hessian.
-// fx[9], fu[8], fxx[81] (row-major), fuu_diag[8]
+// fx[NX], fu[NU], fxx[NX*NX] (row-major), fuu_diag[NU]
 __device__ inline double stage_cost(const DevConst& c, const SplineView& sp, const double* x, const double* u, const RecView& rec, int k,
                                     bool want, double* fx, double* fu, double* fxx, double* fuu_diag) {
     const mpcc_params& p = c.p;
@@ -36,7 +36,7 @@ __device__ inline double stage_cost(const DevConst& c, const SplineView& sp, con
         ql = p.q_l * cubic_blend(ratio, 0.5, 1.0, p.q_l_inc_ratio, 1.0);
         qo = p.q_ori * cubic_blend(ratio, 0.5, 1.0, p.q_ori_red_ratio, 1.0);
     }
-    const double s = x[7], vs = x[8];
+    const double s = x[XS], vs = x[XVS];
     double pr[3], T[3], dd[3];
     spline_pos3(sp, s, pr, T, dd);
     const double ddr[3] = {dd[0], dd[1], dd[1]};  // Q2: ddz_ref = ddpos(1)
@@ -66,7 +66,7 @@ __device__ inline double stage_cost(const DevConst& c, const SplineView& sp, con
         double dq2 = 0;
 #pragma unroll
         for (int j = 0; j < DOF; j++) dq2 += u[j] * u[j];
-        obj_i = p.r_dq * dq2 + p.r_dVs * (u[7] * u[7]);
+        obj_i = p.r_dq * dq2 + p.r_dVs * (u[UVS] * u[UVS]);
     }
     double obj_s = -p.q_sing * mu;
     double obj = obj_c + obj_h + obj_i + obj_s;
@@ -80,13 +80,13 @@ __device__ inline double stage_cost(const DevConst& c, const SplineView& sp, con
         // d_lag = T T^T d_total + (T e^T + |e_l| I) d_T ; d_total q-cols = Jv, s-col = -T ; d_T s-col = ddr
 #pragma unroll
         for (int j = 0; j < NX; j++) {
-            double dt0 = (j < DOF) ? rec[R_J + 0 * 7 + j] : (j == 7 ? -T[0] : 0.0);
-            double dt1 = (j < DOF) ? rec[R_J + 1 * 7 + j] : (j == 7 ? -T[1] : 0.0);
-            double dt2 = (j < DOF) ? rec[R_J + 2 * 7 + j] : (j == 7 ? -T[2] : 0.0);
+            double dt0 = (j < DOF) ? rec[R_J + 0 * DOF + j] : (j == XS ? -T[0] : 0.0);
+            double dt1 = (j < DOF) ? rec[R_J + 1 * DOF + j] : (j == XS ? -T[1] : 0.0);
+            double dt2 = (j < DOF) ? rec[R_J + 2 * DOF + j] : (j == XS ? -T[2] : 0.0);
             double dti = (i == 0) ? dt0 : (i == 1 ? dt1 : dt2);
             double a = T[i] * T[0] * dt0 + T[i] * T[1] * dt1 + T[i] * T[2] * dt2;
             double b = 0;
-            if (j == 7) {
+            if (j == XS) {
 #pragma unroll
                 for (int m = 0; m < 3; m++) b += (T[i] * et[m] + (i == m ? nel : 0.0)) * ddr[m];
             }
@@ -119,16 +119,17 @@ __device__ inline double stage_cost(const DevConst& c, const SplineView& sp, con
     for (int i = 0; i < 3; i++) {
 #pragma unroll
         for (int j = 0; j < DOF; j++)
-            dL[i][j] = JRt[3 * i] * rec[R_J + 21 + j] + JRt[3 * i + 1] * rec[R_J + 28 + j] + JRt[3 * i + 2] * rec[R_J + 35 + j];
-        dL[i][7] = -(JRt[3 * i] * dRref[0] + JRt[3 * i + 1] * dRref[1] + JRt[3 * i + 2] * dRref[2]);
-        dL[i][8] = 0.0;
+            dL[i][j] = JRt[3 * i] * rec[R_J + 3 * DOF + j] + JRt[3 * i + 1] * rec[R_J + 4 * DOF + j] +
+                       JRt[3 * i + 2] * rec[R_J + 5 * DOF + j];
+        dL[i][XS] = -(JRt[3 * i] * dRref[0] + JRt[3 * i + 1] * dRref[1] + JRt[3 * i + 2] * dRref[2]);
+        dL[i][XVS] = 0.0;
     }
 #pragma unroll
     for (int j = 0; j < NX; j++) {
         double s1 = dc[0][j] * ec[0] + dc[1][j] * ec[1] + dc[2][j] * ec[2];
         double s2 = dl[0][j] * el[0] + dl[1][j] * el[1] + dl[2][j] * el[2];
         double g = 2.0 * CC0 * s1 + 2.0 * CC1 * s2;
-        if (j == 8) g += 2.0 * p.q_vs * (vs - des);
+        if (j == XVS) g += 2.0 * p.q_vs * (vs - des);
         double gh = 2.0 * qo * (dL[0][j] * w[0] + dL[1][j] * w[1] + dL[2][j] * w[2]);
         double gs = (j < DOF) ? -p.q_sing * rec[R_DMU + j] : 0.0;
         fx[j] = g + gh + 0.0 + gs;
@@ -140,7 +141,7 @@ __device__ inline double stage_cost(const DevConst& c, const SplineView& sp, con
             double s1 = dc[0][a] * dc[0][b] + dc[1][a] * dc[1][b] + dc[2][a] * dc[2][b];
             double s2 = dl[0][a] * dl[0][b] + dl[1][a] * dl[1][b] + dl[2][a] * dl[2][b];
             double h = 2.0 * CC0 * s1 + 2.0 * CC1 * s2;
-            if (a == 8 && b == 8) h += 2.0 * p.q_vs;
+            if (a == XVS && b == XVS) h += 2.0 * p.q_vs;
             double hh = 2.0 * qo * (dL[0][a] * dL[0][b] + dL[1][a] * dL[1][b] + dL[2][a] * dL[2][b]);
             double v = h + hh + 0.0 + 0.0;
             if (a == b) v += 1e-6;
@@ -151,7 +152,7 @@ __device__ inline double stage_cost(const DevConst& c, const SplineView& sp, con
     for (int j = 0; j < NU; j++) {
         double gi = 0, hi = 0;
         if (k != N) {
-            gi = (j < DOF) ? 2.0 * p.r_dq * u[j] : 2.0 * p.r_dVs * u[7];
+            gi = (j < DOF) ? 2.0 * p.r_dq * u[j] : 2.0 * p.r_dVs * u[UVS];
             hi = (j < DOF) ? 2.0 * p.r_dq : 2.0 * p.r_dVs;
         }
         fu[j] = 0.0 + 0.0 + gi + 0.0;
@@ -173,7 +174,7 @@ __device__ __forceinline__ double drbf(double delta, double h) {
 }
 
 // One polytopic row r of stage k < N: value c(u) and, if want, the normalized linearization
-// a[7] = c_x[q] * Tx, bv[7] = c_u[dq] * Tu.  Returns false if the row is masked (l=-INF,u=+INF).
+// a[DOF] = c_x[q] * Tx, bv[DOF] = c_u[dq] * Tu.  Returns false if the row is masked (l=-INF,u=+INF).
 // Row order: 0 self-collision, 1 singularity, 2..10 env links (config.h:64-74).
 __device__ inline bool poly_row(const DevConst& c, const double* u, const RecView& rec, int r, double* val, bool want,
                                 double* a, double* bv) {
@@ -198,7 +199,7 @@ __device__ inline bool poly_row(const DevConst& c, const double* u, const RecVie
         int m = r - 2;
         double md = 0.01 * (rec[R_ENV + m] - rec[R_OBSR] * 1.2);
 #pragma unroll
-        for (int j = 0; j < DOF; j++) grad[j] = 0.01 * rec[R_DENV + 7 * m + j];
+        for (int j = 0; j < DOF; j++) grad[j] = 0.01 * rec[R_DENV + DOF * m + j];
         h = md - 0.01 * p.con_tol_envcol;
         cu_scale = 1.0;
     }

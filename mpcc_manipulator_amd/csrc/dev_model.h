@@ -146,8 +146,56 @@ __device__ inline void panda_frame(const double* q, int frame, double* pos, doub
         }
 }
 
+// Husky+Panda (MPCC_DOF = 10): planar base joints x, y (prismatic) and theta (revolute
+// about z) of RobotModel::setHusky (robot_model.cpp:321-352) carry panda_link0 at MOBILE_MOUNT in the base
+// frame (identity rotation).  p = [x, y, 0] + Rz(th) (mount + p_arm), R = Rz(th) R_arm; Jacobian columns
+// e_x, e_y, (e_z x (p - [x, y, 0]); e_z) for the base and Rz(th)-rotated arm columns (the oracle's fk).
+constexpr double MOBILE_MOUNT_Z = 0.35;
+// FK of panda_hand_tcp for this build's robot: position, rotation (row-major) and the 6 x DOF Jacobian.
+__device__ inline void robot_fk(const double* q, double* pos, double* Rout, double* J, bool want_J) {
+    if constexpr (NBASE == 0) {
+        panda_fk(q, pos, Rout, J, want_J);
+    } else {
+        double pa[3], Ra[9], Ja[42];
+        panda_fk(q + NBASE, pa, Ra, Ja, want_J);
+        double sn, cs;
+        sincos(q[2], &sn, &cs);
+        const double pl[3] = {0.0 + pa[0], 0.0 + pa[1], MOBILE_MOUNT_Z + pa[2]};
+        const double pw[3] = {cs * pl[0] + -sn * pl[1] + 0 * pl[2], sn * pl[0] + cs * pl[1] + 0 * pl[2],
+                              0 * pl[0] + 0 * pl[1] + 1 * pl[2]};
+        const double p3[3] = {q[0] + pw[0], q[1] + pw[1], 0.0 + pw[2]};
+        if (pos) { pos[0] = p3[0]; pos[1] = p3[1]; pos[2] = p3[2]; }
+        if (Rout) {
+            const double Rz[9] = {cs, -sn, 0, sn, cs, 0, 0, 0, 1};
+            m3mul(Rz, Ra, Rout);
+        }
+        if (want_J) {
+#pragma unroll
+            for (int i = 0; i < 6 * DOF; i++) J[i] = 0.0;
+            J[0 * DOF + 0] = 1.0;
+            J[1 * DOF + 1] = 1.0;
+            J[0 * DOF + 2] = -(p3[1] - q[1]);
+            J[1 * DOF + 2] = p3[0] - q[0];
+            J[5 * DOF + 2] = 1.0;
+#pragma unroll
+            for (int j = 0; j < NARM; j++) {
+                const double v0 = Ja[0 * 7 + j], v1 = Ja[1 * 7 + j], v2 = Ja[2 * 7 + j];
+                const double w0 = Ja[3 * 7 + j], w1 = Ja[4 * 7 + j], w2 = Ja[5 * 7 + j];
+                J[0 * DOF + NBASE + j] = cs * v0 + -sn * v1 + 0 * v2;
+                J[1 * DOF + NBASE + j] = sn * v0 + cs * v1 + 0 * v2;
+                J[2 * DOF + NBASE + j] = 0 * v0 + 0 * v1 + 1 * v2;
+                J[3 * DOF + NBASE + j] = cs * w0 + -sn * w1 + 0 * w2;
+                J[4 * DOF + NBASE + j] = sn * w0 + cs * w1 + 0 * w2;
+                J[5 * DOF + NBASE + j] = 0 * w0 + 0 * w1 + 1 * w2;
+            }
+        }
+    }
+}
+
 // sqrt(det(J J^T)) with a partial-pivot LU of the 6x6 Gram matrix (robot_model.cpp:431-435;
 // Eigen's MatrixXd::determinant for n > 4 is PartialPivLU).
+// NC = Jacobian columns (the robot's DOF; 7 for a Panda frame query)
+template <int NC = DOF>
 __device__ inline double manip_from_J(const double* J) {
     double A[36];
 #pragma unroll
@@ -156,7 +204,7 @@ __device__ inline double manip_from_J(const double* J) {
         for (int j = 0; j < 6; j++) {
             double s = 0;
 #pragma unroll
-            for (int k = 0; k < 7; k++) s += J[7 * i + k] * J[7 * j + k];
+            for (int k = 0; k < NC; k++) s += J[NC * i + k] * J[NC * j + k];
             A[6 * i + j] = s;
         }
     double det = 1.0;
@@ -200,8 +248,8 @@ __device__ inline double manip_from_J(const double* J) {
 }
 
 __device__ inline double manipulability(const double* q) {
-    double J[42];
-    panda_fk(q, nullptr, nullptr, J, true);
+    double J[6 * DOF];
+    robot_fk(q, nullptr, nullptr, J, true);
     return manip_from_J(J);
 }
 
@@ -395,23 +443,23 @@ __device__ inline double project_on_spline(const SplineView& sp, double proj_max
     return s_guess;
 }
 
-// Integrator::RK4 (integrator.cpp:29-43) of the kinematic model (model.cpp:31-45)
+// Integrator::RK4 (integrator.cpp:29-43) of the kinematic model (model.cpp:31-45): q' = dq, s' = vs, vs' = dVs
 __device__ inline void rk4_step(const double* x, const double* u, double ts, double* out) {
-    double k1[9], k2[9], k3[9], k4[9], t[9];
+    double k1[NX], k2[NX], k3[NX], k4[NX], t[NX];
 #pragma unroll
-    for (int j = 0; j < 7; j++) { k1[j] = u[j]; k2[j] = u[j]; k3[j] = u[j]; k4[j] = u[j]; }
-    k1[7] = x[8]; k1[8] = u[7];
+    for (int j = 0; j < DOF; j++) { k1[j] = u[j]; k2[j] = u[j]; k3[j] = u[j]; k4[j] = u[j]; }
+    k1[XS] = x[XVS]; k1[XVS] = u[UVS];
 #pragma unroll
-    for (int i = 0; i < 9; i++) t[i] = x[i] + ts / 2. * k1[i];
-    k2[7] = t[8]; k2[8] = u[7];
+    for (int i = 0; i < NX; i++) t[i] = x[i] + ts / 2. * k1[i];
+    k2[XS] = t[XVS]; k2[XVS] = u[UVS];
 #pragma unroll
-    for (int i = 0; i < 9; i++) t[i] = x[i] + ts / 2. * k2[i];
-    k3[7] = t[8]; k3[8] = u[7];
+    for (int i = 0; i < NX; i++) t[i] = x[i] + ts / 2. * k2[i];
+    k3[XS] = t[XVS]; k3[XVS] = u[UVS];
 #pragma unroll
-    for (int i = 0; i < 9; i++) t[i] = x[i] + ts * k3[i];
-    k4[7] = t[8]; k4[8] = u[7];
+    for (int i = 0; i < NX; i++) t[i] = x[i] + ts * k3[i];
+    k4[XS] = t[XVS]; k4[XVS] = u[UVS];
 #pragma unroll
-    for (int i = 0; i < 9; i++) out[i] = x[i] + ts * (k1[i] / 6. + k2[i] / 3. + k3[i] / 3. + k4[i] / 6.);
+    for (int i = 0; i < NX; i++) out[i] = x[i] + ts * (k1[i] / 6. + k2[i] / 3. + k3[i] / 3. + k4[i] / 6.);
 }
 
 }  // namespace mpcc

@@ -22,33 +22,33 @@ __device__ inline void setqp_stage(const DevConst& c, const SplineView& sp, cons
     const int N = c.N;
     const double* Tx = p.Tx;
     const double* Tu = p.Tu;
-    const double* xk = gb + 17 * k;
-    const double* uk = gb + 17 * k + 9;
-    double fx[9], fu[8], fxx[81], fuu[8];
+    const double* xk = gb + NXU * k;
+    const double* uk = gb + NXU * k + NX;
+    double fx[NX], fu[NU], fxx[NX * NX], fuu[NU];
     double obj = stage_cost(c, sp, xk, uk, rv, k, true, fx, fu, fxx, fuu);
     int flag = 0;
-    for (int a = 0; a < 9; a++) {
+    for (int a = 0; a < NX; a++) {
         q[QS_q + a] = Tx[a] * fx[a];
-        for (int bb = 0; bb < 9; bb++) {
-            double v = Tx[a] * fxx[a * 9 + bb] * Tx[bb];
-            q[QS_Q + a * 9 + bb] = v;
+        for (int bb = 0; bb < NX; bb++) {
+            double v = Tx[a] * fxx[a * NX + bb] * Tx[bb];
+            q[QS_Q + a * NX + bb] = v;
             if (isnan(v)) flag |= 1;
         }
     }
     // PD check of the state block (LLT pivots; NaN pivots pass as in Eigen)
     {
-        double L[45];
+        double L[NX * (NX + 1) / 2];
         int idx = 0;
-        for (int i = 0; i < 9; i++)
-            for (int j = 0; j <= i; j++) L[idx++] = q[QS_Q + i * 9 + j];
-        for (int j = 0; j < 9; j++) {
+        for (int i = 0; i < NX; i++)
+            for (int j = 0; j <= i; j++) L[idx++] = q[QS_Q + i * NX + j];
+        for (int j = 0; j < NX; j++) {
             int jj = j * (j + 1) / 2;
             double dgn = L[jj + j];
             for (int m = 0; m < j; m++) dgn -= L[jj + m] * L[jj + m];
             if (dgn <= 0) { flag |= 2; break; }
             dgn = sqrt(dgn);
             L[jj + j] = dgn;
-            for (int i = j + 1; i < 9; i++) {
+            for (int i = j + 1; i < NX; i++) {
                 int ii = i * (i + 1) / 2;
                 double s = L[ii + j];
                 for (int m = 0; m < j; m++) s -= L[ii + m] * L[jj + m];
@@ -59,33 +59,33 @@ __device__ inline void setqp_stage(const DevConst& c, const SplineView& sp, cons
     const double rddq = p.qp_r_ddq;
     double objd = 0.0;
     if (k < N) {
-        for (int j = 0; j < 8; j++) {
+        for (int j = 0; j < NU; j++) {
             q[QS_r + j] = Tu[j] * fu[j];
             q[QS_R + j] = Tu[j] * fuu[j] * Tu[j];
         }
         // ddq cost (osqp_interface.cpp:166-217)
         if (k != N - 1) {
-            const double* un = gb + 17 * (k + 1) + 9;
+            const double* un = gb + NXU * (k + 1) + NX;
             double sq = 0;
             for (int j = 0; j < DOF; j++) sq += (un[j] - uk[j]) * (un[j] - uk[j]);
             objd = rddq * sq;
         }
         for (int j = 0; j < DOF; j++) {
             double gg;
-            if (k == 0) gg = 2. * rddq * (uk[j] - gb[17 * (k + 1) + 9 + j]);
-            else if (k == N - 1) gg = 2. * rddq * (uk[j] - gb[17 * (k - 1) + 9 + j]);
-            else gg = 2. * rddq * (2. * uk[j] - gb[17 * (k + 1) + 9 + j] - gb[17 * (k - 1) + 9 + j]);
+            if (k == 0) gg = 2. * rddq * (uk[j] - gb[NXU * (k + 1) + NX + j]);
+            else if (k == N - 1) gg = 2. * rddq * (uk[j] - gb[NXU * (k - 1) + NX + j]);
+            else gg = 2. * rddq * (2. * uk[j] - gb[NXU * (k + 1) + NX + j] - gb[NXU * (k - 1) + NX + j]);
             q[QS_r + j] += Tu[j] * gg;
             double cii = (k == 0 || k == N - 1) ? 2. * rddq : 4. * rddq;
             q[QS_R + j] += Tu[j] * cii * Tu[j];
         }
-        for (int j = 0; j < 8; j++) if (isnan(q[QS_R + j])) flag |= 1;
+        for (int j = 0; j < NU; j++) if (isnan(q[QS_R + j])) flag |= 1;
         // dynamics offset b_k = -c_{k+1} = -Tx^-1 (x_{k+1} - (A x_k + B u_k + g))   (:247)
-        const double* xn = gb + 17 * (k + 1);
-        for (int a = 0; a < 9; a++) {
+        const double* xn = gb + NXU * (k + 1);
+        for (int a = 0; a < NX; a++) {
             double s1 = 0, s2 = 0;
-            for (int m = 0; m < 9; m++) s1 += c.A[a * 9 + m] * xk[m];
-            for (int m = 0; m < 8; m++) s2 += c.B[a * 8 + m] * uk[m];
+            for (int m = 0; m < NX; m++) s1 += c.A[a * NX + m] * xk[m];
+            for (int m = 0; m < NU; m++) s2 += c.B[a * NU + m] * uk[m];
             double pred = s1 + s2 + 0.0;
             q[QS_B + a] = -((1.0 / Tx[a]) * (xn[a] - pred));
         }
@@ -98,7 +98,7 @@ __device__ inline void setqp_stage(const DevConst& c, const SplineView& sp, cons
                 lo = p.lddq[j] + 1. / p.Ts * ucur[j];
                 hi = p.uddq[j] + 1. / p.Ts * ucur[j];
             } else {
-                cc = 1. / p.Ts * (uk[j] - gb[17 * (k - 1) + 9 + j]);
+                cc = 1. / p.Ts * (uk[j] - gb[NXU * (k - 1) + NX + j]);
                 lo = p.lddq[j];
                 hi = p.uddq[j];
             }
@@ -108,33 +108,33 @@ __device__ inline void setqp_stage(const DevConst& c, const SplineView& sp, cons
         // polytopic rows (setPolytopicConstraints :302-344); upper bound 0 - c, lower -INF
         int np = 0;
         for (int r = 0; r < NPC; r++) {
-            double val, a[7], bv[7];
+            double val, a[DOF], bv[DOF];
             if (!poly_row(c, uk, rv, r, &val, true, a, bv)) continue;
             double* row = q + QS_POLY + POLY_W * np;
-            for (int j = 0; j < 7; j++) { row[j] = a[j]; row[7 + j] = bv[j]; }
-            row[14] = 0.0 - val;
+            for (int j = 0; j < DOF; j++) { row[j] = a[j]; row[DOF + j] = bv[j]; }
+            row[2 * DOF] = 0.0 - val;
             np++;
         }
         q[QS_NPOLY] = (double)np;
     } else {
-        for (int j = 0; j < 8; j++) { q[QS_r + j] = 0.0; q[QS_R + j] = 0.0; }
-        for (int a = 0; a < 9; a++) q[QS_B + a] = 0.0;
-        for (int j = 0; j < 7; j++) { q[QS_DLB + j] = -INF; q[QS_DUB + j] = INF; }
+        for (int j = 0; j < NU; j++) { q[QS_r + j] = 0.0; q[QS_R + j] = 0.0; }
+        for (int a = 0; a < NX; a++) q[QS_B + a] = 0.0;
+        for (int j = 0; j < DOF; j++) { q[QS_DLB + j] = -INF; q[QS_DUB + j] = INF; }
         q[QS_NPOLY] = 0.0;
     }
     // box on y_k: state bounds (bounds.cpp:85-103, s trust region) intersected with the Q1 rows
     // (input bounds placed on stacked-state columns NU*i, osqp_interface.cpp:273)
     const double L = sp.L;
-    for (int m = 0; m < 9; m++) {
+    for (int m = 0; m < NX; m++) {
         double lo = p.lx[m], hi = p.ux[m];
         bool lo_inf = lo <= -BIG, hi_inf = hi >= BIG;
-        if (m == 7) { lo = fmax(xk[7] - p.s_trust_region, 0.); hi = fmin(xk[7] + p.s_trust_region, L); lo_inf = hi_inf = false; }
+        if (m == XS) { lo = fmax(xk[XS] - p.s_trust_region, 0.); hi = fmin(xk[XS] + p.s_trust_region, L); lo_inf = hi_inf = false; }
         double ylo = lo_inf ? -INF : (lo - xk[m]) / Tx[m];
         double yhi = hi_inf ? INF : (hi - xk[m]) / Tx[m];
-        const int idx = 9 * k + m;
-        const int i = idx / 8, j = idx % 8;
+        const int idx = NX * k + m;
+        const int i = idx / NU, j = idx % NU;
         if (i < N) {
-            const double ui = gb[17 * i + 9 + j];
+            const double ui = gb[NXU * i + NX + j];
             if (p.lu[j] > -BIG) ylo = fmax(ylo, (p.lu[j] - ui) / Tu[j]);
             if (p.uu[j] < BIG) yhi = fmin(yhi, (p.uu[j] - ui) / Tu[j]);
         }
@@ -166,24 +166,24 @@ __device__ inline void soc_stage(const DevConst& c, const SplineView& sp, const 
     const int N = c.N;
     const double* Tx = p.Tx;
     const double* Tu = p.Tu;
-    auto X = [&](int i, int a) { return gb[17 * i + a] + sb[17 * i + a]; };
-    auto U = [&](int i, int a) { return gb[17 * i + 9 + a] + sb[17 * i + 9 + a]; };  // the step's u_N is 0
-    auto Y = [&](int i, int a) { return sb[17 * i + a]; };
-    auto V = [&](int i, int a) { return sb[17 * i + 9 + a]; };
-    double xk[9], uk[8];
-    for (int a = 0; a < 9; a++) xk[a] = X(k, a);
-    for (int a = 0; a < 8; a++) uk[a] = U(k, a);
+    auto X = [&](int i, int a) { return gb[NXU * i + a] + sb[NXU * i + a]; };
+    auto U = [&](int i, int a) { return gb[NXU * i + NX + a] + sb[NXU * i + NX + a]; };  // the step's u_N is 0
+    auto Y = [&](int i, int a) { return sb[NXU * i + a]; };
+    auto V = [&](int i, int a) { return sb[NXU * i + NX + a]; };
+    double xk[NX], uk[NU];
+    for (int a = 0; a < NX; a++) xk[a] = X(k, a);
+    for (int a = 0; a < NU; a++) uk[a] = U(k, a);
     int flag = ((int)q[QS_FLAG]) & 3;  // the Hessian bits of the first QP stay
     if (k < N) {
-        for (int a = 0; a < 9; a++) {  // b' = -c_{k+1}(x') + (y_{k+1} - M y_k - G v_k)
+        for (int a = 0; a < NX; a++) {  // b' = -c_{k+1}(x') + (y_{k+1} - M y_k - G v_k)
             double s1 = 0, s2 = 0;
-            for (int m = 0; m < 9; m++) s1 += c.A[a * 9 + m] * xk[m];
-            for (int m = 0; m < 8; m++) s2 += c.B[a * 8 + m] * uk[m];
+            for (int m = 0; m < NX; m++) s1 += c.A[a * NX + m] * xk[m];
+            for (int m = 0; m < NU; m++) s2 += c.B[a * NU + m] * uk[m];
             double pred = s1 + s2 + 0.0;
             const double bk = -((1.0 / Tx[a]) * (X(k + 1, a) - pred));
             double ay = 0, gv = 0;
-            for (int m = 0; m < 9; m++) ay += c.M[a * 9 + m] * Y(k, m);
-            for (int m = 0; m < 8; m++) gv += c.G[a * 8 + m] * V(k, m);
+            for (int m = 0; m < NX; m++) ay += c.M[a * NX + m] * Y(k, m);
+            for (int m = 0; m < NU; m++) gv += c.G[a * NU + m] * V(k, m);
             q[QS_B + a] = bk + (Y(k + 1, a) - ay - gv);
         }
         for (int j = 0; j < DOF; j++) {  // ddq rows: + v_k[j] - v_{k-1}[j] (k = 0: v_0[j])
@@ -202,27 +202,27 @@ __device__ inline void soc_stage(const DevConst& c, const SplineView& sp, const 
             q[QS_DLB + j] = (lo - cc) / coef + sh;
             q[QS_DUB + j] = (hi - cc) / coef + sh;
         }
-        int np = 0;  // polytopic rows: + a . y_k[0:7] + bv . v_k[0:7]
+        int np = 0;  // polytopic rows: + a . y_k[0:DOF] + bv . v_k[0:DOF]
         for (int r = 0; r < NPC; r++) {
             double val;
             if (!poly_row(c, uk, rv, r, &val, false, nullptr, nullptr)) continue;
             double* row = q + QS_POLY + POLY_W * np;
             double sh = 0;
-            for (int j = 0; j < 7; j++) sh += row[j] * Y(k, j);
-            for (int j = 0; j < 7; j++) sh += row[7 + j] * V(k, j);
-            row[14] = (0.0 - val) + sh;
+            for (int j = 0; j < DOF; j++) sh += row[j] * Y(k, j);
+            for (int j = 0; j < DOF; j++) sh += row[DOF + j] * V(k, j);
+            row[2 * DOF] = (0.0 - val) + sh;
             np++;
         }
     }
     const double L = sp.L;  // y box at x', + y_k[m] (finite bounds only)
-    for (int m = 0; m < 9; m++) {
+    for (int m = 0; m < NX; m++) {
         double lo = p.lx[m], hi = p.ux[m];
         bool lo_inf = lo <= -BIG, hi_inf = hi >= BIG;
-        if (m == 7) { lo = fmax(xk[7] - p.s_trust_region, 0.); hi = fmin(xk[7] + p.s_trust_region, L); lo_inf = hi_inf = false; }
+        if (m == XS) { lo = fmax(xk[XS] - p.s_trust_region, 0.); hi = fmin(xk[XS] + p.s_trust_region, L); lo_inf = hi_inf = false; }
         double ylo = lo_inf ? -INF : (lo - xk[m]) / Tx[m];
         double yhi = hi_inf ? INF : (hi - xk[m]) / Tx[m];
-        const int idx = 9 * k + m;
-        const int i = idx / 8, j = idx % 8;
+        const int idx = NX * k + m;
+        const int i = idx / NU, j = idx % NU;
         if (i < N) {
             const double ui = U(i, j);
             if (p.lu[j] > -BIG) ylo = fmax(ylo, (p.lu[j] - ui) / Tu[j]);
@@ -253,15 +253,17 @@ __device__ inline void trial_stage(const DevConst& c, const DevBuffers& d, int b
     const int N = c.N;
     const mpcc_params& p = c.p;
     const SplineView sp = spl_of(c.spl, b);
-    const double* gb = d.guess + (size_t)b * (N + 1) * 17;
-    const double* sb = d.step + (size_t)b * (N + 1) * 17;
-    auto tx = [&](int i, int a) { return gb[17 * i + a] + alpha * (p.Tx[a] * sb[17 * i + a]); };
-    auto tu = [&](int i, int a) { return (i < N) ? gb[17 * i + 9 + a] + alpha * (p.Tu[a] * sb[17 * i + 9 + a]) : gb[17 * i + 9 + a]; };
-    double x[9], u[8];
-    for (int a = 0; a < 9; a++) x[a] = tx(k, a);
-    for (int a = 0; a < 8; a++) u[a] = tu(k, a);
+    const double* gb = d.guess + (size_t)b * (N + 1) * NXU;
+    const double* sb = d.step + (size_t)b * (N + 1) * NXU;
+    auto tx = [&](int i, int a) { return gb[NXU * i + a] + alpha * (p.Tx[a] * sb[NXU * i + a]); };
+    auto tu = [&](int i, int a) {
+        return (i < N) ? gb[NXU * i + NX + a] + alpha * (p.Tu[a] * sb[NXU * i + NX + a]) : gb[NXU * i + NX + a];
+    };
+    double x[NX], u[NU];
+    for (int a = 0; a < NX; a++) x[a] = tx(k, a);
+    for (int a = 0; a < NU; a++) u[a] = tu(k, a);
     RecView rv{d.rec + (size_t)b * (N + 1) + k, c.S};
-    double fdum[9], udum[8], hdum[81], rdum[8];
+    double fdum[NX], udum[NU], hdum[NX * NX], rdum[NU];
     double obj = stage_cost(c, sp, x, u, rv, k, false, fdum, udum, hdum, rdum);
     double objd = 0;
     if (k < N && k != N - 1) {
@@ -273,26 +275,26 @@ __device__ inline void trial_stage(const DevConst& c, const DevBuffers& d, int b
     const double vf = p.vio_floor;
     auto vfloor = [](double v, double f) { return (v > f) ? v : 0.0; };
     if (k >= 1) {  // dynamics rows, l = u = 0
-        double xp[9], up_[8];
-        for (int a = 0; a < 9; a++) xp[a] = tx(k - 1, a);
-        for (int a = 0; a < 8; a++) up_[a] = tu(k - 1, a);
-        for (int a = 0; a < 9; a++) {
+        double xp[NX], up_[NU];
+        for (int a = 0; a < NX; a++) xp[a] = tx(k - 1, a);
+        for (int a = 0; a < NU; a++) up_[a] = tu(k - 1, a);
+        for (int a = 0; a < NX; a++) {
             double s1 = 0, s2 = 0;
-            for (int m = 0; m < 9; m++) s1 += c.A[a * 9 + m] * xp[m];
-            for (int m = 0; m < 8; m++) s2 += c.B[a * 8 + m] * up_[m];
+            for (int m = 0; m < NX; m++) s1 += c.A[a * NX + m] * xp[m];
+            for (int m = 0; m < NU; m++) s2 += c.B[a * NU + m] * up_[m];
             double cv = (1.0 / p.Tx[a]) * (x[a] - (s1 + s2 + 0.0));
             lo += vfloor(fmax(0.0 - cv, 0.0), vf);
             up += vfloor(fmax(cv - 0.0, 0.0), vf);
         }
     }
-    for (int a = 0; a < 9; a++) {  // state bounds
+    for (int a = 0; a < NX; a++) {  // state bounds
         double l = p.lx[a], h = p.ux[a];
-        if (a == 7) { l = fmax(x[7] - p.s_trust_region, 0.); h = fmin(x[7] + p.s_trust_region, sp.L); }
+        if (a == XS) { l = fmax(x[XS] - p.s_trust_region, 0.); h = fmin(x[XS] + p.s_trust_region, sp.L); }
         lo += vfloor(fmax(l - x[a], 0.0), vf);
         up += vfloor(fmax(x[a] - h, 0.0), vf);
     }
     if (k < N) {
-        for (int a = 0; a < 8; a++) {  // input bounds (constr = u, :274)
+        for (int a = 0; a < NU; a++) {  // input bounds (constr = u, :274)
             lo += vfloor(fmax(p.lu[a] - u[a], 0.0), vf);
             up += vfloor(fmax(u[a] - p.uu[a], 0.0), vf);
         }
@@ -365,15 +367,15 @@ __device__ inline void accept_instance(const DevConst& c, const DevBuffers& d, i
     }
 }
 
-// guess += alpha * deNormalizeStep(step) for element e of the (N+1) x 17 horizon of instance b
+// guess += alpha * deNormalizeStep(step) for element e of the (N+1) x NXU horizon of instance b
 // (osqp_interface.cpp:549-552, 859-869); returns |step_e| for the termination norm (0 for u_N)
 __device__ __forceinline__ double apply_elem(const DevConst& c, const DevBuffers& d, int b, int e, double alpha) {
     const int N = c.N;
-    const int k = e / 17, a = e - 17 * k;
-    if (k == N && a >= 9) return 0.0;
-    double* g = d.guess + (size_t)b * (N + 1) * 17;
-    const double* st = d.step + (size_t)b * (N + 1) * 17;
-    const double T = (a < 9) ? c.p.Tx[a] : c.p.Tu[a - 9];
+    const int k = e / NXU, a = e - NXU * k;
+    if (k == N && a >= NX) return 0.0;
+    double* g = d.guess + (size_t)b * (N + 1) * NXU;
+    const double* st = d.step + (size_t)b * (N + 1) * NXU;
+    const double T = (a < NX) ? c.p.Tx[a] : c.p.Tu[a - NX];
     g[e] = g[e] + alpha * (T * st[e]);
     return fabs(st[e]);
 }

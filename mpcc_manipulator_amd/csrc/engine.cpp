@@ -72,7 +72,7 @@ struct mpcc_engine {
     double *s_x0 = nullptr, *s_u0 = nullptr, *s_obs = nullptr, *s_u0out = nullptr, *s_hor = nullptr;
     int32_t *s_status = nullptr, *s_ok = nullptr;
     NNWeights nn_self, nn_env;
-    double A[81], B[72], M[81], G[72];
+    double A[NX * NX], B[NX * NU], M[NX * NX], G[NX * NU];
     std::vector<hipEvent_t> events;
     // live timing (mpcc_timing_begin/end): event pairs per phase over many calls
     bool live = false;
@@ -103,25 +103,26 @@ struct mpcc_engine {
 
     void set_model() {
         const mpcc_params& p = params;
-        // ZOH of the kinematic model (model.cpp:47-91); the 18x18 expm is exact in closed form because
-        // the continuous A is nilpotent: A = I + Ts e_s e_vs^T, B = Ts [I7 0; 0 Ts/2; 0 1] (dVs column).
-        for (int i = 0; i < 81; i++) A[i] = (i % 10 == 0) ? 1.0 : 0.0;
-        for (int i = 0; i < 72; i++) B[i] = 0.0;
-        A[7 * 9 + 8] = p.Ts;
-        for (int j = 0; j < 7; j++) B[j * 8 + j] = p.Ts;
-        B[7 * 8 + 7] = p.Ts * p.Ts / 2.0;
-        B[8 * 8 + 7] = p.Ts;
-        for (int a = 0; a < 9; a++) {
-            for (int b = 0; b < 9; b++) M[a * 9 + b] = (1.0 / p.Tx[a]) * A[a * 9 + b] * p.Tx[b];
-            for (int b = 0; b < 8; b++) G[a * 8 + b] = (1.0 / p.Tx[a]) * B[a * 8 + b] * p.Tu[b];
+        // ZOH of the kinematic model (model.cpp:47-91); the (NX+NU)^2 expm is exact in closed form because
+        // the continuous A is nilpotent: A = I + Ts e_s e_vs^T, B = Ts [I_DOF 0; 0 Ts/2; 0 1] (dVs column).
+        for (int i = 0; i < NX * NX; i++) A[i] = (i % (NX + 1) == 0) ? 1.0 : 0.0;
+        for (int i = 0; i < NX * NU; i++) B[i] = 0.0;
+        A[XS * NX + XVS] = p.Ts;
+        for (int j = 0; j < DOF; j++) B[j * NU + j] = p.Ts;
+        B[XS * NU + UVS] = p.Ts * p.Ts / 2.0;
+        B[XVS * NU + UVS] = p.Ts;
+        for (int a = 0; a < NX; a++) {
+            for (int b = 0; b < NX; b++) M[a * NX + b] = (1.0 / p.Tx[a]) * A[a * NX + b] * p.Tx[b];
+            for (int b = 0; b < NU; b++) G[a * NU + b] = (1.0 / p.Tx[a]) * B[a * NU + b] * p.Tu[b];
         }
-        // k_ipm writes the Riccati products for M = diag(m) + m78 e7 e8^T, G = diag(g) + g87 e8 e7^T
-        for (int a = 0; a < 9; a++) {
-            for (int b = 0; b < 9; b++)
-                if (M[a * 9 + b] != 0.0 && a != b && !(a == 7 && b == 8))
+        // the interior point writes the Riccati products for M = diag(m) + m_sv e_s e_vs^T and
+        // G = diag(g) + g_v e_vs e_dVs^T (the s row's dVs entry is G's diagonal, XS == UVS)
+        for (int a = 0; a < NX; a++) {
+            for (int b = 0; b < NX; b++)
+                if (M[a * NX + b] != 0.0 && a != b && !(a == XS && b == XVS))
                     throw std::logic_error("discrete model outside the structure k_ipm assumes (M)");
-            for (int b = 0; b < 8; b++)
-                if (G[a * 8 + b] != 0.0 && a != b && !(a == 8 && b == 7))
+            for (int b = 0; b < NU; b++)
+                if (G[a * NU + b] != 0.0 && a != b && !(a == XVS && b == UVS))
                     throw std::logic_error("discrete model outside the structure k_ipm assumes (G)");
         }
     }
@@ -239,8 +240,8 @@ void validate_params(const mpcc_params& p) {
     if (ipm_lds_bytes(p.N, poly_rows_max(p.constraint_mask)) > 160 * 1024)
         throw std::invalid_argument("too many constraint rows for the interior-point LDS block");
     if (!(p.Ts > 0)) throw std::invalid_argument("Ts must be > 0");
-    for (int i = 0; i < 9; i++) if (!(p.Tx[i] > 0)) throw std::invalid_argument("T_x must be > 0");
-    for (int i = 0; i < 8; i++) if (!(p.Tu[i] > 0)) throw std::invalid_argument("T_u must be > 0");
+    for (int i = 0; i < NX; i++) if (!(p.Tx[i] > 0)) throw std::invalid_argument("T_x must be > 0");
+    for (int i = 0; i < NU; i++) if (!(p.Tu[i] > 0)) throw std::invalid_argument("T_u must be > 0");
     if (p.max_iter < 0 || p.line_search_max_iter < 0) throw std::invalid_argument("negative iteration limit");
     // Damped BFGS (osqp_interface.cpp:683-715) replaces the Hessian by rank-2 updates that couple every
     // stage with every other: the dense N_var x N_var matrix has no stage structure for the Riccati
@@ -408,6 +409,8 @@ extern "C" {
 
 int mpcc_abi_version(void) { return MPCC_ABI_VERSION; }
 
+int mpcc_robot_dof(void) { return DOF; }
+
 int mpcc_cubic_spline_host(int n, const double* x, const double* y, int regular, int m, const double* xq, double* out3) {
     if (n < 2 || m < 0 || !x || !y || (m && (!xq || !out3))) return fail(MPCC_E_INVALID, "mpcc_cubic_spline_host: invalid argument");
     host_cubic_spline(n, x, y, regular != 0, m, xq, out3);
@@ -459,25 +462,25 @@ int mpcc_create(const mpcc_config* cfg, const mpcc_params* params, const char* n
         HIPCHK(hipStreamCreateWithFlags(&e->stream, hipStreamDefault));
         const size_t B = (size_t)e->maxB, NS = (size_t)e->N + 1;
         DevBuffers& d = e->d;
-        d.guess = dmalloc<double>(B * NS * 17);
+        d.guess = dmalloc<double>(B * NS * NXU);
         d.valid = dmalloc<int32_t>(B);
         d.fails = dmalloc<int32_t>(B);
         d.rec = dmalloc<double>((size_t)REC * B * NS);
         d.qs = dmalloc<double>(B * NS * QS);
         d.is = dmalloc<double>(B * NS * IS);
-        d.step = dmalloc<double>(B * NS * 17);
+        d.step = dmalloc<double>(B * NS * NXU);
         d.trial = dmalloc<double>(B * NS * 4);
         d.sqi = dmalloc<int32_t>(B * SQI);
         d.sqd = dmalloc<double>(B * SQ);
-        HIPCHK(hipMemset(d.guess, 0, B * NS * 17 * sizeof(double)));
+        HIPCHK(hipMemset(d.guess, 0, B * NS * NXU * sizeof(double)));
         HIPCHK(hipMemset(d.valid, 0, B * sizeof(int32_t)));
         HIPCHK(hipMemset(d.fails, 0, B * sizeof(int32_t)));
         HIPCHK(hipMemset(d.sqi, 0, B * SQI * sizeof(int32_t)));
-        e->s_x0 = dmalloc<double>(B * 9);
-        e->s_u0 = dmalloc<double>(B * 8);
+        e->s_x0 = dmalloc<double>(B * NX);
+        e->s_u0 = dmalloc<double>(B * NU);
         e->s_obs = dmalloc<double>(B * 4);
-        e->s_u0out = dmalloc<double>(B * 8);
-        e->s_hor = dmalloc<double>(B * NS * 17);
+        e->s_u0out = dmalloc<double>(B * NU);
+        e->s_hor = dmalloc<double>(B * NS * NXU);
         e->s_status = dmalloc<int32_t>(B);
         e->s_ok = dmalloc<int32_t>(B);
         e->set_model();
@@ -671,7 +674,7 @@ int mpcc_set_warmstart(mpcc_engine* e, int B, const double* guess, const int32_t
     try {
         quiesce(e);
         const size_t NS = e->N + 1;
-        if (guess) HIPCHK(hipMemcpy(e->d.guess, guess, (size_t)B * NS * 17 * sizeof(double), hipMemcpyHostToDevice));
+        if (guess) HIPCHK(hipMemcpy(e->d.guess, guess, (size_t)B * NS * NXU * sizeof(double), hipMemcpyHostToDevice));
         if (valid) HIPCHK(hipMemcpy(e->d.valid, valid, (size_t)B * sizeof(int32_t), hipMemcpyHostToDevice));
         if (fails) HIPCHK(hipMemcpy(e->d.fails, fails, (size_t)B * sizeof(int32_t), hipMemcpyHostToDevice));
     } catch (const HipError& x) {
@@ -686,7 +689,7 @@ int mpcc_get_warmstart(mpcc_engine* e, int B, double* guess, int32_t* valid, int
     try {
         quiesce(e);
         const size_t NS = e->N + 1;
-        if (guess) HIPCHK(hipMemcpy(guess, e->d.guess, (size_t)B * NS * 17 * sizeof(double), hipMemcpyDeviceToHost));
+        if (guess) HIPCHK(hipMemcpy(guess, e->d.guess, (size_t)B * NS * NXU * sizeof(double), hipMemcpyDeviceToHost));
         if (valid) HIPCHK(hipMemcpy(valid, e->d.valid, (size_t)B * sizeof(int32_t), hipMemcpyDeviceToHost));
         if (fails) HIPCHK(hipMemcpy(fails, e->d.fails, (size_t)B * sizeof(int32_t), hipMemcpyDeviceToHost));
     } catch (const HipError& x) {
@@ -745,7 +748,7 @@ int mpcc_set_warmstart_device(mpcc_engine* e, int B, const double* d_guess, cons
         if (st != e->stream) e->ext_async = true;
         const size_t NS = e->N + 1;
         if (d_guess)
-            HIPCHK(hipMemcpyAsync(e->d.guess, d_guess, (size_t)B * NS * 17 * sizeof(double), hipMemcpyDeviceToDevice, st));
+            HIPCHK(hipMemcpyAsync(e->d.guess, d_guess, (size_t)B * NS * NXU * sizeof(double), hipMemcpyDeviceToDevice, st));
         if (d_valid) HIPCHK(hipMemcpyAsync(e->d.valid, d_valid, (size_t)B * sizeof(int32_t), hipMemcpyDeviceToDevice, st));
         if (d_fails) HIPCHK(hipMemcpyAsync(e->d.fails, d_fails, (size_t)B * sizeof(int32_t), hipMemcpyDeviceToDevice, st));
     } catch (const HipError& x) {
@@ -824,16 +827,16 @@ int mpcc_solve(mpcc_engine* e, int B, double* x0, const double* u0, const double
         quiesce(e);
         hipStream_t st = e->stream;
         const size_t NS = e->N + 1;
-        HIPCHK(hipMemcpyAsync(e->s_x0, x0, B * 9 * sizeof(double), hipMemcpyHostToDevice, st));
-        HIPCHK(hipMemcpyAsync(e->s_u0, u0, B * 8 * sizeof(double), hipMemcpyHostToDevice, st));
+        HIPCHK(hipMemcpyAsync(e->s_x0, x0, B * NX * sizeof(double), hipMemcpyHostToDevice, st));
+        HIPCHK(hipMemcpyAsync(e->s_u0, u0, B * NU * sizeof(double), hipMemcpyHostToDevice, st));
         HIPCHK(hipMemcpyAsync(e->s_obs, obs, B * 4 * sizeof(double), hipMemcpyHostToDevice, st));
         e->d.x0 = e->s_x0; e->d.u0 = e->s_u0; e->d.obs = e->s_obs;
         e->d.u0_out = e->s_u0out; e->d.horizon = e->s_hor; e->d.status = e->s_status; e->d.ok = e->s_ok;
         run_batch(e, B, st, timing);
-        HIPCHK(hipMemcpyAsync(x0, e->s_x0, B * 9 * sizeof(double), hipMemcpyDeviceToHost, st));
-        if (u0_out) HIPCHK(hipMemcpyAsync(u0_out, e->s_u0out, B * 8 * sizeof(double), hipMemcpyDeviceToHost, st));
+        HIPCHK(hipMemcpyAsync(x0, e->s_x0, B * NX * sizeof(double), hipMemcpyDeviceToHost, st));
+        if (u0_out) HIPCHK(hipMemcpyAsync(u0_out, e->s_u0out, B * NU * sizeof(double), hipMemcpyDeviceToHost, st));
         if (horizon_out)
-            HIPCHK(hipMemcpyAsync(horizon_out, e->s_hor, B * NS * 17 * sizeof(double), hipMemcpyDeviceToHost, st));
+            HIPCHK(hipMemcpyAsync(horizon_out, e->s_hor, B * NS * NXU * sizeof(double), hipMemcpyDeviceToHost, st));
         if (status) HIPCHK(hipMemcpyAsync(status, e->s_status, B * sizeof(int32_t), hipMemcpyDeviceToHost, st));
         if (ok) HIPCHK(hipMemcpyAsync(ok, e->s_ok, B * sizeof(int32_t), hipMemcpyDeviceToHost, st));
         HIPCHK(hipStreamSynchronize(st));
@@ -854,13 +857,13 @@ int mpcc_solve_ocp(mpcc_engine* e, int B, const double* guess, const double* u_c
         quiesce(e);
         hipStream_t st = e->stream;
         const size_t NS = e->N + 1;
-        HIPCHK(hipMemcpyAsync(e->d.guess, guess, B * NS * 17 * sizeof(double), hipMemcpyHostToDevice, st));
-        HIPCHK(hipMemcpyAsync(e->s_u0, u_cur, B * 8 * sizeof(double), hipMemcpyHostToDevice, st));
+        HIPCHK(hipMemcpyAsync(e->d.guess, guess, B * NS * NXU * sizeof(double), hipMemcpyHostToDevice, st));
+        HIPCHK(hipMemcpyAsync(e->s_u0, u_cur, B * NU * sizeof(double), hipMemcpyHostToDevice, st));
         HIPCHK(hipMemcpyAsync(e->s_obs, obs, B * 4 * sizeof(double), hipMemcpyHostToDevice, st));
         e->d.x0 = e->s_x0; e->d.u0 = e->s_u0; e->d.obs = e->s_obs;
         e->d.u0_out = e->s_u0out; e->d.horizon = e->s_hor; e->d.status = e->s_status; e->d.ok = e->s_ok;
         run_batch(e, B, st, timing, true);
-        HIPCHK(hipMemcpyAsync(opt_sol, e->s_hor, B * NS * 17 * sizeof(double), hipMemcpyDeviceToHost, st));
+        HIPCHK(hipMemcpyAsync(opt_sol, e->s_hor, B * NS * NXU * sizeof(double), hipMemcpyDeviceToHost, st));
         if (status) HIPCHK(hipMemcpyAsync(status, e->s_status, B * sizeof(int32_t), hipMemcpyDeviceToHost, st));
         if (solved) HIPCHK(hipMemcpyAsync(solved, e->s_ok, B * sizeof(int32_t), hipMemcpyDeviceToHost, st));
         HIPCHK(hipStreamSynchronize(st));
@@ -885,16 +888,16 @@ int mpcc_closed_loop(mpcc_engine* e, int B, int steps, double* x0, double* u0, c
     try {
         quiesce(e);
         hipStream_t st = e->stream;
-        double* dx = (double*)dev((size_t)B * 9 * 8);
-        double* du = (double*)dev((size_t)B * 8 * 8);
+        double* dx = (double*)dev((size_t)B * NX * 8);
+        double* du = (double*)dev((size_t)B * NU * 8);
         double* dobs = (double*)dev((size_t)B * 4 * 8);
         int32_t* alive = (int32_t*)dev((size_t)B * 4);
         int* kstep = (int*)dev(sizeof(int));
-        double* xtraj = (double*)dev((size_t)(steps + 1) * B * 9 * 8);
-        double* utraj = (double*)dev((size_t)steps * B * 8 * 8);
+        double* xtraj = (double*)dev((size_t)(steps + 1) * B * NX * 8);
+        double* utraj = (double*)dev((size_t)steps * B * NU * 8);
         int32_t* straj = (int32_t*)dev((size_t)steps * B * 4);
-        HIPCHK(hipMemcpyAsync(dx, x0, (size_t)B * 9 * 8, hipMemcpyHostToDevice, st));
-        HIPCHK(hipMemcpyAsync(du, u0, (size_t)B * 8 * 8, hipMemcpyHostToDevice, st));
+        HIPCHK(hipMemcpyAsync(dx, x0, (size_t)B * NX * 8, hipMemcpyHostToDevice, st));
+        HIPCHK(hipMemcpyAsync(du, u0, (size_t)B * NU * 8, hipMemcpyHostToDevice, st));
         HIPCHK(hipMemcpyAsync(dobs, obs, (size_t)B * 4 * 8, hipMemcpyHostToDevice, st));
         std::vector<int32_t> ones(B, 1);
         HIPCHK(hipMemcpyAsync(alive, ones.data(), (size_t)B * 4, hipMemcpyHostToDevice, st));
@@ -920,10 +923,10 @@ int mpcc_closed_loop(mpcc_engine* e, int B, int steps, double* x0, double* u0, c
         }
         launch_loop_pre(B, dx, xtraj, kstep, st);  // x_traj[steps] = final state
         HIPCHK(hipGetLastError());
-        HIPCHK(hipMemcpyAsync(x0, dx, (size_t)B * 9 * 8, hipMemcpyDeviceToHost, st));
-        HIPCHK(hipMemcpyAsync(u0, du, (size_t)B * 8 * 8, hipMemcpyDeviceToHost, st));
-        if (x_traj) HIPCHK(hipMemcpyAsync(x_traj, xtraj, (size_t)(steps + 1) * B * 9 * 8, hipMemcpyDeviceToHost, st));
-        if (u_traj && steps) HIPCHK(hipMemcpyAsync(u_traj, utraj, (size_t)steps * B * 8 * 8, hipMemcpyDeviceToHost, st));
+        HIPCHK(hipMemcpyAsync(x0, dx, (size_t)B * NX * 8, hipMemcpyDeviceToHost, st));
+        HIPCHK(hipMemcpyAsync(u0, du, (size_t)B * NU * 8, hipMemcpyDeviceToHost, st));
+        if (x_traj) HIPCHK(hipMemcpyAsync(x_traj, xtraj, (size_t)(steps + 1) * B * NX * 8, hipMemcpyDeviceToHost, st));
+        if (u_traj && steps) HIPCHK(hipMemcpyAsync(u_traj, utraj, (size_t)steps * B * NU * 8, hipMemcpyDeviceToHost, st));
         if (status_traj && steps)
             HIPCHK(hipMemcpyAsync(status_traj, straj, (size_t)steps * B * 4, hipMemcpyDeviceToHost, st));
         HIPCHK(hipStreamSynchronize(st));
@@ -941,14 +944,14 @@ int mpcc_sim_time_step(mpcc_engine* e, int B, const double* x, const double* u, 
     DevGuard dg_(e);
     try {
         quiesce(e);
-        double* dx = dmalloc<double>((size_t)B * 9);
-        double* du = dmalloc<double>((size_t)B * 8);
-        double* dn = dmalloc<double>((size_t)B * 9);
-        HIPCHK(hipMemcpy(dx, x, B * 9 * sizeof(double), hipMemcpyHostToDevice));
-        HIPCHK(hipMemcpy(du, u, B * 8 * sizeof(double), hipMemcpyHostToDevice));
+        double* dx = dmalloc<double>((size_t)B * NX);
+        double* du = dmalloc<double>((size_t)B * NU);
+        double* dn = dmalloc<double>((size_t)B * NX);
+        HIPCHK(hipMemcpy(dx, x, B * NX * sizeof(double), hipMemcpyHostToDevice));
+        HIPCHK(hipMemcpy(du, u, B * NU * sizeof(double), hipMemcpyHostToDevice));
         launch_sim_step(B, dx, du, ts, dn, e->stream);
         HIPCHK(hipStreamSynchronize(e->stream));
-        HIPCHK(hipMemcpy(x_next, dn, B * 9 * sizeof(double), hipMemcpyDeviceToHost));
+        HIPCHK(hipMemcpy(x_next, dn, B * NX * sizeof(double), hipMemcpyDeviceToHost));
         (void)hipFree(dx); (void)hipFree(du); (void)hipFree(dn);
     } catch (const std::bad_alloc&) {
         return fail(MPCC_E_OOM, "mpcc_sim_time_step: allocation failed");
@@ -963,10 +966,10 @@ int mpcc_debug_robot_records(mpcc_engine* e, int M, const double* q, const doubl
     DevGuard dg_(e);
     try {
         quiesce(e);
-        double* dq = dmalloc<double>((size_t)M * 7);
+        double* dq = dmalloc<double>((size_t)M * DOF);
         double* dob = dmalloc<double>((size_t)M * 4);
         double* drec = dmalloc<double>((size_t)M * REC);
-        HIPCHK(hipMemcpy(dq, q, M * 7 * sizeof(double), hipMemcpyHostToDevice));
+        HIPCHK(hipMemcpy(dq, q, M * DOF * sizeof(double), hipMemcpyHostToDevice));
         HIPCHK(hipMemcpy(dob, obs, M * 4 * sizeof(double), hipMemcpyHostToDevice));
         DevConst c = e->make_const(1);
         launch_debug_records(c, M, dq, dob, drec, e->stream);
@@ -1052,17 +1055,17 @@ int mpcc_debug_stage_cost(mpcc_engine* e, int M, const double* x, const double* 
     if (!e->has_track) return fail(MPCC_E_NOTRACK, "mpcc_debug_stage_cost: no track");
     try {
         quiesce(e);
-        const int W = 1 + 9 + 8 + 81 + 64;
-        double* dx = dmalloc<double>((size_t)M * 9);
-        double* du = dmalloc<double>((size_t)M * 8);
+        const int W = 1 + NX + NU + NX * NX + NU * NU;
+        double* dx = dmalloc<double>((size_t)M * NX);
+        double* du = dmalloc<double>((size_t)M * NU);
         double* dr = dmalloc<double>((size_t)M * REC);
         int32_t* dk = dmalloc<int32_t>(M);
         double* dout = dmalloc<double>((size_t)M * W);
         std::vector<double> soa((size_t)M * REC);
         for (int t = 0; t < M; t++)
             for (int f = 0; f < REC; f++) soa[(size_t)f * M + t] = rec[(size_t)t * REC + f];
-        HIPCHK(hipMemcpy(dx, x, M * 9 * sizeof(double), hipMemcpyHostToDevice));
-        HIPCHK(hipMemcpy(du, u, M * 8 * sizeof(double), hipMemcpyHostToDevice));
+        HIPCHK(hipMemcpy(dx, x, M * NX * sizeof(double), hipMemcpyHostToDevice));
+        HIPCHK(hipMemcpy(du, u, M * NU * sizeof(double), hipMemcpyHostToDevice));
         HIPCHK(hipMemcpy(dr, soa.data(), soa.size() * sizeof(double), hipMemcpyHostToDevice));
         HIPCHK(hipMemcpy(dk, k, M * sizeof(int32_t), hipMemcpyHostToDevice));
         DevConst c = e->make_const(1);
@@ -1073,10 +1076,10 @@ int mpcc_debug_stage_cost(mpcc_engine* e, int M, const double* x, const double* 
         for (int t = 0; t < M; t++) {
             const double* r = &o[(size_t)t * W];
             if (obj) obj[t] = r[0];
-            if (fx) std::memcpy(fx + 9 * t, r + 1, 9 * sizeof(double));
-            if (fu) std::memcpy(fu + 8 * t, r + 10, 8 * sizeof(double));
-            if (fxx) std::memcpy(fxx + 81 * t, r + 18, 81 * sizeof(double));
-            if (fuu) std::memcpy(fuu + 64 * t, r + 99, 64 * sizeof(double));
+            if (fx) std::memcpy(fx + NX * t, r + 1, NX * sizeof(double));
+            if (fu) std::memcpy(fu + NU * t, r + 1 + NX, NU * sizeof(double));
+            if (fxx) std::memcpy(fxx + NX * NX * t, r + 1 + NX + NU, NX * NX * sizeof(double));
+            if (fuu) std::memcpy(fuu + NU * NU * t, r + 1 + NX + NU + NX * NX, NU * NU * sizeof(double));
         }
         (void)hipFree(dx); (void)hipFree(du); (void)hipFree(dr); (void)hipFree(dk); (void)hipFree(dout);
     } catch (const std::bad_alloc&) {
@@ -1103,25 +1106,25 @@ int mpcc_debug_solve_qp(mpcc_engine* e, int B, const double* guess, const double
         std::vector<double> soa((size_t)REC * S);
         for (size_t t = 0; t < S; t++)
             for (int f = 0; f < REC; f++) soa[(size_t)f * S + t] = rec[t * REC + f];
-        HIPCHK(hipMemcpy(e->d.guess, guess, S * 17 * sizeof(double), hipMemcpyHostToDevice));
+        HIPCHK(hipMemcpy(e->d.guess, guess, S * NXU * sizeof(double), hipMemcpyHostToDevice));
         HIPCHK(hipMemcpy(e->d.rec, soa.data(), soa.size() * sizeof(double), hipMemcpyHostToDevice));
-        HIPCHK(hipMemcpy(e->s_u0, u_cur, B * 8 * sizeof(double), hipMemcpyHostToDevice));
+        HIPCHK(hipMemcpy(e->s_u0, u_cur, B * NU * sizeof(double), hipMemcpyHostToDevice));
         std::vector<int32_t> sqi((size_t)B * SQI, 0);
         for (int b = 0; b < B; b++) sqi[(size_t)b * SQI + SQ_ACTIVE] = 1;
         HIPCHK(hipMemcpy(e->d.sqi, sqi.data(), sqi.size() * sizeof(int32_t), hipMemcpyHostToDevice));
-        HIPCHK(hipMemset(e->d.step, 0, S * 17 * sizeof(double)));
+        HIPCHK(hipMemset(e->d.step, 0, S * NXU * sizeof(double)));
         launch_setqp(c, e->d, e->s_u0, st);
         launch_ipm(c, e->d, poly_rows_max(c.p.constraint_mask), st);
         HIPCHK(hipStreamSynchronize(st));
-        std::vector<double> stp(S * 17);
+        std::vector<double> stp(S * NXU);
         HIPCHK(hipMemcpy(stp.data(), e->d.step, stp.size() * sizeof(double), hipMemcpyDeviceToHost));
         HIPCHK(hipMemcpy(sqi.data(), e->d.sqi, sqi.size() * sizeof(int32_t), hipMemcpyDeviceToHost));
-        const size_t nv = NS * 9 + (size_t)N * 8;
+        const size_t nv = NS * NX + (size_t)N * NU;
         for (int b = 0; b < B; b++) {
             for (size_t k = 0; k < NS; k++) {
-                for (int a = 0; a < 9; a++) step[b * nv + 9 * k + a] = stp[(b * NS + k) * 17 + a];
+                for (int a = 0; a < NX; a++) step[b * nv + NX * k + a] = stp[(b * NS + k) * NXU + a];
                 if ((int)k < N)
-                    for (int a = 0; a < 8; a++) step[b * nv + 9 * NS + 8 * k + a] = stp[(b * NS + k) * 17 + 9 + a];
+                    for (int a = 0; a < NU; a++) step[b * nv + NX * NS + NU * k + a] = stp[(b * NS + k) * NXU + NX + a];
             }
             int active = sqi[(size_t)b * SQI + SQ_ACTIVE];
             int qs = sqi[(size_t)b * SQI + SQ_QPSTAT];

@@ -105,9 +105,13 @@ extern "C" int mpcc_params_load_json(const mpcc_json_paths* paths, const mpcc_ov
         p.qp_r_ddq = none.get(c, "cost", "rddq");  // Q8
         // BoundsParam: always the file (osqp_interface.cpp:54, 99)
         const JVal& b = s.bounds;
-        const char* qn[7] = {"q1", "q2", "q3", "q4", "q5", "q6", "q7"};
-        const char* dn[7] = {"dq1", "dq2", "dq3", "dq4", "dq5", "dq6", "dq7"};
-        for (int j = 0; j < 7; j++) {
+        // joint names: the Husky base joints (xb, yb, thb; mobile_params.json) precede the Panda joints
+        const char* qn_all[10] = {"xb", "yb", "thb", "q1", "q2", "q3", "q4", "q5", "q6", "q7"};
+        const char* dn_all[10] = {"dxb", "dyb", "dthb", "dq1", "dq2", "dq3", "dq4", "dq5", "dq6", "dq7"};
+        const char* const* qn = qn_all + (10 - MPCC_DOF);
+        const char* const* dn = dn_all + (10 - MPCC_DOF);
+        const int XS = MPCC_DOF, XVS = MPCC_DOF + 1, UVS = MPCC_DOF;
+        for (int j = 0; j < MPCC_DOF; j++) {
             p.lx[j] = b.at(std::string(qn[j]) + "l").number();
             p.ux[j] = b.at(std::string(qn[j]) + "u").number();
             p.lu[j] = b.at(std::string(dn[j]) + "l").number();
@@ -115,17 +119,17 @@ extern "C" int mpcc_params_load_json(const mpcc_json_paths* paths, const mpcc_ov
             p.lddq[j] = b.at(std::string("d") + dn[j] + "l").number();
             p.uddq[j] = b.at(std::string("d") + dn[j] + "u").number();
         }
-        p.lx[7] = b.at("sl").number(); p.ux[7] = b.at("su").number();
-        p.lx[8] = b.at("vsl").number(); p.ux[8] = b.at("vsu").number();
-        p.lu[7] = b.at("dVsl").number(); p.uu[7] = b.at("dVsu").number();
+        p.lx[XS] = b.at("sl").number(); p.ux[XS] = b.at("su").number();
+        p.lx[XVS] = b.at("vsl").number(); p.ux[XVS] = b.at("vsu").number();
+        p.lu[UVS] = b.at("dVsl").number(); p.uu[UVS] = b.at("dVsu").number();
         // NormalizationParam, SQPParam: overrides only with constructor semantics
         const Overrides& on = ctor_semantics ? o : none;
         const JVal& nn = s.norm;
-        for (int j = 0; j < 7; j++) p.Tx[j] = on.get(nn, "normalization", qn[j]);
-        p.Tx[7] = on.get(nn, "normalization", "s");
-        p.Tx[8] = on.get(nn, "normalization", "vs");
-        for (int j = 0; j < 7; j++) p.Tu[j] = on.get(nn, "normalization", dn[j]);
-        p.Tu[7] = on.get(nn, "normalization", "dVs");
+        for (int j = 0; j < MPCC_DOF; j++) p.Tx[j] = on.get(nn, "normalization", qn[j]);
+        p.Tx[XS] = on.get(nn, "normalization", "s");
+        p.Tx[XVS] = on.get(nn, "normalization", "vs");
+        for (int j = 0; j < MPCC_DOF; j++) p.Tu[j] = on.get(nn, "normalization", dn[j]);
+        p.Tu[UVS] = on.get(nn, "normalization", "dVs");
         const JVal& q = s.sqp;
         p.eps_prim = on.get(q, "sqp", "eps_prim");
         p.eps_dual = on.get(q, "sqp", "eps_dual");

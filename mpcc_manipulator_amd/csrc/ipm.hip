@@ -33,6 +33,9 @@
 
 namespace mpcc {
 
+static_assert(DOF == 7, "ipm.hip is the Panda's 16-lane interior point (x~ = [y(9), w(7)] fills a DPP row); "
+                        "the mobile manipulator builds ipm_wide.hip");
+
 #ifndef MPCC_IPM_MAXIT
 #define MPCC_IPM_MAXIT 60
 #endif

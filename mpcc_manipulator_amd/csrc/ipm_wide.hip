@@ -1,0 +1,1007 @@
+// ipm_wide.hip — the QP solve (replacing OSQP, osqp_interface.cpp:592-656) and the fused SQP kernel k_sqp of
+// the Husky+Panda mobile manipulator build (MPCC_DOF = 10; BASELINE configs[3]).
+//
+// Same method, start point, tolerances and parity policies as ipm.hip and the oracle's solve_struct_ipm:
+// Mehrotra predictor-corrector on the stage-structured normalized QP, Riccati recursion over the augmented
+// stage state x~ = [y(NX), w(DOF)] (w_k = v_{k-1}[0:DOF] carries the ddq coupling) with input v(NU).  For
+// this robot x~ has 22 components and a stage 22 box/ddq rows, more than one 16-lane DPP row holds, so:
+//  * one 32-lane group per instance, 2 instances per wavefront.  Lane t owns box row t (t < NX: y_t; NX <= t
+//    < NX + DOF: ddq row t - NX), poly row t, component t of x~ and of v (t < NU) and column t of P.
+//  * broadcasts inside the group: v_permlane16_swap (gfx950) duplicates each 16-lane half over both halves,
+//    then a DPP row_newbcast picks the lane (no LDS); shifts t <- t +- n across the half boundary combine
+//    the same duplicate with a DPP row shift.  Group sums are a DPP row reduction plus one swap.
+//  * F, U = LF^-1 Gm and K of the current stage pass through the instance's LDS block (broadcast reads).
+//  * the forward sweeps form v = K x~ + kff as group reductions over the K column layout (lane c holds
+//    K[i][c]), so the workspace keeps one K layout; F^-1 rows serve the corrector's kff = -F^-1 f.
+//  * per-stage slacks, multipliers, iterate, steps and gains stream through a [field][32 lanes] global
+//    workspace, one stage ahead.  The predictor backward solve is fused into the factorization sweep and the
+//    iterate update applied lazily by the next one, as in ipm.hip.
+#include "dev_common.h"
+#include "dev_dpp.h"
+#include "kernels.h"
+// QP assembly and line-search pieces of k_sqp: oracle operation order, no FP contraction
+#pragma clang fp contract(off)
+#include "dev_sqp.h"
+#pragma clang fp contract(fast)
+
+namespace mpcc {
+
+static_assert(DOF == 10, "ipm_wide.hip is the mobile manipulator's interior point; the Panda builds ipm.hip");
+
+constexpr int IPM_MAX_IT = 60;
+constexpr double IPM_TOL_MU = 1e-13, IPM_TOL_P = 1e-11, IPM_TOL_STEP = 1e-11;
+constexpr double IPM_TOL_FB = 1e-9;  // P2
+constexpr double IPM_DIV = 1e6;      // P3
+constexpr double IPM_S0 = 0.02, IPM_L0 = 0.002;
+constexpr int IPM_MAX_IT_SCALED = 30;
+constexpr double IPM_TAU = 0.995;
+typedef __attribute__((address_space(1))) double gdouble;
+
+constexpr int GW = 32;               // lanes per instance
+constexpr int IPW = 64 / GW;         // instances per wavefront
+constexpr int NXA = NX + DOF;        // augmented stage state [y, w]
+static_assert(NXA <= GW && NU <= 16, "stage dimensions of the 32-lane group");
+
+// workspace fields, ws[(b*(N+1) + k)*IS + field*GW + lane]
+enum : int {
+    WF_SL = 0, WF_LL, WF_SU, WF_LU, WF_SP, WF_LP,  // slack / multiplier of the lower, upper and poly slot of row t
+    WF_ZX, WF_ZV,                                 // iterate: lane c -> x~_c; lane j < NU -> v_j
+    WF_DX, WF_DV,                                 // corrector step
+    WF_AX, WF_AV,                                 // predictor step
+    WF_GX, WF_GV,                                 // objective gradient H z + h
+    WF_KFF,                                       // kff (lanes < NU)
+    WF_KC,                                        // NU fields: field i, lane c = K[i][c]
+    WF_FI = WF_KC + NU,                           // NU fields: field m, lane i = F^-1[i][m]
+    NWF = WF_FI + NU
+};
+static_assert(NWF * GW <= IS, "IPM workspace must fit the per-stage IS allocation");
+
+// per-instance LDS block (doubles): F [i*16 + j], U [i*32 + c]
+constexpr int L_F = 0, L_U = 16 * 16;
+constexpr int GRP_LDS = L_U + NU * GW + 16;  // + 16 doubles: the two instances of a wave start 16 banks apart
+
+size_t ipm_lds_bytes(int /*N*/, int /*npmax*/) { return (size_t)IPW * GRP_LDS * sizeof(double); }
+
+namespace {
+
+using namespace dpp;
+
+__device__ __forceinline__ void lds_sync() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
+
+// ---- 32-lane group exchange ---------------------------------------------------------------------------
+// halves(v): .lo = the group's lower 16 lanes' values in both halves, .hi = the upper 16 lanes' values.
+// v_permlane16_swap swaps the odd rows of its first operand with the even rows of its second; with both
+// operands v the two results are the even and the odd row duplicated over the row pair.  Evaluated with the
+// whole wave active (like DPP) and pinned against sinking into divergent code.
+struct Halves {
+    double lo, hi;
+};
+__device__ __forceinline__ Halves halves(double v) {
+    const unsigned long long x = (unsigned long long)__double_as_longlong(v);
+    const unsigned l = (unsigned)x, h = (unsigned)(x >> 32);
+    const auto a = __builtin_amdgcn_permlane16_swap(l, l, false, false);
+    const auto b = __builtin_amdgcn_permlane16_swap(h, h, false, false);
+    long long lo = (long long)(((unsigned long long)b[0] << 32) | a[0]);
+    long long hi = (long long)(((unsigned long long)b[1] << 32) | a[1]);
+    asm volatile("" : "+v"(lo), "+v"(hi));
+    return {__longlong_as_double(lo), __longlong_as_double(hi)};
+}
+// lane i of the group (i a constant after unrolling)
+__device__ __forceinline__ double bch(const Halves& h, int i) { return bcn(i < 16 ? h.lo : h.hi, i & 15); }
+// lane t <- t + n / t - n inside the group (0 < n < 16); lanes whose source is outside the group get junk
+template <int n>
+__device__ __forceinline__ double up32(double v, const Halves& h, int t) {
+    const double a = from_up<n>(v), b = from_down<16 - n>(h.hi);
+    return ((t & 15) + n < 16) ? a : b;
+}
+template <int n>
+__device__ __forceinline__ double down32(double v, const Halves& h, int t) {
+    const double a = from_down<n>(v), b = from_up<16 - n>(h.lo);
+    return ((t & 15) >= n) ? a : b;
+}
+// lane t <- t + NX / t - NX (NX = 12)
+__device__ __forceinline__ double up_nx(double v, int t) { return up32<NX>(v, halves(v), t); }
+__device__ __forceinline__ double down_nx(double v, int t) { return down32<NX>(v, halves(v), t); }
+__device__ __forceinline__ double up1(double v, int t) { return up32<1>(v, halves(v), t); }
+__device__ __forceinline__ double down1(double v, int t) { return down32<1>(v, halves(v), t); }
+__device__ __forceinline__ double g_sum32(double v) {
+    const Halves h = halves(g_sum(v));
+    return h.lo + h.hi;
+}
+__device__ __forceinline__ double g_max32(double v) {
+    const Halves h = halves(g_max(v));
+    return fmax(h.lo, h.hi);
+}
+__device__ __forceinline__ double g_min32(double v) {
+    const Halves h = halves(g_min(v));
+    return fmin(h.lo, h.hi);
+}
+
+// ---- slot algebra (oracle solve_struct_ipm), slot: sgn*(c^T z) <= sgn*bnd (as ipm.hip) -----------------
+struct SlotStep {
+    double ds, dl;
+};
+__device__ __forceinline__ double slot_rp(double sgn, double cz, double bnd, double s) { return sgn * cz - sgn * bnd + s; }
+__device__ __forceinline__ SlotStep slot_recover(double ri, double l, double rp, double cd, double rc) {
+    const double W = l * ri;
+    return {-rp - cd, W * (cd + rp) - rc * ri};
+}
+__device__ __forceinline__ double slot_coef(double ri, double l, double rp, double rc) { return l + (l * ri) * rp - rc * ri; }
+struct MinRatio {
+    double num, den;
+    __device__ __forceinline__ explicit MinRatio(double cap) : num(cap), den(1.0) {}
+    __device__ __forceinline__ void add(double n, double dneg) {
+        const double d = -dneg;
+        const bool take = dneg < 0 && n * den < num * d;
+        num = take ? n : num;
+        den = take ? d : den;
+    }
+    __device__ __forceinline__ double value() const { return num / den; }
+};
+__device__ __forceinline__ void step_bound(MinRatio& a, double s, double l, SlotStep d) {
+    a.add(s, d.ds);
+    a.add(l, d.dl);
+}
+__device__ __forceinline__ double rcp(double x) {
+    double r = __builtin_amdgcn_rcp(x);
+    r = fma(fma(-x, r, 1.0), r, r);
+    return fma(fma(-x, r, 1.0), r, r);
+}
+__device__ __forceinline__ SlotStep slot_corr(double sgn, double bnd, double cz, double ca, double cd, double s, double l,
+                                              double smu, double* rp_out) {
+    const double ri = rcp(s);
+    const double rp = slot_rp(sgn, cz, bnd, s);
+    const SlotStep pa = slot_recover(ri, l, rp, sgn * ca, s * l);
+    const double rc = s * l + pa.ds * pa.dl - smu;
+    *rp_out = rp;
+    return slot_recover(ri, l, rp, sgn * cd, rc);
+}
+
+// Cholesky of the NU x NU stage F (packed lower triangle), reciprocal pivots; forward / backward solves
+__device__ __forceinline__ bool cholN(double* L, double* dinv) {
+    bool ok = true;
+#pragma unroll
+    for (int j = 0; j < NU; j++) {
+        const int jj = j * (j + 1) / 2;
+        double d = L[jj + j];
+#pragma unroll
+        for (int m = 0; m < j; m++) d -= L[jj + m] * L[jj + m];
+        ok = ok && (d > 0);
+        d = sqrt(d);
+        L[jj + j] = d;
+        const double inv = rcp(d);
+        dinv[j] = inv;
+#pragma unroll
+        for (int i = j + 1; i < NU; i++) {
+            const int ii = i * (i + 1) / 2;
+            double s = L[ii + j];
+#pragma unroll
+            for (int m = 0; m < j; m++) s -= L[ii + m] * L[jj + m];
+            L[ii + j] = s * inv;
+        }
+    }
+    return ok;
+}
+__device__ __forceinline__ void fwdN(const double* L, const double* dinv, double* x) {
+#pragma unroll
+    for (int i = 0; i < NU; i++) {
+        const int ii = i * (i + 1) / 2;
+        double s = x[i];
+#pragma unroll
+        for (int m = 0; m < i; m++) s -= L[ii + m] * x[m];
+        x[i] = s * dinv[i];
+    }
+}
+__device__ __forceinline__ void bwdN(const double* L, const double* dinv, double* x) {
+#pragma unroll
+    for (int i = NU - 1; i >= 0; i--) {
+        double s = x[i];
+#pragma unroll
+        for (int m = i + 1; m < NU; m++) s -= L[m * (m + 1) / 2 + i] * x[m];
+        x[i] = s * dinv[i];
+    }
+}
+
+// per-stage inputs of one lane, loaded one stage ahead of their use
+template <int NPE>
+struct StageIn {
+    double lb, ub, np;
+    double pa[NPE], pb[NPE];      // poly rows p: a_p[t], bv_p[t] (t < DOF)
+    double pub;                   // upper bound of poly row t (t < npmax)
+    double sL, lL, sU, lU, sP, lP, zx, zv;
+    double x0, x1, x2, x3;        // sweep-specific pairs (dz, dza, g0)
+    double m[2 * NU];             // sweep-specific: Q row (NX) + q, R, r | K column (NU) + kff | K column + F^-1 row
+};
+
+// stage sweep i = 0..N in order s(i) with the next stage prefetched (copy-based double buffer)
+template <class In, class LoadF, class BodyF>
+__device__ __forceinline__ void sweep(int N, bool backward, In& b0, In& b1, LoadF load, BodyF body) {
+    auto s = [&](int i) { return backward ? N - i : i; };
+    load(s(0), b0);
+    for (int i = 0; i <= N; i++) {
+        load(s(i + 1 <= N ? i + 1 : N), b1);
+        body(s(i), b0);
+        b0 = b1;
+    }
+}
+
+}  // namespace
+
+// The QP solve of the 2 instances of this wavefront (32 lanes each).  Writes the step (d.step), QP status
+// and IPM iteration count (d.sqi).
+template <int NPM>
+__device__ __forceinline__ void ipm_group(const DevConst& c, const DevBuffers& d, double* smem) {
+    constexpr int NPE = NPM > 0 ? NPM : 1;
+    using In = StageIn<NPE>;
+    const int lane = threadIdx.x;
+    const int grp = lane / GW;
+    const int t = lane % GW;
+    const int b = blockIdx.x * IPW + grp;
+    const int N = c.N;
+    const int NS = N + 1;
+    double* const S = smem + grp * GRP_LDS;
+
+    const bool valid = b < c.Bn;
+    int32_t* si = d.sqi + (size_t)(valid ? b : 0) * SQI;
+    bool run = valid && si[SQ_ACTIVE] != 0;
+    if (__ballot(run) == 0) return;
+
+    const gdouble* QSb = (const gdouble*)(d.qs + (size_t)(valid ? b : 0) * NS * QS);
+    gdouble* WSb = (gdouble*)(d.is + (size_t)(valid ? b : 0) * NS * IS);
+    gdouble* const WSt = WSb + t;
+    auto ws = [&](int k, int f) -> gdouble* {
+        gdouble* wk = WSt + (size_t)k * IS;
+        asm("" : "+v"(wk));
+        return wk + f * GW;
+    };
+    auto qs_stage = [&](int k) -> const gdouble* {
+        const gdouble* qk = QSb + (size_t)k * QS;
+        asm("" : "+v"(qk));
+        return qk;
+    };
+
+    // ---- model constants of this lane: M = diag(m) + m_sv e_s e_vs^T, G = diag(g) + g_v e_vs e_dVs^T
+    const double msv = c.M[XS * NX + XVS], mss = c.M[XS * (NX + 1)];
+    const double gs = c.G[XS * NU + UVS], gv = c.G[XVS * NU + UVS];
+    double mt = 0.0, gt = 0.0, Hct = 0.0;
+    const double HcB = -2. * c.p.qp_r_ddq;
+#pragma unroll
+    for (int a = 0; a < NX; a++)
+        if (t == a) mt = c.M[a * (NX + 1)];
+#pragma unroll
+    for (int a = 0; a < DOF; a++) {
+        if (t == a) gt = c.G[a * (NU + 1)];
+        if (t == a || t == NX + a) Hct = c.p.Tu[a] * HcB * c.p.Tu[a];
+    }
+    if (t == UVS) gt = gs;
+    const bool rowY = t < NX;
+    const bool rowD = t >= NX && t < NXA;
+    const int j9 = t - NX;
+    const int jc = rowD ? j9 : 0;  // clamped ddq row (addresses stay inside the record)
+    constexpr double sgnL = -1.0, sgnU = 1.0;
+
+    // ---- Hessian checks (osqp_interface.cpp:454-473): stage flags + tridiagonal input blocks
+    int fl = 0;
+    if (run) {
+        for (int k = t; k < NS; k += GW) fl |= (int)QSb[(size_t)k * QS + QS_FLAG];
+        if (t < NU) {
+            double prev_d = 0;
+            for (int k = 0; k < N; k++) {
+                const double dk = QSb[(size_t)k * QS + QS_R + t];
+                const double off = (k >= 1 && t < DOF) ? Hct : 0.0;
+                const double l = (k >= 1) ? off / prev_d : 0.0;
+                const double dd = dk - l * l;
+                if (dd <= 0) { fl |= 2; break; }
+                prev_d = sqrt(dd);
+            }
+        }
+    }
+    {
+        int o = 0;
+#pragma unroll
+        for (int bit = 0; bit < 3; bit++)
+            if (g_max32((double)((fl >> bit) & 1)) > 0.5) o |= 1 << bit;
+        fl = o;
+    }
+    if (run && (fl & 2)) { if (t == 0) { si[SQ_STATUS] = MPCC_NON_PD_HESSIAN; si[SQ_ACTIVE] = 0; } run = false; }
+    if (run && (fl & 1)) { if (t == 0) { si[SQ_STATUS] = MPCC_NAN_HESSIAN; si[SQ_ACTIVE] = 0; } run = false; }
+    if (run && (fl & 4)) { if (t == 0) si[SQ_QPSTAT] = MPCC_QP_PrimalInfeasible; run = false; }  // keep old step (Q6)
+    const bool entered = run;
+
+    // ---- stage loaders (unconditional loads, lane/stage conditions as selects)
+    auto load_common = [&](int k, In& o) {
+        const gdouble* q = qs_stage(k);
+        const double ylb = q[QS_YLB + (rowY ? t : 0)], yub = q[QS_YUB + (rowY ? t : 0)];
+        const double dlb = q[QS_DLB + jc], dub = q[QS_DUB + jc];
+        o.lb = rowY ? ylb : (rowD ? dlb : -INF);
+        o.ub = rowY ? yub : (rowD ? dub : INF);
+        o.np = q[QS_NPOLY];
+        const int tp = t < DOF ? t : 0;
+#pragma unroll
+        for (int p = 0; p < NPE; p++) {
+            const double a = q[QS_POLY + POLY_W * p + tp], bv = q[QS_POLY + POLY_W * p + DOF + tp];
+            o.pa[p] = (NPM > 0 && t < DOF) ? a : 0.0;
+            o.pb[p] = (NPM > 0 && t < DOF) ? bv : 0.0;
+        }
+        const double pu = q[QS_POLY + POLY_W * (t < NPE ? t : 0) + 2 * DOF];
+        o.pub = (t < NPM) ? pu : INF;
+        o.sL = *ws(k, WF_SL); o.lL = *ws(k, WF_LL); o.sU = *ws(k, WF_SU); o.lU = *ws(k, WF_LU);
+        o.sP = *ws(k, WF_SP); o.lP = *ws(k, WF_LP);
+        o.zx = *ws(k, WF_ZX); o.zv = *ws(k, WF_ZV);
+    };
+    auto load_factor = [&](int k, In& o, bool upd) {
+        load_common(k, o);
+        const gdouble* q = qs_stage(k);
+        const int tr = rowY ? t : 0;
+#pragma unroll
+        for (int m = 0; m < NX; m++) {
+            const double v = q[QS_Q + tr * NX + m];
+            o.m[m] = rowY ? v : 0.0;
+        }
+        const int tu = t < NU ? t : 0;
+        const double qv = q[QS_q + tr], rv = q[QS_R + tu], rr = q[QS_r + tu];
+        o.m[NX] = rowY ? qv : 0.0;
+        o.m[NX + 1] = (t < NU && k < N) ? rv : 0.0;
+        o.m[NX + 2] = (t < NU && k < N) ? rr : 0.0;
+        const double x0 = *ws(k, WF_DX), x1 = *ws(k, WF_DV), x2 = *ws(k, WF_AX), x3 = *ws(k, WF_AV);
+        o.x0 = upd ? x0 : 0.0; o.x1 = upd ? x1 : 0.0; o.x2 = upd ? x2 : 0.0; o.x3 = upd ? x3 : 0.0;
+    };
+    auto load_fwd = [&](int k, In& o, bool corr) {
+        load_common(k, o);
+#pragma unroll
+        for (int i = 0; i < NU; i++) {
+            const double v = *ws(k, WF_KC + i);
+            o.m[i] = (k < N) ? v : 0.0;
+        }
+        const double kf = *ws(k, WF_KFF);
+        o.m[NU] = (k < N) ? kf : 0.0;
+        if (corr) { o.x0 = *ws(k, WF_AX); o.x1 = *ws(k, WF_AV); } else { o.x0 = o.x1 = 0.0; }
+    };
+    auto load_bwd = [&](int k, In& o) {
+        load_common(k, o);
+        o.x0 = *ws(k, WF_AX); o.x1 = *ws(k, WF_AV); o.x2 = *ws(k, WF_GX); o.x3 = *ws(k, WF_GV);
+#pragma unroll
+        for (int i = 0; i < NU; i++) {
+            const double v = *ws(k, WF_KC + i);
+            o.m[i] = (k < N) ? v : 0.0;
+        }
+#pragma unroll
+        for (int m = 0; m < NU; m++) {
+            const double v = *ws(k, WF_FI + m);
+            o.m[NU + m] = (k < N) ? v : 0.0;
+        }
+    };
+
+    // ---- stage-local helpers
+    auto row_active = [&](int k, double bnd) { return (rowY ? (k >= 1) : (rowD && k < N)) && fabs(bnd) < BIG; };
+    // unsigned c^T z of this lane's box / ddq row; (x, v) = lane components of a stage vector
+    auto row_cz = [&](int k, double x, double v) -> double {
+        const double vj = down_nx(v, t);  // lane NX+j <- v_j
+        if (rowY) return x;
+        return (k == 0) ? vj : vj - x;
+    };
+    // c^T z of poly row t (= p), reduced over the group: sum_m a_p[m] y_m + bv_p[m] v_m
+    auto poly_cz = [&](const In& in, int k, double x, double v) -> double {
+        double r = 0.0;
+#pragma unroll
+        for (int p = 0; p < NPM; p++) {
+            const bool live = (double)p < in.np && k < N;
+            const double term = live ? in.pa[p] * x + in.pb[p] * v : 0.0;
+            const double s = g_sum32(term);
+            if (t == p) r = s;
+        }
+        return r;
+    };
+    auto poly_slot_active = [&](const In& in, int k) {
+        return t < NPM && (double)t < in.np && k < N && fabs(in.pub) < BIG;
+    };
+    // step-system gradient g = g0 + sum_i sgn_i coef_i c_i (dvr: signed coefficient of row t, cP: poly row t)
+    auto assemble_grad = [&](const In& in, int k, double g0x, double g0v, double dvr, double cP, double& gx, double& gvv) {
+        gx = g0x;
+        if (rowY) gx += dvr;
+        else if (rowD && k >= 1) gx -= dvr;
+        gvv = g0v;
+        const double dv_up = up_nx(dvr, t);  // lane j <- ddq row j
+        if (t < DOF && k < N) gvv += dv_up;
+        const Halves hc = halves(cP);
+#pragma unroll
+        for (int p = 0; p < NPM; p++) {
+            const double cp = bch(hc, p);
+            const bool live = (double)p < in.np && k < N;
+            if (live) {
+                gx += cp * in.pa[p];  // zero for lanes >= DOF
+                gvv += cp * in.pb[p];
+            }
+        }
+    };
+    // forward step: v = K x~ + kff (group sums over the K column layout; result on lanes < NU) and
+    // x~' = A~ x~ + B~ v (all lanes)
+    auto fwd_step = [&](const In& in, double xt, double& v, double& xn) {
+        double vv = 0.0;
+#pragma unroll
+        for (int i = 0; i < NU; i++) {
+            const double s = g_sum32(in.m[i] * xt);
+            if (t == i) vv = s;
+        }
+        v = vv + in.m[NU];
+        const Halves hx = halves(xt), hv = halves(v);
+        const double xvs = bch(hx, XVS);
+        const double vprev = down32<1>(v, hv, t);   // lane XVS <- v_dVs (lane XS)
+        const double vj = down32<NX>(v, hv, t);     // lane NX + j <- v_j
+        if (t < DOF) xn = mt * xt + gt * v;
+        else if (t == XS) xn = (mss * xt + msv * xvs) + gs * v;
+        else if (t == XVS) xn = mt * xt + gv * vprev;
+        else xn = rowD ? vj : 0.0;
+    };
+
+    In cur, nxt;
+    int it = 0, it_total = 0;
+    bool conv = false, diverged = false;
+    double alpha = 0.0;
+#pragma unroll 1
+    for (int attempt = 0; attempt < 2; attempt++) {
+        const double s_floor = (attempt == 0) ? IPM_S0 : 1.0;
+        const double lam_scale = (attempt == 0) ? IPM_L0 : 0.0;
+        const int max_it = (attempt == 0) ? IPM_MAX_IT_SCALED : IPM_MAX_IT;
+        if (attempt == 1) {
+            run = entered && !conv;
+            if (__ballot(run) == 0) break;
+            if (run) diverged = false;
+        }
+        // ---- start point: dynamics rollout with v = 0; slacks / multipliers (solve_struct_ipm)
+        double mcount = 0.0;
+        if (run) {
+            double y = 0.0;  // lane a < NX: y_a of stage k
+            for (int k = 0; k <= N; k++) {
+                load_common(k, cur);
+                const double bk = (k < N && rowY) ? QSb[(size_t)k * QS + QS_B + (rowY ? t : 0)] : 0.0;
+                const double yx = rowY ? y : 0.0;
+                const double cz = row_cz(k, yx, 0.0);
+                const double pcz = poly_cz(cur, k, yx, 0.0);
+                const bool aL = row_active(k, cur.lb), aU = row_active(k, cur.ub), aP = poly_slot_active(cur, k);
+                double sL = 1, lL = 0, sU = 1, lU = 0, sP = 1, lP = 0;
+                if (aL) { sL = fmax(-(sgnL * cz - sgnL * cur.lb), s_floor); lL = (lam_scale > 0) ? lam_scale / sL : 1.0; }
+                if (aU) { sU = fmax(-(sgnU * cz - sgnU * cur.ub), s_floor); lU = (lam_scale > 0) ? lam_scale / sU : 1.0; }
+                if (aP) { sP = fmax(-(sgnU * pcz - sgnU * cur.pub), s_floor); lP = (lam_scale > 0) ? lam_scale / sP : 1.0; }
+                mcount += (aL ? 1.0 : 0.0) + (aU ? 1.0 : 0.0) + (aP ? 1.0 : 0.0);
+                *ws(k, WF_SL) = sL; *ws(k, WF_LL) = lL; *ws(k, WF_SU) = sU; *ws(k, WF_LU) = lU;
+                *ws(k, WF_SP) = sP; *ws(k, WF_LP) = lP;
+                *ws(k, WF_ZX) = yx;
+                *ws(k, WF_ZV) = 0.0;
+                // y_{k+1} = M y_k + b_k (oracle order: sum_b M[a][b] y_b, then + b_a)
+                const double yvs = up1(y, t);  // lane XS <- y_vs
+                const double yn = (t == XS) ? mss * y + msv * yvs : mt * y;
+                y = rowY ? yn + bk : 0.0;
+            }
+        }
+        mcount = g_sum32(mcount);
+
+        it = 0;
+        double mu0 = 0.0, dz_prev = 1e30, sigma_mu = 0.0, mu_cur = 1e30, rp_cur = 1e30;
+        bool pending = false;
+        if (run) alpha = 0.0;
+        while (true) {
+            if (__ballot(run) == 0) break;
+            if (run) {
+                // ================= factorization sweep k = N..0 (lazy update, g0, predictor backward solve)
+                double Pc[NXA];  // column t of P_{k+1}
+                double pv = 0.0; // p_{k+1}, component t
+                bool chol_ok = true;
+                sweep(N, true, cur, nxt, [&](int k, In& o) { load_factor(k, o, pending); }, [&](int k, const In& cur) {
+                    const double lb = cur.lb, ub = cur.ub;
+                    const double* Qr = cur.m;
+                    const double qt = cur.m[NX], Rt = cur.m[NX + 1], rt = cur.m[NX + 2];
+                    double sL = cur.sL, lL = cur.lL, sU = cur.sU, lU = cur.lU, sP = cur.sP, lP = cur.lP;
+                    double zx = cur.zx, zv = cur.zv;
+                    const bool aL = row_active(k, lb), aU = row_active(k, ub), aP = poly_slot_active(cur, k);
+                    if (pending) {
+                        const double dx = cur.x0, dv = cur.x1, ax = cur.x2, av = cur.x3;
+                        const double cz = row_cz(k, zx, zv), cd = row_cz(k, dx, dv), ca = row_cz(k, ax, av);
+                        const double pcz = poly_cz(cur, k, zx, zv), pcd = poly_cz(cur, k, dx, dv), pca = poly_cz(cur, k, ax, av);
+                        double rpd;
+                        if (aL) { const SlotStep st = slot_corr(sgnL, lb, cz, ca, cd, sL, lL, sigma_mu, &rpd); sL += alpha * st.ds; lL += alpha * st.dl; }
+                        if (aU) { const SlotStep st = slot_corr(sgnU, ub, cz, ca, cd, sU, lU, sigma_mu, &rpd); sU += alpha * st.ds; lU += alpha * st.dl; }
+                        if (aP) { const SlotStep st = slot_corr(sgnU, cur.pub, pcz, pca, pcd, sP, lP, sigma_mu, &rpd); sP += alpha * st.ds; lP += alpha * st.dl; }
+                        zx += alpha * dx;
+                        zv += alpha * dv;
+                        *ws(k, WF_SL) = sL; *ws(k, WF_LL) = lL; *ws(k, WF_SU) = sU; *ws(k, WF_LU) = lU;
+                        *ws(k, WF_SP) = sP; *ws(k, WF_LP) = lP;
+                        *ws(k, WF_ZX) = zx; *ws(k, WF_ZV) = zv;
+                    }
+                    // ---- slots: barrier weights and predictor coefficients (rc = s l)
+                    const double cz = row_cz(k, zx, zv);
+                    const double pcz = poly_cz(cur, k, zx, zv);
+                    double WL = 0, WU = 0, WP = 0, cL = 0, cU = 0, cP = 0;
+                    if (aL) { const double rp = slot_rp(sgnL, cz, lb, sL); const double ri = rcp(sL); WL = lL * ri; cL = slot_coef(ri, lL, rp, sL * lL); }
+                    if (aU) { const double rp = slot_rp(sgnU, cz, ub, sU); const double ri = rcp(sU); WU = lU * ri; cU = slot_coef(ri, lU, rp, sU * lU); }
+                    if (aP) { const double rp = slot_rp(sgnU, pcz, cur.pub, sP); const double ri = rcp(sP); WP = lP * ri; cP = slot_coef(ri, lP, rp, sP * lP); }
+                    const double wd = WL + WU;
+                    const double dvr = sgnL * cL + sgnU * cU;
+                    // ---- objective gradient g0 = H z + h
+                    double g0x, g0v = 0.0;
+                    {
+                        const Halves hz = halves(zx);
+                        const double vj = down_nx(zv, t);  // lane NX+j <- v_j
+                        const double wj = up32<NX>(zx, hz, t);  // lane j <- w_j
+                        if (rowY) {
+                            double s = 0;
+#pragma unroll
+                            for (int m = 0; m < NX; m++) s += Qr[m] * bch(hz, m);
+                            g0x = s + qt;
+                        } else {
+                            g0x = (rowD && k >= 1 && k < N) ? Hct * vj : 0.0;
+                        }
+                        if (t < NU && k < N) {
+                            double s = (k >= 1 && t < DOF) ? Hct * wj : 0.0;
+                            s += Rt * zv;
+                            g0v = s + rt;
+                        }
+                    }
+                    *ws(k, WF_GX) = g0x;
+                    *ws(k, WF_GV) = g0v;
+                    double gx, gvv;
+                    assemble_grad(cur, k, g0x, g0v, dvr, cP, gx, gvv);
+                    if (k == N) {
+                        // terminal stage: P = Hb_N (y block; Q row t used as column t), p = g_x~
+#pragma unroll
+                        for (int a = 0; a < NXA; a++) {
+                            double v = 0.0;
+                            if (rowY && a < NX) {
+                                v = Qr[a];
+                                if (a == t) v += wd;
+                            }
+                            Pc[a] = v;
+                        }
+                        pv = gx;
+                        return;
+                    }
+                    // ---- (1) Y = B~^T P (column t), f = g_v + B~^T p (lanes < NU)
+                    double Y[NU];
+#pragma unroll
+                    for (int i = 0; i < DOF; i++) Y[i] = c.G[i * (NU + 1)] * Pc[i] + Pc[NX + i];
+                    Y[UVS] = gs * Pc[XS] + gv * Pc[XVS];
+                    const Halves hp = halves(pv);
+                    const double pu = up32<NX>(pv, hp, t), pu1 = up32<1>(pv, hp, t);
+                    const double fv = gvv + gt * pv + ((t < DOF) ? pu : gv * pu1);
+                    // ---- (2) F column t (t < NU), Gm column t (t < NX); poly terms W_p bv_p bv_p^T, W_p bv_p a_p^T
+                    //          (accumulated over p ascending per entry, as ipm.hip)
+                    const double wdv = up_nx(wd, t);  // lane j <- ddq row j weight
+                    const Halves hw = halves(WP);
+                    double Fc[NU], gm[NU];
+#pragma unroll
+                    for (int i = 0; i < NU; i++) {
+                        Fc[i] = (i == t) ? Rt + ((t < DOF) ? wdv : 0.0) : 0.0;
+                        gm[i] = 0.0;
+                    }
+#pragma unroll
+                    for (int p = 0; p < NPM; p++) {
+                        const bool live = (double)p < cur.np && k < N;
+                        const double wp = bch(hw, p);
+                        const double Wp = live ? wp : 0.0;
+                        const Halves hb = halves(cur.pb[p]);
+#pragma unroll
+                        for (int i = 0; i < DOF; i++) {
+                            const double bvi = bch(hb, i);
+                            Fc[i] += Wp * (bvi * cur.pb[p]);   // bv_p[t]: zero for lanes >= DOF
+                            gm[i] += Wp * (bvi * cur.pa[p]);   // a_p[t]: zero for lanes >= DOF
+                        }
+                    }
+#pragma unroll
+                    for (int i = 0; i < NU; i++) {
+                        const Halves hy = halves(Y[i]);
+                        const double yu = up32<NX>(Y[i], hy, t);
+                        const double yu1 = up32<1>(Y[i], hy, t);
+                        const double yd = down32<1>(Y[i], hy, t);
+                        Fc[i] = Fc[i] + (gt * Y[i] + ((t < DOF) ? yu : gv * yu1));
+                        gm[i] = gm[i] + (mt * Y[i] + ((t == XVS) ? msv * yd : 0.0));
+                    }
+                    // ---- (3) chol(F) from the LDS copy of F; U = LF^-1 Gm; K = -LF^-T U; F^-1 row t;
+                    //          kff = -F^-1 f; p = g_x~ + A~^T p + K^T f
+                    if (t < NU)
+#pragma unroll
+                        for (int i = 0; i < NU; i++) S[L_F + i * 16 + t] = Fc[i];
+                    lds_sync();
+                    double LF[NU * (NU + 1) / 2], dinv[NU];
+#pragma unroll
+                    for (int i = 0; i < NU; i++) {
+                        const double2* row = reinterpret_cast<const double2*>(S + L_F + i * 16);
+#pragma unroll
+                        for (int q2 = 0; q2 < (NU + 1) / 2; q2++) {
+                            const double2 w = row[q2];
+                            if (2 * q2 <= i) LF[i * (i + 1) / 2 + 2 * q2] = w.x;
+                            if (2 * q2 + 1 <= i) LF[i * (i + 1) / 2 + 2 * q2 + 1] = w.y;
+                        }
+                    }
+                    chol_ok = cholN(LF, dinv) && chol_ok;
+                    double u[NU];
+                    const double gw = (k >= 1) ? Hct - wd : 0.0;
+#pragma unroll
+                    for (int i = 0; i < NU; i++) u[i] = rowY ? gm[i] : ((rowD && i == j9) ? gw : 0.0);
+                    fwdN(LF, dinv, u);
+                    double kc[NU];
+#pragma unroll
+                    for (int i = 0; i < NU; i++) kc[i] = u[i];
+                    bwdN(LF, dinv, kc);
+#pragma unroll
+                    for (int i = 0; i < NU; i++) kc[i] = -kc[i];
+                    double fi[NU];
+#pragma unroll
+                    for (int i = 0; i < NU; i++) fi[i] = (i == t) ? 1.0 : 0.0;
+                    fwdN(LF, dinv, fi);
+                    bwdN(LF, dinv, fi);
+                    const Halves hf = halves(fv);
+                    double fb[NU];
+#pragma unroll
+                    for (int i = 0; i < NU; i++) fb[i] = bch(hf, i);
+                    double kff = 0.0;
+#pragma unroll
+                    for (int m = 0; m < NU; m++) kff -= fi[m] * fb[m];
+                    double pnew;
+                    {
+                        double atp = 0.0;
+                        const double p7 = down32<1>(pv, hp, t);  // lane XVS <- p_s
+                        if (rowY) {
+                            atp = mt * pv;
+                            if (t == XVS) atp += msv * p7;
+                        }
+                        double ktf = 0.0;
+#pragma unroll
+                        for (int i = 0; i < NU; i++) ktf += kc[i] * fb[i];
+                        pnew = gx + atp + ktf;
+                    }
+#pragma unroll
+                    for (int i = 0; i < NU; i++) {
+                        S[L_U + i * GW + t] = u[i];
+                        *ws(k, WF_KC + i) = kc[i];
+                        *ws(k, WF_FI + i) = fi[i];
+                    }
+                    *ws(k, WF_KFF) = (t < NU) ? kff : 0.0;
+                    // ---- (4) Hb column t and P = Hb - U^T U (column t); U rows are broadcast LDS reads
+                    double hbv[NXA];
+                    {
+                        double Pc7[NX];
+                        const double zero = 0.0;
+#pragma unroll
+                        for (int a = 0; a < NX; a++) Pc7[a] = down1(Pc[a], t);  // lane XVS <- P[a][XS]
+#pragma unroll
+                        for (int a = 0; a < NXA; a++) {
+                            double v = 0.0;
+                            if (a < NX) {
+                                if (rowY) {
+                                    v = Qr[a];
+                                    if (a == t) v += wd;
+                                }
+                            } else if (a == t) {
+                                v = wd;
+                            }
+                            hbv[a] = v;
+                        }
+#pragma unroll
+                        for (int p = 0; p < NPM; p++) {
+                            const bool live = (double)p < cur.np && k < N;
+                            const double Wp = live ? bch(hw, p) : zero;
+                            const Halves ha = halves(cur.pa[p]);
+#pragma unroll
+                            for (int a = 0; a < DOF; a++) {
+                                const double pab = bch(ha, a);
+                                if (rowY) hbv[a] += Wp * (pab * cur.pa[p]);
+                            }
+                        }
+                        if (rowY) {
+#pragma unroll
+                            for (int a = 0; a < NX; a++) {
+                                double mp = (c.M[a * (NX + 1)] * mt) * Pc[a];
+                                if (t == XVS) mp += (c.M[a * (NX + 1)] * msv) * Pc7[a];
+                                if (a == XVS) mp += (msv * mt) * Pc[XS];
+                                if (a == XVS && t == XVS) mp += (msv * msv) * Pc7[XS];
+                                hbv[a] += mp;
+                            }
+                        }
+                    }
+                    lds_sync();
+                    if (k > 0) {
+#pragma unroll
+                        for (int i = 0; i < NU; i++) {
+                            const double2* row = reinterpret_cast<const double2*>(S + L_U + i * GW);
+                            double ur[NXA];
+#pragma unroll
+                            for (int q2 = 0; q2 < NXA / 2; q2++) {
+                                const double2 w = row[q2];
+                                ur[2 * q2] = w.x;
+                                ur[2 * q2 + 1] = w.y;
+                            }
+#pragma unroll
+                            for (int a = 0; a < NXA; a++) hbv[a] -= ur[a] * u[i];
+                        }
+#pragma unroll
+                        for (int a = 0; a < NXA; a++) Pc[a] = hbv[a];
+                    }
+                    pv = pnew;
+                    lds_sync();
+                });
+                if (!chol_ok) {
+                    conv = it > 0 && mu_cur < IPM_TOL_FB && rp_cur < IPM_TOL_FB;  // P2
+                    alpha = 0.0;
+                    run = false;
+                }
+            }
+            if (run) {
+                // ---- predictor forward: x~_0 = 0; recover dsa, dla; max step; mu(alpha) sums
+                double S0 = 0, S1 = 0, S2 = 0;
+                MinRatio amr(1.0);
+                double xt = 0.0;
+                sweep(N, false, cur, nxt, [&](int k, In& o) { load_fwd(k, o, false); }, [&](int k, const In& cur) {
+                    const bool aL = row_active(k, cur.lb), aU = row_active(k, cur.ub), aP = poly_slot_active(cur, k);
+                    double v = 0.0, xn = 0.0;
+                    fwd_step(cur, xt, v, xn);
+                    const double dvv = (t < NU && k < N) ? v : 0.0;
+                    *ws(k, WF_AX) = xt;
+                    *ws(k, WF_AV) = dvv;
+                    const double cz = row_cz(k, cur.zx, cur.zv), ca = row_cz(k, xt, dvv);
+                    const double pcz = poly_cz(cur, k, cur.zx, cur.zv), pca = poly_cz(cur, k, xt, dvv);
+                    auto rec = [&](bool a, double sgn, double bnd, double czz, double caa, double s, double l) {
+                        if (!a) return;
+                        const double rp = slot_rp(sgn, czz, bnd, s);
+                        const SlotStep st = slot_recover(rcp(s), l, rp, sgn * caa, s * l);
+                        step_bound(amr, s, l, st);
+                        S0 += s * l;
+                        S1 += s * st.dl + l * st.ds;
+                        S2 += st.ds * st.dl;
+                    };
+                    rec(aL, sgnL, cur.lb, cz, ca, cur.sL, cur.lL);
+                    rec(aU, sgnU, cur.ub, cz, ca, cur.sU, cur.lU);
+                    rec(aP, sgnU, cur.pub, pcz, pca, cur.sP, cur.lP);
+                    xt = (k < N) ? xn : 0.0;
+                });
+                const double amax = g_min32(amr.value());
+                S0 = g_sum32(S0); S1 = g_sum32(S1); S2 = g_sum32(S2);
+                const double mu = (mcount > 0) ? S0 / mcount : 0.0;
+                if (it == 0) mu0 = mu;
+                double mua = S0 + amax * S1 + amax * amax * S2;
+                mua = (mcount > 0) ? mua / mcount : 0.0;
+                const double ratio = (mu > 0) ? mua / mu : 0.0;
+                const double sigma = (mu > 0) ? ratio * ratio * ratio : 0.0;
+                const double smu = sigma * mu;
+
+                // ---- corrector backward: coef with rc = s l + dsa dla - sigma mu; f = g_v + B~^T p;
+                //      kff = -F^-1 f; p = g_x~ + A~^T p + K^T f
+                double pv = 0.0;
+                sweep(N, true, cur, nxt, [&](int k, In& o) { load_bwd(k, o); }, [&](int k, const In& cur) {
+                    const bool aL = row_active(k, cur.lb), aU = row_active(k, cur.ub), aP = poly_slot_active(cur, k);
+                    const double cz = row_cz(k, cur.zx, cur.zv), ca = row_cz(k, cur.x0, cur.x1);
+                    const double pcz = poly_cz(cur, k, cur.zx, cur.zv), pca = poly_cz(cur, k, cur.x0, cur.x1);
+                    auto coef = [&](bool a, double sgn, double bnd, double czz, double caa, double s, double l) -> double {
+                        if (!a) return 0.0;
+                        const double rp = slot_rp(sgn, czz, bnd, s);
+                        const double ri = rcp(s);
+                        const SlotStep pa = slot_recover(ri, l, rp, sgn * caa, s * l);
+                        const double rc = s * l + pa.ds * pa.dl - smu;
+                        return slot_coef(ri, l, rp, rc);
+                    };
+                    const double cL = coef(aL, sgnL, cur.lb, cz, ca, cur.sL, cur.lL);
+                    const double cU = coef(aU, sgnU, cur.ub, cz, ca, cur.sU, cur.lU);
+                    const double cP = coef(aP, sgnU, cur.pub, pcz, pca, cur.sP, cur.lP);
+                    const double dvr = sgnL * cL + sgnU * cU;
+                    double gx, gvv;
+                    assemble_grad(cur, k, cur.x2, cur.x3, dvr, cP, gx, gvv);
+                    const Halves hp = halves(pv);
+                    const double pu = up32<NX>(pv, hp, t), pu1 = up32<1>(pv, hp, t);
+                    const double fv = gvv + gt * pv + ((t < DOF) ? pu : gv * pu1);
+                    const Halves hf = halves(fv);
+                    double fb[NU];
+#pragma unroll
+                    for (int i = 0; i < NU; i++) fb[i] = bch(hf, i);
+                    double kff = 0.0;
+#pragma unroll
+                    for (int m = 0; m < NU; m++) kff -= cur.m[NU + m] * fb[m];
+                    *ws(k, WF_KFF) = (t < NU && k < N) ? kff : 0.0;
+                    double atp = 0.0;
+                    const double p7 = down32<1>(pv, hp, t);
+                    if (rowY) {
+                        atp = mt * pv;
+                        if (t == XVS) atp += msv * p7;
+                    }
+                    double ktf = 0.0;
+#pragma unroll
+                    for (int i = 0; i < NU; i++) ktf += cur.m[i] * fb[i];
+                    pv = (k == N) ? gx : gx + atp + ktf;
+                });
+
+                // ---- corrector forward: dz, ds, dl, max step, mu(alpha) sums, max |rp|, max |dz|
+                double T0 = 0, T1 = 0, T2 = 0, rpm = 0, dzm = 0;
+                MinRatio amc(1e30);
+                xt = 0.0;
+                sweep(N, false, cur, nxt, [&](int k, In& o) { load_fwd(k, o, true); }, [&](int k, const In& cur) {
+                    const bool aL = row_active(k, cur.lb), aU = row_active(k, cur.ub), aP = poly_slot_active(cur, k);
+                    double v = 0.0, xn = 0.0;
+                    fwd_step(cur, xt, v, xn);
+                    const double dvv = (t < NU && k < N) ? v : 0.0;
+                    const double xtt = (t < NXA) ? xt : 0.0;
+                    *ws(k, WF_DX) = xtt;
+                    *ws(k, WF_DV) = dvv;
+                    dzm = fmax(dzm, fmax(fabs(xtt), fabs(dvv)));
+                    const double cz = row_cz(k, cur.zx, cur.zv), cd = row_cz(k, xtt, dvv), ca = row_cz(k, cur.x0, cur.x1);
+                    const double pcz = poly_cz(cur, k, cur.zx, cur.zv), pcd = poly_cz(cur, k, xtt, dvv);
+                    const double pca = poly_cz(cur, k, cur.x0, cur.x1);
+                    auto rec = [&](bool a, double sgn, double bnd, double czz, double caa, double cdd, double s, double l) {
+                        if (!a) return;
+                        double rp;
+                        const SlotStep st = slot_corr(sgn, bnd, czz, caa, cdd, s, l, smu, &rp);
+                        step_bound(amc, s, l, st);
+                        T0 += s * l;
+                        T1 += s * st.dl + l * st.ds;
+                        T2 += st.ds * st.dl;
+                        rpm = fmax(rpm, fabs(rp));
+                    };
+                    rec(aL, sgnL, cur.lb, cz, ca, cd, cur.sL, cur.lL);
+                    rec(aU, sgnU, cur.ub, cz, ca, cd, cur.sU, cur.lU);
+                    rec(aP, sgnU, cur.pub, pcz, pca, pcd, cur.sP, cur.lP);
+                    xt = (k < N) ? xn : 0.0;
+                });
+                const double amx = g_min32(amc.value());
+                T0 = g_sum32(T0); T1 = g_sum32(T1); T2 = g_sum32(T2);
+                rpm = g_max32(rpm);
+                dzm = g_max32(dzm);
+                alpha = fmin(1.0, fmax(IPM_TAU, 1.0 - sqrt(mu)) * amx);
+                sigma_mu = smu;
+                pending = true;
+                it++;
+                if (it < max_it) {
+                    double mun = T0 + alpha * T1 + alpha * alpha * T2;
+                    mun = (mcount > 0) ? mun / mcount : 0.0;
+                    const double rpn = (1.0 - alpha) * rpm;
+                    mu_cur = mun;
+                    rp_cur = rpn;
+                    const bool step_ok = dzm < IPM_TOL_STEP || dzm * dzm < IPM_TOL_STEP * dz_prev;
+                    dz_prev = dzm;
+                    if (mun < IPM_TOL_MU && rpn < IPM_TOL_P && step_ok) {
+                        conv = true;
+                        run = false;
+                    } else if (mun > IPM_DIV * mu0) {
+                        diverged = true;
+                        run = false;
+                    }
+                } else {
+                    run = false;
+                }
+            }
+        }
+        it_total += it;
+    }  // attempt
+
+    if (!entered) return;
+    if (t == 0) si[SQ_IPMIT] = it_total;
+    if (!conv) {  // keep the previous step (Q6)
+        if (t == 0) si[SQ_QPSTAT] = diverged ? MPCC_QP_PrimalInfeasible : MPCC_QP_MaxIterReached;
+        return;
+    }
+    if (t == 0) si[SQ_QPSTAT] = 0;
+    gdouble* stp = (gdouble*)(d.step + (size_t)b * NS * NXU);
+    for (int k = 0; k <= N; k++) {
+        const double zx = *ws(k, WF_ZX) + alpha * *ws(k, WF_DX);
+        const double zv = *ws(k, WF_ZV) + alpha * *ws(k, WF_DV);
+        if (t < NX) stp[k * NXU + t] = zx;
+        if (t < NU) stp[k * NXU + NX + t] = (k < N) ? zv : 0.0;
+    }
+}
+
+template <int NPM>
+__global__ void __launch_bounds__(64) k_ipm(DevConst c, DevBuffers d) {
+    extern __shared__ __attribute__((aligned(16))) double smem[];
+    ipm_group<NPM>(c, d, smem);
+}
+
+// ------------------------------------------------------------------------------------------------
+// k_sqp: the SQP loop of solveOCP (osqp_interface.cpp:431-574) per instance, one 32-lane group per instance
+// (as ipm.hip's k_sqp: QP solve, line-search trial lane = stage, filter decision, step, next QP assembly)
+// ------------------------------------------------------------------------------------------------
+__device__ __attribute__((noinline)) void sqp_setqp_phase(const DevConst& c, const DevBuffers& d, int b, int t,
+                                                          const double* __restrict__ ucur) {
+    const int N = c.N, NS = N + 1;
+    const SplineView sp = spl_of(c.spl, b);
+    const double* gb = d.guess + (size_t)b * NS * NXU;
+    for (int k = t; k <= N; k += GW)
+        setqp_stage(c, sp, gb, RecView{d.rec + (size_t)b * NS + k, c.S}, k, ucur, d.qs + ((size_t)b * NS + k) * QS);
+}
+__device__ __attribute__((noinline)) void sqp_trial_phase(const DevConst& c, const DevBuffers& d, int b, int t,
+                                                          const double* __restrict__ ucur, double alpha, bool keep) {
+    const int N = c.N, NS = N + 1;
+    for (int k = t; k <= N; k += GW) {
+        double out[4];
+        trial_stage(c, d, b, k, alpha, ucur, out);
+        if (keep) {
+            double* tr = d.trial + ((size_t)b * NS + k) * 4;
+            for (int i = 0; i < 4; i++) tr[i] = out[i];
+        }
+    }
+}
+__device__ __attribute__((noinline)) void sqp_soc_phase(const DevConst& c, const DevBuffers& d, int b, int t,
+                                                        const double* __restrict__ ucur) {
+    const int N = c.N, NS = N + 1;
+    const SplineView sp = spl_of(c.spl, b);
+    const size_t o = (size_t)b * NS * NXU;
+    for (int k = t; k <= N; k += GW)
+        soc_stage(c, sp, d.guess + o, d.step + o, RecView{d.rec + (size_t)b * NS + k, c.S}, k, ucur,
+                  d.qs + ((size_t)b * NS + k) * QS);
+}
+template <int NPM>
+__device__ __attribute__((noinline)) void sqp_ipm_phase(const DevConst& c, const DevBuffers& d, double* smem) {
+    ipm_group<NPM>(c, d, smem);
+}
+
+template <int NPM>
+__global__ void __launch_bounds__(64) k_sqp(DevConst c, DevBuffers d, const double* __restrict__ ucur_all) {
+    extern __shared__ __attribute__((aligned(16))) double smem[];
+    const int t = threadIdx.x % GW;
+    const int b = blockIdx.x * IPW + threadIdx.x / GW;
+    const bool valid = b < c.Bn;
+    const int N = c.N, NS = N + 1;
+    const int bb = valid ? b : 0;
+    int32_t* si = d.sqi + (size_t)bb * SQI;
+    const double* ucur = ucur_all + NU * bb;
+    for (int it = 0; it < c.p.max_iter; it++) {
+        bool act = valid && si[SQ_ACTIVE] != 0;
+        if (__ballot(act) == 0) break;
+        if (it > 0) {
+            if (act) sqp_setqp_phase(c, d, b, t, ucur);
+            __syncthreads();
+        }
+        sqp_ipm_phase<NPM>(c, d, smem);
+        __syncthreads();
+        if (c.p.do_SOC) {  // SecondOrderCorrection (osqp_interface.cpp:506-535)
+            act = valid && si[SQ_ACTIVE] != 0;
+            if (act) sqp_soc_phase(c, d, b, t, ucur);
+            __syncthreads();
+            sqp_ipm_phase<NPM>(c, d, smem);
+            __syncthreads();
+        }
+        act = valid && si[SQ_ACTIVE] != 0;
+        if (act) sqp_trial_phase(c, d, b, t, ucur, 1.0, true);
+        __syncthreads();
+        if (act && t == 0) accept_instance(c, d, b);
+        __syncthreads();
+        if (act && c.faithful_dead_trials && si[SQ_REJECT]) {
+            double alpha = 1.0;
+            for (int l = 1; l < c.p.line_search_max_iter; l++) {
+                alpha *= c.p.line_search_tau;
+                sqp_trial_phase(c, d, b, t, ucur, alpha, false);
+            }
+        }
+        double nrm = 0.0;
+        if (act) {
+            const double alpha = d.sqd[(size_t)b * SQ + SQ_ALPHA];
+            for (int e = t; e < NS * NXU; e += GW) nrm = fmax(nrm, apply_elem(c, d, b, e, alpha));
+        }
+        nrm = g_max32(nrm);
+        if (act && t == 0) finish_iteration(c, d, b, nrm);
+        __syncthreads();
+    }
+}
+
+template <int NPM>
+static void launch_ipm_t(const DevConst& c, const DevBuffers& d, hipStream_t s) {
+    hipLaunchKernelGGL(k_ipm<NPM>, dim3((c.Bn + IPW - 1) / IPW), dim3(64), ipm_lds_bytes(c.N, NPM), s, c, d);
+}
+template <int NPM>
+static void launch_sqp_t(const DevConst& c, const DevBuffers& d, const double* u_cur, hipStream_t s) {
+    hipLaunchKernelGGL(k_sqp<NPM>, dim3((c.Bn + IPW - 1) / IPW), dim3(64), ipm_lds_bytes(c.N, NPM), s, c, d, u_cur);
+}
+
+void launch_ipm(const DevConst& c, const DevBuffers& d, int npmax, hipStream_t s) {
+    switch (npmax) {
+        case 0: launch_ipm_t<0>(c, d, s); break;
+        case 1: launch_ipm_t<1>(c, d, s); break;
+        case 2: launch_ipm_t<2>(c, d, s); break;
+        default: launch_ipm_t<11>(c, d, s); break;
+    }
+}
+void launch_sqp(const DevConst& c, const DevBuffers& d, const double* u_cur, int npmax, hipStream_t s) {
+    switch (npmax) {
+        case 0: launch_sqp_t<0>(c, d, u_cur, s); break;
+        case 1: launch_sqp_t<1>(c, d, u_cur, s); break;
+        case 2: launch_sqp_t<2>(c, d, u_cur, s); break;
+        default: launch_sqp_t<11>(c, d, u_cur, s); break;
+    }
+}
+
+}  // namespace mpcc

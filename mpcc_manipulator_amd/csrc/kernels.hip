@@ -21,47 +21,47 @@ namespace mpcc {
 // MPC::runMPC_ before solveOCP (mpc.cpp:104-124, 54-89): projection, vs estimate, guess shift
 __device__ inline void prepare_mpc(const DevConst& c, const DevBuffers& d, int b) {
     const int N = c.N;
-    double x[9], u[8];
+    double x[NX], u[NU];
 #pragma unroll
-    for (int i = 0; i < 9; i++) x[i] = d.x0[9 * b + i];
+    for (int i = 0; i < NX; i++) x[i] = d.x0[NX * b + i];
 #pragma unroll
-    for (int i = 0; i < 8; i++) u[i] = d.u0[8 * b + i];
-    const double last_s = x[7];
-    double ee[3], J[42];
-    panda_fk(x, ee, nullptr, J, true);
+    for (int i = 0; i < NU; i++) u[i] = d.u0[NU * b + i];
+    const double last_s = x[XS];
+    double ee[3], J[6 * DOF];
+    robot_fk(x, ee, nullptr, J, true);
     const SplineView sp = spl_of(c.spl, b);
-    x[7] = project_on_spline(sp, c.p.proj_max_dist, last_s, ee);
+    x[XS] = project_on_spline(sp, c.p.proj_max_dist, last_s, ee);
     double ev[3];
 #pragma unroll
     for (int i = 0; i < 3; i++) {
         double s = 0;
 #pragma unroll
-        for (int j = 0; j < DOF; j++) s += J[7 * i + j] * u[j];
+        for (int j = 0; j < DOF; j++) s += J[DOF * i + j] * u[j];
         ev[i] = s;
     }
     double dir[3];
-    spline_pos3(sp, x[7], nullptr, dir, nullptr);
-    x[8] = ev[0] * dir[0] + ev[1] * dir[1] + ev[2] * dir[2];
+    spline_pos3(sp, x[XS], nullptr, dir, nullptr);
+    x[XVS] = ev[0] * dir[0] + ev[1] * dir[1] + ev[2] * dir[2];
     int valid = d.valid[b], fails = d.fails[b];
-    if (fabs(last_s - x[7]) > c.p.guess_max_dist) { valid = 0; fails++; }
-    double* g = d.guess + (size_t)b * (N + 1) * 17;
+    if (fabs(last_s - x[XS]) > c.p.guess_max_dist) { valid = 0; fails++; }
+    double* g = d.guess + (size_t)b * (N + 1) * NXU;
     if (valid) {  // updateInitialGuess (mpc.cpp:54-68)
         for (int i = 1; i < N; i++)
-            for (int a = 0; a < 17; a++) g[17 * (i - 1) + a] = g[17 * i + a];
-        for (int a = 0; a < 9; a++) g[a] = x[a];
-        for (int a = 0; a < 17; a++) g[17 * (N - 1) + a] = g[17 * (N - 2) + a];
-        rk4_step(g + 17 * (N - 1), g + 17 * (N - 1) + 9, c.p.Ts, g + 17 * N);
-        for (int a = 0; a < 8; a++) g[17 * N + 9 + a] = 0.0;
+            for (int a = 0; a < NXU; a++) g[NXU * (i - 1) + a] = g[NXU * i + a];
+        for (int a = 0; a < NX; a++) g[a] = x[a];
+        for (int a = 0; a < NXU; a++) g[NXU * (N - 1) + a] = g[NXU * (N - 2) + a];
+        rk4_step(g + NXU * (N - 1), g + NXU * (N - 1) + NX, c.p.Ts, g + NXU * N);
+        for (int a = 0; a < NU; a++) g[NXU * N + NX + a] = 0.0;
     } else {  // generateNewInitialGuess (mpc.cpp:79-89)
         for (int i = 0; i <= N; i++) {
-            for (int a = 0; a < 9; a++) g[17 * i + a] = x[a];
-            for (int a = 0; a < 8; a++) g[17 * i + 9 + a] = 0.0;
+            for (int a = 0; a < NX; a++) g[NXU * i + a] = x[a];
+            for (int a = 0; a < NU; a++) g[NXU * i + NX + a] = 0.0;
         }
         valid = 1;
     }
-    for (int i = 1; i <= N; i++) g[17 * i + 7] = fmin(g[17 * i + 7], sp.L);  // unwrapInitialGuess
+    for (int i = 1; i <= N; i++) g[NXU * i + XS] = fmin(g[NXU * i + XS], sp.L);  // unwrapInitialGuess
 #pragma unroll
-    for (int i = 0; i < 9; i++) d.x0[9 * b + i] = x[i];
+    for (int i = 0; i < NX; i++) d.x0[NX * b + i] = x[i];
     d.valid[b] = valid;
     d.fails[b] = fails;
 }
@@ -78,52 +78,62 @@ __global__ void __launch_bounds__(64) k_prepare(DevConst c, DevBuffers d) {
     si[SQ_NFILT] = 0;
     si[SQ_QPSTAT] = 0;
     si[SQ_IPMIT] = 0;
-    double* st = d.step + (size_t)b * (N + 1) * 17;
-    for (int i = 0; i < (N + 1) * 17; i++) st[i] = 0.0;  // step_.setZero (osqp_interface.cpp:404)
+    double* st = d.step + (size_t)b * (N + 1) * NXU;
+    for (int i = 0; i < (N + 1) * NXU; i++) st[i] = 0.0;  // step_.setZero (osqp_interface.cpp:404)
 }
 
 // ------------------------------------------------------------------------------------------------
 // k_records: FK, Jacobian, manipulability and its central-difference gradient (15 Jacobians).
 // ------------------------------------------------------------------------------------------------
+// RobotData::update (robot_data.h:55-71) of joint vector q into the SoA record at rec (stride S); the
+// self-collision MLP (if masked: infinite distance) and the env MLP outputs are written by k_mlp_*.
+__device__ inline void robot_record(const DevConst& c, const double* q, double obs_r, double* rec, size_t S) {
+    double pos[3], R[9], J[6 * DOF];
+    robot_fk(q, pos, R, J, true);
+#pragma unroll
+    for (int a = 0; a < 3; a++) rec[(R_POS + a) * S] = pos[a];
+#pragma unroll
+    for (int a = 0; a < 9; a++) rec[(R_ROT + a) * S] = R[a];
+#pragma unroll
+    for (int a = 0; a < 6 * DOF; a++) rec[(R_J + a) * S] = J[a];
+    rec[R_MU * S] = manip_from_J(J);
+    const double delta = 1e-4;  // robot_model.cpp:439
+    for (int i = 0; i < DOF; i++) {
+        double qp[DOF], qm[DOF];
+#pragma unroll
+        for (int j = 0; j < DOF; j++) { qp[j] = q[j] + (j == i ? delta : 0.0); qm[j] = q[j] - (j == i ? delta : 0.0); }
+        double m1 = manipulability(qp), m2 = manipulability(qm);
+        rec[(R_DMU + i) * S] = (m1 - m2) / (2 * delta);
+    }
+    const double inf = __longlong_as_double(0x7ff0000000000000LL);
+    if (!(c.p.constraint_mask & MPCC_CON_SELFCOL)) {
+        rec[R_SEL * S] = inf;
+#pragma unroll
+        for (int j = 0; j < DOF; j++) rec[(R_DSEL + j) * S] = 0.0;
+    } else {
+        // the base moves no Panda link relative to another: zero self-collision columns (k_mlp_self
+        // writes the arm columns)
+#pragma unroll
+        for (int j = 0; j < NBASE; j++) rec[(R_DSEL + j) * S] = 0.0;
+    }
+    rec[R_OBSR * S] = obs_r;
+    if (!(c.p.constraint_mask & MPCC_CON_ENVCOL)) {
+        for (int m = 0; m < 9; m++) rec[(R_ENV + m) * S] = inf;
+        for (int m = 0; m < 9 * DOF; m++) rec[(R_DENV + m) * S] = 0.0;
+    }
+}
+
 __global__ void __launch_bounds__(64) k_records(DevConst c, DevBuffers d) {
     const int t = blockIdx.x * blockDim.x + threadIdx.x;
     const int S = c.S;
     if (t >= S) return;
     const int N = c.N;
     const int b = t / (N + 1), k = t - b * (N + 1);
-    const double* g = d.guess + ((size_t)b * (N + 1) + k) * 17;
-    double q[7];
+    const double* g = d.guess + ((size_t)b * (N + 1) + k) * NXU;
+    double q[DOF];
 #pragma unroll
-    for (int j = 0; j < 7; j++) q[j] = g[j];
-    double pos[3], R[9], J[42];
-    panda_fk(q, pos, R, J, true);
-    double* rec = d.rec + t;
-#pragma unroll
-    for (int a = 0; a < 3; a++) rec[(size_t)(R_POS + a) * S] = pos[a];
-#pragma unroll
-    for (int a = 0; a < 9; a++) rec[(size_t)(R_ROT + a) * S] = R[a];
-#pragma unroll
-    for (int a = 0; a < 42; a++) rec[(size_t)(R_J + a) * S] = J[a];
-    rec[(size_t)R_MU * S] = manip_from_J(J);
-    const double delta = 1e-4;  // robot_model.cpp:439
-    for (int i = 0; i < 7; i++) {
-        double qp[7], qm[7];
-#pragma unroll
-        for (int j = 0; j < 7; j++) { qp[j] = q[j] + (j == i ? delta : 0.0); qm[j] = q[j] - (j == i ? delta : 0.0); }
-        double m1 = manipulability(qp), m2 = manipulability(qm);
-        rec[(size_t)(R_DMU + i) * S] = (m1 - m2) / (2 * delta);
-    }
-    const double inf = __longlong_as_double(0x7ff0000000000000LL);
-    if (!(c.p.constraint_mask & MPCC_CON_SELFCOL)) {
-        rec[(size_t)R_SEL * S] = inf;
-#pragma unroll
-        for (int j = 0; j < 7; j++) rec[(size_t)(R_DSEL + j) * S] = 0.0;
-    }
-    rec[(size_t)R_OBSR * S] = d.obs[4 * b + 3];
-    if (!(c.p.constraint_mask & MPCC_CON_ENVCOL)) {
-        for (int m = 0; m < 9; m++) rec[(size_t)(R_ENV + m) * S] = inf;
-        for (int m = 0; m < 63; m++) rec[(size_t)(R_DENV + m) * S] = 0.0;
-    }
+    for (int j = 0; j < DOF; j++) q[j] = g[j];
+    robot_record(c, q, d.obs[4 * b + 3], d.rec + t, (size_t)S);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -135,10 +145,10 @@ __global__ void __launch_bounds__(64) k_setqp(DevConst c, DevBuffers d, const do
     const int N = c.N;
     const int b = t / (N + 1), k = t - b * (N + 1);
     if (!d.sqi[(size_t)b * SQI + SQ_ACTIVE]) return;
-    const double* gb = d.guess + (size_t)b * (N + 1) * 17;
+    const double* gb = d.guess + (size_t)b * (N + 1) * NXU;
     RecView rv{d.rec + t, c.S};
     double* q = d.qs + (size_t)t * QS;
-    setqp_stage(c, spl_of(c.spl, b), gb, rv, k, ucur_all + 8 * b, q);
+    setqp_stage(c, spl_of(c.spl, b), gb, rv, k, ucur_all + NU * b, q);
 }
 
 // k_soc: the SecondOrderCorrection bounds of each (instance, stage) record (soc_stage, dev_sqp.h)
@@ -148,8 +158,8 @@ __global__ void __launch_bounds__(64) k_soc(DevConst c, DevBuffers d, const doub
     const int N = c.N;
     const int b = t / (N + 1), k = t - b * (N + 1);
     if (!d.sqi[(size_t)b * SQI + SQ_ACTIVE]) return;
-    const size_t o = (size_t)b * (N + 1) * 17;
-    soc_stage(c, spl_of(c.spl, b), d.guess + o, d.step + o, RecView{d.rec + t, c.S}, k, ucur_all + 8 * b,
+    const size_t o = (size_t)b * (N + 1) * NXU;
+    soc_stage(c, spl_of(c.spl, b), d.guess + o, d.step + o, RecView{d.rec + t, c.S}, k, ucur_all + NU * b,
               d.qs + (size_t)t * QS);
 }
 
@@ -167,7 +177,7 @@ __global__ void __launch_bounds__(64) k_trial(DevConst c, DevBuffers d, const do
     if (!si[SQ_ACTIVE]) return;
     if (dead && !si[SQ_REJECT]) return;  // dead trials only follow a rejected alpha = 1
     double out[4];
-    trial_stage(c, d, b, k, alpha, ucur_all + 8 * b, out);
+    trial_stage(c, d, b, k, alpha, ucur_all + NU * b, out);
     if (dead) return;  // faithful evaluation of a discarded trial: results are not used
     double* tr = d.trial + (size_t)t * 4;
     for (int i = 0; i < 4; i++) tr[i] = out[i];
@@ -186,7 +196,7 @@ __global__ void __launch_bounds__(64) k_apply(DevConst c, DevBuffers d) {
     if (!d.sqi[(size_t)b * SQI + SQ_ACTIVE]) return;
     const double alpha = d.sqd[(size_t)b * SQ + SQ_ALPHA];
     double nrm = 0;
-    for (int e = 0; e < (c.N + 1) * 17; e++) nrm = fmax(nrm, apply_elem(c, d, b, e, alpha));
+    for (int e = 0; e < (c.N + 1) * NXU; e++) nrm = fmax(nrm, apply_elem(c, d, b, e, alpha));
     finish_iteration(c, d, b, nrm);
 }
 
@@ -196,19 +206,19 @@ __global__ void __launch_bounds__(64) k_apply(DevConst c, DevBuffers d) {
 // ------------------------------------------------------------------------------------------------
 // opt_sol / zero_guess element-wise (thread per horizon element, coalesced): a non-SOLVED instance gets
 // x_0 repeated with u = 0 (osqp_interface.cpp:422-428), a SOLVED one u_N = 0; the horizon output is the
-// result.  x_0 itself (k = 0, a < 9) is never rewritten, so the threads that read it do not race.
+// result.  x_0 itself (k = 0, a < NX) is never rewritten, so the threads that read it do not race.
 __global__ void __launch_bounds__(256) k_finalize_horizon(DevConst c, DevBuffers d) {
     const long e = (long)blockIdx.x * blockDim.x + threadIdx.x;
-    const int W = (c.N + 1) * 17;
+    const int W = (c.N + 1) * NXU;
     if (e >= (long)c.Bn * W) return;
     const int b = (int)(e / W), r = (int)(e - (long)b * W);
-    const int k = r / 17, a = r - 17 * k;
+    const int k = r / NXU, a = r - NXU * k;
     double* g = d.guess + (size_t)b * W;
     const bool solved = d.sqi[(size_t)b * SQI + SQ_STATUS] == MPCC_SOLVED;
     double v = g[r];
-    if (!solved) v = (a < 9) ? g[a] : 0.0;
-    else if (k == c.N && a >= 9) v = 0.0;
-    if (!(k == 0 && a < 9)) g[r] = v;
+    if (!solved) v = (a < NX) ? g[a] : 0.0;
+    else if (k == c.N && a >= NX) v = 0.0;
+    if (!(k == 0 && a < NX)) g[r] = v;
     if (d.horizon) d.horizon[(size_t)b * W + r] = v;
 }
 
@@ -218,7 +228,7 @@ __global__ void __launch_bounds__(64) k_finalize(DevConst c, DevBuffers d) {
     const int N = c.N;
     int32_t* si = d.sqi + (size_t)b * SQI;
     const int status = si[SQ_STATUS];
-    const double* g = d.guess + (size_t)b * (N + 1) * 17;  // already opt_sol / zero_guess (k_finalize_horizon)
+    const double* g = d.guess + (size_t)b * (N + 1) * NXU;  // already opt_sol / zero_guess (k_finalize_horizon)
     if (d.status) d.status[b] = status;
     if (c.ocp) {  // solveOCP's return value only; the MPC bookkeeping belongs to the caller
         if (d.ok) d.ok[b] = (status == MPCC_SOLVED) ? 1 : 0;
@@ -230,7 +240,7 @@ __global__ void __launch_bounds__(64) k_finalize(DevConst c, DevBuffers d) {
         if (d.ok) d.ok[b] = (status == MPCC_SOLVED || (status == MPCC_MAX_ITER_EXCEEDED && fails < 5)) ? 1 : 0;
     }
     if (d.u0_out)
-        for (int a = 0; a < 8; a++) d.u0_out[8 * b + a] = g[9 + a];
+        for (int a = 0; a < NU; a++) d.u0_out[NU * b + a] = g[NX + a];
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -239,17 +249,17 @@ __global__ void __launch_bounds__(64) k_finalize(DevConst c, DevBuffers d) {
 __global__ void k_sim_step(int B, const double* __restrict__ x, const double* __restrict__ u, double ts, double* __restrict__ xn) {
     const int b = blockIdx.x * blockDim.x + threadIdx.x;
     if (b >= B) return;
-    double xc[9], uu[8];
-    for (int a = 0; a < 9; a++) xc[a] = x[9 * b + a];
-    for (int a = 0; a < 8; a++) uu[a] = u[8 * b + a];
+    double xc[NX], uu[NU];
+    for (int a = 0; a < NX; a++) xc[a] = x[NX * b + a];
+    for (int a = 0; a < NU; a++) uu[a] = u[NU * b + a];
     const double fine = 0.001;
     int steps = (int)(ts / fine);
     for (int i = 0; i < steps; i++) {
-        double t[9];
+        double t[NX];
         rk4_step(xc, uu, fine, t);
-        for (int a = 0; a < 9; a++) xc[a] = t[a];
+        for (int a = 0; a < NX; a++) xc[a] = t[a];
     }
-    for (int a = 0; a < 9; a++) xn[9 * b + a] = xc[a];
+    for (int a = 0; a < NX; a++) xn[NX * b + a] = xc[a];
 }
 
 // ---- device closed loop (main.cpp:100-114; mpcc_closed_loop).  The step index lives in device memory
@@ -257,8 +267,8 @@ __global__ void k_sim_step(int B, const double* __restrict__ x, const double* __
 __global__ void k_loop_pre(int B, const double* __restrict__ x, double* __restrict__ xtraj, const int* __restrict__ kstep) {
     const int b = blockIdx.x * blockDim.x + threadIdx.x;
     if (b >= B) return;
-    const size_t o = ((size_t)*kstep * B + b) * 9;
-    for (int a = 0; a < 9; a++) xtraj[o + a] = x[9 * b + a];
+    const size_t o = ((size_t)*kstep * B + b) * NX;
+    for (int a = 0; a < NX; a++) xtraj[o + a] = x[NX * b + a];
 }
 // after runMPC_: a live instance takes u0 and integrates the state runMPC_ updated (simTimeStep); an
 // instance whose runMPC_ returned false stops (main.cpp:108-112) — its state is frozen at the state
@@ -273,23 +283,23 @@ __global__ void k_loop_post(int B, double ts, double* __restrict__ x, double* __
     const bool live = alive[b] != 0;
     const bool go = live && ok[b] != 0;
     if (go) {
-        double xc[9], uu[8];
-        for (int a = 0; a < 8; a++) uu[a] = u0out[8 * b + a];
-        for (int a = 0; a < 9; a++) xc[a] = x[9 * b + a];
+        double xc[NX], uu[NU];
+        for (int a = 0; a < NU; a++) uu[a] = u0out[NU * b + a];
+        for (int a = 0; a < NX; a++) xc[a] = x[NX * b + a];
         const int steps = (int)(ts / 0.001);
         for (int i = 0; i < steps; i++) {
-            double t[9];
+            double t[NX];
             rk4_step(xc, uu, 0.001, t);
-            for (int a = 0; a < 9; a++) xc[a] = t[a];
+            for (int a = 0; a < NX; a++) xc[a] = t[a];
         }
-        for (int a = 0; a < 9; a++) x[9 * b + a] = xc[a];
-        for (int a = 0; a < 8; a++) u[8 * b + a] = uu[a];
+        for (int a = 0; a < NX; a++) x[NX * b + a] = xc[a];
+        for (int a = 0; a < NU; a++) u[NU * b + a] = uu[a];
     } else {
-        for (int a = 0; a < 9; a++) x[9 * b + a] = xtraj[((size_t)k * B + b) * 9 + a];
+        for (int a = 0; a < NX; a++) x[NX * b + a] = xtraj[((size_t)k * B + b) * NX + a];
     }
     if (live && !go) alive[b] = 0;
     straj[(size_t)k * B + b] = live ? status[b] : -1;
-    for (int a = 0; a < 8; a++) utraj[((size_t)k * B + b) * 8 + a] = u[8 * b + a];
+    for (int a = 0; a < NU; a++) utraj[((size_t)k * B + b) * NU + a] = u[NU * b + a];
 }
 __global__ void k_loop_tick(int* kstep) { *kstep += 1; }
 
@@ -298,29 +308,9 @@ __global__ void k_debug_records(DevConst c, int M, const double* __restrict__ qi
                                 double* __restrict__ rec) {
     const int t = blockIdx.x * blockDim.x + threadIdx.x;
     if (t >= M) return;
-    double q[7], pos[3], R[9], J[42];
-    for (int j = 0; j < 7; j++) q[j] = qin[7 * t + j];
-    panda_fk(q, pos, R, J, true);
-    for (int a = 0; a < 3; a++) rec[(size_t)(R_POS + a) * M + t] = pos[a];
-    for (int a = 0; a < 9; a++) rec[(size_t)(R_ROT + a) * M + t] = R[a];
-    for (int a = 0; a < 42; a++) rec[(size_t)(R_J + a) * M + t] = J[a];
-    rec[(size_t)R_MU * M + t] = manip_from_J(J);
-    const double delta = 1e-4;
-    for (int i = 0; i < 7; i++) {
-        double qp[7], qm[7];
-        for (int j = 0; j < 7; j++) { qp[j] = q[j] + (j == i ? delta : 0.0); qm[j] = q[j] - (j == i ? delta : 0.0); }
-        rec[(size_t)(R_DMU + i) * M + t] = (manipulability(qp) - manipulability(qm)) / (2 * delta);
-    }
-    const double inf = __longlong_as_double(0x7ff0000000000000LL);
-    if (!(c.p.constraint_mask & MPCC_CON_SELFCOL)) {
-        rec[(size_t)R_SEL * M + t] = inf;
-        for (int j = 0; j < 7; j++) rec[(size_t)(R_DSEL + j) * M + t] = 0.0;
-    }
-    rec[(size_t)R_OBSR * M + t] = obsin[4 * t + 3];
-    if (!(c.p.constraint_mask & MPCC_CON_ENVCOL)) {
-        for (int m = 0; m < 9; m++) rec[(size_t)(R_ENV + m) * M + t] = inf;
-        for (int m = 0; m < 63; m++) rec[(size_t)(R_DENV + m) * M + t] = 0.0;
-    }
+    double q[DOF];
+    for (int j = 0; j < DOF; j++) q[j] = qin[DOF * t + j];
+    robot_record(c, q, obsin[4 * t + 3], rec + t, (size_t)M);
 }
 
 __global__ void k_debug_spline(DevConst c, int M, const double* __restrict__ sv, double* __restrict__ out) {
@@ -344,11 +334,12 @@ __global__ void k_debug_cost(DevConst c, int M, const double* __restrict__ x, co
     const int t = blockIdx.x * blockDim.x + threadIdx.x;
     if (t >= M) return;
     RecView rv{rec + t, M};
-    double* o = out + (size_t)t * (1 + 9 + 8 + 81 + 64);
-    double fuu[8];
-    o[0] = stage_cost(c, spl_of(c.spl, 0), x + 9 * t, u + 8 * t, rv, kk[t], true, o + 1, o + 10, o + 18, fuu);
-    for (int i = 0; i < 64; i++) o[99 + i] = 0.0;
-    for (int i = 0; i < 8; i++) o[99 + 9 * i] = fuu[i];
+    double* o = out + (size_t)t * (1 + NX + NU + NX * NX + NU * NU);
+    double fuu[NU];
+    double* fuuo = o + 1 + NX + NU + NX * NX;
+    o[0] = stage_cost(c, spl_of(c.spl, 0), x + NX * t, u + NU * t, rv, kk[t], true, o + 1, o + 1 + NX, o + 1 + NX + NU, fuu);
+    for (int i = 0; i < NU * NU; i++) fuuo[i] = 0.0;
+    for (int i = 0; i < NU; i++) fuuo[(NU + 1) * i] = fuu[i];
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -381,7 +372,7 @@ void launch_debug_records(const DevConst& c, int M, const double* q, const doubl
     hipLaunchKernelGGL(k_debug_records, dim3(nblk(M, 64)), dim3(64), 0, s, c, M, q, obs, rec);
 }
 void launch_finalize(const DevConst& c, const DevBuffers& d, hipStream_t s) {
-    hipLaunchKernelGGL(k_finalize_horizon, dim3(nblk((long)c.Bn * (c.N + 1) * 17, 256)), dim3(256), 0, s, c, d);
+    hipLaunchKernelGGL(k_finalize_horizon, dim3(nblk((long)c.Bn * (c.N + 1) * NXU, 256)), dim3(256), 0, s, c, d);
     hipLaunchKernelGGL(k_finalize, dim3(nblk(c.Bn, 64)), dim3(64), 0, s, c, d);
 }
 void launch_sim_step(int B, const double* x, const double* u, double ts, double* xn, hipStream_t s) {

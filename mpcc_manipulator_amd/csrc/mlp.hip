@@ -16,7 +16,7 @@
 //    27% -> 58% of the FP64 roof; k_mlp_self 5.9 -> 4.8 ms.
 //  * v_mfma_f64_16x16x4f64 accumulates as an ascending fma chain over k (bitwise,
 //    tools/probes/mfma_f64_probe.hip); the oracle's MLP uses the same chain.
-#include "dev_common.h"
+#include "dev_model.h"
 #include "dev_dpp.h"
 #include "kernels.h"
 
@@ -91,11 +91,13 @@ __device__ __forceinline__ void mfma_layer_lds(const double* __restrict__ Wp, co
     }
 }
 
-// hidden-layer epilogue: value columns h = relu(z + b); tangent columns dh = (z + b > 0) ? dz : 0
-template <int RT>
+// hidden-layer epilogue: value columns h = relu(z + b); tangent columns dh = (z + b > 0) ? dz : 0.
+// CPS = columns per sample: 8 (value + 7 tangents, 2 samples per 16-column tile) or 16 (value + up to 15
+// tangents, one sample per tile: the mobile env network's 10 input directions).
+template <int RT, int CPS = 8>
 __device__ __forceinline__ void relu_gate(d4 (&a)[RT], const double* __restrict__ bias, int lane) {
-    const bool isv = (lane & 7) == 0;
-    const bool hi = (lane & 8) != 0;
+    const bool isv = (lane & (CPS - 1)) == 0;
+    const bool hi = CPS == 8 && (lane & 8) != 0;
 #pragma unroll
     for (int t = 0; t < RT; t++)
 #pragma unroll
@@ -107,9 +109,9 @@ __device__ __forceinline__ void relu_gate(d4 (&a)[RT], const double* __restrict_
         }
 }
 
-// NeRF input [x, sin x, cos x] (3 NIN rows, zero-padded to 32) with its Jacobian columns for dq_0..dq_6
-// (nerf_jac = [I; diag(cos x); diag(-sin x)], SelfCollisionModel.cpp:143-151, 177-188)
-template <int NIN>
+// NeRF input [x, sin x, cos x] (3 NIN rows, zero-padded to 32) with its Jacobian columns for the input
+// directions 0..CPS-2 (nerf_jac = [I; diag(cos x); diag(-sin x)], SelfCollisionModel.cpp:143-151, 177-188)
+template <int NIN, int CPS = 8>
 __device__ __forceinline__ void nerf_input(const double (&x)[NIN], d4 (&in)[2], int lane) {
     double sx[NIN], cx[NIN];
 #pragma unroll
@@ -117,7 +119,7 @@ __device__ __forceinline__ void nerf_input(const double (&x)[NIN], d4 (&in)[2], 
         sx[i] = sin(x[i]);
         cx[i] = cos(x[i]);
     }
-    const int j = lane & 7;  // 0: value column, 1 + d: tangent of q_d
+    const int j = lane & (CPS - 1);  // 0: value column, 1 + d: tangent of input d
     const int d = j - 1;
 #pragma unroll
     for (int kt = 0; kt < 2; kt++)
@@ -141,7 +143,8 @@ __device__ __forceinline__ void nerf_input(const double (&x)[NIN], d4 (&in)[2], 
         }
 }
 
-// output tile: rows i < NOUT; value column -> out_i + b_i, tangent column 1 + d -> J[i][d]
+// output tile: rows i < NOUT; value column -> out_i + b_i, tangent column 1 + d -> J[i][d] at the record's
+// Jacobian column NBASE + d (the arm joints)
 template <int NOUT>
 __device__ __forceinline__ void write_out(const d4& o, const double* __restrict__ bias, int lane, int m, int M,
                                           double* __restrict__ rec, int S, int r_val, int r_jac) {
@@ -152,32 +155,70 @@ __device__ __forceinline__ void write_out(const d4& o, const double* __restrict_
         const int i = (lane >> 4) + 4 * r;
         if (i >= NOUT) continue;
         if (j == 0) rec[(size_t)(r_val + i) * S + m] = o[r] + bias[i];
-        else rec[(size_t)(r_jac + 7 * i + (j - 1)) * S + m] = o[r];
+        else rec[(size_t)(r_jac + DOF * i + NBASE + (j - 1)) * S + m] = o[r];
     }
 }
 
-// sample m of the call: q (and the obstacle for the env network)
+// Arm-frame obstacle of the mobile manipulator (the oracle's robot_record): o_arm = Rz(th)^T (obs - [x, y, 0])
+// - mount, and dO[a][b] = d o_arm[a] / d (x, y, theta)[b].  The Panda-trained env network sees the obstacle
+// in the panda_link0 frame.
+__device__ __forceinline__ void arm_frame_obstacle(const double* q, const double* obs, double* oa, double (&dO)[3][3]) {
+    double sn, cs;
+    sincos(q[2], &sn, &cs);
+    const double dx = obs[0] - q[0], dy = obs[1] - q[1], dz = obs[2];
+    oa[0] = (cs * dx + sn * dy) - 0.0;
+    oa[1] = (-sn * dx + cs * dy) - 0.0;
+    oa[2] = dz - MOBILE_MOUNT_Z;
+    dO[0][0] = -cs; dO[1][0] = sn; dO[2][0] = 0.0;
+    dO[0][1] = -sn; dO[1][1] = -cs; dO[2][1] = 0.0;
+    dO[0][2] = -sn * dx + cs * dy; dO[1][2] = -cs * dx - sn * dy; dO[2][2] = 0.0;
+}
+
+// output tile of the mobile env network (CPS = 16, one sample per tile): value column 0, arm tangents 1..7,
+// obstacle tangents 8..10.  The base columns of the record are the chain rule through the arm-frame obstacle,
+// sum_a J[i][7 + a] dO[a][b] (the oracle's order), formed on lanes 11..13 of each row from DPP broadcasts.
+template <int NOUT>
+__device__ __forceinline__ void write_out_mobile(const d4& o, const double* __restrict__ bias, int lane, int m, int M,
+                                                 double* __restrict__ rec, int S, const double (&dO)[3][3]) {
+    const int j = lane & 15;
+    const int bb = j - 11;  // base column of lanes 11..13
+    double d0 = 0.0, d1 = 0.0, d2 = 0.0;
+#pragma unroll
+    for (int b = 0; b < NBASE; b++)
+        if (bb == b) { d0 = dO[0][b]; d1 = dO[1][b]; d2 = dO[2][b]; }
+#pragma unroll
+    for (int r = 0; r < 4; r++) {
+        const double j8 = bc<8>(o[r]), j9 = bc<9>(o[r]), j10 = bc<10>(o[r]);  // whole row active
+        const int i = (lane >> 4) + 4 * r;
+        if (m >= M || i >= NOUT) continue;
+        if (j == 0) rec[(size_t)(R_ENV + i) * S + m] = o[r] + bias[i];
+        else if (j <= NARM) rec[(size_t)(R_DENV + DOF * i + NBASE + (j - 1)) * S + m] = o[r];
+        else if (bb >= 0 && bb < NBASE) rec[(size_t)(R_DENV + DOF * i + bb) * S + m] = j8 * d0 + j9 * d1 + j10 * d2;
+    }
+}
+
+// sample m of the call: the robot's joints q (DOF) and the obstacle (x, y, z)
 __device__ __forceinline__ void sample_input(const DevConst& c, const DevBuffers& d, int m, int M, const double* qin,
-                                             const double* obsin, double* x /* 10 */) {
+                                             const double* obsin, double* q /* DOF */, double* obs /* 3 */) {
     const int mm = m < M ? m : 0;
-    const double* q;
-    const double* obs;
+    const double* qs;
+    const double* os;
     if (qin) {  // debug path: explicit q / obs lists
-        q = qin + 7 * mm;
-        obs = obsin + 4 * mm;
+        qs = qin + DOF * mm;
+        os = obsin + 4 * mm;
     } else {
         const int b = mm / (c.N + 1), k = mm - b * (c.N + 1);
-        q = d.guess + ((size_t)b * (c.N + 1) + k) * 17;
-        obs = d.obs + 4 * b;
+        qs = d.guess + ((size_t)b * (c.N + 1) + k) * NXU;
+        os = d.obs + 4 * b;
     }
 #pragma unroll
-    for (int i = 0; i < 7; i++) x[i] = q[i];
-    x[7] = obs[0]; x[8] = obs[1]; x[9] = obs[2];
+    for (int i = 0; i < DOF; i++) q[i] = qs[i];
+    obs[0] = os[0]; obs[1] = os[1]; obs[2] = os[2];
 }
 
 }  // namespace
 
-// self network 21 -> 256 -> 64 -> 1 (osqp_interface.cpp:35-38)
+// self network 21 -> 256 -> 64 -> 1 (osqp_interface.cpp:35-38) on the Panda joints
 __global__ void __launch_bounds__(256) k_mlp_self(DevConst c, DevBuffers d, NNDesc nd, const double* __restrict__ W, int M,
                                                   const double* __restrict__ qin, const double* __restrict__ obsin,
                                                   double* __restrict__ rec, int S) {
@@ -186,11 +227,11 @@ __global__ void __launch_bounds__(256) k_mlp_self(DevConst c, DevBuffers d, NNDe
     const int m = 2 * wave + ((lane >> 3) & 1);
     // no early exit: the input layer synchronizes the block (see k_mlp_env)
     __shared__ __attribute__((aligned(16))) double wl[2 * 16 * 256];
-    double xin[10];
-    sample_input(c, d, m, M, qin, obsin, xin);
+    double q[DOF], obs[3];
+    sample_input(c, d, m, M, qin, obsin, q, obs);
     double x[7];
 #pragma unroll
-    for (int i = 0; i < 7; i++) x[i] = xin[i];
+    for (int i = 0; i < 7; i++) x[i] = q[NBASE + i];
     d4 a0[2], a1[16], a2[4], o[1];
     nerf_input<7>(x, a0, lane);
     mfma_layer_lds<2, 16>(W + nd.offW[0], a0, a1, lane, wl);
@@ -201,40 +242,64 @@ __global__ void __launch_bounds__(256) k_mlp_self(DevConst c, DevBuffers d, NNDe
     write_out<1>(o[0], W + nd.offb[2], lane, m, M, rec, S, R_SEL, R_DSEL);
 }
 
-// env network 30 -> 256 -> 256 -> 256 -> 256 -> 9 (osqp_interface.cpp:40-43)
-__global__ void __launch_bounds__(256) k_mlp_env(DevConst c, DevBuffers d, NNDesc nd, const double* __restrict__ W, int M,
-                                                 const double* __restrict__ qin, const double* __restrict__ obsin,
-                                                 double* __restrict__ rec, int S) {
+// env network 30 -> 256 -> 256 -> 256 -> 256 -> 9 (osqp_interface.cpp:40-43).  Panda: 2 samples per wave,
+// tangents of q_0..q_6.  Mobile manipulator: 1 sample per wave, tangents of the 7 arm joints and the 3
+// arm-frame obstacle coordinates (the base columns follow by the chain rule, write_out_mobile).
+template <int CPS>
+__device__ __forceinline__ void mlp_env_body(const DevConst& c, const DevBuffers& d, const NNDesc& nd, const double* __restrict__ W,
+                                             int M, const double* __restrict__ qin, const double* __restrict__ obsin,
+                                             double* __restrict__ rec, int S, double* wl) {
     const int lane = threadIdx.x & 63;
     const int wave = blockIdx.x * 4 + (threadIdx.x >> 6);
-    const int m = 2 * wave + ((lane >> 3) & 1);
-    // no early exit: the hidden layers synchronize the block (a wave past M computes on a clamped
-    // sample and write_out drops its result)
-    __shared__ __attribute__((aligned(16))) double wl[2 * 16 * 256];
+    const int m = (CPS == 8) ? 2 * wave + ((lane >> 3) & 1) : wave;
+    double q[DOF], obs[3];
+    sample_input(c, d, m, M, qin, obsin, q, obs);
     double x[10];
-    sample_input(c, d, m, M, qin, obsin, x);
+    double dO[3][3] = {};
+#pragma unroll
+    for (int i = 0; i < 7; i++) x[i] = q[NBASE + i];
+    if constexpr (NBASE > 0) {
+        double oa[3];
+        arm_frame_obstacle(q, obs, oa, dO);
+        x[7] = oa[0]; x[8] = oa[1]; x[9] = oa[2];
+    } else {
+        x[7] = obs[0]; x[8] = obs[1]; x[9] = obs[2];
+    }
     d4 a0[2], a[16], h[16], o[1];
-    nerf_input<10>(x, a0, lane);
+    nerf_input<10, CPS>(x, a0, lane);
     mfma_layer_lds<2, 16>(W + nd.offW[0], a0, a, lane, wl);
-    relu_gate<16>(a, W + nd.offb[0], lane);
+    relu_gate<16, CPS>(a, W + nd.offb[0], lane);
     for (int l = 1; l <= 3; l++) {  // three 256 x 256 hidden layers share one unrolled body
         mfma_layer_lds<16, 16>(W + nd.offW[l], a, h, lane, wl);
-        relu_gate<16>(h, W + nd.offb[l], lane);
+        relu_gate<16, CPS>(h, W + nd.offb[l], lane);
 #pragma unroll
         for (int t = 0; t < 16; t++) a[t] = h[t];
     }
     mfma_layer<16, 1>(W + nd.offW[4], a, o, lane);
-    write_out<9>(o[0], W + nd.offb[4], lane, m, M, rec, S, R_ENV, R_DENV);
+    if constexpr (CPS == 8) write_out<9>(o[0], W + nd.offb[4], lane, m, M, rec, S, R_ENV, R_DENV);
+    else write_out_mobile<9>(o[0], W + nd.offb[4], lane, m, M, rec, S, dO);
+}
+
+constexpr int ENV_CPS = (NBASE > 0) ? 16 : 8;  // columns per sample of k_mlp_env
+constexpr int ENV_SPW = 16 / ENV_CPS;          // samples per wave
+
+__global__ void __launch_bounds__(256) k_mlp_env(DevConst c, DevBuffers d, NNDesc nd, const double* __restrict__ W, int M,
+                                                 const double* __restrict__ qin, const double* __restrict__ obsin,
+                                                 double* __restrict__ rec, int S) {
+    // no early exit: the hidden layers synchronize the block (a wave past M computes on a clamped
+    // sample and write_out drops its result)
+    __shared__ __attribute__((aligned(16))) double wl[2 * 16 * 256];
+    mlp_env_body<ENV_CPS>(c, d, nd, W, M, qin, obsin, rec, S, wl);
 }
 
 void launch_nn(const DevConst& c, const DevBuffers& d, const NNDesc& nd, const double* W, int which, int M,
                const double* q, const double* obs, double* rec, int rec_stride, hipStream_t s) {
-    const int blocks = (M + 7) / 8;  // 4 waves x 2 samples
-    if (blocks == 0) return;
-    if (which == 0)
-        hipLaunchKernelGGL(k_mlp_self, dim3(blocks), dim3(256), 0, s, c, d, nd, W, M, q, obs, rec, rec_stride);
+    if (M <= 0) return;
+    if (which == 0)  // 4 waves x 2 samples
+        hipLaunchKernelGGL(k_mlp_self, dim3((M + 7) / 8), dim3(256), 0, s, c, d, nd, W, M, q, obs, rec, rec_stride);
     else
-        hipLaunchKernelGGL(k_mlp_env, dim3(blocks), dim3(256), 0, s, c, d, nd, W, M, q, obs, rec, rec_stride);
+        hipLaunchKernelGGL(k_mlp_env, dim3((M + 4 * ENV_SPW - 1) / (4 * ENV_SPW)), dim3(256), 0, s, c, d, nd, W, M, q, obs,
+                           rec, rec_stride);
 }
 
 }  // namespace mpcc

@@ -116,14 +116,14 @@ __global__ void __launch_bounds__(64) k_robot_frames(int M, const double* __rest
     double J[42];
     panda_frame(qq, frame, r, r + 3, J);
     for (int a = 0; a < 42; a++) r[12 + a] = J[a];
-    r[54] = manip_from_J(J);
+    r[54] = manip_from_J<7>(J);
     const double delta = 1e-4;  // robot_model.cpp:439
     for (int j = 0; j < 7; j++) {
         double qp[7], qm[7], Jp[42], Jm[42];
         for (int a = 0; a < 7; a++) { qp[a] = qq[a] + (a == j ? delta : 0.0); qm[a] = qq[a] - (a == j ? delta : 0.0); }
         panda_frame(qp, frame, nullptr, nullptr, Jp);
         panda_frame(qm, frame, nullptr, nullptr, Jm);
-        r[55 + j] = (manip_from_J(Jp) - manip_from_J(Jm)) / (2 * delta);
+        r[55 + j] = (manip_from_J<7>(Jp) - manip_from_J<7>(Jm)) / (2 * delta);
     }
 }
 

@@ -13,10 +13,20 @@ DATA = os.path.join(PKG, "data")
 NN_DIR = os.path.join(DATA, "nn")
 DEFAULT_PARAMS = os.path.join(DATA, "params", "default_params.json")
 DEFAULT_TRACK = os.path.join(DATA, "params", "default_track.json")
+MOBILE_PARAMS = os.path.join(DATA, "params", "mobile_params.json")
 LIB_PATH = os.environ.get("MPCC_ENGINE_LIB", os.path.join(PKG, "_build", "libmpcc_engine.so"))
+# Robot dimensions are compile-time in the engine, as the reference's NX/NU (config.h:29-38): one library
+# per robot with the same C ABI.  dof 7 = Franka Panda, dof 10 = Husky+Panda mobile manipulator.
+LIB_PATHS = {7: LIB_PATH, 10: os.path.join(PKG, "_build", "libmpcc_engine_mobile.so")}
+ROBOT_DOF = {"panda": 7, "husky_panda": 10}
 
 REC_SIZE = 143
 NX, NU, PANDA_DOF, PANDA_NUM_LINKS = 9, 8, 7, 9
+
+
+def dims(dof):
+    """(NX, NU, NXU, REC) of a robot with dof joints: state [q, s, vs], input [dq, dVs]."""
+    return dof + 2, dof + 1, 2 * dof + 3, 24 + 17 * dof
 
 D, I32 = C.c_double, C.c_int32
 DP, IP = C.POINTER(C.c_double), C.POINTER(C.c_int32)
@@ -29,29 +39,41 @@ SOLVED, MAX_ITER_EXCEEDED = 0, 1
 CON_SELFCOL, CON_SING, CON_ENVCOL = 1, 2, 4
 
 
-class MpccParams(C.Structure):
-    _fields_ = [
-        ("N", I32), ("Ts", D), ("constraint_mask", I32),
-        ("proj_max_dist", D), ("guess_max_dist", D),
-        ("desired_ee_velocity", D), ("deacc_ratio", D), ("cost_tol_selcol", D), ("cost_tol_sing", D),
-        ("q_c", D), ("q_c_N_mult", D), ("q_l", D), ("q_vs", D), ("q_ori", D), ("q_sing", D), ("r_dq", D), ("r_dVs", D),
-        ("q_c_red_ratio", D), ("q_l_inc_ratio", D), ("q_ori_red_ratio", D),
-        ("qp_r_ddq", D),
-        ("con_tol_selcol", D), ("con_tol_sing", D), ("con_tol_envcol", D),
-        ("s_trust_region", D),
-        ("lx", D * 9), ("ux", D * 9), ("lu", D * 8), ("uu", D * 8), ("lddq", D * 7), ("uddq", D * 7),
-        ("Tx", D * 9), ("Tu", D * 8),
-        ("eps_prim", D), ("eps_dual", D), ("line_search_tau", D), ("line_search_eta", D), ("line_search_rho", D),
-        ("max_iter", I32), ("line_search_max_iter", I32), ("do_SOC", I32), ("use_BFGS", I32),
-        ("vio_floor", D),
-    ]
+def _params_struct(dof):
+    """mpcc_params (include/mpcc_engine.h) of the library built with MPCC_DOF = dof."""
+    nx, nu = dof + 2, dof + 1
 
-    def as_dict(self):
-        out = {}
-        for name, _ in self._fields_:
-            v = getattr(self, name)
-            out[name] = list(v) if hasattr(v, "__len__") else v
-        return out
+    class _P(C.Structure):
+        _dof = dof
+        _fields_ = [
+            ("N", I32), ("Ts", D), ("constraint_mask", I32),
+            ("proj_max_dist", D), ("guess_max_dist", D),
+            ("desired_ee_velocity", D), ("deacc_ratio", D), ("cost_tol_selcol", D), ("cost_tol_sing", D),
+            ("q_c", D), ("q_c_N_mult", D), ("q_l", D), ("q_vs", D), ("q_ori", D), ("q_sing", D), ("r_dq", D),
+            ("r_dVs", D), ("q_c_red_ratio", D), ("q_l_inc_ratio", D), ("q_ori_red_ratio", D),
+            ("qp_r_ddq", D),
+            ("con_tol_selcol", D), ("con_tol_sing", D), ("con_tol_envcol", D),
+            ("s_trust_region", D),
+            ("lx", D * nx), ("ux", D * nx), ("lu", D * nu), ("uu", D * nu), ("lddq", D * dof), ("uddq", D * dof),
+            ("Tx", D * nx), ("Tu", D * nu),
+            ("eps_prim", D), ("eps_dual", D), ("line_search_tau", D), ("line_search_eta", D), ("line_search_rho", D),
+            ("max_iter", I32), ("line_search_max_iter", I32), ("do_SOC", I32), ("use_BFGS", I32),
+            ("vio_floor", D),
+        ]
+
+        def as_dict(self):
+            out = {}
+            for name, _ in self._fields_:
+                v = getattr(self, name)
+                out[name] = list(v) if hasattr(v, "__len__") else v
+            return out
+
+    _P.__name__ = "MpccParams" if dof == 7 else f"MpccParams{dof}"
+    return _P
+
+
+PARAMS_STRUCT = {7: _params_struct(7), 10: _params_struct(10)}
+MpccParams = PARAMS_STRUCT[7]
 
 
 class MpccJsonPaths(C.Structure):
@@ -79,16 +101,17 @@ class MpccError(RuntimeError):
     pass
 
 
-_lib = None
+_libs = {}
 
 
-def lib():
-    """Load libmpcc_engine.so (build it first with mpcc_manipulator_amd._build.build())."""
-    global _lib
-    if _lib is not None:
-        return _lib
-    if not os.path.exists(LIB_PATH):
-        raise MpccError(f"libmpcc_engine.so not built ({LIB_PATH}); run python -m mpcc_manipulator_amd._build")
+def lib(dof=7):
+    """Load the engine library of a robot (dof 7: libmpcc_engine.so, 10: libmpcc_engine_mobile.so; build
+    them first with mpcc_manipulator_amd._build.build())."""
+    if dof in _libs:
+        return _libs[dof]
+    path = LIB_PATHS[dof]
+    if not os.path.exists(path):
+        raise MpccError(f"{os.path.basename(path)} not built ({path}); run python -m mpcc_manipulator_amd._build")
     # One HIP runtime per process.  torch ships its own libamdhip64 (SONAME libamdhip64.so.7, loaded by
     # the unversioned name libamdhip64.so).  Loaded first, it satisfies the engine's libamdhip64.so.7
     # dependency; loaded after the engine had pulled in /opt/rocm's copy, it would be a second runtime
@@ -97,10 +120,12 @@ def lib():
         import torch  # noqa: F401
     except ImportError:
         pass
-    L = C.CDLL(LIB_PATH)
+    L = C.CDLL(path)
     V = C.c_void_p
+    MpccParams = PARAMS_STRUCT[dof]
     sig = {
         "mpcc_abi_version": (C.c_int, []),
+        "mpcc_robot_dof": (C.c_int, []),
         "mpcc_last_error": (C.c_char_p, []),
         "mpcc_params_load_json": (C.c_int, [C.POINTER(MpccJsonPaths), C.POINTER(MpccOverride), C.c_int, C.c_int,
                                             C.c_int, C.POINTER(MpccParams)]),
@@ -152,13 +177,15 @@ def lib():
         f.argtypes = args
     if L.mpcc_abi_version() != 1:
         raise MpccError("libmpcc_engine ABI version mismatch")
-    _lib = L
+    if L.mpcc_robot_dof() != dof:
+        raise MpccError(f"{path} was built for {L.mpcc_robot_dof()} joints, expected {dof}")
+    _libs[dof] = L
     return L
 
 
-def _check(rc, what):
+def _check(rc, what, dof=7):
     if rc != 0:
-        msg = lib().mpcc_last_error().decode(errors="replace")
+        msg = lib(dof).mpcc_last_error().decode(errors="replace")
         raise MpccError(f"{what} failed ({rc}): {msg}")
 
 
@@ -194,11 +221,28 @@ SECTION_KEYS = {  # python/MPCC/MPCC.py:37-43 (valid ParamValue keys)
 }
 
 
-def load_params(N=20, paths=None, merged=DEFAULT_PARAMS, overrides=None, ctor_semantics=True, Ts=None):
-    """Params/*.json + ParamValue overrides -> MpccParams (C++ loader, host only).
+def section_keys(dof=7):
+    """Valid ParamValue keys per section for a robot (the mobile base adds xb, yb, thb and their rates)."""
+    if dof == 7:
+        return SECTION_KEYS
+    base = ["xb", "yb", "thb"]
+    k = {s: list(v) for s, v in SECTION_KEYS.items()}
+    k["bounds"] += [f"{n}{s}" for n in base for s in "lu"] + [f"d{n}{s}" for n in base for s in "lu"] + \
+        [f"dd{n}{s}" for n in base for s in "lu"]
+    k["normalization"] += base + [f"d{n}" for n in base]
+    return k
+
+
+def load_params(N=20, paths=None, merged=None, overrides=None, ctor_semantics=True, Ts=None, dof=7):
+    """Params/*.json + ParamValue overrides -> mpcc_params of the robot's library (C++ loader, host only).
 
     paths: dict with PathToJson keys (param_path, cost_path, bounds_path, normalization_path, sqp_path)
-    overrides: {"param": {...}, "cost": {...}, ...} as the reference's ParamValue (types.h:72-79)."""
+    overrides: {"param": {...}, "cost": {...}, ...} as the reference's ParamValue (types.h:72-79).
+    merged defaults to the robot's parameter file (default_params.json / mobile_params.json) when no
+    per-section paths are given."""
+    if merged is None and not paths:
+        merged = DEFAULT_PARAMS if dof == 7 else MOBILE_PARAMS
+    keys = section_keys(dof)
     p = MpccJsonPaths()
     keep = []
     for k in ["param_path", "cost_path", "bounds_path", "normalization_path", "sqp_path"]:
@@ -211,18 +255,18 @@ def load_params(N=20, paths=None, merged=DEFAULT_PARAMS, overrides=None, ctor_se
         p.merged_path = merged.encode()
     ov = []
     for sec, kv in (overrides or {}).items():
-        if sec not in SECTION_KEYS:
-            raise ValueError(f"unknown parameter section {sec!r}; valid: {list(SECTION_KEYS)}")
+        if sec not in keys:
+            raise ValueError(f"unknown parameter section {sec!r}; valid: {list(keys)}")
         for k, v in kv.items():
-            if k not in SECTION_KEYS[sec]:
-                raise ValueError(f"keys for {sec} must be a subset of {SECTION_KEYS[sec]}, got {k!r}")
+            if k not in keys[sec]:
+                raise ValueError(f"keys for {sec} must be a subset of {keys[sec]}, got {k!r}")
             ov.append((sec.encode(), k.encode(), float(v)))
     arr = (MpccOverride * max(1, len(ov)))()
     for i, (s, k, v) in enumerate(ov):
         arr[i].section, arr[i].key, arr[i].value = s, k, v
-    out = MpccParams()
-    _check(lib().mpcc_params_load_json(C.byref(p), arr, len(ov), int(bool(ctor_semantics)), int(N), C.byref(out)),
-           "mpcc_params_load_json")
+    out = PARAMS_STRUCT[dof]()
+    _check(lib(dof).mpcc_params_load_json(C.byref(p), arr, len(ov), int(bool(ctor_semantics)), int(N), C.byref(out)),
+           "mpcc_params_load_json", dof)
     if Ts is not None:
         out.Ts = float(Ts)
     return out
@@ -309,12 +353,14 @@ class Engine:
 
     def __init__(self, params: MpccParams, max_batch: int, device: int = 0, nn_dir: str = NN_DIR,
                  constraint_mask: int = -1, faithful_dead_trials: bool = False):
-        self.L = lib()
+        self.dof = getattr(type(params), "_dof", 7)  # the robot of the params struct picks the library
+        self.NX, self.NU, self.NXU, self.REC = dims(self.dof)
+        self.L = lib(self.dof)
         cfg = MpccConfig(int(params.N), float(params.Ts), int(max_batch), int(device), int(constraint_mask),
                          int(bool(faithful_dead_trials)))
         h = C.c_void_p()
         _check(self.L.mpcc_create(C.byref(cfg), C.byref(params), nn_dir.encode() if nn_dir else None, C.byref(h)),
-               "mpcc_create")
+               "mpcc_create", self.dof)
         self.h = h
         self.N = int(params.N)
         self.max_batch = int(max_batch)
@@ -331,32 +377,35 @@ class Engine:
         except Exception:
             pass
 
+    def _check(self, rc, what):
+        _check(rc, what, self.dof)
+
     @property
     def params(self):
-        p = MpccParams()
-        _check(self.L.mpcc_get_params(self.h, C.byref(p)), "mpcc_get_params")
+        p = PARAMS_STRUCT[self.dof]()
+        self._check(self.L.mpcc_get_params(self.h, C.byref(p)), "mpcc_get_params")
         return p
 
     def set_params(self, params: MpccParams):
-        _check(self.L.mpcc_set_params(self.h, C.byref(params)), "mpcc_set_params")
+        self._check(self.L.mpcc_set_params(self.h, C.byref(params)), "mpcc_set_params")
 
     def set_track(self, X, Y, Z, R):
         X, Y, Z = _f64(X), _f64(Y), _f64(Z)
         R = _f64(R).reshape(-1, 9)
-        _check(self.L.mpcc_set_track(self.h, len(X), _dp(X), _dp(Y), _dp(Z), _dp(R)), "mpcc_set_track")
+        self._check(self.L.mpcc_set_track(self.h, len(X), _dp(X), _dp(Y), _dp(Z), _dp(R)), "mpcc_set_track")
 
     def set_tracks(self, X, Y, Z, R):
         """One track per instance (mpcc_set_tracks): X, Y, Z [B, n], R [B, n, 3, 3]."""
         X, Y, Z = _f64(X), _f64(Y), _f64(Z)
         B, n = X.shape
         R = _f64(R).reshape(B, n, 9)
-        _check(self.L.mpcc_set_tracks(self.h, B, n, _dp(X), _dp(Y), _dp(Z), _dp(R)), "mpcc_set_tracks")
+        self._check(self.L.mpcc_set_tracks(self.h, B, n, _dp(X), _dp(Y), _dp(Z), _dp(R)), "mpcc_set_tracks")
 
     def set_track_path(self, s, X, Y, Z, R):
         """SolverInterface::setTrack(ArcLengthSpline): from getPathData() (100 regular points)."""
         s, X, Y, Z = _f64(s), _f64(X), _f64(Y), _f64(Z)
         R = _f64(R).reshape(-1, 9)
-        _check(self.L.mpcc_set_track_path(self.h, len(s), _dp(s), _dp(X), _dp(Y), _dp(Z), _dp(R)),
+        self._check(self.L.mpcc_set_track_path(self.h, len(s), _dp(s), _dp(X), _dp(Y), _dp(Z), _dp(R)),
                "mpcc_set_track_path")
 
     def track_length(self):
@@ -364,43 +413,43 @@ class Engine:
 
     def track_path(self):
         s, X, Y, Z, R = np.zeros(100), np.zeros(100), np.zeros(100), np.zeros(100), np.zeros(900)
-        _check(self.L.mpcc_get_track_path(self.h, _dp(s), _dp(X), _dp(Y), _dp(Z), _dp(R)), "mpcc_get_track_path")
+        self._check(self.L.mpcc_get_track_path(self.h, _dp(s), _dp(X), _dp(Y), _dp(Z), _dp(R)), "mpcc_get_track_path")
         return s, X, Y, Z, R.reshape(100, 3, 3)
 
     def set_warmstart(self, guess, valid, fails):
         B = guess.shape[0]
-        g = _f64(guess, (B, self.N + 1, 17))
+        g = _f64(guess, (B, self.N + 1, self.NXU))
         v = np.ascontiguousarray(valid, dtype=np.int32)
         f = np.ascontiguousarray(fails, dtype=np.int32)
-        _check(self.L.mpcc_set_warmstart(self.h, B, _dp(g), _ip(v), _ip(f)), "mpcc_set_warmstart")
+        self._check(self.L.mpcc_set_warmstart(self.h, B, _dp(g), _ip(v), _ip(f)), "mpcc_set_warmstart")
 
     def get_warmstart(self, B):
-        g = np.zeros((B, self.N + 1, 17))
+        g = np.zeros((B, self.N + 1, self.NXU))
         v = np.zeros(B, np.int32)
         f = np.zeros(B, np.int32)
-        _check(self.L.mpcc_get_warmstart(self.h, B, _dp(g), _ip(v), _ip(f)), "mpcc_get_warmstart")
+        self._check(self.L.mpcc_get_warmstart(self.h, B, _dp(g), _ip(v), _ip(f)), "mpcc_get_warmstart")
         return g, v, f
 
     def reset_warmstart(self, B, mask=None):
         m = None
         if mask is not None:
             m = np.ascontiguousarray(mask, dtype=np.uint8)
-        _check(self.L.mpcc_reset_warmstart(self.h, B, m.ctypes.data_as(C.POINTER(C.c_uint8)) if m is not None else None),
+        self._check(self.L.mpcc_reset_warmstart(self.h, B, m.ctypes.data_as(C.POINTER(C.c_uint8)) if m is not None else None),
                "mpcc_reset_warmstart")
 
     def solve(self, x0, u0, obs, timing=False):
-        """Batched runMPC_ on host arrays.  x0 [B,9] is updated in place (s, vs), as the reference
+        """Batched runMPC_ on host arrays.  x0 [B,NX] is updated in place (s, vs), as the reference
         mutates its State argument.  Returns dict(u0, horizon, status, ok[, timing])."""
         B = x0.shape[0]
-        assert x0.dtype == np.float64 and x0.flags.c_contiguous and x0.shape == (B, 9)
-        u0 = _f64(u0, (B, 8))
+        assert x0.dtype == np.float64 and x0.flags.c_contiguous and x0.shape == (B, self.NX)
+        u0 = _f64(u0, (B, self.NU))
         obs = _f64(obs, (B, 4))
-        u_out = np.zeros((B, 8))
-        hor = np.zeros((B, self.N + 1, 17))
+        u_out = np.zeros((B, self.NU))
+        hor = np.zeros((B, self.N + 1, self.NXU))
         st = np.zeros(B, np.int32)
         ok = np.zeros(B, np.int32)
         tm = MpccTiming()
-        _check(self.L.mpcc_solve(self.h, B, _dp(x0), _dp(u0), _dp(obs), _dp(u_out), _dp(hor), _ip(st), _ip(ok),
+        self._check(self.L.mpcc_solve(self.h, B, _dp(x0), _dp(u0), _dp(obs), _dp(u_out), _dp(hor), _ip(st), _ip(ok),
                                  C.byref(tm) if timing else None), "mpcc_solve")
         out = dict(u0=u_out, horizon=hor, status=st, ok=ok)
         if timing:
@@ -411,11 +460,11 @@ class Engine:
         """main.cpp:100-114 on the device for B instances (mpcc_closed_loop).  Returns dict(x [steps+1,B,9],
         u [steps,B,8], status [steps,B] (-1 after an instance stopped), x_final, u_final)."""
         B = x0.shape[0]
-        x = _f64(x0, (B, 9)).copy()
-        u = _f64(u0, (B, 8)).copy()
+        x = _f64(x0, (B, self.NX)).copy()
+        u = _f64(u0, (B, self.NU)).copy()
         obs = _f64(obs, (B, 4))
-        xt = np.zeros((steps + 1, B, 9)); ut = np.zeros((steps, B, 8)); stt = np.zeros((steps, B), np.int32)
-        _check(self.L.mpcc_closed_loop(self.h, B, int(steps), _dp(x), _dp(u), _dp(obs), _dp(xt), _dp(ut), _ip(stt),
+        xt = np.zeros((steps + 1, B, self.NX)); ut = np.zeros((steps, B, self.NU)); stt = np.zeros((steps, B), np.int32)
+        self._check(self.L.mpcc_closed_loop(self.h, B, int(steps), _dp(x), _dp(u), _dp(obs), _dp(xt), _dp(ut), _ip(stt),
                                        int(bool(graph))), "mpcc_closed_loop")
         return dict(x=xt, u=ut, status=stt, x_final=x, u_final=u)
 
@@ -423,13 +472,13 @@ class Engine:
         """SolverInterface::setInitialGuess/setCurrentInput/setEnvData/solveOCP for B instances
         (solver_interface.h:44-54).  Returns dict(opt_sol [B,N+1,17], status, solved)."""
         B = guess.shape[0]
-        guess = _f64(guess, (B, self.N + 1, 17))
-        u_cur = _f64(u_cur, (B, 8))
+        guess = _f64(guess, (B, self.N + 1, self.NXU))
+        u_cur = _f64(u_cur, (B, self.NU))
         obs = _f64(obs, (B, 4))
-        sol = np.zeros((B, self.N + 1, 17))
+        sol = np.zeros((B, self.N + 1, self.NXU))
         st = np.zeros(B, np.int32)
         ok = np.zeros(B, np.int32)
-        _check(self.L.mpcc_solve_ocp(self.h, B, _dp(guess), _dp(u_cur), _dp(obs), _dp(sol), _ip(st), _ip(ok), None),
+        self._check(self.L.mpcc_solve_ocp(self.h, B, _dp(guess), _dp(u_cur), _dp(obs), _dp(sol), _ip(st), _ip(ok), None),
                "mpcc_solve_ocp")
         return dict(opt_sol=sol, status=st, solved=ok)
 
@@ -472,85 +521,87 @@ class Engine:
         if not 1 <= B <= self.max_batch:
             raise MpccError(f"B = {B} outside [1, {self.max_batch}]")
         f64, i32 = torch.float64, torch.int32
-        a = [self._dev_ptr(x0, "x0", f64, (B, 9), True), self._dev_ptr(u0, "u0", f64, (B, 8), True),
-             self._dev_ptr(obs, "obs", f64, (B, 4), True), self._dev_ptr(u_out, "u_out", f64, (B, 8)),
-             self._dev_ptr(horizon, "horizon", f64, (B, self.N + 1, 17)), self._dev_ptr(status, "status", i32, (B,)),
+        a = [self._dev_ptr(x0, "x0", f64, (B, self.NX), True), self._dev_ptr(u0, "u0", f64, (B, self.NU), True),
+             self._dev_ptr(obs, "obs", f64, (B, 4), True), self._dev_ptr(u_out, "u_out", f64, (B, self.NU)),
+             self._dev_ptr(horizon, "horizon", f64, (B, self.N + 1, self.NXU)), self._dev_ptr(status, "status", i32, (B,)),
              self._dev_ptr(ok, "ok", i32, (B,))]
         s = self._stream_handle(stream)
-        _check(self.L.mpcc_solve_device(self.h, B, *a, s), "mpcc_solve_device")
+        self._check(self.L.mpcc_solve_device(self.h, B, *a, s), "mpcc_solve_device")
 
     def set_warmstart_device(self, B, guess, valid, fails, stream=None):
-        """Device-to-device warm start of instances [0, B) (float64 guess [B, N+1, 17], int32 valid/fails)."""
+        """Device-to-device warm start of instances [0, B) (float64 guess [B, N+1, NXU], int32 valid/fails)."""
         import torch
         B = int(B)
         if not 0 <= B <= self.max_batch:
             raise MpccError(f"B = {B} outside [0, {self.max_batch}]")
-        a = [self._dev_ptr(guess, "guess", torch.float64, (B, self.N + 1, 17)),
+        a = [self._dev_ptr(guess, "guess", torch.float64, (B, self.N + 1, self.NXU)),
              self._dev_ptr(valid, "valid", torch.int32, (B,)), self._dev_ptr(fails, "fails", torch.int32, (B,))]
         s = self._stream_handle(stream)
-        _check(self.L.mpcc_set_warmstart_device(self.h, B, *a, s), "mpcc_set_warmstart_device")
+        self._check(self.L.mpcc_set_warmstart_device(self.h, B, *a, s), "mpcc_set_warmstart_device")
 
     def timing_begin(self):
-        _check(self.L.mpcc_timing_begin(self.h), "mpcc_timing_begin")
+        self._check(self.L.mpcc_timing_begin(self.h), "mpcc_timing_begin")
 
     def timing_end(self):
         t = MpccTiming()
         nc = C.c_int32()
         ni = C.c_int32()
-        _check(self.L.mpcc_timing_end(self.h, C.byref(t), C.byref(nc), C.byref(ni)), "mpcc_timing_end")
+        self._check(self.L.mpcc_timing_end(self.h, C.byref(t), C.byref(nc), C.byref(ni)), "mpcc_timing_end")
         return t.as_dict(), nc.value, ni.value
 
     def solve_stats(self, B):
         a, b, c = np.zeros(B, np.int32), np.zeros(B, np.int32), np.zeros(B, np.int32)
-        _check(self.L.mpcc_get_solve_stats(self.h, int(B), _ip(a), _ip(b), _ip(c)), "mpcc_get_solve_stats")
+        self._check(self.L.mpcc_get_solve_stats(self.h, int(B), _ip(a), _ip(b), _ip(c)), "mpcc_get_solve_stats")
         return dict(sqp_iter=a, ipm_iters=b, qp_status=c)
 
     def sim_time_step(self, x, u, ts):
         B = x.shape[0]
-        x = _f64(x, (B, 9))
-        u = _f64(u, (B, 8))
-        out = np.zeros((B, 9))
-        _check(self.L.mpcc_sim_time_step(self.h, B, _dp(x), _dp(u), float(ts), _dp(out)), "mpcc_sim_time_step")
+        x = _f64(x, (B, self.NX))
+        u = _f64(u, (B, self.NU))
+        out = np.zeros((B, self.NX))
+        self._check(self.L.mpcc_sim_time_step(self.h, B, _dp(x), _dp(u), float(ts), _dp(out)), "mpcc_sim_time_step")
         return out
 
     # ---- stage-level entry points (parity tests)
     def robot_records(self, q, obs):
-        q = _f64(q).reshape(-1, 7)
+        q = _f64(q).reshape(-1, self.dof)
         M = q.shape[0]
         obs = _f64(obs, (M, 4))
-        rec = np.zeros((M, REC_SIZE))
-        _check(self.L.mpcc_debug_robot_records(self.h, M, _dp(q), _dp(obs), _dp(rec)), "mpcc_debug_robot_records")
+        rec = np.zeros((M, self.REC))
+        self._check(self.L.mpcc_debug_robot_records(self.h, M, _dp(q), _dp(obs), _dp(rec)), "mpcc_debug_robot_records")
         return rec
 
     def spline_eval(self, s):
         s = _f64(s).reshape(-1)
         M = s.shape[0]
         pos, d1, d2, R, dR = np.zeros((M, 3)), np.zeros((M, 3)), np.zeros((M, 3)), np.zeros((M, 9)), np.zeros((M, 3))
-        _check(self.L.mpcc_debug_spline(self.h, M, _dp(s), _dp(pos), _dp(d1), _dp(d2), _dp(R), _dp(dR)),
+        self._check(self.L.mpcc_debug_spline(self.h, M, _dp(s), _dp(pos), _dp(d1), _dp(d2), _dp(R), _dp(dR)),
                "mpcc_debug_spline")
         return pos, d1, d2, R.reshape(M, 3, 3), dR
 
     def stage_cost(self, x, u, rec, k):
-        x = _f64(x).reshape(-1, 9)
+        nx, nu = self.NX, self.NU
+        x = _f64(x).reshape(-1, nx)
         M = x.shape[0]
-        u = _f64(u, (M, 8))
-        rec = _f64(rec, (M, REC_SIZE))
+        u = _f64(u, (M, nu))
+        rec = _f64(rec, (M, self.REC))
         k = np.ascontiguousarray(k, dtype=np.int32).reshape(M)
-        obj, fx, fu, fxx, fuu = np.zeros(M), np.zeros((M, 9)), np.zeros((M, 8)), np.zeros((M, 81)), np.zeros((M, 64))
-        _check(self.L.mpcc_debug_stage_cost(self.h, M, _dp(x), _dp(u), _dp(rec), _ip(k), _dp(obj), _dp(fx), _dp(fu),
+        obj, fx, fu = np.zeros(M), np.zeros((M, nx)), np.zeros((M, nu))
+        fxx, fuu = np.zeros((M, nx * nx)), np.zeros((M, nu * nu))
+        self._check(self.L.mpcc_debug_stage_cost(self.h, M, _dp(x), _dp(u), _dp(rec), _ip(k), _dp(obj), _dp(fx), _dp(fu),
                                             _dp(fxx), _dp(fuu)), "mpcc_debug_stage_cost")
-        return obj, fx, fu, fxx.reshape(M, 9, 9), fuu.reshape(M, 8, 8)
+        return obj, fx, fu, fxx.reshape(M, nx, nx), fuu.reshape(M, nu, nu)
 
     def solve_qp(self, guess, rec, u_cur):
         B = guess.shape[0]
-        g = _f64(guess, (B, self.N + 1, 17))
-        r = _f64(rec, (B, self.N + 1, REC_SIZE))
-        u = _f64(u_cur, (B, 8))
-        nv = 17 * self.N + 9
+        g = _f64(guess, (B, self.N + 1, self.NXU))
+        r = _f64(rec, (B, self.N + 1, self.REC))
+        u = _f64(u_cur, (B, self.NU))
+        nv = self.NXU * self.N + self.NX
         step = np.zeros((B, nv))
         st = np.zeros(B, np.int32)
         it = np.zeros(B, np.int32)
-        _check(self.L.mpcc_debug_solve_qp(self.h, B, _dp(g), _dp(r), _dp(u), _dp(step), _ip(st), _ip(it)),
+        self._check(self.L.mpcc_debug_solve_qp(self.h, B, _dp(g), _dp(r), _dp(u), _dp(step), _ip(st), _ip(it)),
                "mpcc_debug_solve_qp")
         return step, st, it
 
@@ -560,21 +611,21 @@ class Engine:
         M = sg.shape[0]
         e = _f64(ee, (M, 3))
         out = np.zeros(M)
-        _check(self.L.mpcc_debug_project(self.h, M, _dp(sg), _dp(e), _dp(out)), "mpcc_debug_project")
+        self._check(self.L.mpcc_debug_project(self.h, M, _dp(sg), _dp(e), _dp(out)), "mpcc_debug_project")
         return out
 
     def workspace(self, B):
-        """Interior-point workspace of the last solve, [B, N+1, 816] (test instrumentation)."""
-        out = np.zeros((B, self.N + 1, 816))
-        _check(self.L.mpcc_debug_workspace(self.h, B, _dp(out)), "mpcc_debug_workspace")
+        """Interior-point workspace of the last solve, [B, N+1, 816] (Panda; 1280 for the mobile build)."""
+        out = np.zeros((B, self.N + 1, 816 if self.dof == 7 else 1280))
+        self._check(self.L.mpcc_debug_workspace(self.h, B, _dp(out)), "mpcc_debug_workspace")
         return out
 
     def trace_enable(self, on=True):
         """Record per-SQP-iteration decisions of the next solves (test instrumentation)."""
-        _check(self.L.mpcc_debug_trace_enable(self.h, 1 if on else 0), "mpcc_debug_trace_enable")
+        self._check(self.L.mpcc_debug_trace_enable(self.h, 1 if on else 0), "mpcc_debug_trace_enable")
 
     def trace_get(self, B):
         """[B, 4, 8]: qp status, ipm iters, trial obj, trial vio, accepted, |step|_inf, alpha, alpha*|step|_inf."""
         out = np.zeros((B, 4, 8))
-        _check(self.L.mpcc_debug_trace_get(self.h, B, _dp(out)), "mpcc_debug_trace_get")
+        self._check(self.L.mpcc_debug_trace_get(self.h, B, _dp(out)), "mpcc_debug_trace_get")
         return out
