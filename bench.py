@@ -1,4 +1,5 @@
 """Benchmark: MPCC solves/sec (7-DOF Panda, N=20, 2 SQP iterations) — BASELINE.json configs[1].
+Other BASELINE configs as presets (--config 2, 3; parity cases, not the headline line).
 
 One step = one batched MPC::runMPC_ (cpp/src/MPC/mpc.cpp:104-190) over B independent controllers per
 GPU (default B = 4096, bounds + singularity rows: constraint_mask = 2), inputs resident in HBM; for
@@ -26,11 +27,18 @@ METRIC = "MPCC solves/sec (whole node), 7-DOF Panda N=20, 2 SQP iters; 1/2/4/8 G
 Q0 = np.array([0, 0, 0, -np.pi / 2, 0, np.pi / 2, np.pi / 4])
 
 
-def algorithmic_qp_flops(N):
+def q_start(dof):
+    """Start joints of the reference's main.cpp:60-61 (the mobile base at the origin for dof 10)."""
+    return Q0 if dof == 7 else np.concatenate([np.zeros(dof - 7), Q0])
+
+
+def algorithmic_qp_flops(N, dof=7):
     """SURVEY.md §8(d) F_qp per SQP iteration (condensing + Cholesky + solves; inequality handling is
-    solver overhead and not credited): 2(96N^3 + 324N^2) + 616N^2 + n^3/3 + 4n^2, n = 8N."""
-    n = 8 * N
-    return 2 * (96 * N ** 3 + 324 * N ** 2) + 616 * N ** 2 + n ** 3 / 3 + 4 * n ** 2
+    solver overhead and not credited): 2(96N^3 + 324N^2) + 616N^2 + n^3/3 + 4n^2, n = 8N for the Panda,
+    i.e. 2(NU^2 NX N^3 / 6 + NX^2 NU N^2 / 2) + NPC NU DOF N^2 + n^3/3 + 4n^2 with n = NU N for any robot."""
+    nx, nu = dof + 2, dof + 1
+    n = nu * N
+    return 2 * (nu * nu * nx / 6 * N ** 3 + nx * nx * nu / 2 * N ** 2) + 11 * nu * dof * N ** 2 + n ** 3 / 3 + 4 * n ** 2
 
 
 def make_pool(m, params, mask, steps, device, pool_obs=(3.0, 3.0, 3.0, 0.0)):
@@ -38,19 +46,20 @@ def make_pool(m, params, mask, steps, device, pool_obs=(3.0, 3.0, 3.0, 0.0)):
     (tools/make_bench_pool.py), else a B = 1 closed loop on the GPU.  Returns (pool, track)."""
     N = params.N
     eng = m.Engine(params, max_batch=1, device=device, constraint_mask=mask)
-    ee = eng.robot_records(Q0, np.array([[3.0, 3.0, 3.0, 0.0]]))[0, :3]
+    dof, nx, nu = eng.dof, eng.NX, eng.NU
+    ee = eng.robot_records(q_start(dof), np.array([[3.0, 3.0, 3.0, 0.0]]))[0, :3]
     X, Y, Z, q = m.load_default_track()
     track = m.track_from_points(X, Y, Z, q, ee)
     path = os.path.join(ROOT, "mpcc_manipulator_amd", "data", f"bench_pool_n{N}_mask{mask}.npz")
-    if os.path.exists(path):
+    if dof == 7 and os.path.exists(path):
         f = np.load(path, allow_pickle=False)
         if f["x0"].shape[0] >= steps:
             eng.close()
             return {k: f[k][:steps] for k in f.files}, track
     eng.set_track(*track)
     from mpcc_manipulator_amd.integrator import sim_time_step
-    x = np.zeros((1, 9)); x[0, :7] = Q0
-    u = np.zeros((1, 8))
+    x = np.zeros((1, nx)); x[0, :dof] = q_start(dof)
+    u = np.zeros((1, nu))
     obs = np.array([pool_obs])
     pool = {k: [] for k in ["x0", "u0", "guess", "valid", "fails", "status"]}
     for _ in range(steps):
@@ -61,7 +70,7 @@ def make_pool(m, params, mask, steps, device, pool_obs=(3.0, 3.0, 3.0, 0.0)):
         out = eng.solve(xin, u, obs)
         pool["status"].append(out["status"][0])
         u = out["u0"].copy()
-        x = sim_time_step(xin, u, params.Ts)  # the state runMPC mutated (main.cpp:103-105)
+        x = eng.sim_time_step(xin, u, params.Ts) if dof != 7 else sim_time_step(xin, u, params.Ts)  # main.cpp:103-105
     eng.close()
     return {k: np.array(v) for k, v in pool.items()}, track
 
@@ -84,7 +93,8 @@ def cpu_info():
             "model": model}
 
 
-def cpu_baseline(params_dict, track, x0, u0, obs, guess, valid, fails, threads, sample, budget_s, latency_n=200):
+def cpu_baseline(params_dict, track, x0, u0, obs, guess, valid, fails, threads, sample, budget_s, latency_n=200,
+                 dof=7, latency_budget_s=10.0):
     """The oracle (CPU restatement of the reference algorithm, oracle/) on a bounded sample of the same
     workload: repeated passes over the first `sample` instances (each pass from the same inputs, so
     every pass is one full runMPC_ per instance), OpenMP over instances, until `budget_s` seconds of
@@ -92,7 +102,7 @@ def cpu_baseline(params_dict, track, x0, u0, obs, guess, valid, fails, threads, 
     time on one thread (ms per runMPC_, against the Ts = 10 ms real-time budget of config.json:4).
     Test infrastructure used only as the reported baseline."""
     from oracle.pyoracle import Oracle
-    o = Oracle(params_dict, os.path.join(ROOT, "mpcc_manipulator_amd", "data", "nn"), qp_mode=0, nthreads=threads)
+    o = Oracle(params_dict, os.path.join(ROOT, "mpcc_manipulator_amd", "data", "nn"), qp_mode=0, nthreads=threads, dof=dof)
     o.set_track(*track)
     n = min(sample, x0.shape[0])
     o.run_mpc(x0[:2].copy(), u0[:2], obs[:2], guess[:2].copy(), valid[:2].copy(), fails[:2].copy())  # warm caches
@@ -105,10 +115,12 @@ def cpu_baseline(params_dict, track, x0, u0, obs, guess, valid, fails, threads, 
         done += n
         passes += 1
     o.close()
-    o1 = Oracle(params_dict, os.path.join(ROOT, "mpcc_manipulator_amd", "data", "nn"), qp_mode=0, nthreads=1)
+    o1 = Oracle(params_dict, os.path.join(ROOT, "mpcc_manipulator_amd", "data", "nn"), qp_mode=0, nthreads=1, dof=dof)
     o1.set_track(*track)
     lat = []
     for i in range(min(latency_n, x0.shape[0])):
+        if sum(lat) > latency_budget_s:
+            break
         xs, gs, vs, fs = x0[i:i + 1].copy(), guess[i:i + 1].copy(), valid[i:i + 1].copy(), fails[i:i + 1].copy()
         t0 = time.perf_counter()
         o1.run_mpc(xs, u0[i:i + 1], obs[i:i + 1], gs, vs, fs)
@@ -165,9 +177,11 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--config", default="1", choices=["1", "2", "1-all-rows"],
+    ap.add_argument("--config", default="1", choices=["1", "2", "3", "1-all-rows"],
                     help="BASELINE configs[i] preset: 1 = B 4096, N 20, mask 2 (the metric); "
                          "2 = B 65536, N 40, mask 7, per-instance obstacles (parity case, timing only); "
+                         "3 = Husky+Panda 10-DOF mobile manipulator, B 32768, N 30, mask 7 (full cost and constraint "
+                         "set), per-instance obstacles (parity case, timing only); "
                          "1-all-rows = configs[1]'s B 4096, N 20 with the reference's default rows (all 11: self + "
                          "singularity + 9 env collision, config.h:34) and the main_w_sim.py:42-45 obstacles")
     ap.add_argument("--batch", type=int, default=None, help="instances per GPU")
@@ -188,8 +202,13 @@ def main():
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
         launch_ranks(args.gpus)
     preset = {"1": dict(batch=4096, N=20, mask=2), "2": dict(batch=65536, N=40, mask=7),
+              "3": dict(batch=32768, N=30, mask=7, pool_steps=300),
               "1-all-rows": dict(batch=4096, N=20, mask=7)}[args.config]
-    obstacles = args.config in ("2", "1-all-rows")
+    dof = 10 if args.config == "3" else 7
+    obstacles = args.config in ("2", "3", "1-all-rows")
+    if args.config == "3" and args.pool_steps == 1000:
+        args.pool_steps = preset.pop("pool_steps")
+    preset.pop("pool_steps", None)
     for k, v in preset.items():
         if getattr(args, k) is None:
             setattr(args, k, v)
@@ -223,9 +242,13 @@ def main():
     from mpcc_manipulator_amd.distributed import check_equal_shards, gather_u0, max_over_ranks, shard_bounds
 
     N, B = args.N, args.batch
-    params = m.load_params(N, overrides={"sqp": {"max_iter": args.max_iter}})
+    params = m.load_params(N, overrides={"sqp": {"max_iter": args.max_iter}}, dof=dof)
     params.constraint_mask = args.mask
-    pool_obs = (0.48, 0.218, 0.521, 5.0) if obstacles else (3.0, 3.0, 3.0, 0.0)
+    nx, nu, nxu, _ = m.dims(dof)
+    # obstacle scenario: main_w_sim.py:42-45 for the Panda; for the mobile manipulator the same kind of
+    # obstacle near the arm's reach from its start pose (its EE starts 0.35 m higher, on the base)
+    obs_xyz = (0.48, 0.218, 0.521) if dof == 7 else (0.62, 0.28, 0.75)
+    pool_obs = (*obs_xyz, 5.0) if obstacles else (3.0, 3.0, 3.0, 0.0)
     pool, track = make_pool(m, params, args.mask, args.pool_steps, local, pool_obs)
     eng = m.Engine(params, max_batch=B, device=local, constraint_mask=args.mask)
     eng.set_track(*track)
@@ -237,14 +260,14 @@ def main():
     start, _ = shard_bounds(B * world, rank, world)  # contiguous instance block of this rank
     idx = (np.arange(B) + start) % T
     x0 = pool["x0"][idx].copy()
-    x0[:, :7] += rng.normal(0.0, 0.005, size=(B * world, 7))[start:start + B]
+    x0[:, :dof] += rng.normal(0.0, 0.005, size=(B * world, dof))[start:start + B]
     u0 = pool["u0"][idx].copy()
     guess = pool["guess"][idx].copy()
     valid = pool["valid"][idx].astype(np.int32)
     fails = pool["fails"][idx].astype(np.int32)
     if obstacles:  # main_w_sim.py:42-45 scenario: xyz = (0.48, 0.218, z), z ~ U[0.421, 0.621], r = 5 cm
-        z = rng.uniform(0.421, 0.621, B * world)[start:start + B]
-        obs = np.column_stack([np.full(B, 0.48), np.full(B, 0.218), z, np.full(B, 5.0)])
+        z = rng.uniform(obs_xyz[2] - 0.1, obs_xyz[2] + 0.1, B * world)[start:start + B]
+        obs = np.column_stack([np.full(B, obs_xyz[0]), np.full(B, obs_xyz[1]), z, np.full(B, 5.0)])
     else:  # dummy obstacle of MPC::runMPC (mpc.cpp:97-100)
         obs = np.tile(np.array([3.0, 3.0, 3.0, 0.0]), (B, 1))
 
@@ -253,11 +276,11 @@ def main():
     x0_p, u0_d, obs_d = t(x0), t(u0), t(obs)
     g_p, v_p, f_p = t(guess), t(valid, torch.int32), t(fails, torch.int32)
     x0_d = x0_p.clone()
-    u_out = torch.empty((B, 8), dtype=torch.float64, device=dev)
-    hor = torch.empty((B, N + 1, 17), dtype=torch.float64, device=dev)
+    u_out = torch.empty((B, nu), dtype=torch.float64, device=dev)
+    hor = torch.empty((B, N + 1, nxu), dtype=torch.float64, device=dev)
     status = torch.empty(B, dtype=torch.int32, device=dev)
     ok = torch.empty(B, dtype=torch.int32, device=dev)
-    u_all = torch.empty((world * B, 8), dtype=torch.float64, device=dev) if world > 1 else None
+    u_all = torch.empty((world * B, nu), dtype=torch.float64, device=dev) if world > 1 else None
     # One dedicated stream carries the whole step: the x0 restore, the engine's kernels and the u0
     # gather (RCCL waits on the current stream), so every step reads the inputs it restored.
     stream = torch.cuda.Stream(dev)
@@ -305,7 +328,7 @@ def main():
     # iteration i has solved i + 1); a launch is credited with the QPs it actually solved, on average
     qps = int(np.minimum(stats["sqp_iter"] + 1, args.max_iter).sum())
     launches_per_step = max(1, nipm) / max(1, ncalls)
-    flops = qps * algorithmic_qp_flops(N) / launches_per_step
+    flops = qps * algorithmic_qp_flops(N, dof) / launches_per_step
     achieved = flops / t_ipm / 1e12
     traffic = None
     tpath = args.traffic or os.path.join(ROOT, "profiles", f"pmc_traffic_{kname}.json")
@@ -343,7 +366,7 @@ def main():
             threads = args.cpu_threads or min(ci["usable"], ci["omp_num_threads"] or ci["usable"])
             args.cpu_threads = threads
             v, n, passes, dt, lat = cpu_baseline(pd, track, x0, u0, obs, guess, valid, fails, threads,
-                                                 args.cpu_sample, args.cpu_seconds)
+                                                 args.cpu_sample, args.cpu_seconds, dof=dof)
             cpu = {"value": v, "unit": "solves/s", "cores": threads, "kind": "port", "host": ci,
                    "latency_1thread": lat,
                    "sample": f"{passes} passes over the first {n} instances of the same workload "
@@ -368,6 +391,9 @@ def main():
                      f"(mask={args.mask}), {args.max_iter} SQP iters",
                 "2": f"configs[2]: batch={B}/GPU Panda MPCC instances, N={N}, self+env collision NN constraints "
                      f"(mask={args.mask}), per-instance obstacles, {args.max_iter} SQP iters",
+                "3": f"configs[3]: batch={B}/GPU Husky+Panda 10-DOF mobile manipulator MPCC instances, N={N}, full cost "
+                     f"and constraint set (mask={args.mask}: self + singularity + env collision NN rows), per-instance "
+                     f"obstacles, {args.max_iter} SQP iters",
                 "1-all-rows": f"configs[1] shape with the reference's default rows: batch={B}/GPU Panda MPCC instances, "
                               f"N={N}, all 11 polytopic rows incl. both collision NNs (mask={args.mask}), per-instance "
                               f"obstacles, {args.max_iter} SQP iters"}[args.config],
