@@ -36,17 +36,21 @@ def main():
     ap.add_argument("--batch", type=int, default=4096)
     ap.add_argument("--N", type=int, default=20)
     ap.add_argument("--kernel", default="k_sqp")
+    ap.add_argument("--ipw", type=int, default=4, help="instances per wavefront (4 Panda, 2 mobile build)")
+    ap.add_argument("--ns", default="mpcc", help="kernel namespace (mpcc_m10 for the mobile build)")
+    ap.add_argument("--traffic-name", default=None,
+                    help="traffic file name under profiles/ (default pmc_traffic_<kernel>.json, read by bench.py)")
     args = ap.parse_args()
     prof = os.path.join(ROOT, "profiles")
     os.makedirs(prof, exist_ok=True)
     stats = glob.glob(os.path.join(args.dir, "trace", "*kernel_stats.csv"))
     if stats:
         shutil.copy(stats[0], os.path.join(prof, f"{args.round}_kernel_stats.csv"))
-    grid = (args.batch + 3) // 4 * 64
+    grid = (args.batch + args.ipw - 1) // args.ipw * 64
     merged = collections.defaultdict(dict)
     for p in ("p1", "p2", "p3", "p4"):
         for k, v in load_pmc(args.dir, p).items():
-            if v["grid"] == grid and v["kernel"].startswith(f"void mpcc::{args.kernel}<"):
+            if v["grid"] == grid and v["kernel"].startswith(f"void {args.ns}::{args.kernel}<"):
                 merged[p + ":" + str(k)] = v
     per = collections.defaultdict(list)
     for key, v in merged.items():
@@ -62,7 +66,7 @@ def main():
         out["hbm_read_bytes_per_launch"] = rd
         out["hbm_write_bytes_per_launch"] = wr
         out["hbm_bytes_per_launch"] = rd + wr
-        with open(os.path.join(prof, f"pmc_traffic_{args.kernel}.json"), "w") as f:
+        with open(os.path.join(prof, args.traffic_name or f"pmc_traffic_{args.kernel}.json"), "w") as f:
             json.dump({"kernel": args.kernel, "batch": args.batch, "N": args.N, "hbm_bytes_per_launch": rd + wr,
                        "hbm_read_bytes_per_launch": rd, "hbm_write_bytes_per_launch": wr,
                        "source": f"profiles/{args.round}_{args.kernel}_pmc.json"}, f, indent=1)

@@ -1,16 +1,19 @@
 #!/bin/bash
 # Round profile of the benchmark command (GPU box): rocprofv3 kernel trace + stats of bench.py, then
-# separate PMC passes for the dominant kernel k_sqp (never combined with trace domains).  Usage: bash tools/profile_round.sh OUT
+# separate PMC passes for the dominant kernel k_sqp (never combined with trace domains).
+# Usage: bash tools/profile_round.sh OUT [bench.py args, e.g. --config 2]
 set -e
 OUT=${1:-gpurun_out/prof}
+shift || true
+EXTRA="$*"
 ROOT=$(pwd)
 mkdir -p "$ROOT/$OUT"
 cd /tmp && export TMPDIR=/tmp
-BENCH="$ROOT/bench.py --steps 20 --warmup 3 --no-cpu-baseline"
+BENCH="$ROOT/bench.py --steps 20 --warmup 3 --no-cpu-baseline $EXTRA"
 timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d "$ROOT/$OUT/trace" -o trace -- \
     python3 $BENCH > "$ROOT/$OUT/bench_trace.json" 2> "$ROOT/$OUT/bench_trace.err"
 echo "trace done"
-PMCB="$ROOT/bench.py --steps 2 --warmup 1 --no-cpu-baseline"
+PMCB="$ROOT/bench.py --steps 2 --warmup 1 --no-cpu-baseline $EXTRA"
 pmc() {
   local name=$1; shift
   timeout -k 10 300 rocprofv3 --kernel-include-regex 'k_sqp' --pmc "$@" --output-format csv \
