@@ -278,6 +278,12 @@ int mpcc_debug_project(mpcc_engine* e, int M, const double* s_guess, const doubl
 int mpcc_debug_solve_qp(mpcc_engine* e, int B, const double* guess, const double* rec, const double* u_cur,
                         double* step, int32_t* qp_status, int32_t* ipm_iters);
 
+/* the same QP with low-rank Hessian terms sum_j lrc_j u_j u_j^T (the damped-BFGS QP form): lr [nlr*(N+1)*NXU]
+ * (per stage [x | u], u_N = 0), lrc [nlr], nlr <= 4, solved by the 32-lane interior point with the Woodbury
+ * correction */
+int mpcc_debug_solve_qp_lr(mpcc_engine* e, int B, const double* guess, const double* rec, const double* u_cur, int nlr,
+                           const double* lr, const double* lrc, double* step, int32_t* qp_status, int32_t* ipm_iters);
+
 /* SQP trace of the next solves (test instrumentation, off by default): per instance and SQP iteration
  * (at most 4) 8 doubles: qp status, ipm iterations, trial objective and violation at alpha = 1,
  * accepted, |step|_inf, alpha, alpha*|step|_inf (osqp_interface.cpp:540-574, 759-808). */
@@ -287,7 +293,7 @@ int mpcc_debug_trace_enable(mpcc_engine* e, int enable);
 #if MPCC_DOF == 7
 #define MPCC_IPM_WS 816
 #else
-#define MPCC_IPM_WS 1280
+#define MPCC_IPM_WS 2048
 #endif
 int mpcc_debug_workspace(mpcc_engine* e, int B, double* out);
 int mpcc_debug_trace_get(mpcc_engine* e, int B, double* out /* [B*4*8] */);

@@ -12,7 +12,8 @@ CSRC = os.path.join(PKG, "csrc")
 PROF = os.environ.get("MPCC_PROF_BUILD", "0") == "1"  # cycle-accounting variant (tools/ipm_prof.py)
 BUILD = os.path.join(PKG, "_build_prof" if PROF else "_build")
 LIB = os.path.join(BUILD, "libmpcc_engine.so")
-SOURCES = ["kernels.hip", "ipm.hip", "mlp.hip", "nn_generic.hip", "engine.cpp", "host_params.cpp", "host_spline.cpp", "mpc.cpp"]
+SOURCES = ["kernels.hip", "ipm.hip", "ipm_wide.hip", "mlp.hip", "nn_generic.hip", "engine.cpp", "host_params.cpp",
+           "host_spline.cpp", "mpc.cpp"]
 # The Husky+Panda mobile manipulator (BASELINE configs[3]): the same sources built with the
 # robot's compile-time dimensions (as the reference's config.h NX/NU), its own 32-lane interior point and
 # namespace, into a second library with the same C ABI.

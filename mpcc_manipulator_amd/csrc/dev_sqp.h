@@ -16,8 +16,11 @@ namespace mpcc {
 // k_setqp: stage QP record (setCost + setDynamics + setBounds + setPolytopicConstraints,
 // osqp_interface.cpp:129-344) in the stage-structured normalized form.
 // ------------------------------------------------------------------------------------------------
+// keep_hess (damped BFGS, SQP iteration >= 1): the state Hessian block and its NaN / PD flags stay those of
+// SQP iteration 0 (setQP is called without the Hessian, osqp_interface.cpp:441-442); the input diagonal is
+// constant and is rewritten unchanged.
 __device__ inline void setqp_stage(const DevConst& c, const SplineView& sp, const double* __restrict__ gb, const RecView& rv, int k,
-                                   const double* __restrict__ ucur, double* __restrict__ q) {
+                                   const double* __restrict__ ucur, double* __restrict__ q, bool keep_hess = false) {
     const mpcc_params& p = c.p;
     const int N = c.N;
     const double* Tx = p.Tx;
@@ -26,9 +29,10 @@ __device__ inline void setqp_stage(const DevConst& c, const SplineView& sp, cons
     const double* uk = gb + NXU * k + NX;
     double fx[NX], fu[NU], fxx[NX * NX], fuu[NU];
     double obj = stage_cost(c, sp, xk, uk, rv, k, true, fx, fu, fxx, fuu);
-    int flag = 0;
+    int flag = keep_hess ? ((int)q[QS_FLAG] & 3) : 0;
     for (int a = 0; a < NX; a++) {
         q[QS_q + a] = Tx[a] * fx[a];
+        if (keep_hess) continue;
         for (int bb = 0; bb < NX; bb++) {
             double v = Tx[a] * fxx[a * NX + bb] * Tx[bb];
             q[QS_Q + a * NX + bb] = v;
@@ -36,7 +40,7 @@ __device__ inline void setqp_stage(const DevConst& c, const SplineView& sp, cons
         }
     }
     // PD check of the state block (LLT pivots; NaN pivots pass as in Eigen)
-    {
+    if (!keep_hess) {
         double L[NX * (NX + 1) / 2];
         int idx = 0;
         for (int i = 0; i < NX; i++)

@@ -93,6 +93,8 @@ struct mpcc_engine {
         auto f = [](void* p) { if (p) (void)hipFree(p); };
         f(d_spl);
         f(d.guess); f(d.valid); f(d.fails); f(d.rec); f(d.qs); f(d.is); f(d.step); f(d.trial); f(d.sqi); f(d.sqd);
+        if (d.isw != d.is) f(d.isw);
+        f(d.lr); f(d.lrc); f(d.glam); f(d.gprev); f(d.aty); f(d.sp);
         f(d.dbg_trace);
         f(s_x0); f(s_u0); f(s_obs); f(s_u0out); f(s_hor); f(s_status); f(s_ok);
         f(nn_self.d); f(nn_env.d);
@@ -124,6 +126,21 @@ struct mpcc_engine {
             for (int b = 0; b < NU; b++)
                 if (G[a * NU + b] != 0.0 && a != b && !(a == XVS && b == UVS))
                     throw std::logic_error("discrete model outside the structure k_ipm assumes (G)");
+        }
+    }
+
+    // Buffers of the damped-BFGS option (use_BFGS): the 32-lane interior point's workspace (the mobile build's
+    // regular one) and the per-instance BFGS state, allocated when the option is first enabled.
+    void ensure_bfgs_buffers() {
+        const size_t B = (size_t)maxB, NE = ((size_t)N + 1) * NXU;
+        if (!d.isw) d.isw = dmalloc<double>(B * (N + 1) * ISW);
+        if (!d.lr) {
+            d.lr = dmalloc<double>(B * LRM * NE);
+            d.lrc = dmalloc<double>(B * LRM);
+            d.glam = dmalloc<double>(B * NE);
+            d.gprev = dmalloc<double>(B * NE);
+            d.aty = dmalloc<double>(B * NE);
+            d.sp = dmalloc<double>(B * NE);
         }
     }
 
@@ -243,11 +260,12 @@ void validate_params(const mpcc_params& p) {
     for (int i = 0; i < NX; i++) if (!(p.Tx[i] > 0)) throw std::invalid_argument("T_x must be > 0");
     for (int i = 0; i < NU; i++) if (!(p.Tu[i] > 0)) throw std::invalid_argument("T_u must be > 0");
     if (p.max_iter < 0 || p.line_search_max_iter < 0) throw std::invalid_argument("negative iteration limit");
-    // Damped BFGS (osqp_interface.cpp:683-715) replaces the Hessian by rank-2 updates that couple every
-    // stage with every other: the dense N_var x N_var matrix has no stage structure for the Riccati
-    // interior point to exploit.  Off in the reference's sqp.json and off the benchmark path.
-    if (p.use_BFGS)
-        throw std::invalid_argument("use_BFGS (osqp_interface.cpp:683-715) is not supported by this engine");
+    // Damped BFGS (osqp_interface.cpp:683-715): the QP Hessian is the structured Hessian of SQP iteration 0 plus
+    // 2 low-rank terms per update, solved with the Woodbury identity around the Riccati recursion (DESIGN.md
+    // §4.2); at most LRM terms are held, i.e. max_iter <= 1 + LRM / 2.
+    if (p.use_BFGS && p.max_iter > 1 + LRM / 2)
+        throw std::invalid_argument("use_BFGS supports max_iter <= " + std::to_string(1 + LRM / 2) +
+                                    " (low-rank terms of the damped BFGS Hessian)");
 }
 
 // one track's tables in the device layout (dev_common.h SplineDev): SPL_STRIDE doubles
@@ -337,13 +355,15 @@ void run_batch(mpcc_engine* e, int B, hipStream_t st, mpcc_timing* timing, bool 
         launch_nn(c, d, e->nn_env.desc, e->nn_env.d, 1, c.S, nullptr, nullptr, d.rec, c.S, st);
     if (tm) t_env1 = mark();
     const double* ucur = d.u0;
-    if (!e->staged_sqp) {
-        // first QP assembly lane-per-stage, then the whole SQP loop per instance in one kernel
+    if (!e->staged_sqp || c.p.use_BFGS) {
+        // first QP assembly lane-per-stage, then the whole SQP loop per instance in one kernel (the damped-BFGS
+        // option always on the fused 32-lane kernel)
         int a0 = -1, a1 = -1, b1 = -1;
         if (tm) a0 = mark();
         launch_setqp(c, d, ucur, st);
         if (tm) a1 = mark();
-        launch_sqp(c, d, ucur, poly_rows_max(c.p.constraint_mask), st);
+        if (c.p.use_BFGS) launch_sqp_wide(c, d, ucur, poly_rows_max(c.p.constraint_mask), 1, st);
+        else launch_sqp(c, d, ucur, poly_rows_max(c.p.constraint_mask), st);
         if (tm) {
             b1 = mark();
             set_qp.push_back({a0, a1});
@@ -476,6 +496,8 @@ int mpcc_create(const mpcc_config* cfg, const mpcc_params* params, const char* n
         HIPCHK(hipMemset(d.valid, 0, B * sizeof(int32_t)));
         HIPCHK(hipMemset(d.fails, 0, B * sizeof(int32_t)));
         HIPCHK(hipMemset(d.sqi, 0, B * SQI * sizeof(int32_t)));
+        if (DOF != 7) d.isw = d.is;  // the mobile build's interior point is the 32-lane one
+        if (e->params.use_BFGS) e->ensure_bfgs_buffers();
         e->s_x0 = dmalloc<double>(B * NX);
         e->s_u0 = dmalloc<double>(B * NU);
         e->s_obs = dmalloc<double>(B * 4);
@@ -525,6 +547,7 @@ int mpcc_set_params(mpcc_engine* e, const mpcc_params* p) {
         validate_params(np);
         e->params = np;
         e->set_model();
+        if (np.use_BFGS) e->ensure_bfgs_buffers();
     } catch (const std::exception& x) {
         e->params = old;
         e->set_model();
@@ -1090,8 +1113,27 @@ int mpcc_debug_stage_cost(mpcc_engine* e, int M, const double* x, const double* 
     return MPCC_OK;
 }
 
+}  // extern "C"
+static int debug_solve_qp(mpcc_engine* e, int B, const double* guess, const double* rec, const double* u_cur, int nlr,
+                          const double* lr, const double* lrc, double* step, int32_t* qp_status, int32_t* ipm_iters);
+extern "C" {
+
 int mpcc_debug_solve_qp(mpcc_engine* e, int B, const double* guess, const double* rec, const double* u_cur, double* step,
                         int32_t* qp_status, int32_t* ipm_iters) {
+    return debug_solve_qp(e, B, guess, rec, u_cur, -1, nullptr, nullptr, step, qp_status, ipm_iters);
+}
+
+int mpcc_debug_solve_qp_lr(mpcc_engine* e, int B, const double* guess, const double* rec, const double* u_cur, int nlr,
+                           const double* lr, const double* lrc, double* step, int32_t* qp_status, int32_t* ipm_iters) {
+    if (nlr < 0 || nlr > LRM || (nlr && (!lr || !lrc))) return fail(MPCC_E_INVALID, "mpcc_debug_solve_qp_lr: invalid argument");
+    return debug_solve_qp(e, B, guess, rec, u_cur, nlr, lr, lrc, step, qp_status, ipm_iters);
+}
+
+}  // extern "C"
+
+// nlr < 0: the build's regular QP solver; nlr >= 0: the 32-lane interior point with nlr low-rank terms
+static int debug_solve_qp(mpcc_engine* e, int B, const double* guess, const double* rec, const double* u_cur, int nlr,
+                          const double* lr, const double* lrc, double* step, int32_t* qp_status, int32_t* ipm_iters) {
     if (!e || B < 1 || B > e->maxB || !guess || !rec || !u_cur)
         return fail(MPCC_E_INVALID, "mpcc_debug_solve_qp: invalid argument");
     if (!e->has_track) return fail(MPCC_E_NOTRACK, "mpcc_debug_solve_qp: no track");
@@ -1113,8 +1155,23 @@ int mpcc_debug_solve_qp(mpcc_engine* e, int B, const double* guess, const double
         for (int b = 0; b < B; b++) sqi[(size_t)b * SQI + SQ_ACTIVE] = 1;
         HIPCHK(hipMemcpy(e->d.sqi, sqi.data(), sqi.size() * sizeof(int32_t), hipMemcpyHostToDevice));
         HIPCHK(hipMemset(e->d.step, 0, S * NXU * sizeof(double)));
+        if (nlr >= 0) {  // low-rank terms of every instance, then the 32-lane solver
+            e->ensure_bfgs_buffers();
+            const size_t NE = S * NXU / B;
+            std::vector<double> l((size_t)B * LRM * NE, 0.0), lc((size_t)B * LRM, 0.0);
+            for (int b = 0; b < B; b++)
+                for (int j = 0; j < nlr; j++) {
+                    std::memcpy(&l[((size_t)b * LRM + j) * NE], lr + (size_t)j * NE, NE * sizeof(double));
+                    lc[(size_t)b * LRM + j] = lrc[j];
+                }
+            HIPCHK(hipMemcpy(e->d.lr, l.data(), l.size() * sizeof(double), hipMemcpyHostToDevice));
+            HIPCHK(hipMemcpy(e->d.lrc, lc.data(), lc.size() * sizeof(double), hipMemcpyHostToDevice));
+            for (int b = 0; b < B; b++) sqi[(size_t)b * SQI + SQ_NLR] = nlr;
+            HIPCHK(hipMemcpy(e->d.sqi, sqi.data(), sqi.size() * sizeof(int32_t), hipMemcpyHostToDevice));
+        }
         launch_setqp(c, e->d, e->s_u0, st);
-        launch_ipm(c, e->d, poly_rows_max(c.p.constraint_mask), st);
+        if (nlr >= 0) launch_ipm_wide(c, e->d, poly_rows_max(c.p.constraint_mask), 1, st);
+        else launch_ipm(c, e->d, poly_rows_max(c.p.constraint_mask), st);
         HIPCHK(hipStreamSynchronize(st));
         std::vector<double> stp(S * NXU);
         HIPCHK(hipMemcpy(stp.data(), e->d.step, stp.size() * sizeof(double), hipMemcpyDeviceToHost));
@@ -1137,7 +1194,6 @@ int mpcc_debug_solve_qp(mpcc_engine* e, int B, const double* guess, const double
     return MPCC_OK;
 }
 
-}  // extern "C"
 
 int mpcc_debug_trace_enable(mpcc_engine* e, int enable) {
     if (!e) return fail(MPCC_E_INVALID, "mpcc_debug_trace_enable: null engine");

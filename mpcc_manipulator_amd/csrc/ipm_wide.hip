@@ -26,7 +26,8 @@
 
 namespace mpcc {
 
-static_assert(DOF == 10, "ipm_wide.hip is the mobile manipulator's interior point; the Panda builds ipm.hip");
+// The mobile build's QP solver; both builds run the damped-BFGS option on it (the Panda's x~ fills half the
+// group there).
 
 constexpr int IPM_MAX_IT = 60;
 constexpr double IPM_TOL_MU = 1e-13, IPM_TOL_P = 1e-11, IPM_TOL_STEP = 1e-11;
@@ -42,7 +43,7 @@ constexpr int IPW = 64 / GW;         // instances per wavefront
 constexpr int NXA = NX + DOF;        // augmented stage state [y, w]
 static_assert(NXA <= GW && NU <= 16, "stage dimensions of the 32-lane group");
 
-// workspace fields, ws[(b*(N+1) + k)*IS + field*GW + lane]
+// workspace fields, ws[(b*(N+1) + k)*ISW + field*GW + lane]
 enum : int {
     WF_SL = 0, WF_LL, WF_SU, WF_LU, WF_SP, WF_LP,  // slack / multiplier of the lower, upper and poly slot of row t
     WF_ZX, WF_ZV,                                 // iterate: lane c -> x~_c; lane j < NU -> v_j
@@ -52,15 +53,18 @@ enum : int {
     WF_KFF,                                       // kff (lanes < NU)
     WF_KC,                                        // NU fields: field i, lane c = K[i][c]
     WF_FI = WF_KC + NU,                           // NU fields: field m, lane i = F^-1[i][m]
-    NWF = WF_FI + NU
+    WF_KFJ = WF_FI + NU,                          // LRM fields: kff of the low-rank solves Q_j (BFGS)
+    WF_QX = WF_KFJ + LRM,                         // LRM fields: Q_j = M u_j, x~ part
+    WF_QV = WF_QX + LRM,                          // LRM fields: Q_j, v part
+    NWF = WF_QV + LRM
 };
-static_assert(NWF * GW <= IS, "IPM workspace must fit the per-stage IS allocation");
+static_assert(NWF * GW <= ISW, "IPM workspace must fit the per-stage ISW allocation");
 
 // per-instance LDS block (doubles): F [i*16 + j], U [i*32 + c]
 constexpr int L_F = 0, L_U = 16 * 16;
 constexpr int GRP_LDS = L_U + NU * GW + 16;  // + 16 doubles: the two instances of a wave start 16 banks apart
 
-size_t ipm_lds_bytes(int /*N*/, int /*npmax*/) { return (size_t)IPW * GRP_LDS * sizeof(double); }
+size_t ipm_wide_lds_bytes() { return (size_t)IPW * GRP_LDS * sizeof(double); }
 
 namespace {
 
@@ -202,6 +206,49 @@ __device__ __forceinline__ void bwdN(const double* L, const double* dinv, double
     }
 }
 
+// x = A^-1 b for the LRM x LRM Woodbury capacitance matrix (partial pivoting, the oracle's lu_solve_small),
+// redundantly per lane; indices are constants after unrolling, pivot rows are moved by selects
+__device__ __forceinline__ void solve_small(double (&A)[LRM * LRM], double (&b)[LRM]) {
+#pragma unroll
+    for (int k = 0; k < LRM; k++) {
+        int p = k;
+        double mx = fabs(A[k * LRM + k]);
+#pragma unroll
+        for (int i = k + 1; i < LRM; i++) {
+            const bool take = fabs(A[i * LRM + k]) > mx;
+            mx = take ? fabs(A[i * LRM + k]) : mx;
+            p = take ? i : p;
+        }
+#pragma unroll
+        for (int i = k + 1; i < LRM; i++) {  // swap rows k and p
+            const bool sw = (i == p);
+#pragma unroll
+            for (int j = 0; j < LRM; j++) {
+                const double a = A[k * LRM + j], c2 = A[i * LRM + j];
+                A[k * LRM + j] = sw ? c2 : a;
+                A[i * LRM + j] = sw ? a : c2;
+            }
+            const double bk = b[k], bi = b[i];
+            b[k] = sw ? bi : bk;
+            b[i] = sw ? bk : bi;
+        }
+#pragma unroll
+        for (int i = k + 1; i < LRM; i++) {
+            const double f = A[i * LRM + k] / A[k * LRM + k];
+#pragma unroll
+            for (int j = k; j < LRM; j++) A[i * LRM + j] -= f * A[k * LRM + j];
+            b[i] -= f * b[k];
+        }
+    }
+#pragma unroll
+    for (int i = LRM - 1; i >= 0; i--) {
+        double s = b[i];
+#pragma unroll
+        for (int j = i + 1; j < LRM; j++) s -= A[i * LRM + j] * b[j];
+        b[i] = s / A[i * LRM + i];
+    }
+}
+
 // per-stage inputs of one lane, loaded one stage ahead of their use
 template <int NPE>
 struct StageIn {
@@ -228,8 +275,8 @@ __device__ __forceinline__ void sweep(int N, bool backward, In& b0, In& b1, Load
 }  // namespace
 
 // The QP solve of the 2 instances of this wavefront (32 lanes each).  Writes the step (d.step), QP status
-// and IPM iteration count (d.sqi).
-template <int NPM>
+// and IPM iteration count (d.sqi).  LR: the Hessian carries the damped-BFGS low-rank terms.
+template <int NPM, bool LR>
 __device__ __forceinline__ void ipm_group(const DevConst& c, const DevBuffers& d, double* smem) {
     constexpr int NPE = NPM > 0 ? NPM : 1;
     using In = StageIn<NPE>;
@@ -247,10 +294,10 @@ __device__ __forceinline__ void ipm_group(const DevConst& c, const DevBuffers& d
     if (__ballot(run) == 0) return;
 
     const gdouble* QSb = (const gdouble*)(d.qs + (size_t)(valid ? b : 0) * NS * QS);
-    gdouble* WSb = (gdouble*)(d.is + (size_t)(valid ? b : 0) * NS * IS);
+    gdouble* WSb = (gdouble*)(d.isw + (size_t)(valid ? b : 0) * NS * ISW);
     gdouble* const WSt = WSb + t;
     auto ws = [&](int k, int f) -> gdouble* {
-        gdouble* wk = WSt + (size_t)k * IS;
+        gdouble* wk = WSt + (size_t)k * ISW;
         asm("" : "+v"(wk));
         return wk + f * GW;
     };
@@ -307,6 +354,34 @@ __device__ __forceinline__ void ipm_group(const DevConst& c, const DevBuffers& d
     if (run && (fl & 1)) { if (t == 0) { si[SQ_STATUS] = MPCC_NAN_HESSIAN; si[SQ_ACTIVE] = 0; } run = false; }
     if (run && (fl & 4)) { if (t == 0) si[SQ_QPSTAT] = MPCC_QP_PrimalInfeasible; run = false; }  // keep old step (Q6)
     const bool entered = run;
+
+    // ---- low-rank Hessian terms of the damped-BFGS option: B = H_0 + sum_j c_j u_j u_j^T, u_j per stage as
+    //      [x (NX) | u (NU)] (d.lr).  Every Riccati solve dz_s = -M g is corrected by the Woodbury identity,
+    //      dz = dz_s - Q S^-1 (U^T dz_s) with Q_j = M u_j = -solve(u_j) (backward recursion in the factorization
+    //      sweep, forward in the predictor forward sweep) and S = C^-1 + U^T Q (the oracle's lr_solve).
+    int nlr = 0;
+    double lrc[LRM];
+    const gdouble* LRb = (const gdouble*)d.step;  // any valid address when !LR
+#pragma unroll
+    for (int j = 0; j < LRM; j++) lrc[j] = 0.0;
+    if constexpr (LR) {
+        nlr = si[SQ_NLR];
+#pragma unroll
+        for (int j = 0; j < LRM; j++) lrc[j] = (j < nlr) ? d.lrc[(size_t)(valid ? b : 0) * LRM + j] : 0.0;
+        LRb = (const gdouble*)(d.lr + (size_t)(valid ? b : 0) * LRM * NS * NXU);
+    }
+    const bool lrw = LR && __ballot(entered && nlr > 0) != 0;  // this wave runs the split (Woodbury) sweeps
+    auto u_y = [&](int j, int k) -> double {  // u_j, y part of stage k (lanes < NX)
+        const double v = LRb[((size_t)j * NS + k) * NXU + (rowY ? t : 0)];
+        return (LR && rowY && j < nlr) ? v : 0.0;
+    };
+    auto u_v = [&](int j, int k) -> double {  // u_j, v part of stage k (lanes < NU, k < N)
+        const double v = LRb[((size_t)j * NS + k) * NXU + NX + (t < NU ? t : 0)];
+        return (LR && t < NU && k < N && j < nlr) ? v : 0.0;
+    };
+    double uz[LRM];  // u_j^T z of the current iterate
+#pragma unroll
+    for (int j = 0; j < LRM; j++) uz[j] = 0.0;
 
     // ---- stage loaders (unconditional loads, lane/stage conditions as selects)
     auto load_common = [&](int k, In& o) {
@@ -416,14 +491,14 @@ __device__ __forceinline__ void ipm_group(const DevConst& c, const DevBuffers& d
     };
     // forward step: v = K x~ + kff (group sums over the K column layout; result on lanes < NU) and
     // x~' = A~ x~ + B~ v (all lanes)
-    auto fwd_step = [&](const In& in, double xt, double& v, double& xn) {
+    auto fwd_step_k = [&](const In& in, double xt, double kff, double& v, double& xn) {
         double vv = 0.0;
 #pragma unroll
         for (int i = 0; i < NU; i++) {
             const double s = g_sum32(in.m[i] * xt);
             if (t == i) vv = s;
         }
-        v = vv + in.m[NU];
+        v = vv + kff;
         const Halves hx = halves(xt), hv = halves(v);
         const double xvs = bch(hx, XVS);
         const double vprev = down32<1>(v, hv, t);   // lane XVS <- v_dVs (lane XS)
@@ -433,6 +508,7 @@ __device__ __forceinline__ void ipm_group(const DevConst& c, const DevBuffers& d
         else if (t == XVS) xn = mt * xt + gv * vprev;
         else xn = rowD ? vj : 0.0;
     };
+    auto fwd_step = [&](const In& in, double xt, double& v, double& xn) { fwd_step_k(in, xt, in.m[NU], v, xn); };
 
     In cur, nxt;
     int it = 0, it_total = 0;
@@ -450,6 +526,9 @@ __device__ __forceinline__ void ipm_group(const DevConst& c, const DevBuffers& d
         }
         // ---- start point: dynamics rollout with v = 0; slacks / multipliers (solve_struct_ipm)
         double mcount = 0.0;
+        double uzp[LRM];
+#pragma unroll
+        for (int j = 0; j < LRM; j++) uzp[j] = 0.0;
         if (run) {
             double y = 0.0;  // lane a < NX: y_a of stage k
             for (int k = 0; k <= N; k++) {
@@ -468,6 +547,9 @@ __device__ __forceinline__ void ipm_group(const DevConst& c, const DevBuffers& d
                 *ws(k, WF_SP) = sP; *ws(k, WF_LP) = lP;
                 *ws(k, WF_ZX) = yx;
                 *ws(k, WF_ZV) = 0.0;
+                if (lrw)
+#pragma unroll
+                    for (int j = 0; j < LRM; j++) uzp[j] += u_y(j, k) * yx;
                 // y_{k+1} = M y_k + b_k (oracle order: sum_b M[a][b] y_b, then + b_a)
                 const double yvs = up1(y, t);  // lane XS <- y_vs
                 const double yn = (t == XS) ? mss * y + msv * yvs : mt * y;
@@ -475,6 +557,9 @@ __device__ __forceinline__ void ipm_group(const DevConst& c, const DevBuffers& d
             }
         }
         mcount = g_sum32(mcount);
+        if (lrw)
+#pragma unroll
+            for (int j = 0; j < LRM; j++) uz[j] = g_sum32(uzp[j]);
 
         it = 0;
         double mu0 = 0.0, dz_prev = 1e30, sigma_mu = 0.0, mu_cur = 1e30, rp_cur = 1e30;
@@ -486,6 +571,9 @@ __device__ __forceinline__ void ipm_group(const DevConst& c, const DevBuffers& d
                 // ================= factorization sweep k = N..0 (lazy update, g0, predictor backward solve)
                 double Pc[NXA];  // column t of P_{k+1}
                 double pv = 0.0; // p_{k+1}, component t
+                double pj[LRM];  // p of the low-rank solves Q_j
+#pragma unroll
+                for (int j = 0; j < LRM; j++) pj[j] = 0.0;
                 bool chol_ok = true;
                 sweep(N, true, cur, nxt, [&](int k, In& o) { load_factor(k, o, pending); }, [&](int k, const In& cur) {
                     const double lb = cur.lb, ub = cur.ub;
@@ -537,6 +625,13 @@ __device__ __forceinline__ void ipm_group(const DevConst& c, const DevBuffers& d
                             g0v = s + rt;
                         }
                     }
+                    if (lrw)  // + sum_j c_j u_j (u_j^T z)
+#pragma unroll
+                        for (int j = 0; j < LRM; j++) {
+                            const double f = lrc[j] * uz[j];
+                            g0x += f * u_y(j, k);
+                            g0v += f * u_v(j, k);
+                        }
                     *ws(k, WF_GX) = g0x;
                     *ws(k, WF_GV) = g0v;
                     double gx, gvv;
@@ -553,6 +648,9 @@ __device__ __forceinline__ void ipm_group(const DevConst& c, const DevBuffers& d
                             Pc[a] = v;
                         }
                         pv = gx;
+                        if (lrw)
+#pragma unroll
+                            for (int j = 0; j < LRM; j++) pj[j] = u_y(j, k);
                         return;
                     }
                     // ---- (1) Y = B~^T P (column t), f = g_v + B~^T p (lanes < NU)
@@ -656,6 +754,30 @@ __device__ __forceinline__ void ipm_group(const DevConst& c, const DevBuffers& d
                         *ws(k, WF_FI + i) = fi[i];
                     }
                     *ws(k, WF_KFF) = (t < NU) ? kff : 0.0;
+                    if (lrw)  // backward recursion of the low-rank solves, gradient u_j (y and v parts)
+#pragma unroll
+                        for (int j = 0; j < LRM; j++) {
+                            const Halves hq = halves(pj[j]);
+                            // both shifts unconditionally: a DPP read inside a divergent branch sees masked lanes as 0
+                            const double qu = up32<NX>(pj[j], hq, t), qu1 = up32<1>(pj[j], hq, t);
+                            const double fvj = u_v(j, k) + gt * pj[j] + ((t < DOF) ? qu : gv * qu1);
+                            const Halves hfj = halves(fvj);
+                            double kffj = 0.0, ktfj = 0.0;
+#pragma unroll
+                            for (int m = 0; m < NU; m++) {
+                                const double fbm = bch(hfj, m);
+                                kffj -= fi[m] * fbm;
+                                ktfj += kc[m] * fbm;
+                            }
+                            *ws(k, WF_KFJ + j) = (t < NU) ? kffj : 0.0;
+                            double atpj = 0.0;
+                            const double pq7 = down32<1>(pj[j], hq, t);
+                            if (rowY) {
+                                atpj = mt * pj[j];
+                                if (t == XVS) atpj += msv * pq7;
+                            }
+                            pj[j] = u_y(j, k) + atpj + ktfj;
+                        }
                     // ---- (4) Hb column t and P = Hb - U^T U (column t); U rows are broadcast LDS reads
                     double hbv[NXA];
                     {
@@ -730,15 +852,12 @@ __device__ __forceinline__ void ipm_group(const DevConst& c, const DevBuffers& d
                 double S0 = 0, S1 = 0, S2 = 0;
                 MinRatio amr(1.0);
                 double xt = 0.0;
-                sweep(N, false, cur, nxt, [&](int k, In& o) { load_fwd(k, o, false); }, [&](int k, const In& cur) {
+                auto pred_rec = [&](int k, const In& cur, double xs, double dvv) {
                     const bool aL = row_active(k, cur.lb), aU = row_active(k, cur.ub), aP = poly_slot_active(cur, k);
-                    double v = 0.0, xn = 0.0;
-                    fwd_step(cur, xt, v, xn);
-                    const double dvv = (t < NU && k < N) ? v : 0.0;
-                    *ws(k, WF_AX) = xt;
+                    *ws(k, WF_AX) = xs;
                     *ws(k, WF_AV) = dvv;
-                    const double cz = row_cz(k, cur.zx, cur.zv), ca = row_cz(k, xt, dvv);
-                    const double pcz = poly_cz(cur, k, cur.zx, cur.zv), pca = poly_cz(cur, k, xt, dvv);
+                    const double cz = row_cz(k, cur.zx, cur.zv), ca = row_cz(k, xs, dvv);
+                    const double pcz = poly_cz(cur, k, cur.zx, cur.zv), pca = poly_cz(cur, k, xs, dvv);
                     auto rec = [&](bool a, double sgn, double bnd, double czz, double caa, double s, double l) {
                         if (!a) return;
                         const double rp = slot_rp(sgn, czz, bnd, s);
@@ -751,8 +870,82 @@ __device__ __forceinline__ void ipm_group(const DevConst& c, const DevBuffers& d
                     rec(aL, sgnL, cur.lb, cz, ca, cur.sL, cur.lL);
                     rec(aU, sgnU, cur.ub, cz, ca, cur.sU, cur.lU);
                     rec(aP, sgnU, cur.pub, pcz, pca, cur.sP, cur.lP);
-                    xt = (k < N) ? xn : 0.0;
-                });
+                };
+                // Woodbury pieces of this factorization (low-rank option): Q_j, S = C^-1 + U^T Q
+                double Smat[LRM * LRM];
+#ifdef MPCC_IPM_TRACE
+                double trc_t0 = 0.0, trc_S0 = 0.0;
+#endif
+                auto load_fix = [&](int k, In& o, bool corr) {  // stored dz_s (and predictor step) with the Q_j
+                    load_common(k, o);
+                    o.x0 = *ws(k, WF_AX); o.x1 = *ws(k, WF_AV);
+                    o.x2 = corr ? *ws(k, WF_DX) : 0.0; o.x3 = corr ? *ws(k, WF_DV) : 0.0;
+#pragma unroll
+                    for (int j = 0; j < LRM; j++) { o.m[j] = *ws(k, WF_QX + j); o.m[LRM + j] = *ws(k, WF_QV + j); }
+                };
+                if (!lrw) {
+                    sweep(N, false, cur, nxt, [&](int k, In& o) { load_fwd(k, o, false); }, [&](int k, const In& cur) {
+                        double v = 0.0, xn = 0.0;
+                        fwd_step(cur, xt, v, xn);
+                        pred_rec(k, cur, xt, (t < NU && k < N) ? v : 0.0);
+                        xt = (k < N) ? xn : 0.0;
+                    });
+                } else {
+                    double xq[LRM], udp[LRM], uqp[LRM * LRM];
+#pragma unroll
+                    for (int j = 0; j < LRM; j++) { xq[j] = 0.0; udp[j] = 0.0; }
+#pragma unroll
+                    for (int j = 0; j < LRM * LRM; j++) uqp[j] = 0.0;
+                    sweep(N, false, cur, nxt, [&](int k, In& o) { load_fwd(k, o, false); }, [&](int k, const In& cur) {
+                        double v = 0.0, xn = 0.0;
+                        fwd_step(cur, xt, v, xn);
+                        const double dvv = (t < NU && k < N) ? v : 0.0;
+                        *ws(k, WF_AX) = xt;  // dz_s
+                        *ws(k, WF_AV) = dvv;
+                        double uyk[LRM], uvk[LRM];
+#pragma unroll
+                        for (int j = 0; j < LRM; j++) {
+                            uyk[j] = u_y(j, k);
+                            uvk[j] = u_v(j, k);
+                            udp[j] += uyk[j] * xt + uvk[j] * dvv;
+                        }
+#pragma unroll
+                        for (int j = 0; j < LRM; j++) {  // Q_j = -solve(u_j), forward recursion
+                            const double kfj = *ws(k, WF_KFJ + j);
+                            double vq = 0.0, xqn = 0.0;
+                            fwd_step_k(cur, xq[j], (k < N) ? kfj : 0.0, vq, xqn);
+                            const double qx = (t < NXA) ? -xq[j] : 0.0, qv = (t < NU && k < N) ? -vq : 0.0;
+                            *ws(k, WF_QX + j) = qx;
+                            *ws(k, WF_QV + j) = qv;
+#pragma unroll
+                            for (int i = 0; i < LRM; i++) uqp[i * LRM + j] += uyk[i] * qx + uvk[i] * qv;
+                            xq[j] = (k < N) ? xqn : 0.0;
+                        }
+                        xt = (k < N) ? xn : 0.0;
+                    });
+                    double tt[LRM], Sm[LRM * LRM];
+#pragma unroll
+                    for (int i = 0; i < LRM; i++) {
+                        tt[i] = g_sum32(udp[i]);
+#pragma unroll
+                        for (int j = 0; j < LRM; j++) {
+                            const double uq = g_sum32(uqp[i * LRM + j]);
+                            Smat[i * LRM + j] = (i == j ? (i < nlr ? 1.0 / lrc[i] : 1.0) : 0.0) + uq;
+                            Sm[i * LRM + j] = Smat[i * LRM + j];
+                        }
+                    }
+                    solve_small(Sm, tt);
+#ifdef MPCC_IPM_TRACE
+                    trc_t0 = tt[0]; trc_S0 = Smat[0];
+#endif
+                    // dz = dz_s - Q S^-1 U^T dz_s, then the recovery of the predictor step
+                    sweep(N, false, cur, nxt, [&](int k, In& o) { load_fix(k, o, false); }, [&](int k, const In& cur) {
+                        double xs = cur.x0, dvv = cur.x1;
+#pragma unroll
+                        for (int j = 0; j < LRM; j++) { xs -= tt[j] * cur.m[j]; dvv -= tt[j] * cur.m[LRM + j]; }
+                        pred_rec(k, cur, xs, dvv);
+                    });
+                }
                 const double amax = g_min32(amr.value());
                 S0 = g_sum32(S0); S1 = g_sum32(S1); S2 = g_sum32(S2);
                 const double mu = (mcount > 0) ? S0 / mcount : 0.0;
@@ -810,19 +1003,17 @@ __device__ __forceinline__ void ipm_group(const DevConst& c, const DevBuffers& d
                 // ---- corrector forward: dz, ds, dl, max step, mu(alpha) sums, max |rp|, max |dz|
                 double T0 = 0, T1 = 0, T2 = 0, rpm = 0, dzm = 0;
                 MinRatio amc(1e30);
-                xt = 0.0;
-                sweep(N, false, cur, nxt, [&](int k, In& o) { load_fwd(k, o, true); }, [&](int k, const In& cur) {
+                double uzd[LRM], uzdp[LRM];  // u_j^T dz of the corrector step
+#pragma unroll
+                for (int j = 0; j < LRM; j++) { uzd[j] = 0.0; uzdp[j] = 0.0; }
+                auto corr_rec = [&](int k, const In& cur, double xtt, double dvv, double ax, double av) {
                     const bool aL = row_active(k, cur.lb), aU = row_active(k, cur.ub), aP = poly_slot_active(cur, k);
-                    double v = 0.0, xn = 0.0;
-                    fwd_step(cur, xt, v, xn);
-                    const double dvv = (t < NU && k < N) ? v : 0.0;
-                    const double xtt = (t < NXA) ? xt : 0.0;
                     *ws(k, WF_DX) = xtt;
                     *ws(k, WF_DV) = dvv;
                     dzm = fmax(dzm, fmax(fabs(xtt), fabs(dvv)));
-                    const double cz = row_cz(k, cur.zx, cur.zv), cd = row_cz(k, xtt, dvv), ca = row_cz(k, cur.x0, cur.x1);
+                    const double cz = row_cz(k, cur.zx, cur.zv), cd = row_cz(k, xtt, dvv), ca = row_cz(k, ax, av);
                     const double pcz = poly_cz(cur, k, cur.zx, cur.zv), pcd = poly_cz(cur, k, xtt, dvv);
-                    const double pca = poly_cz(cur, k, cur.x0, cur.x1);
+                    const double pca = poly_cz(cur, k, ax, av);
                     auto rec = [&](bool a, double sgn, double bnd, double czz, double caa, double cdd, double s, double l) {
                         if (!a) return;
                         double rp;
@@ -836,13 +1027,58 @@ __device__ __forceinline__ void ipm_group(const DevConst& c, const DevBuffers& d
                     rec(aL, sgnL, cur.lb, cz, ca, cd, cur.sL, cur.lL);
                     rec(aU, sgnU, cur.ub, cz, ca, cd, cur.sU, cur.lU);
                     rec(aP, sgnU, cur.pub, pcz, pca, pcd, cur.sP, cur.lP);
-                    xt = (k < N) ? xn : 0.0;
-                });
+                };
+                xt = 0.0;
+                if (!lrw) {
+                    sweep(N, false, cur, nxt, [&](int k, In& o) { load_fwd(k, o, true); }, [&](int k, const In& cur) {
+                        double v = 0.0, xn = 0.0;
+                        fwd_step(cur, xt, v, xn);
+                        corr_rec(k, cur, (t < NXA) ? xt : 0.0, (t < NU && k < N) ? v : 0.0, cur.x0, cur.x1);
+                        xt = (k < N) ? xn : 0.0;
+                    });
+                } else {
+                    double udp[LRM];
+#pragma unroll
+                    for (int j = 0; j < LRM; j++) udp[j] = 0.0;
+                    sweep(N, false, cur, nxt, [&](int k, In& o) { load_fwd(k, o, false); }, [&](int k, const In& cur) {
+                        double v = 0.0, xn = 0.0;
+                        fwd_step(cur, xt, v, xn);
+                        const double xtt = (t < NXA) ? xt : 0.0, dvv = (t < NU && k < N) ? v : 0.0;
+                        *ws(k, WF_DX) = xtt;  // dz_s
+                        *ws(k, WF_DV) = dvv;
+#pragma unroll
+                        for (int j = 0; j < LRM; j++) udp[j] += u_y(j, k) * xtt + u_v(j, k) * dvv;
+                        xt = (k < N) ? xn : 0.0;
+                    });
+                    double tt[LRM], Sm[LRM * LRM];
+#pragma unroll
+                    for (int i = 0; i < LRM; i++) tt[i] = g_sum32(udp[i]);
+#pragma unroll
+                    for (int i = 0; i < LRM * LRM; i++) Sm[i] = Smat[i];
+                    solve_small(Sm, tt);
+                    sweep(N, false, cur, nxt, [&](int k, In& o) { load_fix(k, o, true); }, [&](int k, const In& cur) {
+                        double xtt = cur.x2, dvv = cur.x3;
+#pragma unroll
+                        for (int j = 0; j < LRM; j++) { xtt -= tt[j] * cur.m[j]; dvv -= tt[j] * cur.m[LRM + j]; }
+                        corr_rec(k, cur, xtt, dvv, cur.x0, cur.x1);
+#pragma unroll
+                        for (int j = 0; j < LRM; j++) uzdp[j] += u_y(j, k) * xtt + u_v(j, k) * dvv;
+                    });
+#pragma unroll
+                    for (int j = 0; j < LRM; j++) uzd[j] = g_sum32(uzdp[j]);
+                }
                 const double amx = g_min32(amc.value());
                 T0 = g_sum32(T0); T1 = g_sum32(T1); T2 = g_sum32(T2);
                 rpm = g_max32(rpm);
                 dzm = g_max32(dzm);
                 alpha = fmin(1.0, fmax(IPM_TAU, 1.0 - sqrt(mu)) * amx);
+#pragma unroll
+                for (int j = 0; j < LRM; j++) uz[j] += alpha * uzd[j];  // u_j^T z of the next iterate
+#ifdef MPCC_IPM_TRACE
+                if (b == 0 && t == 0)
+                    printf("gpu it %2d mu %.6e amax %.6e sig %.6e amx %.6e alpha %.6e rp %.6e dz %.6e uz0 %.9e t0 %.9e S0 %.9e\n",
+                           it, mu, amax, sigma, amx, alpha, rpm, dzm, uz[0], trc_t0, trc_S0);
+#endif
                 sigma_mu = smu;
                 pending = true;
                 it++;
@@ -885,10 +1121,32 @@ __device__ __forceinline__ void ipm_group(const DevConst& c, const DevBuffers& d
     }
 }
 
-template <int NPM>
+template <int NPM, bool LR>
 __global__ void __launch_bounds__(64) k_ipm(DevConst c, DevBuffers d) {
     extern __shared__ __attribute__((aligned(16))) double smem[];
-    ipm_group<NPM>(c, d, smem);
+    ipm_group<NPM, LR>(c, d, smem);
+}
+template <int NPM, bool LR>
+static void launch_ipm_t(const DevConst& c, const DevBuffers& d, hipStream_t s) {
+    hipLaunchKernelGGL((k_ipm<NPM, LR>), dim3((c.Bn + IPW - 1) / IPW), dim3(64), ipm_wide_lds_bytes(), s, c, d);
+}
+// one QP solve per active instance on the 32-lane interior point (lr: with the instances' low-rank terms)
+void launch_ipm_wide(const DevConst& c, const DevBuffers& d, int npmax, int lr, hipStream_t s) {
+    if (lr) {
+        switch (npmax) {
+            case 0: launch_ipm_t<0, true>(c, d, s); break;
+            case 1: launch_ipm_t<1, true>(c, d, s); break;
+            case 2: launch_ipm_t<2, true>(c, d, s); break;
+            default: launch_ipm_t<11, true>(c, d, s); break;
+        }
+        return;
+    }
+    switch (npmax) {
+        case 0: launch_ipm_t<0, false>(c, d, s); break;
+        case 1: launch_ipm_t<1, false>(c, d, s); break;
+        case 2: launch_ipm_t<2, false>(c, d, s); break;
+        default: launch_ipm_t<11, false>(c, d, s); break;
+    }
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -896,12 +1154,13 @@ __global__ void __launch_bounds__(64) k_ipm(DevConst c, DevBuffers d) {
 // (as ipm.hip's k_sqp: QP solve, line-search trial lane = stage, filter decision, step, next QP assembly)
 // ------------------------------------------------------------------------------------------------
 __device__ __attribute__((noinline)) void sqp_setqp_phase(const DevConst& c, const DevBuffers& d, int b, int t,
-                                                          const double* __restrict__ ucur) {
+                                                          const double* __restrict__ ucur, bool keep_hess) {
     const int N = c.N, NS = N + 1;
     const SplineView sp = spl_of(c.spl, b);
     const double* gb = d.guess + (size_t)b * NS * NXU;
     for (int k = t; k <= N; k += GW)
-        setqp_stage(c, sp, gb, RecView{d.rec + (size_t)b * NS + k, c.S}, k, ucur, d.qs + ((size_t)b * NS + k) * QS);
+        setqp_stage(c, sp, gb, RecView{d.rec + (size_t)b * NS + k, c.S}, k, ucur, d.qs + ((size_t)b * NS + k) * QS,
+                    keep_hess);
 }
 __device__ __attribute__((noinline)) void sqp_trial_phase(const DevConst& c, const DevBuffers& d, int b, int t,
                                                           const double* __restrict__ ucur, double alpha, bool keep) {
@@ -924,12 +1183,136 @@ __device__ __attribute__((noinline)) void sqp_soc_phase(const DevConst& c, const
         soc_stage(c, sp, d.guess + o, d.step + o, RecView{d.rec + (size_t)b * NS + k, c.S}, k, ucur,
                   d.qs + ((size_t)b * NS + k) * QS);
 }
-template <int NPM>
+template <int NPM, bool LR>
 __device__ __attribute__((noinline)) void sqp_ipm_phase(const DevConst& c, const DevBuffers& d, double* smem) {
-    ipm_group<NPM>(c, d, smem);
+    ipm_group<NPM, LR>(c, d, smem);
 }
 
-template <int NPM>
+// ---- damped BFGS bookkeeping (osqp_interface.cpp:403-453, 540-555, 683-715), one 32-lane group per instance.
+//      Vectors in the horizon layout [(N+1)][x (NX) | u (NU)] (u_N = 0), normalized as the QP; the oracle's
+//      solve_ocp / bfgs_update.
+// element e of B s: the stage Hessians of SQP iteration 0 (QS_Q, QS_R and the ddq coupling Hct between u_k and
+// u_{k-1}, k in [1, N-1]) plus the low-rank terms sum_j c_j (u_j^T s) u_j (us[j] = u_j^T s)
+__device__ __forceinline__ double bfgs_hmul_elem(const DevConst& c, const double* __restrict__ qsb, const double* __restrict__ sv,
+                                                 const double* __restrict__ lrb, const double* __restrict__ lrcb, const double* us,
+                                                 int nlr, int N, int e) {
+    const int NS = N + 1;
+    const int k = e / NXU, a = e - NXU * k;
+    const double* q = qsb + (size_t)k * QS;
+    double v = 0.0;
+    if (a < NX) {
+        for (int m = 0; m < NX; m++) v += q[QS_Q + a * NX + m] * sv[NXU * k + m];
+    } else if (k < N) {
+        const int i = a - NX;
+        v = q[QS_R + i] * sv[e];
+        if (i < DOF) {
+            const double hct = c.p.Tu[i] * (-2. * c.p.qp_r_ddq) * c.p.Tu[i];
+            if (k >= 1) v += hct * sv[e - NXU];
+            if (k + 1 <= N - 1) v += hct * sv[e + NXU];
+        }
+    }
+    for (int j = 0; j < nlr; j++) v += (lrcb[j] * us[j]) * lrb[(size_t)j * NS * NXU + e];
+    return v;
+}
+// the QP gradient (normalized grad_obj) of element e: Tx f_x / Tu f_u + ddq gradient (QS_q / QS_r)
+__device__ __forceinline__ double bfgs_q_elem(const double* __restrict__ qsb, int N, int e) {
+    const int k = e / NXU, a = e - NXU * k;
+    const double* q = qsb + (size_t)k * QS;
+    return (a < NX) ? q[QS_q + a] : ((k < N) ? q[QS_r + a - NX] : 0.0);
+}
+// u_j^T s over the horizon for the instance's low-rank terms (group reductions)
+__device__ __forceinline__ void bfgs_us(const double* __restrict__ lrb, const double* __restrict__ sv, int nlr, int NE, int t,
+                                        double (&us)[LRM]) {
+#pragma unroll
+    for (int j = 0; j < LRM; j++) {
+        double p = 0.0;
+        if (j < nlr)
+            for (int e = t; e < NE; e += GW) p += lrb[(size_t)j * NE + e] * sv[e];
+        us[j] = g_sum32(p);
+    }
+}
+// SQP iteration it (after setQP): grad_L = q + A^T lambda; for it > 0, dgrad_L = grad_L - grad_L_prev and
+// Hess_ = BFGSUpdate(Hess_, step_prev, dgrad_L) appends -Bs Bs^T / sBs + r r^T / sr to the low-rank terms.
+// Returns false when the update makes the Hessian NaN (sBs = 0 with sr >= eps): NAN_HESSIAN (:474-477).
+__device__ __attribute__((noinline)) bool bfgs_pre(const DevConst& c, const DevBuffers& d, int b, int t, int it) {
+    const int N = c.N, NS = N + 1, NE = NS * NXU;
+    int32_t* si = d.sqi + (size_t)b * SQI;
+    const int nlr = si[SQ_NLR];
+    const double* qsb = d.qs + (size_t)b * NS * QS;
+    double* lrb = d.lr + (size_t)b * LRM * NE;
+    const double* lrcb = d.lrc + (size_t)b * LRM;
+    double* glam = d.glam + (size_t)b * NE;
+    double* gprev = d.gprev + (size_t)b * NE;
+    const double* sp = d.sp + (size_t)b * NE;
+    if (it == 0) {
+        for (int e = t; e < NE; e += GW) gprev[e] = bfgs_q_elem(qsb, N, e) + glam[e];
+        return true;
+    }
+    // dgrad_L into slot nlr + 1, B step_prev into slot nlr (B of the previous iteration)
+    double* bsv = lrb + (size_t)nlr * NE;
+    double* dgv = lrb + (size_t)(nlr + 1) * NE;
+    double us[LRM];
+    bfgs_us(lrb, sp, nlr, NE, t, us);
+    double sbs = 0.0, sy = 0.0;
+    for (int e = t; e < NE; e += GW) {
+        const double gl = bfgs_q_elem(qsb, N, e) + glam[e];
+        const double dg = gl - gprev[e];
+        gprev[e] = gl;
+        const double bs = bfgs_hmul_elem(c, qsb, sp, lrb, lrcb, us, nlr, N, e);  // reads slots < nlr only
+        bsv[e] = bs;
+        dgv[e] = dg;
+        sbs += sp[e] * bs;
+        sy += sp[e] * dg;
+    }
+    sbs = g_sum32(sbs);
+    sy = g_sum32(sy);
+    double theta = 1.0, sr = sy;
+    const bool damp = sy < 0.2 * sbs;
+    if (damp) {
+        theta = 0.8 * sbs / (sbs - sy);
+        sr = theta * sy + (1 - theta) * sbs;
+    }
+    if (sr < 2.220446049250313e-16) return true;  // unchanged Hessian (std::numeric_limits<double>::epsilon())
+    if (!(sbs != 0.0) || !isfinite(sbs) || !isfinite(sr)) return false;
+    for (int e = t; e < NE; e += GW) {
+        const double dg = dgv[e];
+        dgv[e] = damp ? theta * dg + (1 - theta) * bsv[e] : dg;  // r
+    }
+    if (t == 0) {
+        double* lc = d.lrc + (size_t)b * LRM;
+        lc[nlr] = -1.0 / sbs;
+        lc[nlr + 1] = 1.0 / sr;
+        si[SQ_NLR] = nlr + 2;
+    }
+    return true;
+}
+// after the QP (and the correction): A^T y = -(B step + q) of the exact QP solution (its stationarity)
+__device__ __attribute__((noinline)) void bfgs_post_qp(const DevConst& c, const DevBuffers& d, int b, int t) {
+    const int N = c.N, NS = N + 1, NE = NS * NXU;
+    const int nlr = d.sqi[(size_t)b * SQI + SQ_NLR];
+    const double* qsb = d.qs + (size_t)b * NS * QS;
+    const double* lrb = d.lr + (size_t)b * LRM * NE;
+    const double* lrcb = d.lrc + (size_t)b * LRM;
+    const double* stp = d.step + (size_t)b * NE;
+    double* aty = d.aty + (size_t)b * NE;
+    double us[LRM];
+    bfgs_us(lrb, stp, nlr, NE, t, us);
+    for (int e = t; e < NE; e += GW) aty[e] = -(bfgs_hmul_elem(c, qsb, stp, lrb, lrcb, us, nlr, N, e) + bfgs_q_elem(qsb, N, e));
+}
+// after the line search: lambda += alpha (y - lambda) as A^T lambda, step_prev = alpha step (:540-555)
+__device__ __attribute__((noinline)) void bfgs_post_step(const DevConst& c, const DevBuffers& d, int b, int t, double alpha) {
+    const int NE = (c.N + 1) * NXU;
+    double* glam = d.glam + (size_t)b * NE;
+    double* sp = d.sp + (size_t)b * NE;
+    const double* aty = d.aty + (size_t)b * NE;
+    const double* stp = d.step + (size_t)b * NE;
+    for (int e = t; e < NE; e += GW) {
+        glam[e] = glam[e] + alpha * (aty[e] - glam[e]);
+        sp[e] = alpha * stp[e];
+    }
+}
+
+template <int NPM, bool LR>
 __global__ void __launch_bounds__(64) k_sqp(DevConst c, DevBuffers d, const double* __restrict__ ucur_all) {
     extern __shared__ __attribute__((aligned(16))) double smem[];
     const int t = threadIdx.x % GW;
@@ -939,23 +1322,35 @@ __global__ void __launch_bounds__(64) k_sqp(DevConst c, DevBuffers d, const doub
     const int bb = valid ? b : 0;
     int32_t* si = d.sqi + (size_t)bb * SQI;
     const double* ucur = ucur_all + NU * bb;
+    if constexpr (LR) {  // fresh BFGS state per solveOCP (:403-408)
+        if (valid)
+            for (int e = t; e < NS * NXU; e += GW) d.glam[(size_t)b * NS * NXU + e] = 0.0;
+    }
     for (int it = 0; it < c.p.max_iter; it++) {
         bool act = valid && si[SQ_ACTIVE] != 0;
         if (__ballot(act) == 0) break;
         if (it > 0) {
-            if (act) sqp_setqp_phase(c, d, b, t, ucur);
+            if (act) sqp_setqp_phase(c, d, b, t, ucur, LR);
             __syncthreads();
         }
-        sqp_ipm_phase<NPM>(c, d, smem);
+        if constexpr (LR) {
+            if (act && !bfgs_pre(c, d, b, t, it) && t == 0) { si[SQ_STATUS] = MPCC_NAN_HESSIAN; si[SQ_ACTIVE] = 0; }
+            __syncthreads();
+        }
+        sqp_ipm_phase<NPM, LR>(c, d, smem);
         __syncthreads();
         if (c.p.do_SOC) {  // SecondOrderCorrection (osqp_interface.cpp:506-535)
             act = valid && si[SQ_ACTIVE] != 0;
             if (act) sqp_soc_phase(c, d, b, t, ucur);
             __syncthreads();
-            sqp_ipm_phase<NPM>(c, d, smem);
+            sqp_ipm_phase<NPM, LR>(c, d, smem);
             __syncthreads();
         }
         act = valid && si[SQ_ACTIVE] != 0;
+        if constexpr (LR) {
+            if (act) bfgs_post_qp(c, d, b, t);
+            __syncthreads();
+        }
         if (act) sqp_trial_phase(c, d, b, t, ucur, 1.0, true);
         __syncthreads();
         if (act && t == 0) accept_instance(c, d, b);
@@ -970,6 +1365,7 @@ __global__ void __launch_bounds__(64) k_sqp(DevConst c, DevBuffers d, const doub
         double nrm = 0.0;
         if (act) {
             const double alpha = d.sqd[(size_t)b * SQ + SQ_ALPHA];
+            if constexpr (LR) bfgs_post_step(c, d, b, t, alpha);
             for (int e = t; e < NS * NXU; e += GW) nrm = fmax(nrm, apply_elem(c, d, b, e, alpha));
         }
         nrm = g_max32(nrm);
@@ -978,30 +1374,36 @@ __global__ void __launch_bounds__(64) k_sqp(DevConst c, DevBuffers d, const doub
     }
 }
 
-template <int NPM>
-static void launch_ipm_t(const DevConst& c, const DevBuffers& d, hipStream_t s) {
-    hipLaunchKernelGGL(k_ipm<NPM>, dim3((c.Bn + IPW - 1) / IPW), dim3(64), ipm_lds_bytes(c.N, NPM), s, c, d);
-}
-template <int NPM>
+template <int NPM, bool LR>
 static void launch_sqp_t(const DevConst& c, const DevBuffers& d, const double* u_cur, hipStream_t s) {
-    hipLaunchKernelGGL(k_sqp<NPM>, dim3((c.Bn + IPW - 1) / IPW), dim3(64), ipm_lds_bytes(c.N, NPM), s, c, d, u_cur);
+    hipLaunchKernelGGL((k_sqp<NPM, LR>), dim3((c.Bn + IPW - 1) / IPW), dim3(64), ipm_wide_lds_bytes(), s, c, d, u_cur);
 }
 
-void launch_ipm(const DevConst& c, const DevBuffers& d, int npmax, hipStream_t s) {
+void launch_sqp_wide(const DevConst& c, const DevBuffers& d, const double* u_cur, int npmax, int bfgs, hipStream_t s) {
+    if (bfgs) {
+        switch (npmax) {
+            case 0: launch_sqp_t<0, true>(c, d, u_cur, s); break;
+            case 1: launch_sqp_t<1, true>(c, d, u_cur, s); break;
+            case 2: launch_sqp_t<2, true>(c, d, u_cur, s); break;
+            default: launch_sqp_t<11, true>(c, d, u_cur, s); break;
+        }
+        return;
+    }
     switch (npmax) {
-        case 0: launch_ipm_t<0>(c, d, s); break;
-        case 1: launch_ipm_t<1>(c, d, s); break;
-        case 2: launch_ipm_t<2>(c, d, s); break;
-        default: launch_ipm_t<11>(c, d, s); break;
+        case 0: launch_sqp_t<0, false>(c, d, u_cur, s); break;
+        case 1: launch_sqp_t<1, false>(c, d, u_cur, s); break;
+        case 2: launch_sqp_t<2, false>(c, d, u_cur, s); break;
+        default: launch_sqp_t<11, false>(c, d, u_cur, s); break;
     }
 }
+
+#if MPCC_DOF != 7
+// the mobile build's QP solver (the Panda build's is ipm.hip)
+size_t ipm_lds_bytes(int /*N*/, int /*npmax*/) { return ipm_wide_lds_bytes(); }
+void launch_ipm(const DevConst& c, const DevBuffers& d, int npmax, hipStream_t s) { launch_ipm_wide(c, d, npmax, 0, s); }
 void launch_sqp(const DevConst& c, const DevBuffers& d, const double* u_cur, int npmax, hipStream_t s) {
-    switch (npmax) {
-        case 0: launch_sqp_t<0>(c, d, u_cur, s); break;
-        case 1: launch_sqp_t<1>(c, d, u_cur, s); break;
-        case 2: launch_sqp_t<2>(c, d, u_cur, s); break;
-        default: launch_sqp_t<11>(c, d, u_cur, s); break;
-    }
+    launch_sqp_wide(c, d, u_cur, npmax, c.p.use_BFGS, s);
 }
+#endif
 
 }  // namespace mpcc

@@ -39,11 +39,21 @@ struct DevBuffers {
     const double* nn_env;   // packed W0,b0,...,W4,b4
     // debug: per-instance SQP trace (null unless mpcc_debug_trace_enable), TRACE_W doubles per iteration
     double* dbg_trace;
+    // 32-lane interior point (ipm_wide.hip): workspace [maxB*(N+1)*ISW] — the mobile build's QP solver, and the
+    // damped-BFGS option of either build
+    double* isw;
+    // damped BFGS (use_BFGS, osqp_interface.cpp:437-453, 683-715), per instance, horizon layout [(N+1)][NXU]:
+    // low-rank vectors lr [LRM][(N+1)*NXU] and coefficients lrc [LRM], A^T lambda (glam), grad_L of the previous
+    // iteration (gprev), A^T y of the last QP (aty), step_prev = alpha * step (sp)
+    double *lr, *lrc, *glam, *gprev, *aty, *sp;
 };
 constexpr int TRACE_W = 8, TRACE_IT = 4;  // qp status, ipm iters, obj, vio, accepted, |step|_inf, alpha, alpha*|step|
 
-constexpr int SQI = 8;  // int bookkeeping per instance: status, active, iter, nfilt, qp_status, ipm_iters, reject
+constexpr int SQI = 8;  // int bookkeeping per instance: status, active, iter, nfilt, qp_status, ipm_iters, reject, nlr
 constexpr int SQ_REJECT = 6;
+constexpr int SQ_NLR = 7;  // low-rank BFGS terms held (2 per update)
+constexpr int LRM = 4;     // at most LRM low-rank terms: use_BFGS with max_iter <= 1 + LRM / 2
+constexpr int ISW = 2048;  // doubles per stage of the 32-lane interior point's workspace (64 fields x 32 lanes)
 
 struct NNDesc {
     int L;              // number of layers
@@ -62,6 +72,10 @@ void launch_ipm(const DevConst& c, const DevBuffers& d, int npmax, hipStream_t s
 void launch_soc(const DevConst& c, const DevBuffers& d, const double* u_cur, hipStream_t s);
 // the fused SQP loop (QP solve, line search, step, next QP assembly) after the first k_setqp
 void launch_sqp(const DevConst& c, const DevBuffers& d, const double* u_cur, int npmax, hipStream_t s);
+// the fused SQP loop on the 32-lane interior point (ipm_wide.hip); bfgs = 1: damped BFGS Hessian updates
+void launch_sqp_wide(const DevConst& c, const DevBuffers& d, const double* u_cur, int npmax, int bfgs, hipStream_t s);
+size_t ipm_wide_lds_bytes();
+void launch_ipm_wide(const DevConst& c, const DevBuffers& d, int npmax, int lr, hipStream_t s);
 size_t ipm_lds_bytes(int N, int npmax);
 inline int poly_rows_max(int mask) {
     return ((mask & MPCC_CON_SELFCOL) ? 1 : 0) + ((mask & MPCC_CON_SING) ? 1 : 0) + ((mask & MPCC_CON_ENVCOL) ? 9 : 0);

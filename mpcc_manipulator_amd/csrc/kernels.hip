@@ -78,6 +78,7 @@ __global__ void __launch_bounds__(64) k_prepare(DevConst c, DevBuffers d) {
     si[SQ_NFILT] = 0;
     si[SQ_QPSTAT] = 0;
     si[SQ_IPMIT] = 0;
+    si[SQ_NLR] = 0;
     double* st = d.step + (size_t)b * (N + 1) * NXU;
     for (int i = 0; i < (N + 1) * NXU; i++) st[i] = 0.0;  // step_.setZero (osqp_interface.cpp:404)
 }

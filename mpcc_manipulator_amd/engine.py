@@ -155,6 +155,7 @@ def lib(dof=7):
         "mpcc_debug_spline": (C.c_int, [V, C.c_int, DP, DP, DP, DP, DP, DP]),
         "mpcc_debug_stage_cost": (C.c_int, [V, C.c_int, DP, DP, DP, IP, DP, DP, DP, DP, DP]),
         "mpcc_debug_solve_qp": (C.c_int, [V, C.c_int, DP, DP, DP, DP, IP, IP]),
+        "mpcc_debug_solve_qp_lr": (C.c_int, [V, C.c_int, DP, DP, DP, C.c_int, DP, DP, DP, IP, IP]),
         "mpcc_debug_trace_enable": (C.c_int, [V, C.c_int]),
         "mpcc_debug_workspace": (C.c_int, [V, C.c_int, DP]),
         "mpcc_debug_project": (C.c_int, [V, C.c_int, DP, DP, DP]),
@@ -605,6 +606,22 @@ class Engine:
                "mpcc_debug_solve_qp")
         return step, st, it
 
+    def solve_qp_lr(self, guess, rec, u_cur, lr, lrc):
+        """One QP with low-rank Hessian terms sum_j lrc_j u_j u_j^T (the damped-BFGS QP form, 32-lane solver):
+        lr [nlr, N+1, NXU], lrc [nlr]; the same terms for every instance."""
+        B = guess.shape[0]
+        g = _f64(guess, (B, self.N + 1, self.NXU))
+        r = _f64(rec, (B, self.N + 1, self.REC))
+        u = _f64(u_cur, (B, self.NU))
+        lr = _f64(lr).reshape(-1, self.N + 1, self.NXU)
+        lrc = _f64(lrc).reshape(-1)
+        step = np.zeros((B, self.NXU * self.N + self.NX))
+        st = np.zeros(B, np.int32)
+        it = np.zeros(B, np.int32)
+        self._check(self.L.mpcc_debug_solve_qp_lr(self.h, B, _dp(g), _dp(r), _dp(u), int(lr.shape[0]), _dp(lr), _dp(lrc),
+                                                  _dp(step), _ip(st), _ip(it)), "mpcc_debug_solve_qp_lr")
+        return step, st, it
+
     def project(self, s_guess, ee):
         """projectOnSpline for M (s_guess, ee) pairs (arc_length_spline.cpp:318-379)."""
         sg = _f64(np.atleast_1d(s_guess))
@@ -615,8 +632,8 @@ class Engine:
         return out
 
     def workspace(self, B):
-        """Interior-point workspace of the last solve, [B, N+1, 816] (Panda; 1280 for the mobile build)."""
-        out = np.zeros((B, self.N + 1, 816 if self.dof == 7 else 1280))
+        """Interior-point workspace of the last solve, [B, N+1, 816] (Panda; 2048 for the mobile build)."""
+        out = np.zeros((B, self.N + 1, 816 if self.dof == 7 else 2048))
         self._check(self.L.mpcc_debug_workspace(self.h, B, _dp(out)), "mpcc_debug_workspace")
         return out
 

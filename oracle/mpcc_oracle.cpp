@@ -1534,11 +1534,114 @@ struct Riccati {
     }
 };
 
+// ---------------- damped BFGS (SQPParam use_BFGS, osqp_interface.cpp:437-453, 683-715) ----------------
+// After SQP iteration 0 the reference keeps its QP Hessian and updates it by damped BFGS (setQP is called
+// without the Hessian, :441-442).  Held as the structured Hessian H_0 of iteration 0 plus low-rank terms,
+// B = H_0 + sum_j c_j u_j u_j^T, u_j in the stage layout (y and v parts, w = 0).  The interior point solves
+// with B through the Sherman-Morrison-Woodbury identity around each Riccati solve.
+// Gaussian elimination with partial pivoting of a small n x n system (the Woodbury capacitance matrix)
+static void lu_solve_small(std::vector<double>& A, int n, std::vector<double>& b) {
+    for (int k = 0; k < n; k++) {
+        int p = k;
+        for (int i = k + 1; i < n; i++) if (std::fabs(A[(size_t)i * n + k]) > std::fabs(A[(size_t)p * n + k])) p = i;
+        if (p != k) { for (int j = 0; j < n; j++) std::swap(A[(size_t)k * n + j], A[(size_t)p * n + j]); std::swap(b[k], b[p]); }
+        for (int i = k + 1; i < n; i++) {
+            const double f = A[(size_t)i * n + k] / A[(size_t)k * n + k];
+            for (int j = k; j < n; j++) A[(size_t)i * n + j] -= f * A[(size_t)k * n + j];
+            b[i] -= f * b[k];
+        }
+    }
+    for (int i = n - 1; i >= 0; i--) {
+        double s2 = b[i];
+        for (int j = i + 1; j < n; j++) s2 -= A[(size_t)i * n + j] * b[j];
+        b[i] = s2 / A[(size_t)i * n + i];
+    }
+}
+struct LowRank {
+    std::vector<std::vector<double>> u;  // (N+1)*NZ each
+    std::vector<double> c;
+    int r() const { return (int)c.size(); }
+};
+static double vdot(const std::vector<double>& a, const std::vector<double>& b) {
+    double s = 0;
+    for (size_t i = 0; i < a.size(); i++) s += a[i] * b[i];
+    return s;
+}
+// reference layout [x_0..x_N | u_0..u_{N-1}] <-> stage layout z_k = [y_k | w_k | v_k] (w_k left 0)
+static void dense_to_stage(int N, const double* d, std::vector<double>& z) {
+    z.assign((size_t)(N + 1) * NZ, 0.0);
+    for (int k = 0; k <= N; k++) {
+        for (int a = 0; a < NX; a++) z[(size_t)k * NZ + a] = d[(size_t)NX * k + a];
+        if (k < N)
+            for (int b = 0; b < NU; b++) z[(size_t)k * NZ + NXA + b] = d[(size_t)NX * (N + 1) + NU * k + b];
+    }
+}
+// B s in the reference layout: the stage Hessians act on z_k = [x_k | u_{k-1}[0:DOF] | u_k] (the ddq
+// coupling of u_k and u_{k-1} sits in stage k's (v, w) block), plus the low-rank terms
+static void bfgs_hess_mul(const StructQP& S, const LowRank& lr, const std::vector<double>& sd, std::vector<double>& out) {
+    const int N = S.N;
+    const size_t ou = (size_t)NX * (N + 1);
+    out.assign(sd.size(), 0.0);
+    for (int k = 0; k <= N; k++) {
+        double z[NZ] = {};
+        for (int a = 0; a < NX; a++) z[a] = sd[(size_t)NX * k + a];
+        if (k >= 1)
+            for (int j = 0; j < DOF; j++) z[NX + j] = sd[ou + (size_t)NU * (k - 1) + j];
+        if (k < N)
+            for (int b = 0; b < NU; b++) z[NXA + b] = sd[ou + (size_t)NU * k + b];
+        for (int a = 0; a < NZ; a++) {
+            double t = 0;
+            for (int b = 0; b < NZ; b++) t += S.st[k].H[a * NZ + b] * z[b];
+            if (a < NX) out[(size_t)NX * k + a] += t;
+            else if (a < NXA) { if (k >= 1) out[ou + (size_t)NU * (k - 1) + (a - NX)] += t; }
+            else if (k < N) out[ou + (size_t)NU * k + (a - NXA)] += t;
+        }
+    }
+    std::vector<double> ud;
+    for (int j = 0; j < lr.r(); j++) {  // + c_j u_j (u_j^T s), u_j back in the reference layout
+        ud.assign(sd.size(), 0.0);
+        for (int k = 0; k <= N; k++) {
+            for (int a = 0; a < NX; a++) ud[(size_t)NX * k + a] = lr.u[j][(size_t)k * NZ + a];
+            if (k < N)
+                for (int b = 0; b < NU; b++) ud[ou + (size_t)NU * k + b] = lr.u[j][(size_t)k * NZ + NXA + b];
+        }
+        const double f = lr.c[j] * vdot(ud, sd);
+        for (size_t i = 0; i < sd.size(); i++) out[i] += f * ud[i];
+    }
+}
+// BFGSUpdate (osqp_interface.cpp:683-715): B' = B - Bs Bs^T / sBs + r r^T / sr (damped; unchanged if
+// sr < eps).  Returns false if the update makes the Hessian NaN (sBs = 0 with sr >= eps, as the reference's
+// division would), which the caller reports as NAN_HESSIAN (isNan, :474-477).
+static bool bfgs_update(const StructQP& S0, LowRank& lr, const std::vector<double>& sp, const std::vector<double>& dg) {
+    const int N = S0.N;
+    std::vector<double> Bs;
+    bfgs_hess_mul(S0, lr, sp, Bs);
+    const double sBs = vdot(sp, Bs), sy = vdot(sp, dg);
+    std::vector<double> r(sp.size());
+    double sr;
+    if (sy < 0.2 * sBs) {
+        const double theta = 0.8 * sBs / (sBs - sy);
+        for (size_t i = 0; i < r.size(); i++) r[i] = theta * dg[i] + (1 - theta) * Bs[i];
+        sr = theta * sy + (1 - theta) * sBs;
+    } else {
+        r = dg;
+        sr = sy;
+    }
+    if (sr < std::numeric_limits<double>::epsilon()) return true;
+    if (!(sBs != 0.0) || !std::isfinite(sBs) || !std::isfinite(sr)) return false;
+    std::vector<double> zs;
+    dense_to_stage(N, Bs.data(), zs);
+    lr.u.push_back(zs); lr.c.push_back(-1.0 / sBs);
+    dense_to_stage(N, r.data(), zs);
+    lr.u.push_back(zs); lr.c.push_back(1.0 / sr);
+    return true;
+}
+
 // Returns 0 on success (step filled in reference layout: [y_0..y_N | v_0..v_{N-1}]), else Status.
 static const bool g_ipm_debug = std::getenv("MPCC_ORACLE_IPM_DEBUG") != nullptr;  // per-iteration log (debug)
 
 static int solve_struct_ipm_from(const StructQP& S, std::vector<double>& step, int* iters_out, double s_floor,
-                                 double lam_scale, int max_it) {
+                                 double lam_scale, int max_it, const LowRank* lr = nullptr) {
     const int N = S.N;
     if (S.infeasible) return QP_PrimalInfeasible;
     std::vector<Ineq> I;
@@ -1612,6 +1715,11 @@ static int solve_struct_ipm_from(const StructQP& S, std::vector<double>& step, i
                 gs[(size_t)k * NZ + a] = s + S.st[k].h[a];
             }
         }
+        if (lr)  // + sum_j c_j u_j (u_j^T z)
+            for (int j = 0; j < lr->r(); j++) {
+                const double f = lr->c[j] * vdot(lr->u[j], z);
+                for (size_t a = 0; a < gs.size(); a++) gs[a] += f * lr->u[j][a];
+            }
         for (int i = 0; i < m; i++) {
             const SRow& row = S.st[I[i].k].rows[I[i].row];
             double* H = &Hs[(size_t)I[i].k * NZ * NZ];
@@ -1626,6 +1734,26 @@ static int solve_struct_ipm_from(const StructQP& S, std::vector<double>& step, i
             if (it > 0 && mu < IPM_TOL_FB && rpmax < IPM_TOL_FB) conv = true;
             break;
         }
+        // low-rank Hessian terms (BFGS): Q_j = M u_j = -solve(u_j), Smat = C^-1 + U^T Q; every Riccati solve
+        // dz_s = -M g is corrected to -(M - Q Smat^-1 Q^T) g = dz_s - Q Smat^-1 (U^T dz_s)
+        const int nr = lr ? lr->r() : 0;
+        std::vector<std::vector<double>> Q(nr);
+        std::vector<double> Smat((size_t)nr * nr);
+        for (int j = 0; j < nr; j++) {
+            R.solve(S, lr->u[j], Q[j]);
+            for (double& v : Q[j]) v = -v;
+        }
+        for (int i = 0; i < nr; i++)
+            for (int j = 0; j < nr; j++) Smat[(size_t)i * nr + j] = (i == j ? 1.0 / lr->c[i] : 0.0) + vdot(lr->u[i], Q[j]);
+        auto lr_solve = [&](const std::vector<double>& g, std::vector<double>& d) {
+            R.solve(S, g, d);
+            if (!nr) return;
+            std::vector<double> t(nr), Mc = Smat;
+            for (int j = 0; j < nr; j++) t[j] = vdot(lr->u[j], d);
+            lu_solve_small(Mc, nr, t);
+            for (int j = 0; j < nr; j++)
+                for (size_t a = 0; a < d.size(); a++) d[a] -= t[j] * Q[j][a];
+        };
         std::vector<double> g0 = gs;
         auto add_rows = [&](std::vector<double>& g, const std::vector<double>& coef) {
             for (int i = 0; i < m; i++) {
@@ -1654,7 +1782,7 @@ static int solve_struct_ipm_from(const StructQP& S, std::vector<double>& step, i
         std::vector<double> coef(m);
         for (int i = 0; i < m; i++) { rc[i] = sl[i] * lam[i]; coef[i] = lam[i] + W[i] * rp[i] - rc[i] / sl[i]; }
         gs = g0; add_rows(gs, coef);
-        R.solve(S, gs, dza);
+        lr_solve(gs, dza);
         recover(dza, dsa, dla);
         double aa = max_step(dsa, dla, 1.0);
         double mua = 0;
@@ -1664,13 +1792,23 @@ static int solve_struct_ipm_from(const StructQP& S, std::vector<double>& step, i
         // corrector
         for (int i = 0; i < m; i++) { rc[i] = sl[i] * lam[i] + dsa[i] * dla[i] - sigma * mu; coef[i] = lam[i] + W[i] * rp[i] - rc[i] / sl[i]; }
         gs = g0; add_rows(gs, coef);
-        R.solve(S, gs, dz);
+        lr_solve(gs, dz);
         recover(dz, ds, dl);
         // fraction to the boundary: tau = max(0.995, 1 - sqrt(mu)) lets the step approach the boundary as
         // mu -> 0 (superlinear final phase; 10.4 -> 9.2 mean IPM iterations on the configs[1] workload,
         // DESIGN.md §3.2); k_ipm applies the same rule
         const double tau = std::max(IPM_TAU, 1.0 - std::sqrt(mu));
         double a = std::min(1.0, tau * max_step(ds, dl, 1e30));
+        if (g_ipm_debug) {
+            double uz0 = 0, t0 = 0, S0 = 0;
+            if (nr) {
+                uz0 = vdot(lr->u[0], z);
+                S0 = Smat[0];
+            }
+            std::fprintf(stderr, "orc it %2d mu %.6e amax %.6e sig %.6e alpha %.6e uz0 %.9e S0 %.9e\n", it, mu, aa, sigma, a,
+                         uz0, S0);
+            (void)t0;
+        }
         double dzmax = 0;
         for (size_t i = 0; i < z.size(); i++) { z[i] += a * dz[i]; dzmax = std::max(dzmax, std::fabs(dz[i])); }
         for (int i = 0; i < m; i++) { sl[i] += a * ds[i]; lam[i] += a * dl[i]; }
@@ -1699,10 +1837,10 @@ static int solve_struct_ipm_from(const StructQP& S, std::vector<double>& step, i
 // converging QP ends on (~1e-12), never a failure into a different failure.
 constexpr double IPM_S0 = 0.02, IPM_L0 = 0.002;
 constexpr int IPM_MAX_IT_SCALED = 30;
-static int solve_struct_ipm(const StructQP& S, std::vector<double>& step, int* iters_out) {
+static int solve_struct_ipm(const StructQP& S, std::vector<double>& step, int* iters_out, const LowRank* lr = nullptr) {
     int it1 = 0, it2 = 0;
-    int rc = solve_struct_ipm_from(S, step, &it1, IPM_S0, IPM_L0, IPM_MAX_IT_SCALED);
-    if (rc != 0) rc = solve_struct_ipm_from(S, step, &it2, 1.0, 0.0, IPM_MAX_IT);
+    int rc = solve_struct_ipm_from(S, step, &it1, IPM_S0, IPM_L0, IPM_MAX_IT_SCALED, lr);
+    if (rc != 0) rc = solve_struct_ipm_from(S, step, &it2, 1.0, 0.0, IPM_MAX_IT, lr);
     if (iters_out) *iters_out = it1 + it2;
     return rc;
 }
@@ -1882,7 +2020,7 @@ static int soc_dense(const Oracle& o, const DenseQP& q, const double* guess, con
     return solve_dense_ipm(qc, out, iters);
 }
 static int soc_struct(const Oracle& o, const StructQP& S, const double* guess, const double* recs, const double* ucur,
-                      const std::vector<double>& step, std::vector<double>& out, int* iters) {
+                      const std::vector<double>& step, std::vector<double>& out, int* iters, const LowRank* lr = nullptr) {
     std::vector<double> xs;
     soc_point(o, guess, step, xs);
     StructQP S2;
@@ -1891,7 +2029,7 @@ static int soc_struct(const Oracle& o, const StructQP& S, const double* guess, c
         std::memcpy(S2.st[k].H, S.st[k].H, sizeof S.st[k].H);
         std::memcpy(S2.st[k].h, S.st[k].h, sizeof S.st[k].h);
     }
-    return solve_struct_ipm(S2, out, iters);
+    return solve_struct_ipm(S2, out, iters, lr);
 }
 
 static int solve_ocp(const Oracle& o, double* guess, const double* recs, const double* ucur, double* opt_sol, int* iters_out) {
@@ -1906,12 +2044,48 @@ static int solve_ocp(const Oracle& o, double* guess, const double* recs, const d
     bool status_set = false;
     int it;
     std::vector<double> trial((size_t)(N + 1) * NXU);
+    // damped BFGS state (use_BFGS, osqp_interface.cpp:403-453, 540-555): Hessian of iteration 0 (H0 / P0) and
+    // its low-rank updates, grad_L_prev, A^T lambda and step_prev = alpha * step, all normalized, in the
+    // reference layout.  A^T y of an exact QP solution is -(B step + q) (its KKT stationarity), so the
+    // multiplier update lambda += alpha (y - lambda) is carried as A^T lambda (the constraint Jacobian does
+    // not change within a solve: frozen records, Q4) — DESIGN.md §4.2.
+    const bool bfgs = p.use_BFGS != 0;
+    LowRank lr;
+    StructQP S0;
+    std::vector<double> P0, grad_L_prev(nv, 0.0), g_lam(nv, 0.0), step_prev(nv, 0.0), qd(nv, 0.0);
+    bool bfgs_nan = false;
+    auto bfgs_grad = [&](int iter) {  // grad_L = q + A^T lambda; Hess_ = BFGSUpdate(Hess_, step_prev, dgrad_L)
+        std::vector<double> gl(nv);
+        for (int i = 0; i < nv; i++) gl[i] = qd[i] + g_lam[i];
+        if (iter > 0) {
+            std::vector<double> dg(nv);
+            for (int i = 0; i < nv; i++) dg[i] = gl[i] - grad_L_prev[i];
+            if (!bfgs_update(S0, lr, step_prev, dg)) bfgs_nan = true;
+        }
+        grad_L_prev = gl;
+    };
     for (it = 0; it < p.max_iter; it++) {
         // setQP + PD / NaN checks of the normalized Hessian (:445-473)
         bool nan = false, pd = true;
         if (o.opt.qp_mode == 1) {
             DenseQP q;
             set_qp(o, guess, recs, ucur, true, q);
+            if (bfgs) {  // dense form of the same BFGS matrix: P0 + sum_j c_j u_j u_j^T
+                if (it == 0) { P0 = q.P; build_struct_qp(o, guess, recs, ucur, S0); }
+                qd = q.g;
+                bfgs_grad(it);
+                q.P = P0;
+                std::vector<double> ud(nv);
+                for (int j = 0; j < lr.r(); j++) {
+                    for (int k = 0; k <= N; k++) {
+                        for (int a = 0; a < NX; a++) ud[(size_t)NX * k + a] = lr.u[j][(size_t)k * NZ + a];
+                        if (k < N) for (int b = 0; b < NU; b++) ud[(size_t)NX * (N + 1) + NU * k + b] = lr.u[j][(size_t)k * NZ + NXA + b];
+                    }
+                    for (int a = 0; a < nv; a++)
+                        for (int b = 0; b < nv; b++) q.P[(size_t)a * nv + b] += lr.c[j] * ud[a] * ud[b];
+                }
+                if (bfgs_nan) q.P[0] = std::numeric_limits<double>::quiet_NaN();
+            }
             for (double v : q.P) if (std::isnan(v)) nan = true;
             std::vector<double> Pc = q.P;
             // Eigen LLT semantics: fails only on pivot <= 0 (NaN pivots pass)
@@ -1939,9 +2113,28 @@ static int solve_ocp(const Oracle& o, double* guess, const double* recs, const d
                 const int ss = soc_dense(o, q, guess, recs, ucur, step, st, &sit);
                 if (ss == 0) step = st; else { status = ss; status_set = true; }
             }
+            if (bfgs) {  // A^T y = -(B step + q) of the QP just solved (dense product)
+                std::vector<double> Bs(nv, 0.0);
+                for (int a = 0; a < nv; a++) {
+                    double t = 0;
+                    for (int b = 0; b < nv; b++) t += q.P[(size_t)a * nv + b] * step[b];
+                    Bs[a] = t;
+                }
+                for (int i = 0; i < nv; i++) qd[i] = -(Bs[i] + q.g[i]);  // reused below as A^T y
+            }
         } else {
             StructQP S;
             build_struct_qp(o, guess, recs, ucur, S);
+            if (bfgs) {  // the QP keeps the Hessian of iteration 0 (setQP without Hess_, :441-442)
+                if (it == 0) S0 = S;
+                else for (int k = 0; k <= N; k++) std::memcpy(S.st[k].H, S0.st[k].H, sizeof S.st[k].H);
+                for (int k = 0; k <= N; k++) {
+                    for (int a = 0; a < NX; a++) qd[(size_t)NX * k + a] = S.st[k].h[a];
+                    if (k < N) for (int b = 0; b < NU; b++) qd[(size_t)NX * (N + 1) + NU * k + b] = S.st[k].h[NXA + b];
+                }
+                bfgs_grad(it);
+                if (bfgs_nan) nan = true;
+            }
             // PD check on the block structure: state blocks and the per-component tridiagonal input blocks
             for (int k = 0; k <= N && pd; k++) {
                 double Q[NX * NX];
@@ -1975,13 +2168,18 @@ static int solve_ocp(const Oracle& o, double* guess, const double* recs, const d
             if (nan) { status = NAN_HESSIAN; status_set = true; break; }
             std::vector<double> st;
             int qit = 0;
-            int qs = solve_struct_ipm(S, st, &qit);
+            int qs = solve_struct_ipm(S, st, &qit, bfgs ? &lr : nullptr);
             if (g_trace && it < 4) { g_trace[8 * it] = qs; g_trace[8 * it + 1] = qit; }
             if (qs == 0) step = st; else { status = qs; status_set = true; }
             if (p.do_SOC) {  // :506-535
                 int sit = 0;
-                const int ss = soc_struct(o, S, guess, recs, ucur, step, st, &sit);
+                const int ss = soc_struct(o, S, guess, recs, ucur, step, st, &sit, bfgs ? &lr : nullptr);
                 if (ss == 0) step = st; else { status = ss; status_set = true; }
+            }
+            if (bfgs) {  // A^T y = -(B step + q)
+                std::vector<double> Bs;
+                bfgs_hess_mul(S0, lr, step, Bs);
+                for (int i = 0; i < nv; i++) qd[i] = -(Bs[i] + qd[i]);
             }
         }
         // filterLineSearch :759-808
@@ -2008,6 +2206,12 @@ static int solve_ocp(const Oracle& o, double* guess, const double* recs, const d
             }
         }
         // take step :549-551
+        if (bfgs) {  // lambda += alpha (y - lambda) as A^T lambda; step_prev = alpha step (:550-555)
+            for (int i = 0; i < nv; i++) {
+                g_lam[i] = g_lam[i] + alpha * (qd[i] - g_lam[i]);
+                step_prev[i] = alpha * step[i];
+            }
+        }
         denorm_add(o, guess, step, alpha, trial.data());
         std::memcpy(guess, trial.data(), sizeof(double) * (N + 1) * NXU);
         double nrm = 0;
@@ -2181,6 +2385,43 @@ int oracle_solve_qp(void* h, int mode, const double* guess, const double* recs, 
         StructQP S;
         build_struct_qp(*o, guess, recs, u_current, S);
         rc = solve_struct_ipm(S, st, iters);
+    }
+    if (rc == 0) std::memcpy(step, st.data(), st.size() * 8);
+    return rc;
+}
+// One QP with low-rank Hessian terms B = H + sum_j lrc_j u_j u_j^T (u_j in the horizon layout [(N+1)][x | u],
+// u_N = 0): the damped-BFGS QP form.  mode 0: Riccati + Woodbury, 1: dense Hessian.
+int oracle_solve_qp_lr(void* h, int mode, const double* guess, const double* recs, const double* u_current, int nlr,
+                       const double* lr, const double* lrc, double* step, int* iters) {
+    Oracle* o = (Oracle*)h;
+    const int N = o->N(), nv = o->nvar();
+    std::vector<double> st;
+    int rc;
+    std::vector<std::vector<double>> ud(nlr, std::vector<double>(nv, 0.0));
+    for (int j = 0; j < nlr; j++)
+        for (int k = 0; k <= N; k++) {
+            for (int a = 0; a < NX; a++) ud[j][(size_t)NX * k + a] = lr[((size_t)j * (N + 1) + k) * NXU + a];
+            if (k < N)
+                for (int b = 0; b < NU; b++) ud[j][(size_t)NX * (N + 1) + NU * k + b] = lr[((size_t)j * (N + 1) + k) * NXU + NX + b];
+        }
+    if (mode == 1) {
+        DenseQP q;
+        set_qp(*o, guess, recs, u_current, true, q);
+        for (int j = 0; j < nlr; j++)
+            for (int a = 0; a < nv; a++)
+                for (int b = 0; b < nv; b++) q.P[(size_t)a * nv + b] += lrc[j] * ud[j][a] * ud[j][b];
+        rc = solve_dense_ipm(q, st, iters);
+    } else {
+        StructQP S;
+        build_struct_qp(*o, guess, recs, u_current, S);
+        LowRank L;
+        for (int j = 0; j < nlr; j++) {
+            std::vector<double> z;
+            dense_to_stage(N, ud[j].data(), z);
+            L.u.push_back(z);
+            L.c.push_back(lrc[j]);
+        }
+        rc = solve_struct_ipm(S, st, iters, &L);
     }
     if (rc == 0) std::memcpy(step, st.data(), st.size() * 8);
     return rc;

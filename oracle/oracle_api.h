@@ -102,6 +102,9 @@ double oracle_dense_qp(void* h, const double* guess, const double* recs, const d
  * (0 ok, else Status code).  iters = IPM iterations used. */
 int    oracle_solve_qp(void* h, int mode, const double* guess, const double* recs, const double* u_current,
                        double* step, int* iters);
+/* one QP with low-rank Hessian terms sum_j lrc_j u_j u_j^T (u_j [(N+1)*NXU] horizon layout; damped-BFGS form) */
+int    oracle_solve_qp_lr(void* h, int mode, const double* guess, const double* recs, const double* u_current, int nlr,
+                          const double* lr, const double* lrc, double* step, int* iters);
 /* SecondOrderCorrection QP (osqp_interface.cpp:658-681) after the first step step_in [nv]: same P, q, A,
  * bounds at guess + step_in shifted by A step_in; step_out [nv]; returns status. */
 int    oracle_solve_soc(void* h, int mode, const double* guess, const double* recs, const double* u_current,

@@ -97,6 +97,8 @@ def lib(dof=7):
         L.oracle_dense_qp.argtypes = [C.c_void_p, DP, DP, DP, DP, DP, DP, DP, DP, DP]
         L.oracle_solve_qp.restype = C.c_int
         L.oracle_solve_qp.argtypes = [C.c_void_p, C.c_int, DP, DP, DP, DP, IP]
+        L.oracle_solve_qp_lr.restype = C.c_int
+        L.oracle_solve_qp_lr.argtypes = [C.c_void_p, C.c_int, DP, DP, DP, C.c_int, DP, DP, DP, IP]
         L.oracle_solve_soc.restype = C.c_int
         L.oracle_solve_soc.argtypes = [C.c_void_p, C.c_int, DP, DP, DP, DP, DP, IP]
         L.oracle_rk4.argtypes = [DP, DP, D, DP]
@@ -276,6 +278,16 @@ class Oracle:
         rc = self.L.oracle_solve_qp(self.h, int(mode), _dp(_f64(guess)), _dp(_f64(recs)),
                                     _dp(_f64(u_current)), _dp(step), _ip(it))
         return rc, step, int(it[0])
+
+    def solve_qp_lr(self, guess, recs, u_current, lr, lrc, mode=0):
+        """One QP with low-rank Hessian terms (the damped-BFGS form): lr [nlr, N+1, NXU], lrc [nlr]."""
+        lr = _f64(lr).reshape(-1, self.N + 1, self.NXU)
+        lrc = _f64(lrc).reshape(-1)
+        step = np.zeros(self.nvar())
+        it = C.c_int(0)
+        rc = self.L.oracle_solve_qp_lr(self.h, int(mode), _dp(_f64(guess)), _dp(_f64(recs)), _dp(_f64(u_current)),
+                                       int(lr.shape[0]), _dp(lr), _dp(lrc), _dp(step), C.byref(it))
+        return rc, step, it.value
 
     def solve_soc(self, guess, recs, u_current, step, mode=0):
         """SecondOrderCorrection QP (osqp_interface.cpp:658-681) after the first QP's step."""

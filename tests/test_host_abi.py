@@ -126,14 +126,24 @@ def test_engine_fails_loudly_without_gpu(built_lib):
         m.Engine(params, max_batch=4, constraint_mask=2)
 
 
-def test_bfgs_rejected(built_lib):
-    """Damped BFGS (osqp_interface.cpp:683-715) makes the Hessian dense across stages, outside the
-    stage-structured interior point: enabling it is an error raised before any device work, never a
-    silent fallback to plain SQP."""
+def test_bfgs_max_iter_bound(built_lib):
+    """Damped BFGS (osqp_interface.cpp:683-715) is held as the iteration-0 Hessian plus 2 low-rank terms per
+    update, at most LRM = 4 terms: max_iter > 3 with use_BFGS is an error raised before any
+    device work, never a silent fallback to plain SQP."""
     import mpcc_manipulator_amd as m
-    params = m.load_params(N=20, overrides={"sqp": {"use_BFGS": 1.0}})
-    with pytest.raises(m.MpccError, match="not supported"):
+    params = m.load_params(N=20, overrides={"sqp": {"use_BFGS": 1.0, "max_iter": 4}})
+    with pytest.raises(m.MpccError, match="max_iter"):
         m.Engine(params, max_batch=4, constraint_mask=2)
+
+
+@pytest.mark.skipif(torch.cuda.is_available(), reason="checks the no-GPU failure path")
+def test_bfgs_passes_validation(built_lib):
+    import mpcc_manipulator_amd as m
+    params = m.load_params(N=20, overrides={"sqp": {"use_BFGS": 1.0, "max_iter": 3}})
+    assert params.use_BFGS == 1
+    with pytest.raises(m.MpccError) as e:
+        m.Engine(params, max_batch=4, constraint_mask=2)
+    assert "max_iter" not in str(e.value)
 
 
 @pytest.mark.skipif(torch.cuda.is_available(), reason="checks the no-GPU failure path")

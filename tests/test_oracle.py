@@ -310,6 +310,33 @@ def test_soc_closed_loop_layouts_agree(oracle_lib):
         x[0] = o0.sim_time_step(xs[0][0], u[0], P["Ts"])
 
 
+def test_bfgs_layouts_agree(oracle_lib):
+    """Damped BFGS (use_BFGS, osqp_interface.cpp:437-453, 683-715) through runMPC_ with 3 SQP iterations on
+    cold-started controllers (every one takes a BFGS-updated second QP): the structured oracle (iteration-0
+    Riccati Hessian + Woodbury low-rank terms, A^T y = -(B s + q)) and the dense-layout oracle (the reference's
+    dense Hessian_ updated in place) take the same statuses and inputs, and the update changes the result."""
+    from helpers import batch_from_pool, oracle_pool
+    ov = {"sqp": {"max_iter": 3, "use_BFGS": 1}}
+    (o0, P, track), (o1, _, _) = (make_oracle(N=12, max_iter=3, mask=7, qp_mode=m, overrides=ov, nthreads=8)
+                                  for m in (0, 1))
+    assert P["use_BFGS"] == 1
+    ob, _, _ = make_oracle(N=12, max_iter=3, mask=7, overrides={"sqp": {"max_iter": 3}}, nthreads=8)
+    pool = oracle_pool(ob, 40, obs=(0.48, 0.218, 0.521, 5.0))
+    B = 24
+    rng = np.random.default_rng(SEED + 23)
+    x0, u0, obs, g, v, f = batch_from_pool(pool, B, rng, obs=np.tile([0.48, 0.218, 0.521, 5.0], (B, 1)))
+    v[:] = 0  # cold starts: generateNewInitialGuess, two or more SQP iterations
+    outs = [o.run_mpc(x0.copy(), u0, obs, g.copy(), v.copy(), f.copy(), trace=True) for o in (o0, o1, ob)]
+    assert np.array_equal(outs[0]["status"], outs[1]["status"])
+    assert np.all(outs[0]["sqp_iters"] >= 1)
+    # compare where both layouts' QP solves succeeded alike (the dense-layout LU interior point can stall at
+    # its 60-iteration cap on a BFGS-updated Hessian that the Riccati + Woodbury solve handles)
+    same = np.all(outs[0]["trace"][:, :, 0] == outs[1]["trace"][:, :, 0], axis=1)
+    assert same.mean() >= 0.8, same
+    assert np.abs(outs[0]["horizon"][same] - outs[1]["horizon"][same]).max() <= 1e-8
+    assert np.abs(outs[0]["horizon"] - outs[2]["horizon"]).max() > 1e-6  # BFGS is live
+
+
 def test_params_resolution(oracle_lib):
     """Params/*.json with the reference's override semantics: T_x/T_u (normalization.json:3-20)."""
     P = rp.resolve(N=20)
