@@ -58,6 +58,7 @@ struct mpcc_engine {
     // SQP loop: fused per-instance kernel k_sqp (default) or one launch per stage of each iteration
     // (MPCC_STAGED_SQP=1; same arithmetic, kept for A/B timing and debugging)
     bool staged_sqp = false;
+    bool wide_sqp = false;  // MPCC_WIDE_SQP=1: the 32-lane fused kernel for the Panda build too (experiment)
     mpcc_params params{};
     int N = 0, maxB = 0;
     hipStream_t stream = nullptr;
@@ -362,7 +363,7 @@ void run_batch(mpcc_engine* e, int B, hipStream_t st, mpcc_timing* timing, bool 
         if (tm) a0 = mark();
         launch_setqp(c, d, ucur, st);
         if (tm) a1 = mark();
-        if (c.p.use_BFGS) launch_sqp_wide(c, d, ucur, poly_rows_max(c.p.constraint_mask), 1, st);
+        if (c.p.use_BFGS || e->wide_sqp) launch_sqp_wide(c, d, ucur, poly_rows_max(c.p.constraint_mask), c.p.use_BFGS ? 1 : 0, st);
         else launch_sqp(c, d, ucur, poly_rows_max(c.p.constraint_mask), st);
         if (tm) {
             b1 = mark();
@@ -467,6 +468,8 @@ int mpcc_create(const mpcc_config* cfg, const mpcc_params* params, const char* n
         e->cfg = *cfg;
         const char* st = std::getenv("MPCC_STAGED_SQP");
         e->staged_sqp = st && st[0] == '1';
+        const char* wd = std::getenv("MPCC_WIDE_SQP");
+        e->wide_sqp = wd && wd[0] == '1';
         e->params = *params;
         e->params.N = cfg->N;
         e->params.Ts = cfg->Ts;
@@ -497,7 +500,7 @@ int mpcc_create(const mpcc_config* cfg, const mpcc_params* params, const char* n
         HIPCHK(hipMemset(d.fails, 0, B * sizeof(int32_t)));
         HIPCHK(hipMemset(d.sqi, 0, B * SQI * sizeof(int32_t)));
         if (DOF != 7) d.isw = d.is;  // the mobile build's interior point is the 32-lane one
-        if (e->params.use_BFGS) e->ensure_bfgs_buffers();
+        if (e->params.use_BFGS || e->wide_sqp) e->ensure_bfgs_buffers();
         e->s_x0 = dmalloc<double>(B * NX);
         e->s_u0 = dmalloc<double>(B * NU);
         e->s_obs = dmalloc<double>(B * 4);
