@@ -20,6 +20,9 @@ template <int n> __device__ __forceinline__ double from_up(double v) { return dp
 template <int n> __device__ __forceinline__ double from_down(double v) { return dpp_d<0x110 + n>(v); } // row_shr: lane t <- t-n
 template <int n> __device__ __forceinline__ double rot16(double v) { return dpp_d<0x120 + n>(v); }     // row_ror
 template <int n> __device__ __forceinline__ double bc(double v) { return dpp_d<0x150 + n>(v); }        // row_newbcast: lane n
+__device__ __forceinline__ double half_mirror(double v) { return dpp_d<0x141>(v); }  // lane j <- 7 - j in each 8-lane half
+__device__ __forceinline__ double quad_swap2(double v) { return dpp_d<0x4E>(v); }   // quad_perm [2,3,0,1]: lane j <- j ^ 2
+__device__ __forceinline__ double quad_swap1(double v) { return dpp_d<0xB1>(v); }   // quad_perm [1,0,3,2]: lane j <- j ^ 1
 // lane n of the row for an n that is a constant after unrolling
 __device__ __forceinline__ double bcn(double v, int n) {
     switch (n) {

@@ -57,8 +57,7 @@ enum : int {
     WF_AX, WF_AV,                                 // predictor step
     WF_GX, WF_GV,                                 // objective gradient H z + h
     WF_KFF,                                       // kff (lanes 0..7)
-    WF_KC,                                        // 8 fields: K column layout, field i lane c = K[i][c]
-    WF_KR = WF_KC + 8,                            // 8 fields: K row halves, field m: lane i -> K[i][m], lane 8+i -> K[i][8+m]
+    WF_KR,                                        // 8 fields: K row halves, field m: lane i -> K[i][m], lane 8+i -> K[i][8+m]
     WF_FI = WF_KR + 8,                            // 4 fields: F^-1 row halves, field m: lane i -> Fi[i][m], lane 8+i -> Fi[i][4+m]
     NWF = WF_FI + 4
 };
@@ -387,9 +386,9 @@ __device__ __forceinline__ void ipm_group(const DevConst& c, const DevBuffers& d
         load_common(k, o);
         o.x0 = *ws(k, WF_AX); o.x1 = *ws(k, WF_AV); o.x2 = *ws(k, WF_GX); o.x3 = *ws(k, WF_GV);
 #pragma unroll
-        for (int i = 0; i < 8; i++) {
-            const double v = *ws(k, WF_KC + i);
-            o.m[i] = (k < N) ? v : 0.0;
+        for (int m = 0; m < 8; m++) {
+            const double v = *ws(k, WF_KR + m);
+            o.m[m] = (k < N) ? v : 0.0;
         }
 #pragma unroll
         for (int m = 0; m < 4; m++) {
@@ -692,7 +691,6 @@ __device__ __forceinline__ void ipm_group(const DevConst& c, const DevBuffers& d
                 for (int i = 0; i < 8; i++) {
                     S[L_U + i * 16 + t] = u[i];
                     S[L_K + i * 16 + t] = kc[i];
-                    *ws(k, WF_KC + i) = kc[i];
                 }
                 *ws(k, WF_KFF) = (t < 8) ? kff : 0.0;
 #pragma unroll
@@ -851,9 +849,24 @@ __device__ __forceinline__ void ipm_group(const DevConst& c, const DevBuffers& d
                     atp = mt * pv;
                     if (t == 8) atp += m78 * p7;
                 }
-                double ktf = 0.0;
+                // K^T f from the K row halves: column sums over each 8-lane half by a transpose-reduce
+                // butterfly (lane j <-> 7-j, j^2, j^1); lane c ends with column c (c < 8) or 8 + (c & 7)
+                const double f8 = rot16<8>(fv);  // lane 8+i <- f_i (unconditional: DPP in uniform control flow)
+                const double fh = (t < 8) ? fv : f8;
+                double r1[4], r2[2];
 #pragma unroll
-                for (int i = 0; i < 8; i++) ktf += cur.m[i] * fb[i];
+                for (int q = 0; q < 4; q++) {
+                    const bool lo = (t & 4) == 0;
+                    const double a0 = cur.m[q] * fh, a1 = cur.m[4 + q] * fh;
+                    r1[q] = (lo ? a0 : a1) + half_mirror(lo ? a1 : a0);
+                }
+#pragma unroll
+                for (int q = 0; q < 2; q++) {
+                    const bool lo = (t & 2) == 0;
+                    r2[q] = (lo ? r1[q] : r1[2 + q]) + quad_swap2(lo ? r1[2 + q] : r1[q]);
+                }
+                const bool lo1 = (t & 1) == 0;
+                const double ktf = (lo1 ? r2[0] : r2[1]) + quad_swap1(lo1 ? r2[1] : r2[0]);
                 pv = gx + atp + ktf;
             });
             PMARK(4);

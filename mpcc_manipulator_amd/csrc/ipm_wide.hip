@@ -801,7 +801,8 @@ __device__ __forceinline__ void ipm_group(const DevConst& c, const DevBuffers& d
 #pragma unroll
                         for (int p = 0; p < NPM; p++) {
                             const bool live = (double)p < cur.np && k < N;
-                            const double Wp = live ? bch(hw, p) : zero;
+                            const double wpb = bch(hw, p);  // DPP outside the select
+                            const double Wp = live ? wpb : zero;
                             const Halves ha = halves(cur.pa[p]);
 #pragma unroll
                             for (int a = 0; a < DOF; a++) {
