@@ -141,3 +141,24 @@ def test_bfgs_mobile_parity(built_lib, oracle_lib):
     assert np.sum(outo["sqp_iters"] >= 1) >= B // 6
     assert np.abs(outg["horizon"] - outo["horizon"]).max() <= 1e-6
     eng.close()
+
+
+def test_bfgs_with_soc_parity(built_lib, oracle_lib):
+    """Both SQP variants at once (use_BFGS and do_SOC): the correction QP keeps the BFGS Hessian, and the
+    multiplier estimate comes from whichever QP produced the step (osqp_interface.cpp:506-555)."""
+    import mpcc_manipulator_amd as m
+    ov = {"sqp": {"max_iter": 3, "use_BFGS": 1, "do_SOC": 1}}
+    o, P, track = make_oracle(N=20, max_iter=3, mask=2, overrides=ov, nthreads=16)
+    assert P["use_BFGS"] == 1 and P["do_SOC"] == 1
+    pool = oracle_pool(o, 80)
+    B = 256
+    rng = np.random.default_rng(SEED + 740)
+    x0, u0, obs, guess, valid, fails = batch_from_pool(pool, B, rng)
+    valid[::4] = 0
+    eng = m.Engine(m.load_params(N=20, overrides=ov), max_batch=B, constraint_mask=2)
+    eng.set_track(*track)
+    xg, outg, stats, outo = _run(m, eng, o, x0, u0, obs, guess, valid, fails)
+    assert np.array_equal(outg["status"], outo["status"])
+    assert np.array_equal(stats["sqp_iter"], outo["sqp_iters"])
+    assert np.abs(outg["horizon"] - outo["horizon"]).max() <= 1e-6
+    eng.close()
