@@ -374,27 +374,17 @@ __device__ __forceinline__ void ipm_group(const DevConst& c, const DevBuffers& d
     auto load_fwd = [&](int k, In& o, bool corr) {
         load_common(k, o);
 #pragma unroll
-        for (int m = 0; m < 8; m++) {
-            const double v = *ws(k, WF_KR + m);
-            o.m[m] = (k < N) ? v : 0.0;
-        }
-        const double kf = *ws(k, WF_KFF);
-        o.m[8] = (k < N) ? kf : 0.0;
+        for (int m = 0; m < 8; m++) o.m[m] = *ws(k, WF_KR + m);  // zero at k = N (factor sweep)
+        o.m[8] = *ws(k, WF_KFF);
         if (corr) { o.x0 = *ws(k, WF_AX); o.x1 = *ws(k, WF_AV); } else { o.x0 = o.x1 = 0.0; }  // corr: constant
     };
     auto load_bwd = [&](int k, In& o) {
         load_common(k, o);
         o.x0 = *ws(k, WF_AX); o.x1 = *ws(k, WF_AV); o.x2 = *ws(k, WF_GX); o.x3 = *ws(k, WF_GV);
 #pragma unroll
-        for (int m = 0; m < 8; m++) {
-            const double v = *ws(k, WF_KR + m);
-            o.m[m] = (k < N) ? v : 0.0;
-        }
+        for (int m = 0; m < 8; m++) o.m[m] = *ws(k, WF_KR + m);  // zero at k = N (factor sweep)
 #pragma unroll
-        for (int m = 0; m < 4; m++) {
-            const double v = *ws(k, WF_FI + m);
-            o.m[8 + m] = (k < N) ? v : 0.0;
-        }
+        for (int m = 0; m < 4; m++) o.m[8 + m] = *ws(k, WF_FI + m);
     };
 
     // ---- stage-local helpers (registers + DPP only)
@@ -601,6 +591,12 @@ __device__ __forceinline__ void ipm_group(const DevConst& c, const DevBuffers& d
                         Pc[a] = v;
                     }
                     pv = gx;
+                    // no gains at the terminal stage: zeros, so the light sweeps' loads need no stage select
+#pragma unroll
+                    for (int m = 0; m < 8; m++) *ws(k, WF_KR + m) = 0.0;
+                    *ws(k, WF_KFF) = 0.0;
+#pragma unroll
+                    for (int m = 0; m < 4; m++) *ws(k, WF_FI + m) = 0.0;
                     return;
                 }
                 // ---- (1) Y = B~^T P (column t), f = g_v + B~^T p (lanes 0..7)
