@@ -272,6 +272,16 @@ __device__ __forceinline__ void sweep(int N, bool backward, In& b0, In& b1, Load
     }
 }
 
+// The same sweep without the prefetch buffer: each stage's loads are issued at the top of its body.
+template <class In, class LoadF, class BodyF>
+__device__ __forceinline__ void sweep_noprefetch(int N, bool backward, In& b0, LoadF load, BodyF body) {
+    for (int i = 0; i <= N; i++) {
+        const int k = backward ? N - i : i;
+        load(k, b0);
+        body(k, b0);
+    }
+}
+
 }  // namespace
 
 // The QP solve of the 2 instances of this wavefront (32 lanes each).  Writes the step (d.step), QP status
@@ -575,7 +585,14 @@ __device__ __forceinline__ void ipm_group(const DevConst& c, const DevBuffers& d
 #pragma unroll
                 for (int j = 0; j < LRM; j++) pj[j] = 0.0;
                 bool chol_ok = true;
-                sweep(N, true, cur, nxt, [&](int k, In& o) { load_factor(k, o, pending); }, [&](int k, const In& cur) {
+                auto factor_sweep = [&](auto load, auto body) {
+                    // the factorization body holds the most registers: with many poly rows a prefetched stage
+                    // buffer pushes it deep into scratch (regalloc: 109 spills + 172 reloads per stage against
+                    // 52 + 115 without it), so those variants load each stage at the top of its body
+                    if constexpr (NPM > 2) sweep_noprefetch(N, true, cur, load, body);
+                    else sweep(N, true, cur, nxt, load, body);
+                };
+                factor_sweep([&](int k, In& o) { load_factor(k, o, pending); }, [&](int k, const In& cur) {
                     const double lb = cur.lb, ub = cur.ub;
                     const double* Qr = cur.m;
                     const double qt = cur.m[NX], Rt = cur.m[NX + 1], rt = cur.m[NX + 2];
