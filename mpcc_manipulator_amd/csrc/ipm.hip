@@ -213,6 +213,17 @@ __device__ __forceinline__ void sweep(int N, bool backward, In& b0, In& b1, Load
     }
 }
 
+// The same sweep without a prefetch buffer: each stage's loads are issued at the top of its body (the
+// factorization sweep of the wide-poly variants, whose body already holds most of the registers).
+template <class In, class LoadF, class BodyF>
+__device__ __forceinline__ void sweep_noprefetch(int N, bool backward, In& b0, LoadF load, BodyF body) {
+    for (int i = 0; i <= N; i++) {
+        const int k = backward ? N - i : i;
+        load(k, b0);
+        body(k, b0);
+    }
+}
+
 // Stage sweep with a ring of D stage buffers: stage s(i + D - 1) is loaded while stage s(i) is processed,
 // so D - 1 stages of loads are in flight.  Loads are unconditional (the stages past the end re-read
 // s(N)); the ring index is a constant after unrolling, so the buffers stay in registers.
@@ -520,7 +531,11 @@ __device__ __forceinline__ void ipm_group(const DevConst& c, const DevBuffers& d
             double Pc[16];   // column t of P_{k+1}
             double pv = 0.0; // p_{k+1}, component t
             bool chol_ok = true;
-            sweep<(NPM <= 2)>(N, true, cur, nxt, [&](int k, In& o) { load_factor(k, o, pending); }, [&](int k, const In& cur) {
+            auto factor_sweep = [&](auto load, auto body) {
+                if constexpr (NPM <= 2) sweep<true>(N, true, cur, nxt, load, body);
+                else sweep_noprefetch(N, true, cur, load, body);
+            };
+            factor_sweep([&](int k, In& o) { load_factor(k, o, pending); }, [&](int k, const In& cur) {
                 const double lb = cur.lb, ub = cur.ub;
                 const double* Qr = cur.m;
                 const double qt = cur.m[9], Rt = cur.m[10], rt = cur.m[11];
