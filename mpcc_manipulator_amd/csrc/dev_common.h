@@ -35,17 +35,19 @@ constexpr int QS_q = QS_Q + NX * NX;        // NX   Tx f_x                   (:1
 constexpr int QS_R = QS_q + NX;             // NU   diag(Tu f_uu Tu) + ddq diag (:162, :210)           [90]
 constexpr int QS_r = QS_R + NU;             // NU   Tu f_u + Tu ddq_grad     (:161, :191)              [98]
 constexpr int QS_B = QS_r + NU;             // NX   y_{k+1} = M y_k + G v_k + b_k, b_k = -c_{k+1} (:247) [106]
-constexpr int QS_YLB = QS_B + NX;           // NX   box on y_k (state bounds ∩ Q1 rows)                 [115]
-constexpr int QS_YUB = QS_YLB + NX;         // NX                                                        [124]
-constexpr int QS_DLB = QS_YUB + NX;         // DOF  ddq rows: v_0[j] (k=0) or v_k[j]-v_{k-1}[j] in [lb, ub] [133]
-constexpr int QS_DUB = QS_DLB + DOF;        // DOF                                                       [140]
-constexpr int QS_NPOLY = QS_DUB + DOF;      // 1    number of live polytopic rows                        [147]
-constexpr int QS_POLY = QS_NPOLY + 1;       // NPC x POLY_W                                              [148]
+// The bound block (y box, ddq box, poly rows) is what every interior-point sweep reads: it starts on a
+// 128-byte line, so with <= 2 poly rows it is 4 lines per stage (5 when it straddled line 7).
+constexpr int QS_YLB = (QS_B + NX + 15) / 16 * 16;  // NX   box on y_k (state bounds ∩ Q1 rows)        [128]
+constexpr int QS_YUB = QS_YLB + NX;         // NX                                                        [137]
+constexpr int QS_DLB = QS_YUB + NX;         // DOF  ddq rows: v_0[j] (k=0) or v_k[j]-v_{k-1}[j] in [lb, ub] [146]
+constexpr int QS_DUB = QS_DLB + DOF;        // DOF                                                       [153]
+constexpr int QS_NPOLY = QS_DUB + DOF;      // 1    number of live polytopic rows                        [160]
+constexpr int QS_POLY = QS_NPOLY + 1;       // NPC x POLY_W                                              [161]
 constexpr int QS_FLAG = QS_POLY + NPC * POLY_W;  // bit0: NaN in stage Hessian, bit1: non-PD state block,
-                                                 // bit2: infeasible constant rows                      [313]
-constexpr int QS_OBJ = QS_FLAG + 1;         // stage objective (cost + ddq term)                         [314]
-constexpr int QS = (QS_OBJ + 1 + 7) / 8 * 8;  // 64-byte records                                         [320]
-static_assert(DOF != 7 || (QS_POLY == 148 && QS == 320), "Panda QP record layout");
+                                                 // bit2: infeasible constant rows                      [326]
+constexpr int QS_OBJ = QS_FLAG + 1;         // stage objective (cost + ddq term)                         [327]
+constexpr int QS = (QS_OBJ + 1 + 15) / 16 * 16;  // whole 128-byte lines per stage record               [336]
+static_assert(DOF != 7 || (QS_YLB == 128 && QS_POLY == 161 && QS == 336), "Panda QP record layout");
 
 // ---- IPM workspace per (instance, stage): ipm.hip (Panda, 16 lanes x 35 fields) / ipm_wide.hip (mobile)
 constexpr int IS = MPCC_IPM_WS;

@@ -23,6 +23,8 @@
 //    iteration i is applied lazily by the factorization sweep of iteration i+1.  The convergence test
 //    uses mu(alpha) = (S0 + alpha S1 + alpha^2 S2)/m and rp(alpha) = (1 - alpha) rp, accumulated by
 //    the corrector forward sweep (exact identities of the oracle's update, rounding aside).
+#include <type_traits>
+
 #include "dev_common.h"
 #include "dev_dpp.h"
 #include "kernels.h"
@@ -49,25 +51,45 @@ constexpr double IPM_TAU = 0.995;    // fraction-to-boundary floor: tau = max(IP
 typedef __attribute__((address_space(1))) double gdouble;  // global-memory double (global_* loads/stores)
 constexpr int IPW = 4;               // instances per wavefront (16 lanes each)
 
-// workspace fields, ws[(b*(N+1) + k)*IS + field*16 + lane]
+// workspace fields, ws[(b*(N+1) + k)*IS + field*16 + lane].  Ordered so that what each light sweep reads is
+// one run of fields from WF_SL: predictor forward [0, LF_PRED), corrector forward [0, LF_CFWD), corrector
+// backward [0, LF_CBWD) (the LDS ring of those sweeps copies whole runs, see glds_stage).
 enum : int {
-    WF_SL = 0, WF_LL, WF_SU, WF_LU, WF_SP, WF_LP,  // slack / multiplier of the lower, upper and poly slot of row t
-    WF_ZX, WF_ZV,                                 // iterate: lane c -> x~_c (y, w); lane j < 8 -> v_j
-    WF_DX, WF_DV,                                 // corrector step (same layout)
-    WF_AX, WF_AV,                                 // predictor step
-    WF_GX, WF_GV,                                 // objective gradient H z + h
-    WF_KFF,                                       // kff (lanes 0..7)
+    WF_SL = 0, WF_LL, WF_SU, WF_LU,               // slack / multiplier of the lower and upper slot of row t
+    WF_ZX, WF_ZV,                                 // iterate: lane c -> x~_c (y, w); lane j < 8 -> v_j; with <= 4
+                                                  // poly rows (PACKP) lanes 8 + p / 12 + p hold s / lambda of poly
+                                                  // slot p, and WF_SP / WF_LP are not used
     WF_KR,                                        // 8 fields: K row halves, field m: lane i -> K[i][m], lane 8+i -> K[i][8+m]
-    WF_FI = WF_KR + 8,                            // 4 fields: F^-1 row halves, field m: lane i -> Fi[i][m], lane 8+i -> Fi[i][4+m]
-    NWF = WF_FI + 4
+    WF_GVK = WF_KR + 8,                           // lanes 0..7: objective gradient (H z + h)_v; lanes 8+i: kff_i
+    WF_AX, WF_AV,                                 // predictor step (x~ on all lanes, v on lanes 0..7)
+    WF_GX,                                        // objective gradient (H z + h)_x~
+    WF_FI,                                        // 4 fields: F^-1 row halves, field m: lane i -> Fi[i][m], lane 8+i -> Fi[i][4+m]
+    WF_SP = WF_FI + 4, WF_LP,                     // slack / multiplier of poly slot t (more than 4 poly rows)
+    WF_DX, WF_DV,                                 // corrector step (same layout as the predictor step)
+    NWF
 };
+constexpr int LF_PRED = WF_GVK + 1, LF_CFWD = WF_AV + 1, LF_CBWD = WF_FI + 4;
 static_assert(NWF * 16 <= IS, "IPM workspace must fit the per-stage IS allocation");
 
 // per-instance LDS block (doubles): U and K of the current stage, [i*16 + c]
 constexpr int L_U = 0, L_K = 128;
 constexpr int GRP_LDS = 256 + 16;  // 16 mod 32 doubles: the two instances of a half-wave start 32 banks apart
 
-size_t ipm_lds_bytes(int /*N*/, int /*npmax*/) { return (size_t)IPW * GRP_LDS * sizeof(double); }
+// LDS ring of the light sweeps (NPM <= 2): LRING slots, each holding one stage of the 4 instances of the
+// wave: the 4-line bound block of the QP record, then the sweep's workspace fields.  One global_load_lds
+// (16 B per lane) fills 2 lines of each instance, so a slot is LG(nf) KiB; the ring aliases U / K of the
+// factorization sweep (the phases never overlap).
+constexpr int LRING = 3;                              // stages s(i), s(i+1), s(i+2): two in flight
+constexpr int QLINES = 4;                             // QS_YLB .. QS_YLB + 63: bounds, NPOLY, 2 poly rows
+__host__ __device__ constexpr int LG(int nf) { return (QLINES + nf + 1) / 2; }
+static_assert(QS_POLY + 2 * 15 <= QS_YLB + 16 * QLINES, "bound block of <= 2 poly rows in QLINES lines");
+static_assert(LF_CBWD + 1 <= NWF, "the odd last line of a ring slot reads one field past the run");
+
+size_t ipm_lds_bytes(int /*N*/, int npmax) {
+    const size_t uk = (size_t)IPW * GRP_LDS * sizeof(double);
+    const size_t ring = (npmax <= 2) ? (size_t)LRING * LG(LF_CBWD) * 1024 : 0;
+    return ring > uk ? ring : uk;
+}
 
 #ifdef MPCC_IPM_PROF
 // cycle accounting per k_ipm section (profiling build only, see _build.py / tools/ipm_prof.py)
@@ -84,6 +106,30 @@ using namespace dpp;
 // One wavefront per workgroup: cross-lane LDS hand-offs only need this wave's LDS operations retired
 // and a compiler barrier; __syncthreads() would also drain outstanding global loads (vmcnt(0)).
 __device__ __forceinline__ void lds_sync() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
+
+// global_load_lds_dwordx4: 16 bytes per lane from src + OFF into LDS at lds_dst + 16 * lane (lds_dst
+// wave-uniform, through M0, which the statement saves and restores).  The immediate offset applies to the
+// LDS address as well, so M0 = lds_dst - OFF.  hipcc does not count asm memory operations, so completion
+// is waited for explicitly (s_waitcnt vmcnt).
+template <int OFF>
+__device__ __forceinline__ void glds16(const void* src, unsigned lds_dst) {
+    lds_dst -= OFF;
+    unsigned keep;
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off offset:%3\n\ts_mov_b32 m0, %0"
+                 : "=&s"(keep) : "v"(src), "s"(lds_dst), "n"(OFF) : "memory");
+}
+// one ring slot: instruction i copies 2 lines of each instance (i < QL2: the QP record's bound block at qk,
+// then the workspace fields at wk), immediate offsets from the two per-lane bases
+template <int I, int G, int QL2>
+struct GldsBatch {
+    __device__ __forceinline__ static void run(const char* qk, const char* wk, unsigned dst) {
+        if constexpr (I < G) {
+            if constexpr (I < QL2) glds16<I * 256>(qk, dst + I * 1024u);
+            else glds16<(I - QL2) * 256>(wk, dst + I * 1024u);
+            GldsBatch<I + 1, G, QL2>::run(qk, wk, dst);
+        }
+    }
+};
 
 // ---- slot algebra (oracle solve_struct_ipm), slot: sgn*(c^T z) <= sgn*bnd ----------------------
 struct SlotStep {
@@ -132,7 +178,18 @@ __device__ __forceinline__ SlotStep slot_corr(double sgn, double bnd, double cz,
     return slot_recover(ri, l, rp, sgn * cd, rc);
 }
 
-// Cholesky of the 8x8 stage F (lower triangle, packed row-major in L on entry); reciprocal pivots
+// 1/sqrt(x) for x > 0: v_rsq_f64 refined by two Newton steps, r <- r (1.5 - x/2 r^2).  On the Cholesky's
+// pivot chain this is 7 dependent instructions where sqrt (the ~12-instruction IEEE sequence) and then
+// rcp were 17; the solves only use the reciprocal pivots.
+__device__ __forceinline__ double rsqrt_pos(double x) {
+    const double h = 0.5 * x;
+    double r = __builtin_amdgcn_rsq(x);
+    r = r * fma(-h * r, r, 1.5);
+    return r * fma(-h * r, r, 1.5);
+}
+
+// Cholesky of the 8x8 stage F (lower triangle, packed row-major in L on entry); reciprocal pivots in dinv
+// (the diagonal of L itself is not formed: fwd8 / bwd8 only read dinv and the strict lower triangle)
 __device__ __forceinline__ bool chol8(double* L, double* dinv) {
     bool ok = true;
 #pragma unroll
@@ -142,9 +199,7 @@ __device__ __forceinline__ bool chol8(double* L, double* dinv) {
 #pragma unroll
         for (int m = 0; m < j; m++) d -= L[jj + m] * L[jj + m];
         ok = ok && (d > 0);
-        d = sqrt(d);
-        L[jj + j] = d;
-        const double inv = rcp(d);
+        const double inv = rsqrt_pos(d);
         dinv[j] = inv;
 #pragma unroll
         for (int i = j + 1; i < 8; i++) {
@@ -347,6 +402,25 @@ __device__ __forceinline__ void ipm_group(const DevConst& c, const DevBuffers& d
     if (run && (fl & 4)) { if (t == 0) si[SQ_QPSTAT] = MPCC_QP_PrimalInfeasible; run = false; }  // keep old step (Q6)
     const bool entered = run;
 
+    // Poly slot state packed into the upper lanes of the v field (<= 4 poly rows): every sweep then loads
+    // 6 workspace lines of slot and iterate state per stage instead of 8.
+    constexpr bool PACKP = NPM <= 4;
+    auto zv_pack = [&](double zv, double sP, double lP) -> double {
+        if constexpr (PACKP) {
+            const double s8 = from_down<8>(sP), l12 = from_down<12>(lP);  // DPP with the whole row active
+            return (t < 8) ? zv : ((t < 12) ? s8 : l12);
+        } else {
+            return zv;
+        }
+    };
+    auto store_slots = [&](int k, double sL, double lL, double sU, double lU, double sP, double lP, double zx,
+                           double zv) {
+        *ws(k, WF_SL) = sL; *ws(k, WF_LL) = lL; *ws(k, WF_SU) = sU; *ws(k, WF_LU) = lU;
+        if constexpr (!PACKP) { *ws(k, WF_SP) = sP; *ws(k, WF_LP) = lP; }
+        *ws(k, WF_ZX) = zx;
+        *ws(k, WF_ZV) = zv_pack(zv, sP, lP);
+    };
+
     // ---- stage loaders: every load unconditional (addresses clamped inside the stage record), the
     //      lane/stage conditions applied as selects afterwards (see sweep())
     auto load_common = [&](int k, In& o) {
@@ -364,8 +438,16 @@ __device__ __forceinline__ void ipm_group(const DevConst& c, const DevBuffers& d
         const double pu = q[QS_POLY + 15 * (t < NPE ? t : 0) + 14];
         o.pub = (t < NPM) ? pu : INF;
         o.sL = *ws(k, WF_SL); o.lL = *ws(k, WF_LL); o.sU = *ws(k, WF_SU); o.lU = *ws(k, WF_LU);
-        o.sP = *ws(k, WF_SP); o.lP = *ws(k, WF_LP);
-        o.zx = *ws(k, WF_ZX); o.zv = *ws(k, WF_ZV);
+        o.zx = *ws(k, WF_ZX);
+        const double zraw = *ws(k, WF_ZV);
+        if constexpr (PACKP) {
+            o.sP = from_up<8>(zraw);   // lane p <- lane 8 + p
+            o.lP = from_up<12>(zraw);  // lane p <- lane 12 + p
+            o.zv = (t < 8) ? zraw : 0.0;
+        } else {
+            o.sP = *ws(k, WF_SP); o.lP = *ws(k, WF_LP);
+            o.zv = zraw;
+        }
     };
     auto load_factor = [&](int k, In& o, bool upd) {
         load_common(k, o);
@@ -386,16 +468,104 @@ __device__ __forceinline__ void ipm_group(const DevConst& c, const DevBuffers& d
         load_common(k, o);
 #pragma unroll
         for (int m = 0; m < 8; m++) o.m[m] = *ws(k, WF_KR + m);  // zero at k = N (factor sweep)
-        o.m[8] = *ws(k, WF_KFF);
+        o.m[8] = from_up<8>(*ws(k, WF_GVK));  // lane i <- kff_i (lanes 8..15: 0)
         if (corr) { o.x0 = *ws(k, WF_AX); o.x1 = *ws(k, WF_AV); } else { o.x0 = o.x1 = 0.0; }  // corr: constant
     };
     auto load_bwd = [&](int k, In& o) {
         load_common(k, o);
-        o.x0 = *ws(k, WF_AX); o.x1 = *ws(k, WF_AV); o.x2 = *ws(k, WF_GX); o.x3 = *ws(k, WF_GV);
+        o.x0 = *ws(k, WF_AX); o.x1 = *ws(k, WF_AV); o.x2 = *ws(k, WF_GX);
+        const double gvk = *ws(k, WF_GVK);
+        o.x3 = (t < 8) ? gvk : 0.0;
 #pragma unroll
         for (int m = 0; m < 8; m++) o.m[m] = *ws(k, WF_KR + m);  // zero at k = N (factor sweep)
 #pragma unroll
         for (int m = 0; m < 4; m++) o.m[8 + m] = *ws(k, WF_FI + m);
+    };
+
+    // ---- the light sweeps of NPM <= 2 read their stages from an LDS ring filled by global_load_lds:
+    //      LRING - 1 = 2 stages in flight at no register cost (a register ring that deep spilled, and
+    //      every scratch reload waited for all loads in flight).  Slot image of one instance: line j at
+    //      (j >> 1) * 128 + (j & 1) * 16 doubles from the instance's base (grp * 32), lines 0..3 = the QP
+    //      record's bound block (QS_YLB ..), lines 4.. = workspace fields 0.. .  Lane (grp, t) copies chunk
+    //      t & 7 of lines 2i + (t >> 3) of its own instance, so groups that are not running load nothing
+    //      and read nothing.
+    const unsigned lds_base = (unsigned)(uintptr_t)(__attribute__((address_space(3))) char*)(char*)smem;
+    auto img_at = [](int j) { return (j >> 1) * 128 + (j & 1) * 16; };
+    auto qoff = [&](int r) { const int x = r - QS_YLB; return img_at(x >> 4) + (x & 15); };
+    const int o_lb = qoff(rowY ? QS_YLB + t : QS_DLB + j9), o_ub = qoff(rowY ? QS_YUB + t : QS_DUB + j9);
+    const int o_np = qoff(QS_NPOLY), o_pub = qoff(QS_POLY + 15 * (t < NPE ? t : 0) + 14);
+    int o_pa[NPE], o_pb[NPE];  // a_p[t], bv_p[t] (t < 7)
+#pragma unroll
+    for (int p = 0; p < NPE; p++) {
+        o_pa[p] = qoff(QS_POLY + 15 * p + (t < 7 ? t : 0));
+        o_pb[p] = qoff(QS_POLY + 15 * p + 7 + (t < 7 ? t : 0));
+    }
+    auto glds_stage = [&](int k, int slot, auto nfc) {
+        constexpr int G = LG(decltype(nfc)::value);
+        const char* qk = (const char*)(QSb + (size_t)k * QS + QS_YLB) + (t & 7) * 16 + (t >> 3) * 128;
+        const char* wk = (const char*)(WSb + (size_t)k * IS) + (t & 7) * 16 + (t >> 3) * 128;
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // reads of the slot's previous stage retired
+        const unsigned dst = lds_base + (unsigned)(slot * G) * 1024u;
+        GldsBatch<0, G, QLINES / 2>::run(qk, wk, dst);
+    };
+    auto lds_common = [&](const double* im, In& o) {
+        o.lb = im[o_lb];
+        o.ub = im[o_ub];
+        o.np = im[o_np];
+#pragma unroll
+        for (int p = 0; p < NPE; p++) {
+            const double a = im[o_pa[p]], bv = im[o_pb[p]];
+            o.pa[p] = (NPM > 0 && t < 7) ? a : 0.0;
+            o.pb[p] = (NPM > 0 && t < 7) ? bv : 0.0;
+        }
+        const double pu = im[o_pub];
+        o.pub = (t < NPM) ? pu : INF;
+        auto f = [&](int field) { return im[img_at(QLINES + field) + t]; };
+        o.sL = f(WF_SL); o.lL = f(WF_LL); o.sU = f(WF_SU); o.lU = f(WF_LU);
+        o.zx = f(WF_ZX);
+        const double zraw = f(WF_ZV);
+        o.sP = from_up<8>(zraw);   // PACKP: lane p <- lane 8 + p
+        o.lP = from_up<12>(zraw);  // lane p <- lane 12 + p
+        o.zv = (t < 8) ? zraw : 0.0;
+    };
+    auto fld = [&](const double* im, int field) { return im[img_at(QLINES + field) + t]; };
+    auto lds_fwd = [&](const double* im, In& o, bool corr) {
+        lds_common(im, o);
+#pragma unroll
+        for (int m = 0; m < 8; m++) o.m[m] = fld(im, WF_KR + m);
+        o.m[8] = from_up<8>(fld(im, WF_GVK));
+        if (corr) { o.x0 = fld(im, WF_AX); o.x1 = fld(im, WF_AV); } else { o.x0 = o.x1 = 0.0; }
+    };
+    auto lds_bwd = [&](const double* im, In& o) {
+        lds_common(im, o);
+        o.x0 = fld(im, WF_AX); o.x1 = fld(im, WF_AV); o.x2 = fld(im, WF_GX);
+        const double gvk = fld(im, WF_GVK);
+        o.x3 = (t < 8) ? gvk : 0.0;
+#pragma unroll
+        for (int m = 0; m < 8; m++) o.m[m] = fld(im, WF_KR + m);
+#pragma unroll
+        for (int m = 0; m < 4; m++) o.m[8 + m] = fld(im, WF_FI + m);
+    };
+    // stage sweep over the ring: stage s(i + 2) is issued while s(i) is read and processed; every issue
+    // is unconditional (the stages past the end re-read s(N)), so the wait count is fixed: after issuing
+    // s(i + 2), stage s(i) has landed once at most 2 G memory operations are outstanding (the bodies'
+    // stores only make that wait stricter).  The extra loads are drained before the ring's LDS is reused.
+    auto lds_sweep = [&](bool backward, auto nfc, auto read, auto body) {
+        constexpr int G = LG(decltype(nfc)::value);
+        auto s = [&](int i) { return backward ? N - i : i; };
+        auto cl = [&](int i) { return s(i <= N ? i : N); };
+        glds_stage(cl(0), 0, nfc);
+        glds_stage(cl(1), 1, nfc);
+        int slot = 0;
+        for (int i = 0; i <= N; i++) {
+            glds_stage(cl(i + 2), slot == 0 ? 2 : slot - 1, nfc);
+            asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * G) : "memory");
+            In o;
+            read(smem + slot * G * 128 + grp * 32, o);
+            body(s(i), o);
+            slot = slot == 2 ? 0 : slot + 1;
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     };
 
     // ---- stage-local helpers (registers + DPP only)
@@ -464,8 +634,8 @@ __device__ __forceinline__ void ipm_group(const DevConst& c, const DevBuffers& d
     // the three sweeps without the factorization (predictor forward, corrector backward and forward)
     // are short bodies that wait on their stage loads: they keep MPCC_LIGHT_DEPTH - 1 stages in flight
     In ring[MPCC_LIGHT_DEPTH];
-    auto light_sweep = [&](bool backward, auto load, auto body) {
-        if constexpr (NPM <= 2) sweep_ring<MPCC_LIGHT_DEPTH>(N, backward, ring, load, body);
+    auto light_sweep = [&](bool backward, auto nfc, auto load, auto read, auto body) {
+        if constexpr (NPM <= 2) lds_sweep(backward, nfc, read, body);
         else sweep<false>(N, backward, cur, nxt, load, body);
     };
     int it = 0, it_total = 0;
@@ -501,10 +671,7 @@ __device__ __forceinline__ void ipm_group(const DevConst& c, const DevBuffers& d
             if (aU) { sU = fmax(-(sgnU * cz - sgnU * cur.ub), s_floor); lU = (lam_scale > 0) ? lam_scale / sU : 1.0; }
             if (aP) { sP = fmax(-(sgnU * pcz - sgnU * cur.pub), s_floor); lP = (lam_scale > 0) ? lam_scale / sP : 1.0; }
             mcount += (aL ? 1.0 : 0.0) + (aU ? 1.0 : 0.0) + (aP ? 1.0 : 0.0);
-            *ws(k, WF_SL) = sL; *ws(k, WF_LL) = lL; *ws(k, WF_SU) = sU; *ws(k, WF_LU) = lU;
-            *ws(k, WF_SP) = sP; *ws(k, WF_LP) = lP;
-            *ws(k, WF_ZX) = yx;
-            *ws(k, WF_ZV) = 0.0;
+            store_slots(k, sL, lL, sU, lU, sP, lP, yx, 0.0);
             // y_{k+1} = M y_k + b_k (oracle order: sum_b M[a][b] y_b, then + b_a)
             const double y8 = from_up<1>(y);  // lane 7 <- y_8
             const double yn = (t == 7) ? m77 * y + m78 * y8 : mt * y;
@@ -553,9 +720,7 @@ __device__ __forceinline__ void ipm_group(const DevConst& c, const DevBuffers& d
                     if (aP) { const SlotStep st = slot_corr(sgnU, cur.pub, pcz, pca, pcd, sP, lP, sigma_mu, &rpd); sP += alpha * st.ds; lP += alpha * st.dl; }
                     zx += alpha * dx;
                     zv += alpha * dv;
-                    *ws(k, WF_SL) = sL; *ws(k, WF_LL) = lL; *ws(k, WF_SU) = sU; *ws(k, WF_LU) = lU;
-                    *ws(k, WF_SP) = sP; *ws(k, WF_LP) = lP;
-                    *ws(k, WF_ZX) = zx; *ws(k, WF_ZV) = zv;
+                    store_slots(k, sL, lL, sU, lU, sP, lP, zx, zv);
                 }
                 PMARK(8);
                 // ---- slots: barrier weights and predictor coefficients (rc = s l)
@@ -590,7 +755,6 @@ __device__ __forceinline__ void ipm_group(const DevConst& c, const DevBuffers& d
                     }
                 }
                 *ws(k, WF_GX) = g0x;
-                *ws(k, WF_GV) = g0v;
                 double gx, gv;
                 assemble_grad(cur, k, g0x, g0v, dvr, cP, gx, gv);
                 PMARK(9);
@@ -609,7 +773,7 @@ __device__ __forceinline__ void ipm_group(const DevConst& c, const DevBuffers& d
                     // no gains at the terminal stage: zeros, so the light sweeps' loads need no stage select
 #pragma unroll
                     for (int m = 0; m < 8; m++) *ws(k, WF_KR + m) = 0.0;
-                    *ws(k, WF_KFF) = 0.0;
+                    *ws(k, WF_GVK) = (t < 8) ? g0v : 0.0;
 #pragma unroll
                     for (int m = 0; m < 4; m++) *ws(k, WF_FI + m) = 0.0;
                     return;
@@ -703,7 +867,10 @@ __device__ __forceinline__ void ipm_group(const DevConst& c, const DevBuffers& d
                     S[L_U + i * 16 + t] = u[i];
                     S[L_K + i * 16 + t] = kc[i];
                 }
-                *ws(k, WF_KFF) = (t < 8) ? kff : 0.0;
+                {
+                    const double kffd = from_down<8>(kff);  // lane 8+i <- kff_i
+                    *ws(k, WF_GVK) = (t < 8) ? g0v : kffd;
+                }
 #pragma unroll
                 for (int m = 0; m < 4; m++) *ws(k, WF_FI + m) = (t < 8) ? fi[m] : fi[4 + m];
                 // ---- (4) Hb column t and P = Hb - U^T U (column t); U rows are broadcast LDS reads
@@ -785,7 +952,8 @@ __device__ __forceinline__ void ipm_group(const DevConst& c, const DevBuffers& d
             double S0 = 0, S1 = 0, S2 = 0;
             MinRatio amr(1.0);
             double xt = 0.0;
-            light_sweep(false, [&](int k, In& o) { load_fwd(k, o, false); }, [&](int k, const In& cur) {
+            light_sweep(false, std::integral_constant<int, LF_PRED>{}, [&](int k, In& o) { load_fwd(k, o, false); },
+                        [&](const double* im, In& o) { lds_fwd(im, o, false); }, [&](int k, const In& cur) {
                 const bool aL = row_active(k, cur.lb), aU = row_active(k, cur.ub), aP = poly_slot_active(cur, k);
                 double v = 0.0, xn = 0.0;
                 if (k < N) fwd_step(cur, xt, v, xn);
@@ -822,7 +990,8 @@ __device__ __forceinline__ void ipm_group(const DevConst& c, const DevBuffers& d
             // ---- corrector backward: coef with rc = s l + dsa dla - sigma mu; f = g_v + B~^T p;
             //      kff = -F^-1 f; p = g_x~ + A~^T p + K^T f
             double pv = 0.0;
-            light_sweep(true, [&](int k, In& o) { load_bwd(k, o); }, [&](int k, const In& cur) {
+            light_sweep(true, std::integral_constant<int, LF_CBWD>{}, [&](int k, In& o) { load_bwd(k, o); },
+                        [&](const double* im, In& o) { lds_bwd(im, o); }, [&](int k, const In& cur) {
                 const bool aL = row_active(k, cur.lb), aU = row_active(k, cur.ub), aP = poly_slot_active(cur, k);
                 const double cz = row_cz(k, cur.zx, cur.zv), ca = row_cz(k, cur.x0, cur.x1);
                 const double pcz = poly_cz(cur, k, cur.zx, cur.zv), pca = poly_cz(cur, k, cur.x0, cur.x1);
@@ -853,7 +1022,8 @@ __device__ __forceinline__ void ipm_group(const DevConst& c, const DevBuffers& d
 #pragma unroll
                 for (int m = 0; m < 4; m++) part -= cur.m[8 + m] * ((t < 8) ? fb[m] : fb[4 + m]);
                 const double kff = part + from_up<8>(part);
-                *ws(k, WF_KFF) = (t < 8) ? kff : 0.0;
+                const double kffd = from_down<8>(kff);  // lane 8+i <- kff_i
+                if (t >= 8) *ws(k, WF_GVK) = kffd;
                 double atp = 0.0;
                 const double p7 = from_down<1>(pv);
                 if (t < 9) {
@@ -886,7 +1056,8 @@ __device__ __forceinline__ void ipm_group(const DevConst& c, const DevBuffers& d
             double T0 = 0, T1 = 0, T2 = 0, rpm = 0, dzm = 0;
             MinRatio amc(1e30);
             xt = 0.0;
-            light_sweep(false, [&](int k, In& o) { load_fwd(k, o, true); }, [&](int k, const In& cur) {
+            light_sweep(false, std::integral_constant<int, LF_CFWD>{}, [&](int k, In& o) { load_fwd(k, o, true); },
+                        [&](const double* im, In& o) { lds_fwd(im, o, true); }, [&](int k, const In& cur) {
                 const bool aL = row_active(k, cur.lb), aU = row_active(k, cur.ub), aP = poly_slot_active(cur, k);
                 double v = 0.0, xn = 0.0;
                 if (k < N) fwd_step(cur, xt, v, xn);
@@ -964,7 +1135,7 @@ __device__ __forceinline__ void ipm_group(const DevConst& c, const DevBuffers& d
     gdouble* stp = (gdouble*)(d.step + (size_t)b * NS * 17);
     for (int k = 0; k <= N; k++) {
         const double zx = *ws(k, WF_ZX) + alpha * *ws(k, WF_DX);
-        const double zv = *ws(k, WF_ZV) + alpha * *ws(k, WF_DV);
+        const double zv = *ws(k, WF_ZV) + alpha * *ws(k, WF_DV);  // lanes < 8
         if (t < 9) stp[k * 17 + t] = zx;
         if (t < 8) stp[k * 17 + 9 + t] = (k < N) ? zv : 0.0;
     }
