@@ -161,16 +161,7 @@ __device__ __forceinline__ SlotStep slot_corr(double sgn, double bnd, double cz,
     return slot_recover(ri, l, rp, sgn * cd, rc);
 }
 
-// 1/sqrt(x) for x > 0: v_rsq_f64 refined by two Newton steps (ipm.hip rsqrt_pos)
-__device__ __forceinline__ double rsqrt_pos(double x) {
-    const double h = 0.5 * x;
-    double r = __builtin_amdgcn_rsq(x);
-    r = r * fma(-h * r, r, 1.5);
-    return r * fma(-h * r, r, 1.5);
-}
-
-// Cholesky of the NU x NU stage F (packed lower triangle), reciprocal pivots (the diagonal of L is not
-// formed: the solves read dinv and the strict lower triangle); forward / backward solves
+// Cholesky of the NU x NU stage F (packed lower triangle), reciprocal pivots; forward / backward solves
 __device__ __forceinline__ bool cholN(double* L, double* dinv) {
     bool ok = true;
 #pragma unroll
@@ -180,7 +171,9 @@ __device__ __forceinline__ bool cholN(double* L, double* dinv) {
 #pragma unroll
         for (int m = 0; m < j; m++) d -= L[jj + m] * L[jj + m];
         ok = ok && (d > 0);
-        const double inv = rsqrt_pos(d);
+        d = sqrt(d);
+        L[jj + j] = d;
+        const double inv = rcp(d);
         dinv[j] = inv;
 #pragma unroll
         for (int i = j + 1; i < NU; i++) {
