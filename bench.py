@@ -335,7 +335,8 @@ def main():
     if os.path.exists(tpath):
         with open(tpath) as f:
             tr = json.load(f)
-        if tr.get("batch") == B and tr.get("N") == N and tr.get("kernel", "k_ipm") == kname:
+        if (tr.get("batch") == B and tr.get("N") == N and tr.get("mask") == args.mask
+                and tr.get("kernel", "k_ipm") == kname):
             traffic = tr.get("hbm_bytes_per_launch")
     roof = {"kernel": kname, "bound": "mfma", "achieved": achieved, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
             "frac": achieved / FP64_PEAK_TFLOPS, "traffic": traffic,

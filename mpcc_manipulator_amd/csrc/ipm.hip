@@ -284,6 +284,14 @@ __device__ __forceinline__ void sweep_noprefetch(int N, bool backward, In& b0, L
 // s(N)); the ring index is a constant after unrolling, so the buffers stay in registers.
 // D = 2 since the stage addresses stopped spilling: same box, configs[1], k_sqp
 // 3.83 ms at D = 2, 3.88 ms at D = 3, 4.14 ms at D = 4 (tools/bench_variants.sh).
+// experiment switches of the wide-poly variants (NPM >= 9): factorization sweep with a copy-based
+// prefetch, light sweeps without one
+#ifndef MPCC_WIDE_FACTOR_PF
+#define MPCC_WIDE_FACTOR_PF 0
+#endif
+#ifndef MPCC_WIDE_LIGHT_NOPF
+#define MPCC_WIDE_LIGHT_NOPF 0
+#endif
 #ifndef MPCC_LIGHT_DEPTH
 #define MPCC_LIGHT_DEPTH 2
 #endif
@@ -636,6 +644,7 @@ __device__ __forceinline__ void ipm_group(const DevConst& c, const DevBuffers& d
     In ring[MPCC_LIGHT_DEPTH];
     auto light_sweep = [&](bool backward, auto nfc, auto load, auto read, auto body) {
         if constexpr (NPM <= 2) lds_sweep(backward, nfc, read, body);
+        else if constexpr (MPCC_WIDE_LIGHT_NOPF) sweep_noprefetch(N, backward, cur, load, body);
         else sweep<false>(N, backward, cur, nxt, load, body);
     };
     int it = 0, it_total = 0;
@@ -700,6 +709,7 @@ __device__ __forceinline__ void ipm_group(const DevConst& c, const DevBuffers& d
             bool chol_ok = true;
             auto factor_sweep = [&](auto load, auto body) {
                 if constexpr (NPM <= 2) sweep<true>(N, true, cur, nxt, load, body);
+                else if constexpr (MPCC_WIDE_FACTOR_PF) sweep<false>(N, true, cur, nxt, load, body);
                 else sweep_noprefetch(N, true, cur, load, body);
             };
             factor_sweep([&](int k, In& o) { load_factor(k, o, pending); }, [&](int k, const In& cur) {
@@ -786,32 +796,38 @@ __device__ __forceinline__ void ipm_group(const DevConst& c, const DevBuffers& d
                 const double pu9 = from_up<9>(pv), pu1 = from_up<1>(pv);  // DPP in uniform control flow
                 const double fv = gv + gt * pv + ((t < 7) ? pu9 : g87 * pu1);
                 // ---- (2) F column t (t < 8), Gm column t (t < 9); poly terms W_p bv_p bv_p^T, W_p bv_p a_p^T
-                double Wb[NPE], bvb[NPE][8];
+                // The rank-NPM poly terms accumulate row p by row p: each broadcast bv_p[i] is consumed as
+                // soon as it is made (DPP results are pinned in program order, so broadcasting every
+                // bv_p[i] first kept 8 NPM values live; at NPM = 11 that spilled).  Per accumulator the
+                // operations and their order are those of the oracle's sum over p.
+                double Wb[NPE];
+                const double wdv = from_up<9>(wd);  // lane j <- ddq row j weight
+                double hF[8], hG[8];
+#pragma unroll
+                for (int i = 0; i < 8; i++) {
+                    hF[i] = (i == t) ? Rt + ((t < 7) ? wdv : 0.0) : 0.0;
+                    hG[i] = 0.0;
+                }
 #pragma unroll
                 for (int p = 0; p < NPM; p++) {
                     const bool live = (double)p < cur.np && k < N;
                     const double wp = bcn(WP, p);
                     Wb[p] = live ? wp : 0.0;
 #pragma unroll
-                    for (int i = 0; i < 8; i++) bvb[p][i] = bcn(cur.pb[p], i);
+                    for (int i = 0; i < 7; i++) {
+                        const double bv = bcn(cur.pb[p], i);
+                        hF[i] += Wb[p] * (bv * cur.pb[p]);  // bv_p[t]: zero for lanes >= 7
+                        hG[i] += Wb[p] * (bv * cur.pa[p]);  // a_p[t]: zero for lanes >= 7
+                    }
                 }
-                const double wdv = from_up<9>(wd);  // lane j <- ddq row j weight
                 double Fc[8], gm[8];
 #pragma unroll
                 for (int i = 0; i < 8; i++) {
                     const double yu9 = from_up<9>(Y[i]);
                     const double yu1 = from_up<1>(Y[i]);
                     const double yd = from_down<1>(Y[i]);
-                    double h = 0.0, hv = 0.0;
-                    if (i == t) h = Rt + ((t < 7) ? wdv : 0.0);
-                    if (i < 7)
-#pragma unroll
-                        for (int p = 0; p < NPM; p++) {
-                            h += Wb[p] * (bvb[p][i] * cur.pb[p]);   // bv_p[t]: zero for lanes >= 7
-                            hv += Wb[p] * (bvb[p][i] * cur.pa[p]);  // a_p[t]: zero for lanes >= 7
-                        }
-                    Fc[i] = h + (gt * Y[i] + ((t < 7) ? yu9 : g87 * yu1));
-                    gm[i] = hv + (mt * Y[i] + ((t == 8) ? m78 * yd : 0.0));
+                    Fc[i] = hF[i] + (gt * Y[i] + ((t < 7) ? yu9 : g87 * yu1));
+                    gm[i] = hG[i] + (mt * Y[i] + ((t == 8) ? m78 * yd : 0.0));
                 }
                 PMARK(10);
                 // ---- (3) chol(F) from the broadcast columns; U = LF^-1 Gm; K = -LF^-T U; Finv column (t & 7);
@@ -879,21 +895,31 @@ __device__ __forceinline__ void ipm_group(const DevConst& c, const DevBuffers& d
                     double Pc7[9];
 #pragma unroll
                     for (int a = 0; a < 9; a++) Pc7[a] = from_down<1>(Pc[a]);  // lane 8 <- P[a][7]
-                    double pab[NPE][7];
+                    // poly terms row p by row p, as for F above
+                    double hq[7];
+#pragma unroll
+                    for (int a = 0; a < 7; a++) {
+                        hq[a] = Qr[a];
+                        if (a == t) hq[a] += wd;
+                    }
 #pragma unroll
                     for (int p = 0; p < NPM; p++)
 #pragma unroll
-                        for (int a = 0; a < 7; a++) pab[p][a] = bcn(cur.pa[p], a);
+                        for (int a = 0; a < 7; a++) {
+                            const double pa_ = bcn(cur.pa[p], a);
+                            hq[a] += Wb[p] * (pa_ * cur.pa[p]);
+                        }
 #pragma unroll
                     for (int a = 0; a < 16; a++) {
                         double v = 0.0;
                         if (a < 9) {
                             if (t < 9) {
-                                v = Qr[a];
-                                if (a == t) v += wd;
-                                if (a < 7)
-#pragma unroll
-                                    for (int p = 0; p < NPM; p++) v += Wb[p] * (pab[p][a] * cur.pa[p]);
+                                if (a < 7) {
+                                    v = hq[a];
+                                } else {
+                                    v = Qr[a];
+                                    if (a == t) v += wd;
+                                }
                                 double mp = (mdiag[a] * mt) * Pc[a];
                                 if (t == 8) mp += (mdiag[a] * m78) * Pc7[a];
                                 if (a == 8) mp += (m78 * mt) * Pc[7];
