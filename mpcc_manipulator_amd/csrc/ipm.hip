@@ -284,13 +284,15 @@ __device__ __forceinline__ void sweep_noprefetch(int N, bool backward, In& b0, L
 // s(N)); the ring index is a constant after unrolling, so the buffers stay in registers.
 // D = 2 since the stage addresses stopped spilling: same box, configs[1], k_sqp
 // 3.83 ms at D = 2, 3.88 ms at D = 3, 4.14 ms at D = 4 (tools/bench_variants.sh).
-// experiment switches of the wide-poly variants (NPM >= 9): factorization sweep with a copy-based
-// prefetch, light sweeps without one
+// Sweeps of the wide-poly variants (NPM >= 9), whose stage buffers hold 11 poly rows: register pressure
+// costs them more than load latency.  Same box, reference default rows (bench --config 1-all-rows), k_sqp<11>:
+// light sweeps with the copy-based prefetch 15.72 ms, without it 14.57 ms (the default); the factorization
+// sweep with that prefetch 16.63 ms (it stays without).  profiles/r02e_c1all_*.json
 #ifndef MPCC_WIDE_FACTOR_PF
 #define MPCC_WIDE_FACTOR_PF 0
 #endif
 #ifndef MPCC_WIDE_LIGHT_NOPF
-#define MPCC_WIDE_LIGHT_NOPF 0
+#define MPCC_WIDE_LIGHT_NOPF 1
 #endif
 #ifndef MPCC_LIGHT_DEPTH
 #define MPCC_LIGHT_DEPTH 2

@@ -260,6 +260,11 @@ struct StageIn {
     double m[2 * NU];             // sweep-specific: Q row (NX) + q, R, r | K column (NU) + kff | K column + F^-1 row
 };
 
+// Light sweeps of the many-poly-row variants without the prefetch buffer: measured slower here (mobile
+// configs[3] k_sqp<11> 348.7 ms against 341.7 ms with it, profiles/r02f_c3*.json), unlike ipm.hip, so off
+#ifndef MPCC_WIDE_LIGHT_NOPF
+#define MPCC_WIDE_LIGHT_NOPF 0
+#endif
 // stage sweep i = 0..N in order s(i) with the next stage prefetched (copy-based double buffer)
 template <class In, class LoadF, class BodyF>
 __device__ __forceinline__ void sweep(int N, bool backward, In& b0, In& b1, LoadF load, BodyF body) {
@@ -521,6 +526,11 @@ __device__ __forceinline__ void ipm_group(const DevConst& c, const DevBuffers& d
     auto fwd_step = [&](const In& in, double xt, double& v, double& xn) { fwd_step_k(in, xt, in.m[NU], v, xn); };
 
     In cur, nxt;
+    // light sweeps (no factorization), optionally without the prefetch buffer (MPCC_WIDE_LIGHT_NOPF)
+    auto light_sweep = [&](bool backward, auto load, auto body) {
+        if constexpr (NPM > 2 && MPCC_WIDE_LIGHT_NOPF) sweep_noprefetch(N, backward, cur, load, body);
+        else sweep(N, backward, cur, nxt, load, body);
+    };
     int it = 0, it_total = 0;
     bool conv = false, diverged = false;
     double alpha = 0.0;
@@ -902,7 +912,7 @@ __device__ __forceinline__ void ipm_group(const DevConst& c, const DevBuffers& d
                     for (int j = 0; j < LRM; j++) { o.m[j] = *ws(k, WF_QX + j); o.m[LRM + j] = *ws(k, WF_QV + j); }
                 };
                 if (!lrw) {
-                    sweep(N, false, cur, nxt, [&](int k, In& o) { load_fwd(k, o, false); }, [&](int k, const In& cur) {
+                    light_sweep(false, [&](int k, In& o) { load_fwd(k, o, false); }, [&](int k, const In& cur) {
                         double v = 0.0, xn = 0.0;
                         fwd_step(cur, xt, v, xn);
                         pred_rec(k, cur, xt, (t < NU && k < N) ? v : 0.0);
@@ -914,7 +924,7 @@ __device__ __forceinline__ void ipm_group(const DevConst& c, const DevBuffers& d
                     for (int j = 0; j < LRM; j++) { xq[j] = 0.0; udp[j] = 0.0; }
 #pragma unroll
                     for (int j = 0; j < LRM * LRM; j++) uqp[j] = 0.0;
-                    sweep(N, false, cur, nxt, [&](int k, In& o) { load_fwd(k, o, false); }, [&](int k, const In& cur) {
+                    light_sweep(false, [&](int k, In& o) { load_fwd(k, o, false); }, [&](int k, const In& cur) {
                         double v = 0.0, xn = 0.0;
                         fwd_step(cur, xt, v, xn);
                         const double dvv = (t < NU && k < N) ? v : 0.0;
@@ -957,7 +967,7 @@ __device__ __forceinline__ void ipm_group(const DevConst& c, const DevBuffers& d
                     trc_t0 = tt[0]; trc_S0 = Smat[0];
 #endif
                     // dz = dz_s - Q S^-1 U^T dz_s, then the recovery of the predictor step
-                    sweep(N, false, cur, nxt, [&](int k, In& o) { load_fix(k, o, false); }, [&](int k, const In& cur) {
+                    light_sweep(false, [&](int k, In& o) { load_fix(k, o, false); }, [&](int k, const In& cur) {
                         double xs = cur.x0, dvv = cur.x1;
 #pragma unroll
                         for (int j = 0; j < LRM; j++) { xs -= tt[j] * cur.m[j]; dvv -= tt[j] * cur.m[LRM + j]; }
@@ -977,7 +987,7 @@ __device__ __forceinline__ void ipm_group(const DevConst& c, const DevBuffers& d
                 // ---- corrector backward: coef with rc = s l + dsa dla - sigma mu; f = g_v + B~^T p;
                 //      kff = -F^-1 f; p = g_x~ + A~^T p + K^T f
                 double pv = 0.0;
-                sweep(N, true, cur, nxt, [&](int k, In& o) { load_bwd(k, o); }, [&](int k, const In& cur) {
+                light_sweep(true, [&](int k, In& o) { load_bwd(k, o); }, [&](int k, const In& cur) {
                     const bool aL = row_active(k, cur.lb), aU = row_active(k, cur.ub), aP = poly_slot_active(cur, k);
                     const double cz = row_cz(k, cur.zx, cur.zv), ca = row_cz(k, cur.x0, cur.x1);
                     const double pcz = poly_cz(cur, k, cur.zx, cur.zv), pca = poly_cz(cur, k, cur.x0, cur.x1);
@@ -1048,7 +1058,7 @@ __device__ __forceinline__ void ipm_group(const DevConst& c, const DevBuffers& d
                 };
                 xt = 0.0;
                 if (!lrw) {
-                    sweep(N, false, cur, nxt, [&](int k, In& o) { load_fwd(k, o, true); }, [&](int k, const In& cur) {
+                    light_sweep(false, [&](int k, In& o) { load_fwd(k, o, true); }, [&](int k, const In& cur) {
                         double v = 0.0, xn = 0.0;
                         fwd_step(cur, xt, v, xn);
                         corr_rec(k, cur, (t < NXA) ? xt : 0.0, (t < NU && k < N) ? v : 0.0, cur.x0, cur.x1);
@@ -1058,7 +1068,7 @@ __device__ __forceinline__ void ipm_group(const DevConst& c, const DevBuffers& d
                     double udp[LRM];
 #pragma unroll
                     for (int j = 0; j < LRM; j++) udp[j] = 0.0;
-                    sweep(N, false, cur, nxt, [&](int k, In& o) { load_fwd(k, o, false); }, [&](int k, const In& cur) {
+                    light_sweep(false, [&](int k, In& o) { load_fwd(k, o, false); }, [&](int k, const In& cur) {
                         double v = 0.0, xn = 0.0;
                         fwd_step(cur, xt, v, xn);
                         const double xtt = (t < NXA) ? xt : 0.0, dvv = (t < NU && k < N) ? v : 0.0;
@@ -1074,7 +1084,7 @@ __device__ __forceinline__ void ipm_group(const DevConst& c, const DevBuffers& d
 #pragma unroll
                     for (int i = 0; i < LRM * LRM; i++) Sm[i] = Smat[i];
                     solve_small(Sm, tt);
-                    sweep(N, false, cur, nxt, [&](int k, In& o) { load_fix(k, o, true); }, [&](int k, const In& cur) {
+                    light_sweep(false, [&](int k, In& o) { load_fix(k, o, true); }, [&](int k, const In& cur) {
                         double xtt = cur.x2, dvv = cur.x3;
 #pragma unroll
                         for (int j = 0; j < LRM; j++) { xtt -= tt[j] * cur.m[j]; dvv -= tt[j] * cur.m[LRM + j]; }

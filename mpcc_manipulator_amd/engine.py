@@ -17,7 +17,7 @@ MOBILE_PARAMS = os.path.join(DATA, "params", "mobile_params.json")
 LIB_PATH = os.environ.get("MPCC_ENGINE_LIB", os.path.join(PKG, "_build", "libmpcc_engine.so"))
 # Robot dimensions are compile-time in the engine, as the reference's NX/NU (config.h:29-38): one library
 # per robot with the same C ABI.  dof 7 = Franka Panda, dof 10 = Husky+Panda mobile manipulator.
-LIB_PATHS = {7: LIB_PATH, 10: os.path.join(PKG, "_build", "libmpcc_engine_mobile.so")}
+LIB_PATHS = {7: LIB_PATH, 10: os.environ.get("MPCC_ENGINE_LIB_MOBILE", os.path.join(PKG, "_build", "libmpcc_engine_mobile.so"))}
 ROBOT_DOF = {"panda": 7, "husky_panda": 10}
 
 REC_SIZE = 143
