@@ -9,6 +9,7 @@ over RCCL each step.  Prints one JSON line (rank 0).
     python bench.py [--gpus N --steps K --warmup W --batch B]
 """
 import argparse
+import glob
 import json
 import os
 import socket
@@ -331,13 +332,18 @@ def main():
     flops = qps * algorithmic_qp_flops(N, dof) / launches_per_step
     achieved = flops / t_ipm / 1e12
     traffic = None
-    tpath = args.traffic or os.path.join(ROOT, "profiles", f"pmc_traffic_{kname}.json")
-    if os.path.exists(tpath):
+    # the committed PMC summary of this workload (tools/pmc_summary.py): the first file whose kernel, batch,
+    # horizon and constraint mask match this run, or null
+    tpaths = [args.traffic] if args.traffic else sorted(glob.glob(os.path.join(ROOT, "profiles", f"pmc_traffic_{kname}*.json")))
+    for tpath in tpaths:
+        if not os.path.exists(tpath):
+            continue
         with open(tpath) as f:
             tr = json.load(f)
         if (tr.get("batch") == B and tr.get("N") == N and tr.get("mask") == args.mask
-                and tr.get("kernel", "k_ipm") == kname):
+                and tr.get("kernel", "k_ipm") == kname and tr.get("dof", 7) == dof):
             traffic = tr.get("hbm_bytes_per_launch")
+            break
     roof = {"kernel": kname, "bound": "mfma", "achieved": achieved, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
             "frac": achieved / FP64_PEAK_TFLOPS, "traffic": traffic,
             "avg_launch_ms": t_ipm * 1e3, "launches_timed": nipm, "algorithmic_flops_per_launch": flops,

@@ -36,6 +36,7 @@ def main():
     ap.add_argument("--batch", type=int, default=4096)
     ap.add_argument("--N", type=int, default=20)
     ap.add_argument("--mask", type=int, default=2, help="constraint mask of the profiled run (bench.py matches it)")
+    ap.add_argument("--dof", type=int, default=7, help="robot DOF of the profiled build (10: mobile)")
     ap.add_argument("--kernel", default="k_sqp")
     ap.add_argument("--ipw", type=int, default=4, help="instances per wavefront (4 Panda, 2 mobile build)")
     ap.add_argument("--ns", default="mpcc", help="kernel namespace (mpcc_m10 for the mobile build)")
@@ -68,7 +69,7 @@ def main():
         out["hbm_write_bytes_per_launch"] = wr
         out["hbm_bytes_per_launch"] = rd + wr
         with open(os.path.join(prof, args.traffic_name or f"pmc_traffic_{args.kernel}.json"), "w") as f:
-            json.dump({"kernel": args.kernel, "batch": args.batch, "N": args.N, "mask": args.mask, "hbm_bytes_per_launch": rd + wr,
+            json.dump({"kernel": args.kernel, "batch": args.batch, "N": args.N, "mask": args.mask, "dof": args.dof, "hbm_bytes_per_launch": rd + wr,
                        "hbm_read_bytes_per_launch": rd, "hbm_write_bytes_per_launch": wr,
                        "source": f"profiles/{args.round}_{args.kernel}_pmc.json"}, f, indent=1)
     if "SQ_WAVE_CYCLES" in avg:
