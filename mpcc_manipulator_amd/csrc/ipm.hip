@@ -81,13 +81,26 @@ constexpr int GRP_LDS = 256 + 16;  // 16 mod 32 doubles: the two instances of a 
 // factorization sweep (the phases never overlap).
 constexpr int LRING = 3;                              // stages s(i), s(i+1), s(i+2): two in flight
 constexpr int QLINES = 4;                             // QS_YLB .. QS_YLB + 63: bounds, NPOLY, 2 poly rows
-__host__ __device__ constexpr int LG(int nf) { return (QLINES + nf + 1) / 2; }
+__host__ __device__ constexpr int LG(int nf, int ql = QLINES) { return (ql + nf + 1) / 2; }
 static_assert(QS_POLY + 2 * 15 <= QS_YLB + 16 * QLINES, "bound block of <= 2 poly rows in QLINES lines");
+// The wide-poly variants (NPM >= 9, MPCC_WIDE_RING): a 2-slot ring (one stage in flight) of a 14-line
+// bound block (11 poly rows) and the fields up to the unpacked poly slot state; 19 KiB per slot, so 4 waves
+// of 38 KiB fit a CU's 160 KiB.
+#ifndef MPCC_WIDE_RING
+#define MPCC_WIDE_RING 1
+#endif
+constexpr int LRING_W = 2, QLINES_W = 14;
+static_assert(QS_POLY + NPC * 15 <= QS_YLB + 16 * QLINES_W, "bound block of all poly rows in QLINES_W lines");
+__host__ __device__ constexpr bool use_ring(int npm) { return npm <= 2 || (MPCC_WIDE_RING && npm >= 9); }
+__host__ __device__ constexpr int ring_q(int npm) { return npm <= 2 ? QLINES : QLINES_W; }
+__host__ __device__ constexpr int ring_d(int npm) { return npm <= 2 ? LRING : LRING_W; }
 static_assert(LF_CBWD + 1 <= NWF, "the odd last line of a ring slot reads one field past the run");
 
 size_t ipm_lds_bytes(int /*N*/, int npmax) {
     const size_t uk = (size_t)IPW * GRP_LDS * sizeof(double);
-    const size_t ring = (npmax <= 2) ? (size_t)LRING * LG(LF_CBWD) * 1024 : 0;
+    const size_t ring = (npmax <= 2)          ? (size_t)LRING * LG(LF_CBWD) * 1024
+                        : use_ring(npmax)       ? (size_t)LRING_W * LG(WF_LP + 1, QLINES_W) * 1024
+                                                : 0;
     return ring > uk ? ring : uk;
 }
 
@@ -492,7 +505,8 @@ __device__ __forceinline__ void ipm_group(const DevConst& c, const DevBuffers& d
         for (int m = 0; m < 4; m++) o.m[8 + m] = *ws(k, WF_FI + m);
     };
 
-    // ---- the light sweeps of NPM <= 2 read their stages from an LDS ring filled by global_load_lds:
+    // ---- the light sweeps of NPM <= 2 (and of NPM >= 9 with MPCC_WIDE_RING: 2 slots, 14 record lines from
+    //      QS_YLB - 16, fields 0..WF_LP) read their stages from an LDS ring filled by global_load_lds:
     //      LRING - 1 = 2 stages in flight at no register cost (a register ring that deep spilled, and
     //      every scratch reload waited for all loads in flight).  Slot image of one instance: line j at
     //      (j >> 1) * 128 + (j & 1) * 16 doubles from the instance's base (grp * 32), lines 0..3 = the QP
@@ -501,22 +515,29 @@ __device__ __forceinline__ void ipm_group(const DevConst& c, const DevBuffers& d
     //      and read nothing.
     const unsigned lds_base = (unsigned)(uintptr_t)(__attribute__((address_space(3))) char*)(char*)smem;
     auto img_at = [](int j) { return (j >> 1) * 128 + (j & 1) * 16; };
-    auto qoff = [&](int r) { const int x = r - QS_YLB; return img_at(x >> 4) + (x & 15); };
+    constexpr int QL = ring_q(NPM), RD = ring_d(NPM);
+    // first record line of the slot image: the bound block; the wide ring starts one line earlier so that its
+    // 14 lines end with the stage record (a line past it would leave the buffer at the last stage)
+    constexpr int QB = (NPM <= 2) ? QS_YLB : QS_YLB - 16;
+    static_assert(QB + 16 * QL <= QS, "ring image inside the stage record");
+    auto qoff = [&](int r) { const int x = r - QB; return img_at(x >> 4) + (x & 15); };
     const int o_lb = qoff(rowY ? QS_YLB + t : QS_DLB + j9), o_ub = qoff(rowY ? QS_YUB + t : QS_DUB + j9);
     const int o_np = qoff(QS_NPOLY), o_pub = qoff(QS_POLY + 15 * (t < NPE ? t : 0) + 14);
-    int o_pa[NPE], o_pb[NPE];  // a_p[t], bv_p[t] (t < 7)
+    int o_pa[NPE], o_pb[NPE];  // a_p[t], bv_p[t] (t < 7); NPM <= 2 only
 #pragma unroll
-    for (int p = 0; p < NPE; p++) {
+    for (int p = 0; p < (NPM <= 2 ? NPE : 0); p++) {
         o_pa[p] = qoff(QS_POLY + 15 * p + (t < 7 ? t : 0));
         o_pb[p] = qoff(QS_POLY + 15 * p + 7 + (t < 7 ? t : 0));
     }
+    // fields in a slot image: the sweep's run; the wide ring also needs the unpacked poly slot state
+    auto ring_nf = [](auto nfc) { return (NPM <= 2) ? decltype(nfc)::value : WF_LP + 1; };
     auto glds_stage = [&](int k, int slot, auto nfc) {
-        constexpr int G = LG(decltype(nfc)::value);
-        const char* qk = (const char*)(QSb + (size_t)k * QS + QS_YLB) + (t & 7) * 16 + (t >> 3) * 128;
+        constexpr int G = LG(ring_nf(nfc), QL);
+        const char* qk = (const char*)(QSb + (size_t)k * QS + QB) + (t & 7) * 16 + (t >> 3) * 128;
         const char* wk = (const char*)(WSb + (size_t)k * IS) + (t & 7) * 16 + (t >> 3) * 128;
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // reads of the slot's previous stage retired
         const unsigned dst = lds_base + (unsigned)(slot * G) * 1024u;
-        GldsBatch<0, G, QLINES / 2>::run(qk, wk, dst);
+        GldsBatch<0, G, QL / 2>::run(qk, wk, dst);
     };
     auto lds_common = [&](const double* im, In& o) {
         o.lb = im[o_lb];
@@ -524,21 +545,29 @@ __device__ __forceinline__ void ipm_group(const DevConst& c, const DevBuffers& d
         o.np = im[o_np];
 #pragma unroll
         for (int p = 0; p < NPE; p++) {
-            const double a = im[o_pa[p]], bv = im[o_pb[p]];
+            // the wide ring computes the offsets per use (22 offsets held through the solve spilled)
+            const int opa = (NPM <= 2) ? o_pa[p] : qoff(QS_POLY + 15 * p + (t < 7 ? t : 0));
+            const int opb = (NPM <= 2) ? o_pb[p] : qoff(QS_POLY + 15 * p + 7 + (t < 7 ? t : 0));
+            const double a = im[opa], bv = im[opb];
             o.pa[p] = (NPM > 0 && t < 7) ? a : 0.0;
             o.pb[p] = (NPM > 0 && t < 7) ? bv : 0.0;
         }
         const double pu = im[o_pub];
         o.pub = (t < NPM) ? pu : INF;
-        auto f = [&](int field) { return im[img_at(QLINES + field) + t]; };
+        auto f = [&](int field) { return im[img_at(QL + field) + t]; };
         o.sL = f(WF_SL); o.lL = f(WF_LL); o.sU = f(WF_SU); o.lU = f(WF_LU);
         o.zx = f(WF_ZX);
         const double zraw = f(WF_ZV);
-        o.sP = from_up<8>(zraw);   // PACKP: lane p <- lane 8 + p
-        o.lP = from_up<12>(zraw);  // lane p <- lane 12 + p
-        o.zv = (t < 8) ? zraw : 0.0;
+        if constexpr (PACKP) {
+            o.sP = from_up<8>(zraw);   // lane p <- lane 8 + p
+            o.lP = from_up<12>(zraw);  // lane p <- lane 12 + p
+            o.zv = (t < 8) ? zraw : 0.0;
+        } else {
+            o.sP = f(WF_SP); o.lP = f(WF_LP);
+            o.zv = zraw;
+        }
     };
-    auto fld = [&](const double* im, int field) { return im[img_at(QLINES + field) + t]; };
+    auto fld = [&](const double* im, int field) { return im[img_at(QL + field) + t]; };
     auto lds_fwd = [&](const double* im, In& o, bool corr) {
         lds_common(im, o);
 #pragma unroll
@@ -561,19 +590,19 @@ __device__ __forceinline__ void ipm_group(const DevConst& c, const DevBuffers& d
     // s(i + 2), stage s(i) has landed once at most 2 G memory operations are outstanding (the bodies'
     // stores only make that wait stricter).  The extra loads are drained before the ring's LDS is reused.
     auto lds_sweep = [&](bool backward, auto nfc, auto read, auto body) {
-        constexpr int G = LG(decltype(nfc)::value);
+        constexpr int G = LG(ring_nf(nfc), QL);
         auto s = [&](int i) { return backward ? N - i : i; };
         auto cl = [&](int i) { return s(i <= N ? i : N); };
-        glds_stage(cl(0), 0, nfc);
-        glds_stage(cl(1), 1, nfc);
+#pragma unroll
+        for (int j = 0; j < RD - 1; j++) glds_stage(cl(j), j, nfc);
         int slot = 0;
         for (int i = 0; i <= N; i++) {
-            glds_stage(cl(i + 2), slot == 0 ? 2 : slot - 1, nfc);
-            asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * G) : "memory");
+            glds_stage(cl(i + RD - 1), slot == 0 ? RD - 1 : slot - 1, nfc);
+            asm volatile("s_waitcnt vmcnt(%0)" ::"n"((RD - 1) * G) : "memory");
             In o;
             read(smem + slot * G * 128 + grp * 32, o);
             body(s(i), o);
-            slot = slot == 2 ? 0 : slot + 1;
+            slot = slot == RD - 1 ? 0 : slot + 1;
         }
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     };
@@ -645,7 +674,7 @@ __device__ __forceinline__ void ipm_group(const DevConst& c, const DevBuffers& d
     // are short bodies that wait on their stage loads: they keep MPCC_LIGHT_DEPTH - 1 stages in flight
     In ring[MPCC_LIGHT_DEPTH];
     auto light_sweep = [&](bool backward, auto nfc, auto load, auto read, auto body) {
-        if constexpr (NPM <= 2) lds_sweep(backward, nfc, read, body);
+        if constexpr (use_ring(NPM)) lds_sweep(backward, nfc, read, body);
         else if constexpr (MPCC_WIDE_LIGHT_NOPF) sweep_noprefetch(N, backward, cur, load, body);
         else sweep<false>(N, backward, cur, nxt, load, body);
     };
