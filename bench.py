@@ -33,6 +33,22 @@ def q_start(dof):
     return Q0 if dof == 7 else np.concatenate([np.zeros(dof - 7), Q0])
 
 
+def find_traffic(kname, B, N, mask, dof, override=None, prof_dir=None):
+    """HBM bytes per launch from the committed PMC summary of this workload (tools/pmc_summary.py): the
+    first pmc_traffic_<kernel>*.json whose kernel, batch, horizon, constraint mask and DOF match, or None."""
+    prof_dir = prof_dir or os.path.join(ROOT, "profiles")
+    tpaths = [override] if override else sorted(glob.glob(os.path.join(prof_dir, f"pmc_traffic_{kname}*.json")))
+    for tpath in tpaths:
+        if not os.path.exists(tpath):
+            continue
+        with open(tpath) as f:
+            tr = json.load(f)
+        if (tr.get("batch") == B and tr.get("N") == N and tr.get("mask") == mask
+                and tr.get("kernel", "k_ipm") == kname and tr.get("dof", 7) == dof):
+            return tr.get("hbm_bytes_per_launch")
+    return None
+
+
 def algorithmic_qp_flops(N, dof=7):
     """SURVEY.md §8(d) F_qp per SQP iteration (condensing + Cholesky + solves; inequality handling is
     solver overhead and not credited): 2(96N^3 + 324N^2) + 616N^2 + n^3/3 + 4n^2, n = 8N for the Panda,
@@ -331,19 +347,7 @@ def main():
     launches_per_step = max(1, nipm) / max(1, ncalls)
     flops = qps * algorithmic_qp_flops(N, dof) / launches_per_step
     achieved = flops / t_ipm / 1e12
-    traffic = None
-    # the committed PMC summary of this workload (tools/pmc_summary.py): the first file whose kernel, batch,
-    # horizon and constraint mask match this run, or null
-    tpaths = [args.traffic] if args.traffic else sorted(glob.glob(os.path.join(ROOT, "profiles", f"pmc_traffic_{kname}*.json")))
-    for tpath in tpaths:
-        if not os.path.exists(tpath):
-            continue
-        with open(tpath) as f:
-            tr = json.load(f)
-        if (tr.get("batch") == B and tr.get("N") == N and tr.get("mask") == args.mask
-                and tr.get("kernel", "k_ipm") == kname and tr.get("dof", 7) == dof):
-            traffic = tr.get("hbm_bytes_per_launch")
-            break
+    traffic = find_traffic(kname, B, N, args.mask, dof, args.traffic)
     roof = {"kernel": kname, "bound": "mfma", "achieved": achieved, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
             "frac": achieved / FP64_PEAK_TFLOPS, "traffic": traffic,
             "avg_launch_ms": t_ipm * 1e3, "launches_timed": nipm, "algorithmic_flops_per_launch": flops,
