@@ -33,9 +33,10 @@ def q_start(dof):
     return Q0 if dof == 7 else np.concatenate([np.zeros(dof - 7), Q0])
 
 
-def find_traffic(kname, B, N, mask, dof, override=None, prof_dir=None):
-    """HBM bytes per launch from the committed PMC summary of this workload (tools/pmc_summary.py): the
-    first pmc_traffic_<kernel>*.json whose kernel, batch, horizon, constraint mask and DOF match, or None."""
+def find_pmc(kname, B, N, mask, dof, override=None, prof_dir=None):
+    """The committed PMC summary of this workload (tools/pmc_summary.py): the first pmc_traffic_<kernel>*.json
+    whose kernel, batch, horizon, constraint mask and DOF match, with the per-launch counters of the summary it
+    names ("source"), or None."""
     prof_dir = prof_dir or os.path.join(ROOT, "profiles")
     tpaths = [override] if override else sorted(glob.glob(os.path.join(prof_dir, f"pmc_traffic_{kname}*.json")))
     for tpath in tpaths:
@@ -45,8 +46,39 @@ def find_traffic(kname, B, N, mask, dof, override=None, prof_dir=None):
             tr = json.load(f)
         if (tr.get("batch") == B and tr.get("N") == N and tr.get("mask") == mask
                 and tr.get("kernel", "k_ipm") == kname and tr.get("dof", 7) == dof):
-            return tr.get("hbm_bytes_per_launch")
+            src = os.path.join(ROOT, tr["source"]) if tr.get("source") else None
+            if src and os.path.exists(src):
+                with open(src) as f:
+                    tr["counters"] = json.load(f).get("counters_avg_per_launch", {})
+            tr["file"] = os.path.relpath(tpath, ROOT)
+            return tr
     return None
+
+
+def find_traffic(kname, B, N, mask, dof, override=None, prof_dir=None):
+    """HBM bytes per launch from the matching PMC summary (find_pmc), or None."""
+    tr = find_pmc(kname, B, N, mask, dof, override, prof_dir)
+    return tr.get("hbm_bytes_per_launch") if tr else None
+
+
+def pmc_fp64_flops(counters):
+    """FP64 flops per launch from the VALU instruction counters: 64 lanes x (ADD + MUL + 2 FMA) wave
+    instructions (an upper bound: lanes masked off inside a 16-lane group are counted), or None."""
+    if not counters or "SQ_INSTS_VALU_FMA_F64" not in counters:
+        return None
+    return 64.0 * (counters["SQ_INSTS_VALU_ADD_F64"] + counters["SQ_INSTS_VALU_MUL_F64"] +
+                   2.0 * counters["SQ_INSTS_VALU_FMA_F64"])
+
+
+HBM_PEAK_BPS = 8.0e12  # MI355X HBM3E peak (spec), MI355X_MICROARCH.md
+
+
+def mlp_flops_per_sample(which, dof=7):
+    """value + the DOF forward-mode Jacobian columns of one collision-MLP sample.
+    self: 21 -> 256 -> 64 -> 1; env: 30 -> 256 x 4 -> 9 (F_self 0.285, F_env 3.21 MFLOP for the Panda)."""
+    if which == "k_mlp_self":
+        return 2 * (256 * 21 + 64 * 256 + 64 + dof * 256 * 3 + dof * 64 * 256 + dof * 64)
+    return 2 * (256 * 30 + 3 * 256 ** 2 + 9 * 256 + dof * 256 * 3 + dof * 3 * 256 ** 2 + dof * 9 * 256)
 
 
 def algorithmic_qp_flops(N, dof=7):
@@ -328,6 +360,7 @@ def main():
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
     tm, ncalls, nipm = eng.timing_end()
+    tmlp = eng.timing_mlp()
     if world > 1:
         elapsed = max_over_ranks(elapsed, device=dev)
 
@@ -337,8 +370,10 @@ def main():
     value = B * world * args.steps / elapsed
     ms = elapsed / args.steps * 1e3
 
-    # roofline of the dominant kernel: k_sqp (the SQP loop with its interior-point QP solves, 16 lanes
-    # per instance), or k_ipm alone when the staged SQP loop is selected (MPCC_STAGED_SQP=1)
+    # Roofline of the dominant kernel, by measured time per step: k_sqp (the SQP loop with its interior-point
+    # QP solves, 16 lanes per instance; k_ipm alone when the staged SQP loop is selected, MPCC_STAGED_SQP=1) or,
+    # with the collision networks on (configs[2]), k_mlp_env.  Launch durations are HIP events on the engine
+    # stream around those launches alone, over the timed steps.
     kname = "k_ipm" if os.environ.get("MPCC_STAGED_SQP", "0") == "1" else "k_sqp"
     t_ipm = tm["solve_qp"] / max(1, nipm)
     # QP solves per step: an instance solves min(sqp_iter + 1, max_iter) QPs (a SOLVED exit at SQP
@@ -347,11 +382,34 @@ def main():
     launches_per_step = max(1, nipm) / max(1, ncalls)
     flops = qps * algorithmic_qp_flops(N, dof) / launches_per_step
     achieved = flops / t_ipm / 1e12
-    traffic = find_traffic(kname, B, N, args.mask, dof, args.traffic)
-    roof = {"kernel": kname, "bound": "mfma", "achieved": achieved, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
+    pmc = find_pmc(kname, B, N, args.mask, dof, args.traffic)
+    traffic = pmc.get("hbm_bytes_per_launch") if pmc else None
+    pflops = pmc_fp64_flops(pmc.get("counters")) if pmc else None
+    # k_sqp is a latency-bound FP64 VALU + DPP kernel (no MFMA in it): its roof is the FP64 vector peak, its
+    # work the SURVEY's condensed-dense F_qp per QP actually solved; the PMC-counted FP64 flops it executed and
+    # its HBM fraction (PMC traffic / launch time / 8 TB/s) are reported beside it
+    roof = {"kernel": kname, "bound": "valu", "achieved": achieved, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
             "frac": achieved / FP64_PEAK_TFLOPS, "traffic": traffic,
+            "hbm_frac": (traffic / t_ipm / HBM_PEAK_BPS) if traffic else None,
+            "pmc_fp64_flops_per_launch": pflops,
+            "pmc_fp64_frac": (pflops / t_ipm / 1e12 / FP64_PEAK_TFLOPS) if pflops else None,
+            "pmc_source": pmc.get("file") if pmc else None,
             "avg_launch_ms": t_ipm * 1e3, "launches_timed": nipm, "algorithmic_flops_per_launch": flops,
+            "work": "F_qp (SURVEY 8(d), condensed-dense QP) x QPs solved per launch",
             "qp_solves_per_step": qps}
+    t_env, n_env = tmlp["k_mlp_env"]
+    if n_env and t_env / max(1, ncalls) > tm["solve_qp"] / max(1, ncalls):  # env MLP dominates (configs[2])
+        t_l = t_env / n_env
+        samples = B * (N + 1)
+        fl = samples * mlp_flops_per_sample("k_mlp_env", dof)
+        pm = find_pmc("k_mlp_env", B, N, args.mask, dof)
+        tr = pm.get("hbm_bytes_per_launch") if pm else None
+        roof = {"kernel": "k_mlp_env", "bound": "mfma", "achieved": fl / t_l / 1e12, "peak": FP64_PEAK_TFLOPS,
+                "unit": "TFLOP/s", "frac": fl / t_l / 1e12 / FP64_PEAK_TFLOPS, "traffic": tr,
+                "hbm_frac": (tr / t_l / HBM_PEAK_BPS) if tr else None, "avg_launch_ms": t_l * 1e3,
+                "launches_timed": n_env, "algorithmic_flops_per_launch": fl,
+                "work": "F_env (SURVEY 8(d): value + DOF Jacobian columns) x B (N+1) samples",
+                "k_sqp": {"avg_launch_ms": t_ipm * 1e3, "frac": achieved / FP64_PEAK_TFLOPS, "traffic": traffic}}
 
     # PCIe-inclusive rate (host buffers in and out through mpcc_solve): a diagnostic, never `value`
     pcie = None
@@ -388,6 +446,7 @@ def main():
 
     if rank == 0:
         phases = {k: round(v / max(1, ncalls) * 1e3, 4) for k, v in tm.items()}
+        phases.update({k: round(v[0] / max(1, ncalls) * 1e3, 4) for k, v in tmlp.items() if v[1]})
         print(json.dumps({"phase_ms_per_step": phases, "solved_frac": solved,
                           "sqp_iter_hist": np.bincount(stats["sqp_iter"], minlength=3).tolist(),
                           "ipm_iters_mean": float(stats["ipm_iters"].mean()),

@@ -198,6 +198,9 @@ int mpcc_set_warmstart_device(mpcc_engine* e, int B, const double* d_guess, cons
  * and the number of calls and of IPM (k_ipm) launches timed. */
 int mpcc_timing_begin(mpcc_engine* e);
 int mpcc_timing_end(mpcc_engine* e, mpcc_timing* sum, int32_t* n_calls, int32_t* n_ipm_launches);
+/* the collision-MLP launches of the last timing window (after mpcc_timing_end): total seconds and launch count of
+ * k_mlp_self and of k_mlp_env, from HIP events around those launches alone on the engine stream */
+int mpcc_timing_mlp(mpcc_engine* e, double* self_s, int32_t* self_n, double* env_s, int32_t* env_n);
 
 /* Per-instance iteration counts of the last solve: SQP iteration index at exit and IPM iterations of
  * the last QP (host arrays, may be NULL). */
@@ -297,6 +300,17 @@ int mpcc_debug_trace_enable(mpcc_engine* e, int enable);
 #endif
 int mpcc_debug_workspace(mpcc_engine* e, int B, double* out);
 int mpcc_debug_trace_get(mpcc_engine* e, int B, double* out /* [B*4*8] */);
+/* bounds-checked build only (mpcc_build_flags() & MPCC_BUILD_BOUNDS_CHECK): OR of the violation bits every kernel
+ * recorded since the last clear (0 = every computed workspace / record / ring / LDS / spline index in range;
+ * bits: csrc/dev_common.h BC_*); MPCC_E_INVALID on a normal build */
+int mpcc_debug_bounds(mpcc_engine* e, uint32_t* flags, int clear);
+
+/* Build provenance (no reference counterpart): a hash of the sources the library was compiled from
+ * (csrc/ and include/, mpcc_manipulator_amd/_build.py source_hash) and the build's variant bits. */
+const char* mpcc_build_id(void);
+#define MPCC_BUILD_BOUNDS_CHECK 1
+#define MPCC_BUILD_PROF 2
+int mpcc_build_flags(void);
 
 #ifdef __cplusplus
 }

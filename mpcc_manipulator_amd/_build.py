@@ -10,7 +10,11 @@ PKG = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(PKG)
 CSRC = os.path.join(PKG, "csrc")
 PROF = os.environ.get("MPCC_PROF_BUILD", "0") == "1"  # cycle-accounting variant (tools/ipm_prof.py)
-BUILD = os.path.join(PKG, "_build_prof" if PROF else "_build")
+# bounds-checked variant: every computed workspace / record / ring / LDS / spline index is tested and clamped,
+# violations are recorded per lane (dev_common.h MPCC_BCHK, mpcc_debug_bounds); tests load it through
+# MPCC_ENGINE_LIB / MPCC_ENGINE_LIB_MOBILE (tools/bounds_check.sh)
+BCHK = os.environ.get("MPCC_BOUNDS_CHECK", "0") == "1"
+BUILD = os.path.join(PKG, "_build_prof" if PROF else ("_build_bchk" if BCHK else "_build"))
 LIB = os.path.join(BUILD, "libmpcc_engine.so")
 SOURCES = ["kernels.hip", "ipm.hip", "ipm_wide.hip", "mlp.hip", "nn_generic.hip", "engine.cpp", "host_params.cpp",
            "host_spline.cpp", "mpc.cpp"]
@@ -27,8 +31,29 @@ HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 # oracle's operation order without FMA contraction, so their discrete decisions (projection Newton,
 # warm-start validity, filter comparisons) see the same values as the reference CPU arithmetic.
 FILE_FLAGS = {"kernels.hip": ["-ffp-contract=off"], "mlp.hip": ["-ffp-contract=off"], "nn_generic.hip": ["-ffp-contract=off"]}
+
+
+def source_hash():
+    """Build provenance: sha256 (first 16 hex digits) over the product sources and headers (csrc/, include/),
+    file names and contents in sorted order.  Compiled into the libraries as mpcc_build_id(); the tests check
+    that the library they load was built from the tree they run in (tests/conftest.py built_lib)."""
+    import hashlib
+    h = hashlib.sha256()
+    for d in (CSRC, os.path.join(ROOT, "include")):
+        for f in sorted(os.listdir(d)):
+            p = os.path.join(d, f)
+            if os.path.isfile(p) and f.endswith((".h", ".hpp", ".hip", ".cpp")):
+                h.update(f.encode() + b"\0")
+                with open(p, "rb") as fh:
+                    h.update(fh.read())
+                h.update(b"\0")
+    return h.hexdigest()[:16]
+
+
+BUILD_ID = source_hash()
 CFLAGS = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-I", os.path.join(ROOT, "include"),
-          "-I", CSRC, "-Wno-unused-result"] + (["-DMPCC_IPM_PROF"] if PROF else [])
+          "-I", CSRC, "-Wno-unused-result"] + (["-DMPCC_IPM_PROF"] if PROF else []) + \
+         (["-DMPCC_BOUNDS_CHECK"] if BCHK else [])
 
 
 def _compile(src, variant=""):
@@ -37,11 +62,15 @@ def _compile(src, variant=""):
     deps = [path] + [os.path.join(CSRC, h) for h in os.listdir(CSRC) if h.endswith(".h")]
     inc = os.path.join(ROOT, "include")
     deps += [os.path.join(inc, h) for h in os.listdir(inc)]
+    idf = []
+    if src == "engine.cpp":  # carries mpcc_build_id(): rebuilt whenever any product source changes
+        deps += [os.path.join(CSRC, f) for f in os.listdir(CSRC)]
+        idf = [f'-DMPCC_BUILD_ID="{BUILD_ID}"']
     if os.path.exists(obj) and os.path.getmtime(obj) >= max(os.path.getmtime(d) for d in deps):
         return obj
     lang = ["-x", "hip"] if src.endswith(".cpp") else []
     extra = MOBILE_FLAGS if variant == "_mobile" else []
-    cmd = [HIPCC] + CFLAGS + extra + lang + FILE_FLAGS.get(src, []) + ["-c", path, "-o", obj]
+    cmd = [HIPCC] + CFLAGS + extra + idf + lang + FILE_FLAGS.get(src, []) + ["-c", path, "-o", obj]
     r = subprocess.run(cmd, capture_output=True, text=True)
     if r.returncode != 0:
         raise RuntimeError(f"compile failed: {' '.join(cmd)}\n{r.stdout}\n{r.stderr}")

@@ -68,11 +68,17 @@ constexpr int SPL_A = NSPL, SPL_R = 13 * NSPL, SPL_CR = 22 * NSPL, SPL_DR = 23 *
 struct SplineDev {
     const double* base;
     long stride;
+#ifdef MPCC_BOUNDS_CHECK
+    uint32_t* err;
+#endif
 };
 // one track (cubic_spline.cpp / cubic_spline_rot.cpp tables of the final regular fit)
 struct SplineView {
     const double* t;
     double delta, L;
+#ifdef MPCC_BOUNDS_CHECK
+    uint32_t* err;
+#endif
     __device__ __forceinline__ double s(int i) const { return t[i]; }
     __device__ __forceinline__ double a(int ax, int i) const { return t[SPL_A + 4 * NSPL * ax + i]; }
     __device__ __forceinline__ double b(int ax, int i) const { return t[SPL_A + 4 * NSPL * ax + NSPL + i]; }
@@ -85,7 +91,11 @@ struct SplineView {
 };
 __device__ __forceinline__ SplineView spl_of(const SplineDev& sp, int b) {
     const double* t = sp.base + (size_t)b * sp.stride;
+#ifdef MPCC_BOUNDS_CHECK
+    return {t, t[SPL_DELTA], t[SPL_L], sp.err};
+#else
     return {t, t[SPL_DELTA], t[SPL_L]};
+#endif
 }
 
 // Everything a kernel needs that is constant over a batch call (passed by value).
@@ -99,7 +109,28 @@ struct DevConst {
     int Bn;                          // batch size of this call
     int faithful_dead_trials;
     int ocp;                         // 1: SolverInterface::solveOCP only (mpcc_solve_ocp), no MPC bookkeeping
+    uint32_t* bchk;                  // bounds-checked build: per-lane violation bits (null otherwise)
 };
+
+// ---- bounds-checked build (MPCC_BOUNDS_CHECK=1 python -m mpcc_manipulator_amd._build -> _build_bchk/): every
+//      computed index into a workspace, QP record, low-rank buffer, LDS block / ring or spline table is tested
+//      against its extent.  A violation ORs its bit into the lane's word of c.bchk (a vector atomic on a
+//      per-lane address) and the index is clamped, so the kernel stays inside its buffers and the host reads
+//      the bits afterwards (mpcc_debug_bounds).  Normal builds compile MPCC_BCHK to the index itself.
+enum : uint32_t {
+    BC_WS_STAGE = 1, BC_WS_FIELD = 2, BC_QS_STAGE = 4, BC_LR = 8, BC_LDS = 16, BC_RING = 32, BC_SPLINE = 64,
+    BC_INSTANCE = 128, BC_QS_FIELD = 256
+};
+#ifdef MPCC_BOUNDS_CHECK
+__device__ __forceinline__ long bchk_idx(uint32_t* err, long i, long n, uint32_t code) {
+    if (i >= 0 && i < n) return i;
+    if (err) __hip_atomic_fetch_or(err + (threadIdx.x & 63), code, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return i < 0 ? 0 : n - 1;
+}
+#define MPCC_BCHK(err, i, n, code) ((int)bchk_idx((err), (long)(i), (long)(n), (code)))
+#else
+#define MPCC_BCHK(err, i, n, code) (i)
+#endif
 
 // ------------------------------------------------------------------------------------------------
 __device__ __forceinline__ double wave_sum(double v) {

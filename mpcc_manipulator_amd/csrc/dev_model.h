@@ -356,7 +356,7 @@ __device__ __forceinline__ double spl_unwrap(const SplineView& sp, double x) {
 }
 __device__ __forceinline__ int spl_index(const SplineView& sp, double x) {
     if (x == sp.L) return NSPL - 1;
-    return (int)floor(x / sp.delta);
+    return MPCC_BCHK(sp.err, (int)floor(x / sp.delta), NSPL, BC_SPLINE);
 }
 // position, first and second derivative of the x/y/z splines at arc length t
 __device__ inline void spline_pos3(const SplineView& sp, double t, double* p, double* dp, double* ddp) {

@@ -59,6 +59,8 @@ struct mpcc_engine {
     // (MPCC_STAGED_SQP=1; same arithmetic, kept for A/B timing and debugging)
     bool staged_sqp = false;
     bool wide_sqp = false;  // MPCC_WIDE_SQP=1: the 32-lane fused kernel for the Panda build too (experiment)
+    bool last_wide = DOF != 7;  // the last solve's interior point ran on the 32-lane workspace (d.isw)
+    uint32_t* bchk = nullptr;  // bounds-checked build: per-lane violation bits (dev_common.h MPCC_BCHK)
     mpcc_params params{};
     int N = 0, maxB = 0;
     hipStream_t stream = nullptr;
@@ -80,6 +82,9 @@ struct mpcc_engine {
     std::vector<hipEvent_t> live_pool;
     size_t live_used = 0;
     std::vector<std::pair<hipEvent_t, hipEvent_t>> lv_env, lv_setqp, lv_ipm, lv_alpha, lv_total;
+    std::vector<std::pair<hipEvent_t, hipEvent_t>> lv_mlp_self, lv_mlp_env;  // the collision-MLP launches alone
+    double last_mlp_self_s = 0, last_mlp_env_s = 0;                         // totals of the last timing window
+    int last_mlp_self_n = 0, last_mlp_env_n = 0;
     int live_calls = 0;
     hipEvent_t live_ev() {
         if (live_used == live_pool.size()) {
@@ -97,6 +102,7 @@ struct mpcc_engine {
         if (d.isw != d.is) f(d.isw);
         f(d.lr); f(d.lrc); f(d.glam); f(d.gprev); f(d.aty); f(d.sp);
         f(d.dbg_trace);
+        f(bchk);
         f(s_x0); f(s_u0); f(s_obs); f(s_u0out); f(s_hor); f(s_status); f(s_ok);
         f(nn_self.d); f(nn_env.d);
         for (auto ev : events) (void)hipEventDestroy(ev);
@@ -154,6 +160,10 @@ struct mpcc_engine {
         std::memcpy(c.M, M, sizeof M);
         std::memcpy(c.G, G, sizeof G);
         c.spl = spl;
+        c.bchk = bchk;
+#ifdef MPCC_BOUNDS_CHECK
+        c.spl.err = bchk;
+#endif
         c.N = N;
         c.Bn = Bn;
         c.S = Bn * (N + 1);
@@ -350,10 +360,18 @@ void run_batch(mpcc_engine* e, int B, hipStream_t st, mpcc_timing* timing, bool 
     launch_prepare(c, d, st);
     if (tm) t_env0 = mark();
     launch_stage_records(c, d, st);
+    int m0 = -1, m1 = -1, m2 = -1;
+    if (e->live) m0 = mark();
     if (c.p.constraint_mask & MPCC_CON_SELFCOL)
         launch_nn(c, d, e->nn_self.desc, e->nn_self.d, 0, c.S, nullptr, nullptr, d.rec, c.S, st);
+    if (e->live) m1 = mark();
     if (c.p.constraint_mask & MPCC_CON_ENVCOL)
         launch_nn(c, d, e->nn_env.desc, e->nn_env.d, 1, c.S, nullptr, nullptr, d.rec, c.S, st);
+    if (e->live) {
+        m2 = mark();
+        if (c.p.constraint_mask & MPCC_CON_SELFCOL) e->lv_mlp_self.push_back({evs[m0], evs[m1]});
+        if (c.p.constraint_mask & MPCC_CON_ENVCOL) e->lv_mlp_env.push_back({evs[m1], evs[m2]});
+    }
     if (tm) t_env1 = mark();
     const double* ucur = d.u0;
     if (!e->staged_sqp || c.p.use_BFGS) {
@@ -363,6 +381,7 @@ void run_batch(mpcc_engine* e, int B, hipStream_t st, mpcc_timing* timing, bool 
         if (tm) a0 = mark();
         launch_setqp(c, d, ucur, st);
         if (tm) a1 = mark();
+        e->last_wide = DOF != 7 || c.p.use_BFGS || e->wide_sqp;
         if (c.p.use_BFGS || e->wide_sqp) launch_sqp_wide(c, d, ucur, poly_rows_max(c.p.constraint_mask), c.p.use_BFGS ? 1 : 0, st);
         else launch_sqp(c, d, ucur, poly_rows_max(c.p.constraint_mask), st);
         if (tm) {
@@ -500,6 +519,10 @@ int mpcc_create(const mpcc_config* cfg, const mpcc_params* params, const char* n
         HIPCHK(hipMemset(d.fails, 0, B * sizeof(int32_t)));
         HIPCHK(hipMemset(d.sqi, 0, B * SQI * sizeof(int32_t)));
         if (DOF != 7) d.isw = d.is;  // the mobile build's interior point is the 32-lane one
+#ifdef MPCC_BOUNDS_CHECK
+        e->bchk = dmalloc<uint32_t>(64);
+        HIPCHK(hipMemset(e->bchk, 0, 64 * sizeof(uint32_t)));
+#endif
         if (e->params.use_BFGS || e->wide_sqp) e->ensure_bfgs_buffers();
         e->s_x0 = dmalloc<double>(B * NX);
         e->s_u0 = dmalloc<double>(B * NU);
@@ -790,6 +813,7 @@ int mpcc_timing_begin(mpcc_engine* e) {
     e->live_used = 0;
     e->live_calls = 0;
     e->lv_env.clear(); e->lv_setqp.clear(); e->lv_ipm.clear(); e->lv_alpha.clear(); e->lv_total.clear();
+    e->lv_mlp_self.clear(); e->lv_mlp_env.clear();
     return MPCC_OK;
 }
 
@@ -813,6 +837,10 @@ int mpcc_timing_end(mpcc_engine* e, mpcc_timing* sum, int32_t* n_calls, int32_t*
         t.set_qp = acc(e->lv_setqp);
         t.solve_qp = acc(e->lv_ipm);
         t.get_alpha = acc(e->lv_alpha);
+        e->last_mlp_self_s = acc(e->lv_mlp_self);
+        e->last_mlp_env_s = acc(e->lv_mlp_env);
+        e->last_mlp_self_n = (int)e->lv_mlp_self.size();
+        e->last_mlp_env_n = (int)e->lv_mlp_env.size();
         if (sum) *sum = t;
         if (n_calls) *n_calls = e->live_calls;
         if (n_ipm) *n_ipm = (int32_t)e->lv_ipm.size();
@@ -1173,6 +1201,7 @@ static int debug_solve_qp(mpcc_engine* e, int B, const double* guess, const doub
             HIPCHK(hipMemcpy(e->d.sqi, sqi.data(), sqi.size() * sizeof(int32_t), hipMemcpyHostToDevice));
         }
         launch_setqp(c, e->d, e->s_u0, st);
+        e->last_wide = DOF != 7 || nlr >= 0;
         if (nlr >= 0) launch_ipm_wide(c, e->d, poly_rows_max(c.p.constraint_mask), 1, st);
         else launch_ipm(c, e->d, poly_rows_max(c.p.constraint_mask), st);
         HIPCHK(hipStreamSynchronize(st));
@@ -1226,6 +1255,11 @@ int mpcc_debug_trace_get(mpcc_engine* e, int B, double* out) {
 
 int mpcc_debug_workspace(mpcc_engine* e, int B, double* out) {
     if (!e || !out || B < 1 || B > e->cfg.max_batch) return fail(MPCC_E_INVALID, "mpcc_debug_workspace: invalid argument");
+    // the Panda library's BFGS / MPCC_WIDE_SQP solves use the 32-lane workspace (ISW doubles per stage), which
+    // does not fit the caller's [B*(N+1)*MPCC_IPM_WS] buffer: refused rather than returning the stale 16-lane one
+    if (DOF == 7 && e->last_wide)
+        return fail(MPCC_E_INVALID, "mpcc_debug_workspace: the last solve used the 32-lane interior point (use_BFGS / "
+                                    "MPCC_WIDE_SQP); its workspace is not in the 16-lane layout");
     DevGuard dg_(e);
     try {
         HIPCHK(hipDeviceSynchronize());
@@ -1233,5 +1267,47 @@ int mpcc_debug_workspace(mpcc_engine* e, int B, double* out) {
     } catch (const std::exception& x) {
         return fail(MPCC_E_HIP, std::string("mpcc_debug_workspace: ") + x.what());
     }
+    return MPCC_OK;
+}
+
+int mpcc_debug_bounds(mpcc_engine* e, uint32_t* flags, int clear) {
+    if (!e || !flags) return fail(MPCC_E_INVALID, "mpcc_debug_bounds: null argument");
+    if (!e->bchk) return fail(MPCC_E_INVALID, "mpcc_debug_bounds: not a bounds-checked build (MPCC_BOUNDS_CHECK)");
+    DevGuard dg_(e);
+    try {
+        HIPCHK(hipDeviceSynchronize());
+        uint32_t w[64];
+        HIPCHK(hipMemcpy(w, e->bchk, sizeof w, hipMemcpyDeviceToHost));
+        uint32_t o = 0;
+        for (uint32_t x : w) o |= x;
+        *flags = o;
+        if (clear) HIPCHK(hipMemset(e->bchk, 0, sizeof w));
+    } catch (const std::exception& x) {
+        return fail(MPCC_E_HIP, std::string("mpcc_debug_bounds: ") + x.what());
+    }
+    return MPCC_OK;
+}
+
+#ifndef MPCC_BUILD_ID
+#define MPCC_BUILD_ID "unknown"
+#endif
+const char* mpcc_build_id(void) { return MPCC_BUILD_ID; }
+int mpcc_build_flags(void) {
+    int f = 0;
+#ifdef MPCC_BOUNDS_CHECK
+    f |= MPCC_BUILD_BOUNDS_CHECK;
+#endif
+#ifdef MPCC_IPM_PROF
+    f |= MPCC_BUILD_PROF;
+#endif
+    return f;
+}
+
+int mpcc_timing_mlp(mpcc_engine* e, double* self_s, int32_t* self_n, double* env_s, int32_t* env_n) {
+    if (!e) return fail(MPCC_E_INVALID, "mpcc_timing_mlp: null engine");
+    if (self_s) *self_s = e->last_mlp_self_s;
+    if (self_n) *self_n = e->last_mlp_self_n;
+    if (env_s) *env_s = e->last_mlp_env_s;
+    if (env_n) *env_n = e->last_mlp_env_n;
     return MPCC_OK;
 }

@@ -355,7 +355,7 @@ __device__ __forceinline__ void ipm_group(const DevConst& c, const DevBuffers& d
     // to global_* instructions, which count only in vmcnt.  Through the generic pointers of DevBuffers they
     // were flat_*, which also count in lgkmcnt, so every LDS wait (lgkmcnt(0), the U/K reads of the factor
     // sweep) drained the in-flight stage prefetch as well.
-    const gdouble* QSb = (const gdouble*)(d.qs + (size_t)(valid ? b : 0) * NS * QS);
+    const gdouble* QSb = (const gdouble*)(d.qs + (size_t)MPCC_BCHK(c.bchk, valid ? b : 0, c.Bn, BC_INSTANCE) * NS * QS);
     gdouble* WSb = (gdouble*)(d.is + (size_t)(valid ? b : 0) * NS * IS);
     // Stage base addresses pass through an empty asm: the optimizer cannot strength-reduce every
     // (field, stage) address into its own 64-bit induction variable.  It did, ran out of registers,
@@ -363,12 +363,12 @@ __device__ __forceinline__ void ipm_group(const DevConst& c, const DevBuffers& d
     // prefetch.  Fields are then immediate offsets from one stage pointer.
     gdouble* const WSt = WSb + t;
     auto ws = [&](int k, int f) -> gdouble* {
-        gdouble* wk = WSt + (size_t)k * IS;
+        gdouble* wk = WSt + (size_t)MPCC_BCHK(c.bchk, k, NS, BC_WS_STAGE) * IS;
         asm("" : "+v"(wk));
-        return wk + f * 16;
+        return wk + MPCC_BCHK(c.bchk, f, NWF, BC_WS_FIELD) * 16;
     };
     auto qs_stage = [&](int k) -> const gdouble* {
-        const gdouble* qk = QSb + (size_t)k * QS;
+        const gdouble* qk = QSb + (size_t)MPCC_BCHK(c.bchk, k, NS, BC_QS_STAGE) * QS;
         asm("" : "+v"(qk));
         return qk;
     };
@@ -533,6 +533,12 @@ __device__ __forceinline__ void ipm_group(const DevConst& c, const DevBuffers& d
     auto ring_nf = [](auto nfc) { return (NPM <= 2) ? decltype(nfc)::value : WF_LP + 1; };
     auto glds_stage = [&](int k, int slot, auto nfc) {
         constexpr int G = LG(ring_nf(nfc), QL);
+        // the image's last record line and workspace line stay inside the stage (static), the stage inside the
+        // instance and the slot inside the ring (checked build)
+        static_assert(QB + 16 * 2 * (G > QL / 2 ? QL / 2 : G) <= QS, "ring record lines inside the stage record");
+        static_assert(16 * 2 * (G - QL / 2) <= IS, "ring workspace lines inside the stage workspace");
+        k = MPCC_BCHK(c.bchk, k, NS, BC_RING);
+        slot = MPCC_BCHK(c.bchk, slot, RD, BC_RING);
         const char* qk = (const char*)(QSb + (size_t)k * QS + QB) + (t & 7) * 16 + (t >> 3) * 128;
         const char* wk = (const char*)(WSb + (size_t)k * IS) + (t & 7) * 16 + (t >> 3) * 128;
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // reads of the slot's previous stage retired
@@ -600,7 +606,9 @@ __device__ __forceinline__ void ipm_group(const DevConst& c, const DevBuffers& d
             glds_stage(cl(i + RD - 1), slot == 0 ? RD - 1 : slot - 1, nfc);
             asm volatile("s_waitcnt vmcnt(%0)" ::"n"((RD - 1) * G) : "memory");
             In o;
-            read(smem + slot * G * 128 + grp * 32, o);
+            // the slot's image of this instance (last line of the slot: (G - 1) * 128 + grp * 32 + 16 + 15)
+            static_assert((size_t)RD * G * 1024 <= 160 * 1024, "ring inside the LDS of a CU");
+            read(smem + MPCC_BCHK(c.bchk, slot * G * 128, RD * G * 128 - G * 128 + 1, BC_LDS) + grp * 32, o);
             body(s(i), o);
             slot = slot == RD - 1 ? 0 : slot + 1;
         }

@@ -161,7 +161,16 @@ __device__ __forceinline__ SlotStep slot_corr(double sgn, double bnd, double cz,
     return slot_recover(ri, l, rp, sgn * cd, rc);
 }
 
-// Cholesky of the NU x NU stage F (packed lower triangle), reciprocal pivots; forward / backward solves
+// 1/sqrt(x) for x > 0: v_rsq_f64 refined by two Newton steps (ipm.hip rsqrt_pos)
+__device__ __forceinline__ double rsqrt_pos(double x) {
+    const double h = 0.5 * x;
+    double r = __builtin_amdgcn_rsq(x);
+    r = r * fma(-h * r, r, 1.5);
+    return r * fma(-h * r, r, 1.5);
+}
+
+// Cholesky of the NU x NU stage F (packed lower triangle), reciprocal pivots (the diagonal of L is not
+// formed: the solves read dinv and the strict lower triangle); forward / backward solves
 __device__ __forceinline__ bool cholN(double* L, double* dinv) {
     bool ok = true;
 #pragma unroll
@@ -171,9 +180,7 @@ __device__ __forceinline__ bool cholN(double* L, double* dinv) {
 #pragma unroll
         for (int m = 0; m < j; m++) d -= L[jj + m] * L[jj + m];
         ok = ok && (d > 0);
-        d = sqrt(d);
-        L[jj + j] = d;
-        const double inv = rcp(d);
+        const double inv = rsqrt_pos(d);
         dinv[j] = inv;
 #pragma unroll
         for (int i = j + 1; i < NU; i++) {
@@ -308,16 +315,16 @@ __device__ __forceinline__ void ipm_group(const DevConst& c, const DevBuffers& d
     bool run = valid && si[SQ_ACTIVE] != 0;
     if (__ballot(run) == 0) return;
 
-    const gdouble* QSb = (const gdouble*)(d.qs + (size_t)(valid ? b : 0) * NS * QS);
+    const gdouble* QSb = (const gdouble*)(d.qs + (size_t)MPCC_BCHK(c.bchk, valid ? b : 0, c.Bn, BC_INSTANCE) * NS * QS);
     gdouble* WSb = (gdouble*)(d.isw + (size_t)(valid ? b : 0) * NS * ISW);
     gdouble* const WSt = WSb + t;
     auto ws = [&](int k, int f) -> gdouble* {
-        gdouble* wk = WSt + (size_t)k * ISW;
+        gdouble* wk = WSt + (size_t)MPCC_BCHK(c.bchk, k, NS, BC_WS_STAGE) * ISW;
         asm("" : "+v"(wk));
-        return wk + f * GW;
+        return wk + MPCC_BCHK(c.bchk, f, NWF, BC_WS_FIELD) * GW;
     };
     auto qs_stage = [&](int k) -> const gdouble* {
-        const gdouble* qk = QSb + (size_t)k * QS;
+        const gdouble* qk = QSb + (size_t)MPCC_BCHK(c.bchk, k, NS, BC_QS_STAGE) * QS;
         asm("" : "+v"(qk));
         return qk;
     };
@@ -387,11 +394,11 @@ __device__ __forceinline__ void ipm_group(const DevConst& c, const DevBuffers& d
     }
     const bool lrw = LR && __ballot(entered && nlr > 0) != 0;  // this wave runs the split (Woodbury) sweeps
     auto u_y = [&](int j, int k) -> double {  // u_j, y part of stage k (lanes < NX)
-        const double v = LRb[((size_t)j * NS + k) * NXU + (rowY ? t : 0)];
+        const double v = LRb[((size_t)MPCC_BCHK(c.bchk, j, LRM, BC_LR) * NS + MPCC_BCHK(c.bchk, k, NS, BC_LR)) * NXU + (rowY ? t : 0)];
         return (LR && rowY && j < nlr) ? v : 0.0;
     };
     auto u_v = [&](int j, int k) -> double {  // u_j, v part of stage k (lanes < NU, k < N)
-        const double v = LRb[((size_t)j * NS + k) * NXU + NX + (t < NU ? t : 0)];
+        const double v = LRb[((size_t)MPCC_BCHK(c.bchk, j, LRM, BC_LR) * NS + MPCC_BCHK(c.bchk, k, NS, BC_LR)) * NXU + NX + (t < NU ? t : 0)];
         return (LR && t < NU && k < N && j < nlr) ? v : 0.0;
     };
     double uz[LRM];  // u_j^T z of the current iterate
@@ -724,7 +731,7 @@ __device__ __forceinline__ void ipm_group(const DevConst& c, const DevBuffers& d
                     //          kff = -F^-1 f; p = g_x~ + A~^T p + K^T f
                     if (t < NU)
 #pragma unroll
-                        for (int i = 0; i < NU; i++) S[L_F + i * 16 + t] = Fc[i];
+                        for (int i = 0; i < NU; i++) S[MPCC_BCHK(c.bchk, L_F + i * 16 + t, L_U, BC_LDS)] = Fc[i];
                     lds_sync();
                     double LF[NU * (NU + 1) / 2], dinv[NU];
 #pragma unroll
@@ -776,7 +783,7 @@ __device__ __forceinline__ void ipm_group(const DevConst& c, const DevBuffers& d
                     }
 #pragma unroll
                     for (int i = 0; i < NU; i++) {
-                        S[L_U + i * GW + t] = u[i];
+                        S[MPCC_BCHK(c.bchk, L_U + i * GW + t, GRP_LDS, BC_LDS)] = u[i];
                         *ws(k, WF_KC + i) = kc[i];
                         *ws(k, WF_FI + i) = fi[i];
                     }

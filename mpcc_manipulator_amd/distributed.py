@@ -31,7 +31,7 @@ def check_equal_shards(n_local: int, device=None, group=None) -> None:
 def gather_u0(u_local: torch.Tensor, world: int, out: torch.Tensor = None, group=None) -> torch.Tensor:
     """All-gather equal-size per-rank u0 blocks [B_local, 8] -> [world * B_local, 8] on every rank
     (check the sizes once with check_equal_shards)."""
-    if world == 1:
+    if world == 1 and not dist.is_initialized():
         return u_local
     if out is not None and out.shape[0] != world * u_local.shape[0]:
         raise ValueError(f"gather_u0: out has {out.shape[0]} rows, expected {world} x {u_local.shape[0]}")

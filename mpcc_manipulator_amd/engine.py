@@ -102,6 +102,14 @@ class MpccError(RuntimeError):
 
 
 _libs = {}
+BUILD_BOUNDS_CHECK, BUILD_PROF = 1, 2
+import weakref  # noqa: E402
+LIVE_CHECKED = weakref.WeakSet()  # engines of a bounds-checked library (tests/conftest.py reads their flags)
+
+
+def build_id(dof=7):
+    """Hash of the sources the loaded library was compiled from (mpcc_manipulator_amd._build.source_hash)."""
+    return lib(dof).mpcc_build_id().decode()
 
 
 def lib(dof=7):
@@ -171,6 +179,10 @@ def lib(dof=7):
         "mpcc_mlp_dims": (C.c_int, [V, IP, IP]),
         "mpcc_mlp_destroy": (None, [V]),
         "mpcc_robot_frames": (C.c_int, [C.c_int, C.c_int, DP, C.c_int, DP, DP, DP, DP, DP]),
+        "mpcc_debug_bounds": (C.c_int, [V, C.POINTER(C.c_uint32), C.c_int]),
+        "mpcc_build_id": (C.c_char_p, []),
+        "mpcc_build_flags": (C.c_int, []),
+        "mpcc_timing_mlp": (C.c_int, [V, C.POINTER(D), IP, C.POINTER(D), IP]),
     }
     for name, (res, args) in sig.items():
         f = getattr(L, name)
@@ -366,6 +378,8 @@ class Engine:
         self.N = int(params.N)
         self.max_batch = int(max_batch)
         self.device = int(device)
+        if self.L.mpcc_build_flags() & BUILD_BOUNDS_CHECK:
+            LIVE_CHECKED.add(self)
 
     def close(self):
         if getattr(self, "h", None):
@@ -550,6 +564,14 @@ class Engine:
         self._check(self.L.mpcc_timing_end(self.h, C.byref(t), C.byref(nc), C.byref(ni)), "mpcc_timing_end")
         return t.as_dict(), nc.value, ni.value
 
+    def timing_mlp(self):
+        """After timing_end: {kernel: (total seconds, launches)} of k_mlp_self / k_mlp_env in that window."""
+        ss, se = C.c_double(), C.c_double()
+        ns, ne = C.c_int32(), C.c_int32()
+        self._check(self.L.mpcc_timing_mlp(self.h, C.byref(ss), C.byref(ns), C.byref(se), C.byref(ne)),
+                    "mpcc_timing_mlp")
+        return {"k_mlp_self": (ss.value, ns.value), "k_mlp_env": (se.value, ne.value)}
+
     def solve_stats(self, B):
         a, b, c = np.zeros(B, np.int32), np.zeros(B, np.int32), np.zeros(B, np.int32)
         self._check(self.L.mpcc_get_solve_stats(self.h, int(B), _ip(a), _ip(b), _ip(c)), "mpcc_get_solve_stats")
@@ -630,6 +652,13 @@ class Engine:
         out = np.zeros(M)
         self._check(self.L.mpcc_debug_project(self.h, M, _dp(sg), _dp(e), _dp(out)), "mpcc_debug_project")
         return out
+
+    def bounds_flags(self, clear=True):
+        """Bounds-checked build (MPCC_BOUNDS_CHECK): OR of the index-violation bits recorded by every kernel since
+        the last clear (0 = every computed index in range; bits: csrc/dev_common.h BC_*)."""
+        f = C.c_uint32(0)
+        self._check(self.L.mpcc_debug_bounds(self.h, C.byref(f), 1 if clear else 0), "mpcc_debug_bounds")
+        return int(f.value)
 
     def workspace(self, B):
         """Interior-point workspace of the last solve, [B, N+1, 816] (Panda; 2048 for the mobile build)."""

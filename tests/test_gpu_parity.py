@@ -411,6 +411,7 @@ def test_config2_full_scale(setup40):
     gf, vf, ff = eng.get_warmstart(B)
     assert np.all(np.isfinite(full["horizon"])) and np.all(np.isfinite(xf))
     assert set(np.unique(full["status"]).tolist()) <= {0, 1, 10, 11}
+    assert np.mean(full["status"] == 0) > 0.97, np.bincount(full["status"])  # bench configs[2]: 99.5% SOLVED
     sub = np.sort(rng.choice(B, 256, replace=False))
     eng.set_warmstart(guess[sub], valid[sub], fails[sub])
     xs = x0[sub].copy()

@@ -133,3 +133,67 @@ def test_device_entry_points_check_tensors(built_lib):
     eng.solve_device(8, x0, u0, obs)  # the well-formed call still runs
     torch.cuda.synchronize()
     eng.close()
+
+
+RCCL_WORLD1 = r"""
+import os, sys, json
+import numpy as np
+import torch
+import torch.distributed as dist
+sys.path.insert(0, os.environ["MPCC_ROOT"])
+sys.path.insert(0, os.path.join(os.environ["MPCC_ROOT"], "tests"))
+torch.cuda.set_device(0)
+dist.init_process_group("nccl", init_method="tcp://127.0.0.1:" + os.environ["MPCC_PORT"], rank=0, world_size=1,
+                        device_id=torch.device("cuda", 0))
+assert dist.get_backend() == "nccl"
+import mpcc_manipulator_amd as m
+from mpcc_manipulator_amd.distributed import check_equal_shards, gather_u0, max_over_ranks
+from helpers import Q0
+dev = torch.device("cuda", 0)
+B = 64
+params = m.load_params(N=20, overrides={"sqp": {"max_iter": 2}})
+eng = m.Engine(params, max_batch=B, constraint_mask=2)
+X, Y, Z, q = m.load_default_track()
+eng.set_track(*m.track_from_points(X, Y, Z, q, np.array([0.5545, 0.0, 0.5211])))
+rng = np.random.default_rng(7)
+x0 = np.zeros((B, 9)); x0[:, :7] = Q0 + rng.normal(0, 0.002, (B, 7))
+xd = torch.from_numpy(x0).to(dev)
+u0 = torch.zeros((B, 8), dtype=torch.float64, device=dev)
+obs = torch.tensor([[3.0, 3.0, 3.0, 0.0]] * B, dtype=torch.float64, device=dev)
+uo = torch.empty((B, 8), dtype=torch.float64, device=dev)
+check_equal_shards(B, device=dev)  # all_reduce over RCCL
+eng.solve_device(B, xd, u0, obs, uo)
+torch.cuda.synchronize()
+out = torch.full((B, 8), float("nan"), dtype=torch.float64, device=dev)
+g = gather_u0(uo, 1, out=out)  # all_gather_into_tensor over RCCL
+t = max_over_ranks(1.25, device=dev)
+torch.cuda.synchronize()
+ok = g.data_ptr() == out.data_ptr() and torch.equal(out, uo) and t == 1.25 and bool(torch.isfinite(uo).all())
+print(json.dumps({"ok": bool(ok), "backend": dist.get_backend(), "max_abs_u0": float(uo.abs().max())}))
+eng.close()
+dist.destroy_process_group()
+"""
+
+
+@pytest.mark.gpu
+def test_rccl_world1_gather(built_lib):
+    """The RCCL ("nccl") branch of the multi-GPU path, executed: a world-size-1 process group on GPU 0 runs
+    check_equal_shards (all_reduce), gather_u0 (all_gather_into_tensor of the engine's u0) and max_over_ranks
+    through RCCL; the gathered u0 equals the solve's output bitwise.  2+ ranks over RCCL need one GPU per rank
+    (the driver's 8-GPU runs)."""
+    env = dict(os.environ, MPCC_ROOT=ROOT, MPCC_PORT=str(_free_port()))
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT"):
+        env.pop(k, None)
+    r = subprocess.run([sys.executable, "-c", RCCL_WORLD1], env=env, capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, r.stderr[-3000:]
+    res = json.loads(r.stdout.strip().splitlines()[-1])
+    assert res["ok"] and res["backend"] == "nccl", res
+
+
+def _free_port():
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
