@@ -47,6 +47,12 @@ extern "C" {
 #ifndef MPCC_DOF
 #define MPCC_DOF 7                       /* joints: 7 = Panda, 10 = Husky base (x, y, theta) + Panda */
 #endif
+/* Husky+Panda: panda_link0 sits at (0, 0, MPCC_MOBILE_MOUNT_Z) m in the base frame, a compile-time part of the
+ * robot definition like the joint frames; mpcc_params_load_json refuses a parameter file whose
+ * robot.mount differs, so editing it cannot silently have no effect */
+#ifndef MPCC_MOBILE_MOUNT_Z
+#define MPCC_MOBILE_MOUNT_Z 0.35
+#endif
 #define MPCC_NX (MPCC_DOF + 2)           /* state  [q, s, vs]   (config.h:29 NX = 9)  */
 #define MPCC_NU (MPCC_DOF + 1)           /* input  [dq, dVs]    (config.h:30 NU = 8)  */
 #define MPCC_NXU (MPCC_NX + MPCC_NU)     /* one horizon stage of OptVariables         */

@@ -150,7 +150,7 @@ __device__ inline void panda_frame(const double* q, int frame, double* pos, doub
 // about z) of RobotModel::setHusky (robot_model.cpp:321-352) carry panda_link0 at MOBILE_MOUNT in the base
 // frame (identity rotation).  p = [x, y, 0] + Rz(th) (mount + p_arm), R = Rz(th) R_arm; Jacobian columns
 // e_x, e_y, (e_z x (p - [x, y, 0]); e_z) for the base and Rz(th)-rotated arm columns (the oracle's fk).
-constexpr double MOBILE_MOUNT_Z = 0.35;
+constexpr double MOBILE_MOUNT_Z = MPCC_MOBILE_MOUNT_Z;  // include/mpcc_engine.h
 // FK of panda_hand_tcp for this build's robot: position, rotation (row-major) and the 6 x DOF Jacobian.
 __device__ inline void robot_fk(const double* q, double* pos, double* Rout, double* J, bool want_J) {
     if constexpr (NBASE == 0) {

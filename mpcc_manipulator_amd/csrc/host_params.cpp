@@ -13,6 +13,7 @@
 //       Cost, Constraints, Bounds, MPC::param_; normalization and SQP keep their values, and the
 //       track spline's projection distance keeps its construction value.
 #include <cstring>
+#include <vector>
 #include <stdexcept>
 #include <string>
 
@@ -39,6 +40,14 @@ Sections load_sections(const mpcc_json_paths* p) {
         s.model = m.at("model"); s.cost = m.at("cost"); s.bounds = m.at("bounds");
         s.norm = m.at("normalization"); s.sqp = m.at("sqp");
         if (m.has("config")) { s.config = m.at("config"); s.has_config = true; }
+        if (m.has("robot") && m.at("robot").has("mount")) {  // the mount is compiled in (MPCC_MOBILE_MOUNT_Z)
+            const std::vector<double> mt = m.at("robot").at("mount").numbers();
+            const double want[3] = {0.0, 0.0, MPCC_DOF == 10 ? MPCC_MOBILE_MOUNT_Z : 0.0};
+            if (mt.size() != 3 || mt[0] != want[0] || mt[1] != want[1] || mt[2] != want[2])
+                throw std::runtime_error("robot.mount differs from the library's compiled mount (0, 0, " +
+                                         std::to_string(want[2]) + "); it is part of the robot definition "
+                                         "(MPCC_MOBILE_MOUNT_Z, include/mpcc_engine.h): rebuild to change it");
+        }
     }
     if (p->param_path) s.model = json_load_file(p->param_path);
     if (p->cost_path) s.cost = json_load_file(p->cost_path);

@@ -1270,8 +1270,10 @@ __device__ __attribute__((noinline)) void sqp_ipm_phase(const DevConst& c, const
 }
 
 template <int NPM>
-__global__ void __launch_bounds__(64) k_sqp(DevConst c, DevBuffers d, const double* __restrict__ ucur_all) {
+__global__ void __launch_bounds__(64) k_sqp(DevConst, DevBuffers, const double* __restrict__ ucur_all) {
     extern __shared__ __attribute__((aligned(16))) double smem[];
+    const DevConst& c = kernarg_const();     // the arguments in place (kernels.h kernarg_const)
+    const DevBuffers& d = kernarg_buffers();
     const int t = threadIdx.x & 15;
     const int b = blockIdx.x * IPW + (threadIdx.x >> 4);
     const bool valid = b < c.Bn;

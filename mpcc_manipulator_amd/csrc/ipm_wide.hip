@@ -60,9 +60,9 @@ enum : int {
 };
 static_assert(NWF * GW <= ISW, "IPM workspace must fit the per-stage ISW allocation");
 
-// per-instance LDS block (doubles): F [i*16 + j], U [i*32 + c]
-constexpr int L_F = 0, L_U = 16 * 16;
-constexpr int GRP_LDS = L_U + NU * GW + 16;  // + 16 doubles: the two instances of a wave start 16 banks apart
+// per-instance LDS block (doubles): F [i*16 + j], U [i*32 + c], model constants diag(M) [L_C + a], diag(G) [L_C + 16 + j]
+constexpr int L_F = 0, L_U = 16 * 16, L_C = L_U + NU * GW;
+constexpr int GRP_LDS = L_C + 32 + 16;  // + 16 doubles: the two instances of a wave start 16 banks apart
 
 size_t ipm_wide_lds_bytes() { return (size_t)IPW * GRP_LDS * sizeof(double); }
 
@@ -343,6 +343,10 @@ __device__ __forceinline__ void ipm_group(const DevConst& c, const DevBuffers& d
         if (t == a || t == NX + a) Hct = c.p.Tu[a] * HcB * c.p.Tu[a];
     }
     if (t == UVS) gt = gs;
+    // diag(M), diag(G) for the factor body's Y = B~^T P and Hb products: read there per stage, from LDS
+    if (t < NX) S[L_C + t] = c.M[t * (NX + 1)];
+    if (t < DOF) S[L_C + 16 + t] = c.G[t * (NU + 1)];
+    lds_sync();
     const bool rowY = t < NX;
     const bool rowD = t >= NX && t < NXA;
     const int j9 = t - NX;
@@ -690,7 +694,7 @@ __device__ __forceinline__ void ipm_group(const DevConst& c, const DevBuffers& d
                     // ---- (1) Y = B~^T P (column t), f = g_v + B~^T p (lanes < NU)
                     double Y[NU];
 #pragma unroll
-                    for (int i = 0; i < DOF; i++) Y[i] = c.G[i * (NU + 1)] * Pc[i] + Pc[NX + i];
+                    for (int i = 0; i < DOF; i++) Y[i] = S[L_C + 16 + i] * Pc[i] + Pc[NX + i];
                     Y[UVS] = gs * Pc[XS] + gv * Pc[XVS];
                     const Halves hp = halves(pv);
                     const double pu = up32<NX>(pv, hp, t), pu1 = up32<1>(pv, hp, t);
@@ -783,7 +787,7 @@ __device__ __forceinline__ void ipm_group(const DevConst& c, const DevBuffers& d
                     }
 #pragma unroll
                     for (int i = 0; i < NU; i++) {
-                        S[MPCC_BCHK(c.bchk, L_U + i * GW + t, GRP_LDS, BC_LDS)] = u[i];
+                        S[MPCC_BCHK(c.bchk, L_U + i * GW + t, L_C, BC_LDS)] = u[i];
                         *ws(k, WF_KC + i) = kc[i];
                         *ws(k, WF_FI + i) = fi[i];
                     }
@@ -847,8 +851,9 @@ __device__ __forceinline__ void ipm_group(const DevConst& c, const DevBuffers& d
                         if (rowY) {
 #pragma unroll
                             for (int a = 0; a < NX; a++) {
-                                double mp = (c.M[a * (NX + 1)] * mt) * Pc[a];
-                                if (t == XVS) mp += (c.M[a * (NX + 1)] * msv) * Pc7[a];
+                                const double ma = S[L_C + a];
+                                double mp = (ma * mt) * Pc[a];
+                                if (t == XVS) mp += (ma * msv) * Pc7[a];
                                 if (a == XVS) mp += (msv * mt) * Pc[XS];
                                 if (a == XVS && t == XVS) mp += (msv * msv) * Pc7[XS];
                                 hbv[a] += mp;
@@ -1348,8 +1353,10 @@ __device__ __attribute__((noinline)) void bfgs_post_step(const DevConst& c, cons
 }
 
 template <int NPM, bool LR>
-__global__ void __launch_bounds__(64) k_sqp(DevConst c, DevBuffers d, const double* __restrict__ ucur_all) {
+__global__ void __launch_bounds__(64) k_sqp(DevConst, DevBuffers, const double* __restrict__ ucur_all) {
     extern __shared__ __attribute__((aligned(16))) double smem[];
+    const DevConst& c = kernarg_const();     // the arguments in place (kernels.h kernarg_const)
+    const DevBuffers& d = kernarg_buffers();
     const int t = threadIdx.x % GW;
     const int b = blockIdx.x * IPW + threadIdx.x / GW;
     const bool valid = b < c.Bn;

@@ -47,6 +47,18 @@ struct DevBuffers {
     // iteration (gprev), A^T y of the last QP (aty), step_prev = alpha * step (sp)
     double *lr, *lrc, *glam, *gprev, *aty, *sp;
 };
+// The fused SQP kernels (k_sqp of ipm.hip / ipm_wide.hip) are declared (DevConst c, DevBuffers d, const double*)
+// and hand c and d to their non-inlined phases by reference into the kernel-argument segment: a reference to the
+// by-value parameter itself makes the compiler copy the 5.4 KB DevConst into every lane's private segment (a
+// 5.8 KB per-lane stack frame) and read it back through flat private-aperture loads in the interior point.
+static_assert(sizeof(DevConst) % alignof(DevBuffers) == 0, "DevBuffers follows DevConst in the kernel arguments");
+__device__ __forceinline__ const DevConst& kernarg_const() {
+    return *(const DevConst*)__builtin_amdgcn_kernarg_segment_ptr();
+}
+__device__ __forceinline__ const DevBuffers& kernarg_buffers() {
+    return *(const DevBuffers*)((const char*)__builtin_amdgcn_kernarg_segment_ptr() + sizeof(DevConst));
+}
+
 constexpr int TRACE_W = 8, TRACE_IT = 4;  // qp status, ipm iters, obj, vio, accepted, |step|_inf, alpha, alpha*|step|
 
 constexpr int SQI = 8;  // int bookkeeping per instance: status, active, iter, nfilt, qp_status, ipm_iters, reject, nlr

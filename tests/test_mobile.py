@@ -228,3 +228,19 @@ def test_mobile_config3_full_scale(mobile):
     assert np.array_equal(outo["status"], full["status"][smp])
     assert np.abs(outo["horizon"][:, :-1, NX:] - full["horizon"][smp, :-1, NX:]).max() <= 1e-6
     eng.close()
+
+
+def test_mobile_mount_is_compiled_in(built_lib, tmp_path):
+    """robot.mount of the parameter file must equal the library's compiled mount (MPCC_MOBILE_MOUNT_Z): an edited
+    mount is refused instead of silently ignored."""
+    import json
+    import mpcc_manipulator_amd as m
+    with open(m.engine.MOBILE_PARAMS) as f:
+        d = json.load(f)
+    assert d["robot"]["mount"] == [0.0, 0.0, 0.35]
+    m.load_params(N=30, dof=10)  # the shipped file loads
+    d["robot"]["mount"] = [0.0, 0.0, 0.40]
+    p = tmp_path / "mobile_params_mount.json"
+    p.write_text(json.dumps(d))
+    with pytest.raises(m.MpccError, match="mount"):
+        m.load_params(N=30, merged=str(p), dof=10)
