@@ -70,6 +70,19 @@ def pmc_fp64_flops(counters):
                    2.0 * counters["SQ_INSTS_VALU_FMA_F64"])
 
 
+def union_length(starts, ends):
+    """Length of the union of the intervals [starts[i], ends[i]]."""
+    tot, cur_s, cur_e = 0.0, None, None
+    for a, b in sorted(zip(starts, ends)):
+        if cur_e is None or a > cur_e:
+            if cur_e is not None:
+                tot += cur_e - cur_s
+            cur_s, cur_e = a, b
+        else:
+            cur_e = max(cur_e, b)
+    return tot + ((cur_e - cur_s) if cur_e is not None else 0.0)
+
+
 HBM_PEAK_BPS = 8.0e12  # MI355X HBM3E peak (spec), MI355X_MICROARCH.md
 
 
@@ -245,6 +258,9 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--traffic", default=None, help="PMC traffic summary (default profiles/pmc_traffic_<kernel>.json)")
     ap.add_argument("--dump-u0", default=None, help="rank 0 writes the last step's gathered u0 [world*B, 8] (.npy)")
+    ap.add_argument("--sub-batches", type=int, default=2,
+                    help="controller groups per GPU, each an engine of B/S instances stepping on its own HIP stream, so "
+                         "one group's next control step overlaps another's interior-point tail (1: one engine)")
     args = ap.parse_args()
     if args.gpus < 1:
         ap.error("--gpus must be >= 1")
@@ -274,6 +290,13 @@ def main():
     rehearse = os.environ.get("MPCC_BENCH_REHEARSE", "0") == "1"
     if rehearse:
         local = 0
+    # Every controller group's stream needs a hardware queue of its own, or the groups' kernels run back to back:
+    # HIP multiplexes all streams onto GPU_MAX_HW_QUEUES queues (4 by default) and torch's stream pool, created
+    # whole at the first torch.cuda.Stream(), lands consecutive pool streams on one queue (measured:
+    # tools/probes/stream_overlap.py, profiles/r03g_stream_overlap.log, r03h_stream_overlap.log).  Read by HIP when it initialises, below.
+    hwq = min(32, max(8, 2 * args.sub_batches + 4))
+    if args.sub_batches > 1 and int(os.environ.get("GPU_MAX_HW_QUEUES", "4")) < hwq:
+        os.environ["GPU_MAX_HW_QUEUES"] = str(hwq)
     import torch
     if torch.cuda.device_count() <= local:
         print(f"bench.py: rank {rank} needs GPU {local} but {torch.cuda.device_count()} GPU(s) visible", file=sys.stderr)
@@ -299,8 +322,15 @@ def main():
     obs_xyz = (0.48, 0.218, 0.521) if dof == 7 else (0.62, 0.28, 0.75)
     pool_obs = (*obs_xyz, 5.0) if obstacles else (3.0, 3.0, 3.0, 0.0)
     pool, track = make_pool(m, params, args.mask, args.pool_steps, local, pool_obs)
-    eng = m.Engine(params, max_batch=B, device=local, constraint_mask=args.mask)
-    eng.set_track(*track)
+    S = args.sub_batches
+    if S < 1 or B % S:
+        print(f"bench.py: --sub-batches {S} must divide the batch {B}", file=sys.stderr)
+        sys.exit(2)
+    Bs = B // S
+    engs = [m.Engine(params, max_batch=Bs, device=local, constraint_mask=args.mask) for _ in range(S)]
+    for e in engs:
+        e.set_track(*track)
+    eng = engs[0]
 
     # instances: pool step t = (global index) mod T, q += N(0, 0.005); the noise is
     # drawn for the global batch, so instance i gets the same input whatever the number of ranks
@@ -325,22 +355,44 @@ def main():
     x0_p, u0_d, obs_d = t(x0), t(u0), t(obs)
     g_p, v_p, f_p = t(guess), t(valid, torch.int32), t(fails, torch.int32)
     x0_d = x0_p.clone()
-    u_out = torch.empty((B, nu), dtype=torch.float64, device=dev)
+    # u0 outputs double-buffered by step parity: with N > 1 ranks the gather of step i reads its buffer on the
+    # gather stream while step i + 1 writes the other one
+    u_out = [torch.empty((B, nu), dtype=torch.float64, device=dev) for _ in range(2)]
     hor = torch.empty((B, N + 1, nxu), dtype=torch.float64, device=dev)
     status = torch.empty(B, dtype=torch.int32, device=dev)
     ok = torch.empty(B, dtype=torch.int32, device=dev)
-    u_all = torch.empty((world * B, nu), dtype=torch.float64, device=dev) if world > 1 else None
-    # One dedicated stream carries the whole step: the x0 restore, the engine's kernels and the u0
-    # gather (RCCL waits on the current stream), so every step reads the inputs it restored.
-    stream = torch.cuda.Stream(dev)
+    u_all = [torch.empty((world * B, nu), dtype=torch.float64, device=dev) for _ in range(2)] if world > 1 else None
+    # Each controller group (engine s: instances [s Bs, (s+1) Bs)) steps on its own stream: the x0 restore, the
+    # warm-start restore and the engine's kernels, so every step reads the inputs it restored and group s only
+    # waits for its own previous step.  The u0 gather (RCCL, N > 1 ranks) runs on a third stream after all groups
+    # of the step; it needs every rank's u0 of that step, nothing of the next one.
+    streams = [torch.cuda.Stream(dev) for _ in range(S)]
+    gstream = torch.cuda.Stream(dev)
+    done = [[torch.cuda.Event() for _ in range(S)] for _ in range(2)]
+    gathered = [torch.cuda.Event() for _ in range(2)]
+    sl = [slice(s_ * Bs, (s_ + 1) * Bs) for s_ in range(S)]
+    nstep = [0]
 
     def step():
-        with torch.cuda.stream(stream):
-            x0_d.copy_(x0_p)
-            eng.set_warmstart_device(B, g_p, v_p, f_p, stream=stream)
-            eng.solve_device(B, x0_d, u0_d, obs_d, u_out, hor, status, ok, stream=stream)
-            if world > 1:
-                gather_u0(u_out, world, out=u_all)  # RCCL all-gather of u0 over xGMI
+        i = nstep[0]
+        buf = i % 2
+        for s_ in range(S):
+            st_ = streams[s_]
+            with torch.cuda.stream(st_):
+                if world > 1 and i >= 2:
+                    st_.wait_event(gathered[buf])  # the gather of step i - 2 has read this u0 buffer
+                x0_d[sl[s_]].copy_(x0_p[sl[s_]])
+                engs[s_].set_warmstart_device(Bs, g_p[sl[s_]], v_p[sl[s_]], f_p[sl[s_]], stream=st_)
+                engs[s_].solve_device(Bs, x0_d[sl[s_]], u0_d[sl[s_]], obs_d[sl[s_]], u_out[buf][sl[s_]], hor[sl[s_]],
+                                      status[sl[s_]], ok[sl[s_]], stream=st_)
+                done[buf][s_].record(st_)
+        if world > 1:
+            with torch.cuda.stream(gstream):
+                for s_ in range(S):
+                    gstream.wait_event(done[buf][s_])
+                gather_u0(u_out[buf], world, out=u_all[buf])  # RCCL all-gather of u0 over xGMI
+                gathered[buf].record(gstream)
+        nstep[0] += 1
 
     if world > 1:
         check_equal_shards(B, device=dev)
@@ -350,7 +402,8 @@ def main():
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
-    eng.timing_begin()
+    for e in engs:
+        e.timing_begin()
     t0 = time.perf_counter()
     for _ in range(args.steps):
         step()
@@ -359,13 +412,23 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
-    tm, ncalls, nipm = eng.timing_end()
-    tmlp = eng.timing_mlp()
+    last = (nstep[0] - 1) % 2
+    tms = [e.timing_end() for e in engs]
+    tmlps = [e.timing_mlp() for e in engs]
+    # the QP-solve launches of all groups, as intervals on engine 0's clock (its window's first event, recorded
+    # before any group's first kernel of the timed region): their union is the time the kernel family ran
+    ivs = [e.timing_intervals("qp", anchor=engs[0], max_n=4 * args.steps + 8) for e in engs]
+    ivs_env = [e.timing_intervals("k_mlp_env", anchor=engs[0], max_n=4 * args.steps + 8) for e in engs]
     if world > 1:
         elapsed = max_over_ranks(elapsed, device=dev)
+    tm = {k: sum(x[0][k] for x in tms) for k in tms[0][0]}  # summed over groups
+    ncalls = tms[0][1]
+    nipm = sum(x[2] for x in tms)
+    tmlp = {k: (sum(x[k][0] for x in tmlps), sum(x[k][1] for x in tmlps)) for k in tmlps[0]}
 
     st = status.cpu().numpy()
-    stats = eng.solve_stats(B)
+    stats_g = [e.solve_stats(Bs) for e in engs]
+    stats = {k: np.concatenate([sg[k] for sg in stats_g]) for k in stats_g[0]}
     solved = float(np.mean(st == 0))
     value = B * world * args.steps / elapsed
     ms = elapsed / args.steps * 1e3
@@ -375,57 +438,65 @@ def main():
     # with the collision networks on (configs[2]), k_mlp_env.  Launch durations are HIP events on the engine
     # stream around those launches alone, over the timed steps.
     kname = "k_ipm" if os.environ.get("MPCC_STAGED_SQP", "0") == "1" else "k_sqp"
-    t_ipm = tm["solve_qp"] / max(1, nipm)
+    t_ipm = tm["solve_qp"] / max(1, nipm)  # mean duration of one launch (B/S instances)
     # QP solves per step: an instance solves min(sqp_iter + 1, max_iter) QPs (a SOLVED exit at SQP
-    # iteration i has solved i + 1); a launch is credited with the QPs it actually solved, on average
+    # iteration i has solved i + 1); the launches are credited with the QPs they actually solved
     qps = int(np.minimum(stats["sqp_iter"] + 1, args.max_iter).sum())
-    launches_per_step = max(1, nipm) / max(1, ncalls)
-    flops = qps * algorithmic_qp_flops(N, dof) / launches_per_step
-    achieved = flops / t_ipm / 1e12
-    pmc = find_pmc(kname, B, N, args.mask, dof, args.traffic)
+    flops_step = qps * algorithmic_qp_flops(N, dof)
+    flops = flops_step * ncalls / max(1, nipm)  # per launch, on average
+    # time the kernel ran: the union of all groups' launch intervals (S = 1: the sum of launch durations)
+    busy = union_length(np.concatenate([a for a, _ in ivs]), np.concatenate([b for _, b in ivs])) * 1e-3
+    achieved = flops_step * ncalls / busy / 1e12 if busy > 0 else flops / t_ipm / 1e12
+    pmc = find_pmc(kname, Bs, N, args.mask, dof, args.traffic)
     traffic = pmc.get("hbm_bytes_per_launch") if pmc else None
     pflops = pmc_fp64_flops(pmc.get("counters")) if pmc else None
     # k_sqp is a latency-bound FP64 VALU + DPP kernel (no MFMA in it): its roof is the FP64 vector peak, its
     # work the SURVEY's condensed-dense F_qp per QP actually solved; the PMC-counted FP64 flops it executed and
-    # its HBM fraction (PMC traffic / launch time / 8 TB/s) are reported beside it
+    # its HBM fraction (PMC traffic of all launches / the time they ran / 8 TB/s) are reported beside it
     roof = {"kernel": kname, "bound": "valu", "achieved": achieved, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
             "frac": achieved / FP64_PEAK_TFLOPS, "traffic": traffic,
-            "hbm_frac": (traffic / t_ipm / HBM_PEAK_BPS) if traffic else None,
+            "hbm_frac": (traffic * nipm / busy / HBM_PEAK_BPS) if traffic and busy > 0 else None,
             "pmc_fp64_flops_per_launch": pflops,
-            "pmc_fp64_frac": (pflops / t_ipm / 1e12 / FP64_PEAK_TFLOPS) if pflops else None,
+            "pmc_fp64_frac": (pflops * nipm / busy / 1e12 / FP64_PEAK_TFLOPS) if pflops and busy > 0 else None,
             "pmc_source": pmc.get("file") if pmc else None,
-            "avg_launch_ms": t_ipm * 1e3, "launches_timed": nipm, "algorithmic_flops_per_launch": flops,
-            "work": "F_qp (SURVEY 8(d), condensed-dense QP) x QPs solved per launch",
+            "avg_launch_ms": t_ipm * 1e3, "launches_timed": nipm, "concurrent_groups": S,
+            "busy_ms_per_step": busy / max(1, ncalls) * 1e3, "algorithmic_flops_per_launch": flops,
+            "work": "F_qp (SURVEY 8(d), condensed-dense QP) x QPs solved, over the union of the launches' intervals",
             "qp_solves_per_step": qps}
     t_env, n_env = tmlp["k_mlp_env"]
-    if n_env and t_env / max(1, ncalls) > tm["solve_qp"] / max(1, ncalls):  # env MLP dominates (configs[2])
+    busy_env = union_length(np.concatenate([a for a, _ in ivs_env]), np.concatenate([b for _, b in ivs_env])) * 1e-3
+    if n_env and busy_env > busy:  # the env MLP ran longer than the QP solve (configs[2])
         t_l = t_env / n_env
-        samples = B * (N + 1)
+        samples = Bs * (N + 1)
         fl = samples * mlp_flops_per_sample("k_mlp_env", dof)
-        pm = find_pmc("k_mlp_env", B, N, args.mask, dof)
+        pm = find_pmc("k_mlp_env", Bs, N, args.mask, dof)
         tr = pm.get("hbm_bytes_per_launch") if pm else None
-        roof = {"kernel": "k_mlp_env", "bound": "mfma", "achieved": fl / t_l / 1e12, "peak": FP64_PEAK_TFLOPS,
-                "unit": "TFLOP/s", "frac": fl / t_l / 1e12 / FP64_PEAK_TFLOPS, "traffic": tr,
-                "hbm_frac": (tr / t_l / HBM_PEAK_BPS) if tr else None, "avg_launch_ms": t_l * 1e3,
-                "launches_timed": n_env, "algorithmic_flops_per_launch": fl,
-                "work": "F_env (SURVEY 8(d): value + DOF Jacobian columns) x B (N+1) samples",
-                "k_sqp": {"avg_launch_ms": t_ipm * 1e3, "frac": achieved / FP64_PEAK_TFLOPS, "traffic": traffic}}
+        ach = fl * n_env / busy_env / 1e12
+        roof = {"kernel": "k_mlp_env", "bound": "mfma", "achieved": ach, "peak": FP64_PEAK_TFLOPS,
+                "unit": "TFLOP/s", "frac": ach / FP64_PEAK_TFLOPS, "traffic": tr,
+                "hbm_frac": (tr * n_env / busy_env / HBM_PEAK_BPS) if tr else None, "avg_launch_ms": t_l * 1e3,
+                "launches_timed": n_env, "concurrent_groups": S, "busy_ms_per_step": busy_env / max(1, ncalls) * 1e3,
+                "algorithmic_flops_per_launch": fl,
+                "work": "F_env (SURVEY 8(d): value + DOF Jacobian columns) x B/S (N+1) samples per launch, over the "
+                        "union of the launches' intervals",
+                "k_sqp": {"avg_launch_ms": t_ipm * 1e3, "frac": achieved / FP64_PEAK_TFLOPS, "traffic": traffic,
+                          "busy_ms_per_step": busy / max(1, ncalls) * 1e3}}
 
     # PCIe-inclusive rate (host buffers in and out through mpcc_solve): a diagnostic, never `value`
     pcie = None
-    if rank == 0 and world == 1:
+    if rank == 0 and world == 1:  # one group's engine, its instances through host buffers
         reps = 5
-        xh = np.ascontiguousarray(x0)
+        xh = np.ascontiguousarray(x0[sl[0]])
         dt_h = 0.0
         for r in range(reps + 1):
-            eng.set_warmstart_device(B, g_p, v_p, f_p, stream=stream)
+            eng.set_warmstart_device(Bs, g_p[sl[0]], v_p[sl[0]], f_p[sl[0]], stream=streams[0])
             torch.cuda.synchronize()
             xs = xh.copy()
             t1 = time.perf_counter()
-            eng.solve(xs, u0, obs)
+            eng.solve(xs, u0[sl[0]], obs[sl[0]])
             if r:
                 dt_h += time.perf_counter() - t1
-        pcie = B * reps / dt_h
+        pcie = Bs * reps / dt_h
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
@@ -468,6 +539,8 @@ def main():
                               f"N={N}, all 11 polytopic rows incl. both collision NNs (mask={args.mask}), per-instance "
                               f"obstacles, {args.max_iter} SQP iters"}[args.config],
                        "batch_per_gpu": B, "global_batch": B * world, "horizon": N, "sqp_iters": args.max_iter,
+                       "sub_batches": S, "instances_per_engine": Bs,
+                       "gpu_max_hw_queues": int(os.environ.get("GPU_MAX_HW_QUEUES", "4")),
                        "parallelism": f"instance-sharded x{world}" + ((", gloo rehearsal, all ranks on GPU 0" if rehearse else
                                                                   ", RCCL all_gather(u0)") if world > 1 else "")},
             "roofline": roof,
@@ -475,7 +548,7 @@ def main():
         }
         print(json.dumps(line))
     if args.dump_u0 and rank == 0:
-        np.save(args.dump_u0, (u_all if world > 1 else u_out).cpu().numpy())
+        np.save(args.dump_u0, (u_all[last] if world > 1 else u_out[last]).cpu().numpy())
     if dist is not None:
         dist.destroy_process_group()
 

@@ -207,6 +207,15 @@ int mpcc_timing_end(mpcc_engine* e, mpcc_timing* sum, int32_t* n_calls, int32_t*
 /* the collision-MLP launches of the last timing window (after mpcc_timing_end): total seconds and launch count of
  * k_mlp_self and of k_mlp_env, from HIP events around those launches alone on the engine stream */
 int mpcc_timing_mlp(mpcc_engine* e, double* self_s, int32_t* self_n, double* env_s, int32_t* env_n);
+/* the launches of one kernel of e's last timing window (kind: MPCC_TIMING_QP = the QP solve, k_sqp or k_ipm in
+ * the staged path; MPCC_TIMING_MLP_SELF / _MLP_ENV = the collision networks) as [start, end] in ms after the
+ * first event of `anchor`'s window (anchor = e, or another engine on the same device): several engines stepping
+ * on their own streams measure the union of their kernels' busy time */
+#define MPCC_TIMING_QP 0
+#define MPCC_TIMING_MLP_SELF 1
+#define MPCC_TIMING_MLP_ENV 2
+int mpcc_timing_intervals(mpcc_engine* e, mpcc_engine* anchor, int kind, int max, double* start_ms, double* end_ms,
+                          int32_t* n);
 
 /* Per-instance iteration counts of the last solve: SQP iteration index at exit and IPM iterations of
  * the last QP (host arrays, may be NULL). */

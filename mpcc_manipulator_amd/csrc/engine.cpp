@@ -1311,3 +1311,32 @@ int mpcc_timing_mlp(mpcc_engine* e, double* self_s, int32_t* self_n, double* env
     if (env_n) *env_n = e->last_mlp_env_n;
     return MPCC_OK;
 }
+
+int mpcc_timing_intervals(mpcc_engine* e, mpcc_engine* anchor, int kind, int max, double* start_ms, double* end_ms,
+                          int32_t* n) {
+    if (!e || !anchor || !n || max < 0 || (max && (!start_ms || !end_ms)) || kind < 0 || kind > 2)
+        return fail(MPCC_E_INVALID, "mpcc_timing_intervals: invalid argument");
+    if (anchor->lv_total.empty() || e->cfg.device != anchor->cfg.device)
+        return fail(MPCC_E_INVALID, "mpcc_timing_intervals: the anchor engine has no timing window on this device");
+    const auto& lv = kind == MPCC_TIMING_QP ? e->lv_ipm : (kind == MPCC_TIMING_MLP_SELF ? e->lv_mlp_self : e->lv_mlp_env);
+    DevGuard dg_(e);
+    try {
+        const hipEvent_t a0 = anchor->lv_total.front().first;
+        HIPCHK(hipEventSynchronize(a0));
+        int k = 0;
+        for (auto& pr : lv) {
+            if (k >= max) break;
+            HIPCHK(hipEventSynchronize(pr.second));
+            float s = 0, t = 0;
+            HIPCHK(hipEventElapsedTime(&s, a0, pr.first));
+            HIPCHK(hipEventElapsedTime(&t, a0, pr.second));
+            start_ms[k] = s;
+            end_ms[k] = t;
+            k++;
+        }
+        *n = k;
+    } catch (const HipError& x) {
+        return fail(MPCC_E_HIP, x.what());
+    }
+    return MPCC_OK;
+}

@@ -859,6 +859,26 @@ __device__ __forceinline__ void ipm_group(const DevConst& c, const DevBuffers& d
                         hG[i] += Wb[p] * (bv * cur.pa[p]);  // a_p[t]: zero for lanes >= 7
                     }
                 }
+                // Hb's poly terms (q block, rows a < 7), row p by row p as for F above.  The wide-poly variants form
+                // them here, so that a_p (NPM values per lane) dies before the Cholesky instead of living through
+                // it into the Hb section (it spilled there); <= 2 rows keep the late placement, where the 7 sums
+                // would be the longer live range.  Same terms in the same order either way.
+                double hq[7];
+                auto poly_hq = [&]() {
+#pragma unroll
+                    for (int a = 0; a < 7; a++) {
+                        hq[a] = Qr[a];
+                        if (a == t) hq[a] += wd;
+                    }
+#pragma unroll
+                    for (int p = 0; p < NPM; p++)
+#pragma unroll
+                        for (int a = 0; a < 7; a++) {
+                            const double pa_ = bcn(cur.pa[p], a);
+                            hq[a] += Wb[p] * (pa_ * cur.pa[p]);
+                        }
+                };
+                if constexpr (NPM > 2) poly_hq();
                 double Fc[8], gm[8];
 #pragma unroll
                 for (int i = 0; i < 8; i++) {
@@ -934,20 +954,7 @@ __device__ __forceinline__ void ipm_group(const DevConst& c, const DevBuffers& d
                     double Pc7[9];
 #pragma unroll
                     for (int a = 0; a < 9; a++) Pc7[a] = from_down<1>(Pc[a]);  // lane 8 <- P[a][7]
-                    // poly terms row p by row p, as for F above
-                    double hq[7];
-#pragma unroll
-                    for (int a = 0; a < 7; a++) {
-                        hq[a] = Qr[a];
-                        if (a == t) hq[a] += wd;
-                    }
-#pragma unroll
-                    for (int p = 0; p < NPM; p++)
-#pragma unroll
-                        for (int a = 0; a < 7; a++) {
-                            const double pa_ = bcn(cur.pa[p], a);
-                            hq[a] += Wb[p] * (pa_ * cur.pa[p]);
-                        }
+                    if constexpr (NPM <= 2) poly_hq();
 #pragma unroll
                     for (int a = 0; a < 16; a++) {
                         double v = 0.0;

@@ -183,6 +183,7 @@ def lib(dof=7):
         "mpcc_build_id": (C.c_char_p, []),
         "mpcc_build_flags": (C.c_int, []),
         "mpcc_timing_mlp": (C.c_int, [V, C.POINTER(D), IP, C.POINTER(D), IP]),
+        "mpcc_timing_intervals": (C.c_int, [V, V, C.c_int, C.c_int, DP, DP, IP]),
     }
     for name, (res, args) in sig.items():
         f = getattr(L, name)
@@ -571,6 +572,18 @@ class Engine:
         self._check(self.L.mpcc_timing_mlp(self.h, C.byref(ss), C.byref(ns), C.byref(se), C.byref(ne)),
                     "mpcc_timing_mlp")
         return {"k_mlp_self": (ss.value, ns.value), "k_mlp_env": (se.value, ne.value)}
+
+    TIMING_KINDS = {"qp": 0, "k_mlp_self": 1, "k_mlp_env": 2}
+
+    def timing_intervals(self, kind="qp", anchor=None, max_n=4096):
+        """After timing_end: (start_ms, end_ms) arrays of one kernel's launches in the window ("qp": the QP solve,
+        "k_mlp_self", "k_mlp_env"), relative to the first event of `anchor`'s window (default: this engine)."""
+        s, t = np.zeros(max_n), np.zeros(max_n)
+        n = C.c_int32()
+        a = (anchor or self).h
+        self._check(self.L.mpcc_timing_intervals(self.h, a, self.TIMING_KINDS[kind], int(max_n), _dp(s), _dp(t),
+                                                 C.byref(n)), "mpcc_timing_intervals")
+        return s[:n.value], t[:n.value]
 
     def solve_stats(self, B):
         a, b, c = np.zeros(B, np.int32), np.zeros(B, np.int32), np.zeros(B, np.int32)

@@ -41,3 +41,13 @@ def test_find_traffic_ignores_unlabelled_summaries(tmp_path):
 def test_committed_configs1_summary_is_found():
     import bench
     assert bench.find_traffic("k_sqp", 4096, 20, 2, 7) is not None
+
+
+def test_union_length_of_launch_intervals():
+    """bench.union_length: the time a kernel family ran when several groups' launches overlap."""
+    import bench
+    assert bench.union_length([], []) == 0.0
+    assert bench.union_length([0.0], [2.0]) == 2.0
+    assert bench.union_length([0.0, 1.0, 5.0], [2.0, 3.0, 6.0]) == 4.0       # [0,3] + [5,6]
+    assert bench.union_length([5.0, 0.0], [6.0, 10.0]) == 10.0               # nested, unsorted
+    assert bench.union_length([-1.0, 0.0], [0.5, 0.25]) == 1.5               # times before the anchor

@@ -24,6 +24,7 @@ def main():
     ap.add_argument("--batch", type=int, default=4096)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--timing", action="store_true", help="engines in live-timing mode (HIP events around launches)")
     args = ap.parse_args()
     import torch
     import mpcc_manipulator_amd as m
@@ -64,16 +65,28 @@ def main():
         for _ in range(args.warmup):
             step()
         torch.cuda.synchronize()
+        if args.timing:
+            for e in engs:
+                e.timing_begin()
         t0 = time.perf_counter()
         for _ in range(args.steps):
             step()
         torch.cuda.synchronize()
         dt = time.perf_counter() - t0
+        if args.timing:
+            busy = []
+            for e in engs:
+                e.timing_end()
+                a, b = e.timing_intervals("qp", anchor=engs[0], max_n=4 * args.steps + 8)
+                busy.append((a, b))
+            res_busy = bench.union_length(np.concatenate([a for a, _ in busy]), np.concatenate([b for _, b in busy]))
         u = torch.cat([b["uo"] for b in bufs]).cpu().numpy()
         if ref is None:
             ref = u
         res[S] = {"solves_per_s": B * args.steps / dt, "ms_per_step": dt / args.steps * 1e3,
                   "bitwise_equal_to_S1": bool(np.array_equal(u, ref))}
+        if args.timing:
+            res[S]["qp_busy_ms_per_step"] = res_busy / args.steps
         print(json.dumps({"S": S, **res[S]}), flush=True)
         for e in engs:
             e.close()
