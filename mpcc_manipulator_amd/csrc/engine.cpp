@@ -346,27 +346,42 @@ void run_batch(mpcc_engine* e, int B, hipStream_t st, mpcc_timing* timing, bool 
     const bool tm = timing != nullptr || e->live;
     std::vector<hipEvent_t> evs;
     int ei = 0;
+    // a boundary with no launch since the previous one reuses its event: every event record is a marker packet
+    // on the stream, and a chain of them between two kernels (the MLP and phase brackets of a configuration
+    // that runs no MLP) widened that gap to ~25 us per step
+    bool launched = true;
     auto mark = [&]() -> int {
+        if (!launched && !evs.empty()) return (int)evs.size() - 1;
         hipEvent_t ev = e->live ? e->live_ev() : e->ev(ei);
         ei++;
         HIPCHK(hipEventRecord(ev, st));
         evs.push_back(ev);
+        launched = false;
         return (int)evs.size() - 1;
     };
     std::vector<std::pair<int, int>> set_qp, solve_qp, get_alpha;
     int t0 = -1, t_env0 = -1, t_env1 = -1, t_end = -1;
     if (tm) t0 = mark();
     if (d.dbg_trace) HIPCHK(hipMemsetAsync(d.dbg_trace, 0, sizeof(double) * B * TRACE_IT * TRACE_W, st));
+    launched = true;
     launch_prepare(c, d, st);
+    launched = true;
     if (tm) t_env0 = mark();
     launch_stage_records(c, d, st);
+    launched = true;
     int m0 = -1, m1 = -1, m2 = -1;
     if (e->live) m0 = mark();
     if (c.p.constraint_mask & MPCC_CON_SELFCOL)
+    {
         launch_nn(c, d, e->nn_self.desc, e->nn_self.d, 0, c.S, nullptr, nullptr, d.rec, c.S, st);
+        launched = true;
+    }
     if (e->live) m1 = mark();
     if (c.p.constraint_mask & MPCC_CON_ENVCOL)
+    {
         launch_nn(c, d, e->nn_env.desc, e->nn_env.d, 1, c.S, nullptr, nullptr, d.rec, c.S, st);
+        launched = true;
+    }
     if (e->live) {
         m2 = mark();
         if (c.p.constraint_mask & MPCC_CON_SELFCOL) e->lv_mlp_self.push_back({evs[m0], evs[m1]});
@@ -380,10 +395,12 @@ void run_batch(mpcc_engine* e, int B, hipStream_t st, mpcc_timing* timing, bool 
         int a0 = -1, a1 = -1, b1 = -1;
         if (tm) a0 = mark();
         launch_setqp(c, d, ucur, st);
+        launched = true;
         if (tm) a1 = mark();
         e->last_wide = DOF != 7 || c.p.use_BFGS || e->wide_sqp;
         if (c.p.use_BFGS || e->wide_sqp) launch_sqp_wide(c, d, ucur, poly_rows_max(c.p.constraint_mask), c.p.use_BFGS ? 1 : 0, st);
         else launch_sqp(c, d, ucur, poly_rows_max(c.p.constraint_mask), st);
+        launched = true;
         if (tm) {
             b1 = mark();
             set_qp.push_back({a0, a1});
@@ -394,8 +411,10 @@ void run_batch(mpcc_engine* e, int B, hipStream_t st, mpcc_timing* timing, bool 
         int a0 = -1, a1 = -1, b1 = -1, c1 = -1;
         if (tm) a0 = mark();
         launch_setqp(c, d, ucur, st);
+        launched = true;
         if (tm) a1 = mark();
         launch_ipm(c, d, poly_rows_max(c.p.constraint_mask), st);
+        launched = true;
         if (c.p.do_SOC) {  // SecondOrderCorrection (osqp_interface.cpp:506-535)
             launch_soc(c, d, ucur, st);
             launch_ipm(c, d, poly_rows_max(c.p.constraint_mask), st);
@@ -411,6 +430,7 @@ void run_batch(mpcc_engine* e, int B, hipStream_t st, mpcc_timing* timing, bool 
             }
         }
         launch_apply(c, d, st);
+        launched = true;
         if (tm) {
             c1 = mark();
             set_qp.push_back({a0, a1});
@@ -420,6 +440,7 @@ void run_batch(mpcc_engine* e, int B, hipStream_t st, mpcc_timing* timing, bool 
     }
     }
     launch_finalize(c, d, st);
+    launched = true;
     HIPCHK(hipGetLastError());
     if (!tm) return;
     t_end = mark();

@@ -245,6 +245,40 @@ __device__ __forceinline__ void bwd8(const double* L, const double* dinv, double
     }
 }
 
+typedef double d4 __attribute__((ext_vector_type(4)));
+
+// ---- 4x4 transpose of the wave's 16-lane groups: afterwards lane (g, c) holds in x[j][r] what lane (j, c) held
+//      in x[g][r].  Two butterflies, on the group bit 1 (v_permlane32_swap: the first operand's upper 32
+//      lanes <-> the second's lower 32) and the group bit 0 (v_permlane16_swap: the first operand's odd rows <->
+//      the second's even rows), each on both dwords of a double.  Needs the whole wave active.
+__device__ __forceinline__ void swap_rows32(double& a, double& b) {
+    const unsigned long long x = (unsigned long long)__double_as_longlong(a), y = (unsigned long long)__double_as_longlong(b);
+    const auto lo = __builtin_amdgcn_permlane32_swap((unsigned)x, (unsigned)y, false, false);
+    const auto hi = __builtin_amdgcn_permlane32_swap((unsigned)(x >> 32), (unsigned)(y >> 32), false, false);
+    a = __longlong_as_double((long long)(((unsigned long long)hi[0] << 32) | lo[0]));
+    b = __longlong_as_double((long long)(((unsigned long long)hi[1] << 32) | lo[1]));
+}
+__device__ __forceinline__ void swap_rows16(double& a, double& b) {
+    const unsigned long long x = (unsigned long long)__double_as_longlong(a), y = (unsigned long long)__double_as_longlong(b);
+    const auto lo = __builtin_amdgcn_permlane16_swap((unsigned)x, (unsigned)y, false, false);
+    const auto hi = __builtin_amdgcn_permlane16_swap((unsigned)(x >> 32), (unsigned)(y >> 32), false, false);
+    a = __longlong_as_double((long long)(((unsigned long long)hi[0] << 32) | lo[0]));
+    b = __longlong_as_double((long long)(((unsigned long long)hi[1] << 32) | lo[1]));
+}
+template <int R>
+__device__ __forceinline__ void group_transpose(double (&x)[4][R]) {
+#pragma unroll
+    for (int r = 0; r < R; r++) {
+        swap_rows32(x[0][r], x[2][r]);
+        swap_rows32(x[1][r], x[3][r]);
+    }
+#pragma unroll
+    for (int r = 0; r < R; r++) {
+        swap_rows16(x[0][r], x[1][r]);
+        swap_rows16(x[2][r], x[3][r]);
+    }
+}
+
 // per-stage inputs of one lane, loaded one stage ahead of their use
 template <int NPE>
 struct StageIn {
@@ -740,9 +774,11 @@ __device__ __forceinline__ void ipm_group(const DevConst& c, const DevBuffers& d
     if (run) alpha = 0.0;
     while (true) {
         if (__ballot(run) == 0) break;
-        if (run) {
+        {
             // ================= factorization sweep k = N..0 with the lazy update of the previous step,
-            // the objective gradient g0 = H z + h and the predictor backward solve
+            // the objective gradient g0 = H z + h and the predictor backward solve.  The whole wave runs it,
+            // the instances that are done included (their lanes re-read stage N and store nothing): P's update
+            // U^T U runs on the matrix cores over the wave's 4 instances, which needs every lane (see (4)).
             double Pc[16];   // column t of P_{k+1}
             double pv = 0.0; // p_{k+1}, component t
             bool chol_ok = true;
@@ -751,7 +787,7 @@ __device__ __forceinline__ void ipm_group(const DevConst& c, const DevBuffers& d
                 else if constexpr (MPCC_WIDE_FACTOR_PF) sweep<false>(N, true, cur, nxt, load, body);
                 else sweep_noprefetch(N, true, cur, load, body);
             };
-            factor_sweep([&](int k, In& o) { load_factor(k, o, pending); }, [&](int k, const In& cur) {
+            factor_sweep([&](int k, In& o) { load_factor(run ? k : N, o, pending); }, [&](int k, const In& cur) {
                 const double lb = cur.lb, ub = cur.ub;
                 const double* Qr = cur.m;
                 const double qt = cur.m[9], Rt = cur.m[10], rt = cur.m[11];
@@ -769,7 +805,7 @@ __device__ __forceinline__ void ipm_group(const DevConst& c, const DevBuffers& d
                     if (aP) { const SlotStep st = slot_corr(sgnU, cur.pub, pcz, pca, pcd, sP, lP, sigma_mu, &rpd); sP += alpha * st.ds; lP += alpha * st.dl; }
                     zx += alpha * dx;
                     zv += alpha * dv;
-                    store_slots(k, sL, lL, sU, lU, sP, lP, zx, zv);
+                    if (run) store_slots(k, sL, lL, sU, lU, sP, lP, zx, zv);
                 }
                 PMARK(8);
                 // ---- slots: barrier weights and predictor coefficients (rc = s l)
@@ -803,7 +839,7 @@ __device__ __forceinline__ void ipm_group(const DevConst& c, const DevBuffers& d
                         g0v = s + rt;
                     }
                 }
-                *ws(k, WF_GX) = g0x;
+                if (run) *ws(k, WF_GX) = g0x;
                 double gx, gv;
                 assemble_grad(cur, k, g0x, g0v, dvr, cP, gx, gv);
                 PMARK(9);
@@ -820,11 +856,13 @@ __device__ __forceinline__ void ipm_group(const DevConst& c, const DevBuffers& d
                     }
                     pv = gx;
                     // no gains at the terminal stage: zeros, so the light sweeps' loads need no stage select
+                    if (run) {
 #pragma unroll
-                    for (int m = 0; m < 8; m++) *ws(k, WF_KR + m) = 0.0;
-                    *ws(k, WF_GVK) = (t < 8) ? g0v : 0.0;
+                        for (int m = 0; m < 8; m++) *ws(k, WF_KR + m) = 0.0;
+                        *ws(k, WF_GVK) = (t < 8) ? g0v : 0.0;
 #pragma unroll
-                    for (int m = 0; m < 4; m++) *ws(k, WF_FI + m) = 0.0;
+                        for (int m = 0; m < 4; m++) *ws(k, WF_FI + m) = 0.0;
+                    }
                     return;
                 }
                 // ---- (1) Y = B~^T P (column t), f = g_v + B~^T p (lanes 0..7)
@@ -934,21 +972,20 @@ __device__ __forceinline__ void ipm_group(const DevConst& c, const DevBuffers& d
                 }
                 PMARK(11);
 #ifdef MPCC_IPM_DBGF
-                *ws(k, 35) = gx; *ws(k, 36) = gv; *ws(k, 37) = pv; *ws(k, 38) = fv; *ws(k, 39) = dvr; *ws(k, 40) = cP;
-                *ws(k, 41) = wd; *ws(k, 42) = pnew; *ws(k, 43) = kff;
+                if (run) { *ws(k, 35) = gx; *ws(k, 36) = gv; *ws(k, 37) = pv; *ws(k, 38) = fv; *ws(k, 39) = dvr; *ws(k, 40) = cP;
+                *ws(k, 41) = wd; *ws(k, 42) = pnew; *ws(k, 43) = kff; }
 #endif
 #pragma unroll
-                for (int i = 0; i < 8; i++) {
-                    S[L_U + i * 16 + t] = u[i];
-                    S[L_K + i * 16 + t] = kc[i];
-                }
+                for (int i = 0; i < 8; i++) S[L_K + i * 16 + t] = kc[i];
                 {
                     const double kffd = from_down<8>(kff);  // lane 8+i <- kff_i
-                    *ws(k, WF_GVK) = (t < 8) ? g0v : kffd;
+                    if (run) *ws(k, WF_GVK) = (t < 8) ? g0v : kffd;
                 }
+                if (run) {
 #pragma unroll
-                for (int m = 0; m < 4; m++) *ws(k, WF_FI + m) = (t < 8) ? fi[m] : fi[4 + m];
-                // ---- (4) Hb column t and P = Hb - U^T U (column t); U rows are broadcast LDS reads
+                    for (int m = 0; m < 4; m++) *ws(k, WF_FI + m) = (t < 8) ? fi[m] : fi[4 + m];
+                }
+                // ---- (4) Hb column t and P = Hb - U^T U (column t)
                 double hb[16];
                 {
                     double Pc7[9];
@@ -978,39 +1015,60 @@ __device__ __forceinline__ void ipm_group(const DevConst& c, const DevBuffers& d
                         hb[a] = v;
                     }
                 }
-                lds_sync();
                 if (k > 0) {
+                    // On the matrix cores, per instance j of the wave: P_j = Hb_j - U_j^T U_j as two
+                    // v_mfma_f64_16x16x4f64 (rows 0..3, then 4..7 of U_j) with C = Hb_j.  The instruction is
+                    // bitwise an ascending fma chain over k (tools/probes/mfma_f64_probe.hip), so every entry
+                    // is fma(-U[7][a], U[7][t], ... fma(-U[0][a], U[0][t], Hb[a][t])), the VALU form's order.
+                    // Operand maps (A lane (g, c) -> A[c][g], B -> B[g][c], C/D register r -> [g + 4r][c]) from
+                    // the instance layout (lane (j, t): column t of instance j) by 4x4 transposes of the
+                    // wave's 16-lane groups: lane (g, c) gets U_j[g][c], U_j[4 + g][c] and Hb_j[g + 4r][c]
+                    // of every instance j, and the products go back the same way.  (U^T U issued from C = 0
+                    // right after U is formed, to overlap the solves, held its 16 results through them: more
+                    // spills, k_sqp 3.40 ms against 3.31 ms; profiles/r03m_*.)
+                    double x[4][4], ua[4][1], ub[4][1];
 #pragma unroll
-                    for (int i = 0; i < 8; i++) {
-                        const double2* row = reinterpret_cast<const double2*>(S + L_U + i * 16);
-                        double ur[16];
+                    for (int g = 0; g < 4; g++) {
 #pragma unroll
-                        for (int q2 = 0; q2 < 8; q2++) {
-                            const double2 w = row[q2];
-                            ur[2 * q2] = w.x;
-                            ur[2 * q2 + 1] = w.y;
-                        }
-#pragma unroll
-                        for (int a = 0; a < 16; a++) hb[a] -= ur[a] * u[i];
+                        for (int r = 0; r < 4; r++) x[g][r] = hb[g + 4 * r];
+                        ua[g][0] = u[g];
+                        ub[g][0] = u[4 + g];
                     }
+                    group_transpose(x);
+                    group_transpose(ua);
+                    group_transpose(ub);
 #pragma unroll
-                    for (int a = 0; a < 16; a++) Pc[a] = hb[a];
+                    for (int j = 0; j < 4; j++) {
+                        d4 acc = {x[j][0], x[j][1], x[j][2], x[j][3]};
+                        acc = __builtin_amdgcn_mfma_f64_16x16x4f64(-ua[j][0], ua[j][0], acc, 0, 0, 0);
+                        acc = __builtin_amdgcn_mfma_f64_16x16x4f64(-ub[j][0], ub[j][0], acc, 0, 0, 0);
+#pragma unroll
+                        for (int r = 0; r < 4; r++) x[j][r] = acc[r];
+                    }
+                    group_transpose(x);
+#pragma unroll
+                    for (int g = 0; g < 4; g++)
+#pragma unroll
+                        for (int r = 0; r < 4; r++) Pc[g + 4 * r] = x[g][r];
                 }
+                lds_sync();
                 {
                     const int ri = t & 7, hoff = (t < 8) ? 0 : 8;
                     const double2* row = reinterpret_cast<const double2*>(S + L_K + ri * 16 + hoff);
 #pragma unroll
                     for (int q2 = 0; q2 < 4; q2++) {
                         const double2 w = row[q2];
-                        *ws(k, WF_KR + 2 * q2) = w.x;
-                        *ws(k, WF_KR + 2 * q2 + 1) = w.y;
+                        if (run) {
+                            *ws(k, WF_KR + 2 * q2) = w.x;
+                            *ws(k, WF_KR + 2 * q2 + 1) = w.y;
+                        }
                     }
                 }
                 pv = pnew;
                 lds_sync();
                 PMARK(13);
             });
-            if (!chol_ok) {
+            if (run && !chol_ok) {
                 // Riccati breakdown: MaxIterReached unless the current iterate is converged to IPM_TOL_FB (P2);
                 // the sweep has already applied the pending update, so the iterate is the stored z
                 conv = it > 0 && mu_cur < IPM_TOL_FB && rp_cur < IPM_TOL_FB;

@@ -3,14 +3,14 @@
 // One batch call = one MPC::runMPC_ (cpp/src/MPC/mpc.cpp:104-190) for each of B independent
 // controllers.  Kernel sequence:
 //   k_prepare      thread / instance        projection, vs estimate, warm-start shift  (mpc.cpp:104-124, 54-89)
-//   k_records      thread / (instance,stage) RobotData::update: FK, J, manipulability + FD gradient (robot_data.h:55-71)
+//   k_records      RPT threads / (instance,stage) RobotData::update: FK, J, manipulability + FD gradient (robot_data.h:55-71)
 //   k_mlp_*        (mlp.hip) 2 samples / wave, FP64 MFMA: self / env collision MLPs + input Jacobians
 //   per SQP iteration (osqp_interface.cpp:431-574):
 //     k_setqp      thread / (instance,stage) stage QP record: cost, constraint rows, bounds, dynamics residual
 //     k_ipm        wave / instance           Mehrotra interior point, Riccati factorization (replaces OSQP)
 //     k_trial      thread / (instance,stage) filter line-search trial at alpha = 1 (objective, violation)
 //     k_accept     thread / instance         filter, step, termination
-//   k_finalize     thread / instance         Status -> warm start / outputs (osqp_interface.cpp:575-589, mpc.cpp:140-189)
+//   k_finalize     thread / horizon element  Status -> warm start / outputs (osqp_interface.cpp:575-589, mpc.cpp:140-189)
 #include "dev_sqp.h"
 
 namespace mpcc {
@@ -88,7 +88,17 @@ __global__ void __launch_bounds__(64) k_prepare(DevConst c, DevBuffers d) {
 // ------------------------------------------------------------------------------------------------
 // RobotData::update (robot_data.h:55-71) of joint vector q into the SoA record at rec (stride S); the
 // self-collision MLP (if masked: infinite distance) and the env MLP outputs are written by k_mlp_*.
-__device__ inline void robot_record(const DevConst& c, const double* q, double obs_r, double* rec, size_t S) {
+// The central-difference term of joint i: (mu(q + delta e_i) - mu(q - delta e_i)) / (2 delta)
+__device__ inline double manip_fd(const double* q, int i) {
+    const double delta = 1e-4;  // robot_model.cpp:439
+    double qp[DOF], qm[DOF];
+#pragma unroll
+    for (int j = 0; j < DOF; j++) { qp[j] = q[j] + (j == i ? delta : 0.0); qm[j] = q[j] - (j == i ? delta : 0.0); }
+    const double m1 = manipulability(qp), m2 = manipulability(qm);
+    return (m1 - m2) / (2 * delta);
+}
+// the record without its gradient column block R_DMU (fd = false: k_records writes it from other threads)
+__device__ inline void robot_record(const DevConst& c, const double* q, double obs_r, double* rec, size_t S, bool fd = true) {
     double pos[3], R[9], J[6 * DOF];
     robot_fk(q, pos, R, J, true);
 #pragma unroll
@@ -98,14 +108,8 @@ __device__ inline void robot_record(const DevConst& c, const double* q, double o
 #pragma unroll
     for (int a = 0; a < 6 * DOF; a++) rec[(R_J + a) * S] = J[a];
     rec[R_MU * S] = manip_from_J(J);
-    const double delta = 1e-4;  // robot_model.cpp:439
-    for (int i = 0; i < DOF; i++) {
-        double qp[DOF], qm[DOF];
-#pragma unroll
-        for (int j = 0; j < DOF; j++) { qp[j] = q[j] + (j == i ? delta : 0.0); qm[j] = q[j] - (j == i ? delta : 0.0); }
-        double m1 = manipulability(qp), m2 = manipulability(qm);
-        rec[(R_DMU + i) * S] = (m1 - m2) / (2 * delta);
-    }
+    if (fd)
+        for (int i = 0; i < DOF; i++) rec[(R_DMU + i) * S] = manip_fd(q, i);
     const double inf = __longlong_as_double(0x7ff0000000000000LL);
     if (!(c.p.constraint_mask & MPCC_CON_SELFCOL)) {
         rec[R_SEL * S] = inf;
@@ -124,17 +128,24 @@ __device__ inline void robot_record(const DevConst& c, const double* q, double o
     }
 }
 
+// RPT threads per (instance, stage) record: thread 0 the FK, Jacobian and manipulability, thread 1 + i the
+// central difference of joint i (robot_model.cpp:436-447), so a record costs the latency of two FK evaluations
+// instead of 1 + 2 DOF.  Same arithmetic per term as robot_record.
+constexpr int RPT = (DOF + 1 <= 8) ? 8 : 16;
+static_assert(DOF + 1 <= RPT, "one thread per gradient term");
 __global__ void __launch_bounds__(64) k_records(DevConst c, DevBuffers d) {
-    const int t = blockIdx.x * blockDim.x + threadIdx.x;
+    const long g_t = (long)blockIdx.x * blockDim.x + threadIdx.x;
     const int S = c.S;
-    if (t >= S) return;
+    const int t = (int)(g_t / RPT), u = (int)(g_t % RPT);
+    if (t >= S || u > DOF) return;
     const int N = c.N;
     const int b = t / (N + 1), k = t - b * (N + 1);
     const double* g = d.guess + ((size_t)b * (N + 1) + k) * NXU;
     double q[DOF];
 #pragma unroll
     for (int j = 0; j < DOF; j++) q[j] = g[j];
-    robot_record(c, q, d.obs[4 * b + 3], d.rec + t, (size_t)S);
+    if (u == 0) robot_record(c, q, d.obs[4 * b + 3], d.rec + t, (size_t)S, false);
+    else d.rec[(size_t)(R_DMU + u - 1) * S + t] = manip_fd(q, u - 1);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -207,41 +218,35 @@ __global__ void __launch_bounds__(64) k_apply(DevConst c, DevBuffers d) {
 // ------------------------------------------------------------------------------------------------
 // opt_sol / zero_guess element-wise (thread per horizon element, coalesced): a non-SOLVED instance gets
 // x_0 repeated with u = 0 (osqp_interface.cpp:422-428), a SOLVED one u_N = 0; the horizon output is the
-// result.  x_0 itself (k = 0, a < NX) is never rewritten, so the threads that read it do not race.
-__global__ void __launch_bounds__(256) k_finalize_horizon(DevConst c, DevBuffers d) {
+// result.  x_0 itself (k = 0, a < NX) is never rewritten, so the threads that read it do not race.  One launch per solve: thread (instance b, element r of the opt_sol / zero_guess horizon).  The element
+// threads of stage 0's inputs also write u0 (the value they store); thread r = 0 writes the status and the MPC
+// bookkeeping (mpc.cpp:143-189).
+__global__ void __launch_bounds__(256) k_finalize(DevConst c, DevBuffers d) {
     const long e = (long)blockIdx.x * blockDim.x + threadIdx.x;
     const int W = (c.N + 1) * NXU;
     if (e >= (long)c.Bn * W) return;
     const int b = (int)(e / W), r = (int)(e - (long)b * W);
     const int k = r / NXU, a = r - NXU * k;
     double* g = d.guess + (size_t)b * W;
-    const bool solved = d.sqi[(size_t)b * SQI + SQ_STATUS] == MPCC_SOLVED;
+    const int status = d.sqi[(size_t)b * SQI + SQ_STATUS];
+    const bool solved = status == MPCC_SOLVED;
     double v = g[r];
     if (!solved) v = (a < NX) ? g[a] : 0.0;
     else if (k == c.N && a >= NX) v = 0.0;
     if (!(k == 0 && a < NX)) g[r] = v;
     if (d.horizon) d.horizon[(size_t)b * W + r] = v;
-}
-
-__global__ void __launch_bounds__(64) k_finalize(DevConst c, DevBuffers d) {
-    const int b = blockIdx.x * blockDim.x + threadIdx.x;
-    if (b >= c.Bn) return;
-    const int N = c.N;
-    int32_t* si = d.sqi + (size_t)b * SQI;
-    const int status = si[SQ_STATUS];
-    const double* g = d.guess + (size_t)b * (N + 1) * NXU;  // already opt_sol / zero_guess (k_finalize_horizon)
+    if (k == 0 && a >= NX && d.u0_out) d.u0_out[(size_t)NU * b + (a - NX)] = v;
+    if (r != 0) return;
     if (d.status) d.status[b] = status;
     if (c.ocp) {  // solveOCP's return value only; the MPC bookkeeping belongs to the caller
-        if (d.ok) d.ok[b] = (status == MPCC_SOLVED) ? 1 : 0;
+        if (d.ok) d.ok[b] = solved ? 1 : 0;
     } else {
         int fails = d.fails[b];
-        if (status == MPCC_SOLVED) { d.valid[b] = 1; fails = 0; }
+        if (solved) { d.valid[b] = 1; fails = 0; }
         else { d.valid[b] = 0; fails++; }
         d.fails[b] = fails;
-        if (d.ok) d.ok[b] = (status == MPCC_SOLVED || (status == MPCC_MAX_ITER_EXCEEDED && fails < 5)) ? 1 : 0;
+        if (d.ok) d.ok[b] = (solved || (status == MPCC_MAX_ITER_EXCEEDED && fails < 5)) ? 1 : 0;
     }
-    if (d.u0_out)
-        for (int a = 0; a < NU; a++) d.u0_out[NU * b + a] = g[NX + a];
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -352,7 +357,7 @@ void launch_prepare(const DevConst& c, const DevBuffers& d, hipStream_t s) {
     hipLaunchKernelGGL(k_prepare, dim3(nblk(c.Bn, 64)), dim3(64), 0, s, c, d);
 }
 void launch_stage_records(const DevConst& c, const DevBuffers& d, hipStream_t s) {
-    hipLaunchKernelGGL(k_records, dim3(nblk(c.S, 64)), dim3(64), 0, s, c, d);
+    hipLaunchKernelGGL(k_records, dim3(nblk((long)c.S * RPT, 64)), dim3(64), 0, s, c, d);
 }
 void launch_setqp(const DevConst& c, const DevBuffers& d, const double* u_cur, hipStream_t s) {
     hipLaunchKernelGGL(k_setqp, dim3(nblk(c.S, 64)), dim3(64), 0, s, c, d, u_cur);
@@ -373,8 +378,7 @@ void launch_debug_records(const DevConst& c, int M, const double* q, const doubl
     hipLaunchKernelGGL(k_debug_records, dim3(nblk(M, 64)), dim3(64), 0, s, c, M, q, obs, rec);
 }
 void launch_finalize(const DevConst& c, const DevBuffers& d, hipStream_t s) {
-    hipLaunchKernelGGL(k_finalize_horizon, dim3(nblk((long)c.Bn * (c.N + 1) * NXU, 256)), dim3(256), 0, s, c, d);
-    hipLaunchKernelGGL(k_finalize, dim3(nblk(c.Bn, 64)), dim3(64), 0, s, c, d);
+    hipLaunchKernelGGL(k_finalize, dim3(nblk((long)c.Bn * (c.N + 1) * NXU, 256)), dim3(256), 0, s, c, d);
 }
 void launch_sim_step(int B, const double* x, const double* u, double ts, double* xn, hipStream_t s) {
     hipLaunchKernelGGL(k_sim_step, dim3(nblk(B, 64)), dim3(64), 0, s, B, x, u, ts, xn);
