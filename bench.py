@@ -465,6 +465,17 @@ def main():
             "qp_solves_per_step": qps}
     t_env, n_env = tmlp["k_mlp_env"]
     busy_env = union_length(np.concatenate([a for a, _ in ivs_env]), np.concatenate([b for _, b in ivs_env])) * 1e-3
+    # the collision MLPs of this configuration (mask bits 1, 4), each against the FP64 MFMA roof: mean launch
+    # duration and the fraction over it (one launch = the B/S (N + 1) samples of a group)
+    mlps = {}
+    for kn in ("k_mlp_self", "k_mlp_env"):
+        t_k, n_k = tmlp[kn]
+        if n_k:
+            fl_k = Bs * (N + 1) * mlp_flops_per_sample(kn, dof)
+            mlps[kn] = {"avg_launch_ms": t_k / n_k * 1e3, "launches_timed": n_k,
+                        "frac": fl_k / (t_k / n_k) / 1e12 / FP64_PEAK_TFLOPS}
+    if mlps:
+        roof["mlp"] = mlps
     if n_env and busy_env > busy:  # the env MLP ran longer than the QP solve (configs[2])
         t_l = t_env / n_env
         samples = Bs * (N + 1)
@@ -480,7 +491,7 @@ def main():
                 "work": "F_env (SURVEY 8(d): value + DOF Jacobian columns) x B/S (N+1) samples per launch, over the "
                         "union of the launches' intervals",
                 "k_sqp": {"avg_launch_ms": t_ipm * 1e3, "frac": achieved / FP64_PEAK_TFLOPS, "traffic": traffic,
-                          "busy_ms_per_step": busy / max(1, ncalls) * 1e3}}
+                          "busy_ms_per_step": busy / max(1, ncalls) * 1e3}, "mlp": mlps}
 
     # PCIe-inclusive rate (host buffers in and out through mpcc_solve): a diagnostic, never `value`
     pcie = None

@@ -65,6 +65,8 @@ enum : int {
     WF_GX,                                        // objective gradient (H z + h)_x~
     WF_FI,                                        // 4 fields: F^-1 row halves, field m: lane i -> Fi[i][m], lane 8+i -> Fi[i][4+m]
     WF_SP = WF_FI + 4, WF_LP,                     // slack / multiplier of poly slot t (more than 4 poly rows)
+    WF_PZ, WF_PA, WF_PD,                          // wide-poly variants (PCACHE): lane p -> c_p^T z, c_p^T dza, c_p^T dz
+                                                  // of poly row p, each formed once per iteration (poly_cz)
     WF_DX, WF_DV,                                 // corrector step (same layout as the predictor step)
     NWF
 };
@@ -99,7 +101,7 @@ static_assert(LF_CBWD + 1 <= NWF, "the odd last line of a ring slot reads one fi
 size_t ipm_lds_bytes(int /*N*/, int npmax) {
     const size_t uk = (size_t)IPW * GRP_LDS * sizeof(double);
     const size_t ring = (npmax <= 2)          ? (size_t)LRING * LG(LF_CBWD) * 1024
-                        : use_ring(npmax)       ? (size_t)LRING_W * LG(WF_LP + 1, QLINES_W) * 1024
+                        : use_ring(npmax)       ? (size_t)LRING_W * LG(WF_PD + 1, QLINES_W) * 1024
                                                 : 0;
     return ring > uk ? ring : uk;
 }
@@ -286,6 +288,7 @@ struct StageIn {
     double pa[NPE], pb[NPE];      // poly rows p: a_p[t], bv_p[t] (t < 7)
     double pub;                   // upper bound of poly row t (t < npmax)
     double sL, lL, sU, lU, sP, lP, zx, zv;
+    double pz, pca, pcd;          // PCACHE: c_p^T z, c_p^T dza, c_p^T dz of poly row t (WF_PZ, WF_PA, WF_PD)
     double x0, x1, x2, x3;        // sweep-specific pairs (dz, dza, g0)
     double m[12];                 // sweep-specific: Q row + q, R, r | K row halves + kff | K column + F^-1 half
 };
@@ -462,6 +465,11 @@ __device__ __forceinline__ void ipm_group(const DevConst& c, const DevBuffers& d
     // Poly slot state packed into the upper lanes of the v field (<= 4 poly rows): every sweep then loads
     // 6 workspace lines of slot and iterate state per stage instead of 8.
     constexpr bool PACKP = NPM <= 4;
+    // Wide-poly variants: c_p^T z, c_p^T dza and c_p^T dz (11 reductions over the row's 16 lanes each) are formed
+    // once per iteration where z, dza, dz are made, kept in the workspace (WF_PZ, WF_PA, WF_PD) and read by the
+    // other sweeps, which recomputed them from the same stored vectors (the same values: 3 evaluations per stage
+    // and iteration instead of 11)
+    constexpr bool PCACHE = NPM >= 9;
     auto zv_pack = [&](double zv, double sP, double lP) -> double {
         if constexpr (PACKP) {
             const double s8 = from_down<8>(sP), l12 = from_down<12>(lP);  // DPP with the whole row active
@@ -496,6 +504,7 @@ __device__ __forceinline__ void ipm_group(const DevConst& c, const DevBuffers& d
         o.pub = (t < NPM) ? pu : INF;
         o.sL = *ws(k, WF_SL); o.lL = *ws(k, WF_LL); o.sU = *ws(k, WF_SU); o.lU = *ws(k, WF_LU);
         o.zx = *ws(k, WF_ZX);
+        if constexpr (PCACHE) { o.pz = *ws(k, WF_PZ); o.pca = *ws(k, WF_PA); o.pcd = *ws(k, WF_PD); }
         const double zraw = *ws(k, WF_ZV);
         if constexpr (PACKP) {
             o.sP = from_up<8>(zraw);   // lane p <- lane 8 + p
@@ -564,7 +573,7 @@ __device__ __forceinline__ void ipm_group(const DevConst& c, const DevBuffers& d
         o_pb[p] = qoff(QS_POLY + 15 * p + 7 + (t < 7 ? t : 0));
     }
     // fields in a slot image: the sweep's run; the wide ring also needs the unpacked poly slot state
-    auto ring_nf = [](auto nfc) { return (NPM <= 2) ? decltype(nfc)::value : WF_LP + 1; };
+    auto ring_nf = [](auto nfc) { return (NPM <= 2) ? decltype(nfc)::value : WF_PD + 1; };
     auto glds_stage = [&](int k, int slot, auto nfc) {
         constexpr int G = LG(ring_nf(nfc), QL);
         // the image's last record line and workspace line stay inside the stage (static), the stage inside the
@@ -597,6 +606,7 @@ __device__ __forceinline__ void ipm_group(const DevConst& c, const DevBuffers& d
         auto f = [&](int field) { return im[img_at(QL + field) + t]; };
         o.sL = f(WF_SL); o.lL = f(WF_LL); o.sU = f(WF_SU); o.lU = f(WF_LU);
         o.zx = f(WF_ZX);
+        if constexpr (PCACHE) { o.pz = f(WF_PZ); o.pca = f(WF_PA); o.pcd = f(WF_PD); }
         const double zraw = f(WF_ZV);
         if constexpr (PACKP) {
             o.sP = from_up<8>(zraw);   // lane p <- lane 8 + p
@@ -747,6 +757,7 @@ __device__ __forceinline__ void ipm_group(const DevConst& c, const DevBuffers& d
             const double yx = rowY ? y : 0.0;
             const double cz = row_cz(k, yx, 0.0);
             const double pcz = poly_cz(cur, k, yx, 0.0);
+            if constexpr (PCACHE) *ws(k, WF_PZ) = pcz;
             const bool aL = row_active(k, cur.lb), aU = row_active(k, cur.ub), aP = poly_slot_active(cur, k);
             double sL = 1, lL = 0, sU = 1, lU = 0, sP = 1, lP = 0;
             if (aL) { sL = fmax(-(sgnL * cz - sgnL * cur.lb), s_floor); lL = (lam_scale > 0) ? lam_scale / sL : 1.0; }
@@ -798,7 +809,12 @@ __device__ __forceinline__ void ipm_group(const DevConst& c, const DevBuffers& d
                     // previous iteration's update at this stage (oracle: z += a dz, s += a ds, l += a dl)
                     const double dx = cur.x0, dv = cur.x1, ax = cur.x2, av = cur.x3;
                     const double cz = row_cz(k, zx, zv), cd = row_cz(k, dx, dv), ca = row_cz(k, ax, av);
-                    const double pcz = poly_cz(cur, k, zx, zv), pcd = poly_cz(cur, k, dx, dv), pca = poly_cz(cur, k, ax, av);
+                    double pcz, pcd, pca;
+                    if constexpr (PCACHE) {
+                        pcz = cur.pz; pcd = cur.pcd; pca = cur.pca;
+                    } else {
+                        pcz = poly_cz(cur, k, zx, zv); pcd = poly_cz(cur, k, dx, dv); pca = poly_cz(cur, k, ax, av);
+                    }
                     double rpd;
                     if (aL) { const SlotStep st = slot_corr(sgnL, lb, cz, ca, cd, sL, lL, sigma_mu, &rpd); sL += alpha * st.ds; lL += alpha * st.dl; }
                     if (aU) { const SlotStep st = slot_corr(sgnU, ub, cz, ca, cd, sU, lU, sigma_mu, &rpd); sU += alpha * st.ds; lU += alpha * st.dl; }
@@ -811,6 +827,9 @@ __device__ __forceinline__ void ipm_group(const DevConst& c, const DevBuffers& d
                 // ---- slots: barrier weights and predictor coefficients (rc = s l)
                 const double cz = row_cz(k, zx, zv);
                 const double pcz = poly_cz(cur, k, zx, zv);
+                if constexpr (PCACHE) {
+                    if (run) *ws(k, WF_PZ) = pcz;
+                }
                 double WL = 0, WU = 0, WP = 0, cL = 0, cU = 0, cP = 0;
                 if (aL) { const double rp = slot_rp(sgnL, cz, lb, sL); const double ri = rcp(sL); WL = lL * ri; cL = slot_coef(ri, lL, rp, sL * lL); }
                 if (aU) { const double rp = slot_rp(sgnU, cz, ub, sU); const double ri = rcp(sU); WU = lU * ri; cU = slot_coef(ri, lU, rp, sU * lU); }
@@ -1091,7 +1110,8 @@ __device__ __forceinline__ void ipm_group(const DevConst& c, const DevBuffers& d
                 *ws(k, WF_AX) = xt;
                 *ws(k, WF_AV) = dvv;
                 const double cz = row_cz(k, cur.zx, cur.zv), ca = row_cz(k, xt, dvv);
-                const double pcz = poly_cz(cur, k, cur.zx, cur.zv), pca = poly_cz(cur, k, xt, dvv);
+                const double pcz = PCACHE ? cur.pz : poly_cz(cur, k, cur.zx, cur.zv), pca = poly_cz(cur, k, xt, dvv);
+                if constexpr (PCACHE) *ws(k, WF_PA) = pca;
                 auto rec = [&](bool a, double sgn, double bnd, double czz, double caa, double s, double l) {
                     if (!a) return;
                     const double rp = slot_rp(sgn, czz, bnd, s);
@@ -1124,7 +1144,8 @@ __device__ __forceinline__ void ipm_group(const DevConst& c, const DevBuffers& d
                         [&](const double* im, In& o) { lds_bwd(im, o); }, [&](int k, const In& cur) {
                 const bool aL = row_active(k, cur.lb), aU = row_active(k, cur.ub), aP = poly_slot_active(cur, k);
                 const double cz = row_cz(k, cur.zx, cur.zv), ca = row_cz(k, cur.x0, cur.x1);
-                const double pcz = poly_cz(cur, k, cur.zx, cur.zv), pca = poly_cz(cur, k, cur.x0, cur.x1);
+                const double pcz = PCACHE ? cur.pz : poly_cz(cur, k, cur.zx, cur.zv);
+                const double pca = PCACHE ? cur.pca : poly_cz(cur, k, cur.x0, cur.x1);
                 auto coef = [&](bool a, double sgn, double bnd, double czz, double caa, double s, double l) -> double {
                     if (!a) return 0.0;
                     const double rp = slot_rp(sgn, czz, bnd, s);
@@ -1196,8 +1217,9 @@ __device__ __forceinline__ void ipm_group(const DevConst& c, const DevBuffers& d
                 *ws(k, WF_DV) = dvv;
                 dzm = fmax(dzm, fmax(fabs(xt), fabs(dvv)));
                 const double cz = row_cz(k, cur.zx, cur.zv), cd = row_cz(k, xt, dvv), ca = row_cz(k, cur.x0, cur.x1);
-                const double pcz = poly_cz(cur, k, cur.zx, cur.zv), pcd = poly_cz(cur, k, xt, dvv);
-                const double pca = poly_cz(cur, k, cur.x0, cur.x1);
+                const double pcz = PCACHE ? cur.pz : poly_cz(cur, k, cur.zx, cur.zv), pcd = poly_cz(cur, k, xt, dvv);
+                const double pca = PCACHE ? cur.pca : poly_cz(cur, k, cur.x0, cur.x1);
+                if constexpr (PCACHE) *ws(k, WF_PD) = pcd;
                 auto rec = [&](bool a, double sgn, double bnd, double czz, double caa, double cdd, double s, double l) {
                     if (!a) return;
                     double rp;

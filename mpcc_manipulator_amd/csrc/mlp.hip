@@ -91,6 +91,58 @@ __device__ __forceinline__ void mfma_layer_lds(const double* __restrict__ Wp, co
     }
 }
 
+// The same layer with the k-tiles of W streamed into a 3-slot LDS ring by global_load_lds_dwordx4 (16 bytes per
+// lane straight to LDS, no register staging), two k-tiles ahead: the block's 4 waves each copy a quarter of a
+// tile, wait for their own copies (vmcnt), then one barrier per k-tile makes the tile visible to all and retires
+// the slot read two tiles ago, which the next copy overwrites.  The register-staged double buffer (mfma_layer_lds)
+// waited on the L2 latency of the tile it had just fetched at every stash.  Same fragments, same ascending k
+// order per row tile: bitwise the result of mfma_layer.  All 256 threads of the block must call it.
+constexpr int RING_SLOTS = 3;
+__device__ __forceinline__ void glds16_to(const void* src, unsigned lds_dst) {
+    unsigned keep;
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+                 : "=&s"(keep) : "v"(src), "s"(lds_dst) : "memory");
+}
+template <int KT, int RT>
+__device__ __forceinline__ void mfma_layer_ring(const double* __restrict__ Wp, const d4 (&in)[KT], d4 (&out)[RT],
+                                                int lane, double* __restrict__ ring /* RING_SLOTS x RT*256 */) {
+    constexpr int KS = 4 * KT;
+    constexpr int CH = RT * 256;          // doubles per k-tile
+    constexpr int PT = CH / 2 / 256;      // 16-byte copies per thread per k-tile
+    static_assert(CH % 512 == 0, "mfma_layer_ring: whole 16-byte copies per thread");
+    const int tid = threadIdx.x, w = tid >> 6;
+    const unsigned base = (unsigned)(uintptr_t)(__attribute__((address_space(3))) char*)(char*)ring;
+    auto issue = [&](int kt) {  // k-tile kt into slot kt % RING_SLOTS; copy j of wave w: 1 KB at 4 KB j + 1 KB w
+        const unsigned slot = base + (unsigned)((kt % RING_SLOTS) * CH * 8);
+#pragma unroll
+        for (int j = 0; j < PT; j++) {
+            const int e = tid + 256 * j;  // 16-byte element of the tile: double 2e = [t][r][lane]
+            const int t = e >> 7;
+            glds16_to(Wp + ((size_t)t * KS + 4 * kt) * 64 + 2 * (e & 127),
+                      __builtin_amdgcn_readfirstlane(slot + 4096u * j + 1024u * w));
+        }
+    };
+#pragma unroll
+    for (int t = 0; t < RT; t++) out[t] = d4{0.0, 0.0, 0.0, 0.0};
+    issue(0);
+    if (KT > 1) issue(1);
+#pragma unroll
+    for (int kt = 0; kt < KT; kt++) {
+        // this wave's copies of tile kt have landed once at most those of tile kt + 1 are outstanding
+        if (kt + 1 < KT) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PT) : "memory");
+        else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        if (kt + 2 < KT) issue(kt + 2);
+        const double* L = ring + (kt % RING_SLOTS) * CH;
+#pragma unroll
+        for (int r = 0; r < 4; r++)
+#pragma unroll
+            for (int t = 0; t < RT; t++)
+                out[t] = __builtin_amdgcn_mfma_f64_16x16x4f64(L[(t * 4 + r) * 64 + lane], in[kt][r], out[t], 0, 0, 0);
+    }
+    __syncthreads();  // the ring is free for the next layer's first copies
+}
+
 // hidden-layer epilogue: value columns h = relu(z + b); tangent columns dh = (z + b > 0) ? dz : 0.
 // CPS = columns per sample: 8 (value + 7 tangents, 2 samples per 16-column tile) or 16 (value + up to 15
 // tangents, one sample per tile: the mobile env network's 10 input directions).
@@ -226,7 +278,7 @@ __global__ void __launch_bounds__(256) k_mlp_self(DevConst c, DevBuffers d, NNDe
     const int wave = blockIdx.x * 4 + (threadIdx.x >> 6);
     const int m = 2 * wave + ((lane >> 3) & 1);
     // no early exit: the input layer synchronizes the block (see k_mlp_env)
-    __shared__ __attribute__((aligned(16))) double wl[2 * 16 * 256];
+    __shared__ __attribute__((aligned(16))) double wl[RING_SLOTS * 16 * 256];
     double q[DOF], obs[3];
     sample_input(c, d, m, M, qin, obsin, q, obs);
     double x[7];
@@ -234,9 +286,9 @@ __global__ void __launch_bounds__(256) k_mlp_self(DevConst c, DevBuffers d, NNDe
     for (int i = 0; i < 7; i++) x[i] = q[NBASE + i];
     d4 a0[2], a1[16], a2[4], o[1];
     nerf_input<7>(x, a0, lane);
-    mfma_layer_lds<2, 16>(W + nd.offW[0], a0, a1, lane, wl);
+    mfma_layer_ring<2, 16>(W + nd.offW[0], a0, a1, lane, wl);
     relu_gate<16>(a1, W + nd.offb[0], lane);
-    mfma_layer<16, 4>(W + nd.offW[1], a1, a2, lane);  // LDS staging measured 6% slower at RT = 4
+    mfma_layer_ring<16, 4>(W + nd.offW[1], a1, a2, lane, wl);
     relu_gate<4>(a2, W + nd.offb[1], lane);
     mfma_layer<4, 1>(W + nd.offW[2], a2, o, lane);
     write_out<1>(o[0], W + nd.offb[2], lane, m, M, rec, S, R_SEL, R_DSEL);
@@ -267,10 +319,10 @@ __device__ __forceinline__ void mlp_env_body(const DevConst& c, const DevBuffers
     }
     d4 a0[2], a[16], h[16], o[1];
     nerf_input<10, CPS>(x, a0, lane);
-    mfma_layer_lds<2, 16>(W + nd.offW[0], a0, a, lane, wl);
+    mfma_layer_ring<2, 16>(W + nd.offW[0], a0, a, lane, wl);
     relu_gate<16, CPS>(a, W + nd.offb[0], lane);
     for (int l = 1; l <= 3; l++) {  // three 256 x 256 hidden layers share one unrolled body
-        mfma_layer_lds<16, 16>(W + nd.offW[l], a, h, lane, wl);
+        mfma_layer_ring<16, 16>(W + nd.offW[l], a, h, lane, wl);
         relu_gate<16, CPS>(h, W + nd.offb[l], lane);
 #pragma unroll
         for (int t = 0; t < 16; t++) a[t] = h[t];
@@ -288,7 +340,7 @@ __global__ void __launch_bounds__(256) k_mlp_env(DevConst c, DevBuffers d, NNDes
                                                  double* __restrict__ rec, int S) {
     // no early exit: the hidden layers synchronize the block (a wave past M computes on a clamped
     // sample and write_out drops its result)
-    __shared__ __attribute__((aligned(16))) double wl[2 * 16 * 256];
+    __shared__ __attribute__((aligned(16))) double wl[RING_SLOTS * 16 * 256];
     mlp_env_body<ENV_CPS>(c, d, nd, W, M, qin, obsin, rec, S, wl);
 }
 
