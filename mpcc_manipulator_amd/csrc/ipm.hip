@@ -88,6 +88,9 @@ static_assert(QS_POLY + 2 * 15 <= QS_YLB + 16 * QLINES, "bound block of <= 2 pol
 // The wide-poly variants (NPM >= 9, MPCC_WIDE_RING): a 2-slot ring (one stage in flight) of a 14-line
 // bound block (11 poly rows) and the fields up to the unpacked poly slot state; 19 KiB per slot, so 4 waves
 // of 38 KiB fit a CU's 160 KiB.
+#ifndef MPCC_PCN
+#define MPCC_PCN 0  // 1: cached c_p^T (z, dza, dz) in spare lanes for 1 or 2 poly rows: 1% slower (profiles/r03w_ab_pcn.log)
+#endif
 #ifndef MPCC_WIDE_RING
 #define MPCC_WIDE_RING 1
 #endif
@@ -470,8 +473,15 @@ __device__ __forceinline__ void ipm_group(const DevConst& c, const DevBuffers& d
     // other sweeps, which recomputed them from the same stored vectors (the same values: 3 evaluations per stage
     // and iteration instead of 11)
     constexpr bool PCACHE = NPM >= 9;
-    auto zv_pack = [&](double zv, double sP, double lP) -> double {
-        if constexpr (PACKP) {
+    // The same for 1 or 2 poly rows at no extra traffic: c_p^T z rides in the free lanes 10 + p of the packed WF_ZV,
+    // c_p^T dza and c_p^T dz in lanes 8 + p of WF_AV and WF_DV (whose v occupies lanes 0..7; readers mask them)
+    constexpr bool PCN = MPCC_PCN && NPM >= 1 && NPM <= 2;
+    constexpr bool PCV = PCACHE || PCN;
+    auto zv_pack = [&](double zv, double sP, double lP, double pz) -> double {
+        if constexpr (PCN) {
+            const double s8 = from_down<8>(sP), l12 = from_down<12>(lP), z10 = from_down<10>(pz);  // whole row active
+            return (t < 8) ? zv : ((t < 10) ? s8 : ((t < 12) ? z10 : l12));
+        } else if constexpr (PACKP) {
             const double s8 = from_down<8>(sP), l12 = from_down<12>(lP);  // DPP with the whole row active
             return (t < 8) ? zv : ((t < 12) ? s8 : l12);
         } else {
@@ -479,11 +489,11 @@ __device__ __forceinline__ void ipm_group(const DevConst& c, const DevBuffers& d
         }
     };
     auto store_slots = [&](int k, double sL, double lL, double sU, double lU, double sP, double lP, double zx,
-                           double zv) {
+                           double zv, double pz) {
         *ws(k, WF_SL) = sL; *ws(k, WF_LL) = lL; *ws(k, WF_SU) = sU; *ws(k, WF_LU) = lU;
         if constexpr (!PACKP) { *ws(k, WF_SP) = sP; *ws(k, WF_LP) = lP; }
         *ws(k, WF_ZX) = zx;
-        *ws(k, WF_ZV) = zv_pack(zv, sP, lP);
+        *ws(k, WF_ZV) = zv_pack(zv, sP, lP, pz);
     };
 
     // ---- stage loaders: every load unconditional (addresses clamped inside the stage record), the
@@ -509,6 +519,7 @@ __device__ __forceinline__ void ipm_group(const DevConst& c, const DevBuffers& d
         if constexpr (PACKP) {
             o.sP = from_up<8>(zraw);   // lane p <- lane 8 + p
             o.lP = from_up<12>(zraw);  // lane p <- lane 12 + p
+            if constexpr (PCN) o.pz = from_up<10>(zraw);  // lane p <- lane 10 + p
             o.zv = (t < 8) ? zraw : 0.0;
         } else {
             o.sP = *ws(k, WF_SP); o.lP = *ws(k, WF_LP);
@@ -528,18 +539,30 @@ __device__ __forceinline__ void ipm_group(const DevConst& c, const DevBuffers& d
         o.m[10] = (t < 8 && k < N) ? rv : 0.0;
         o.m[11] = (t < 8 && k < N) ? rr : 0.0;
         const double x0 = *ws(k, WF_DX), x1 = *ws(k, WF_DV), x2 = *ws(k, WF_AX), x3 = *ws(k, WF_AV);
-        o.x0 = upd ? x0 : 0.0; o.x1 = upd ? x1 : 0.0; o.x2 = upd ? x2 : 0.0; o.x3 = upd ? x3 : 0.0;
+        const bool vl = !PCN || t < 8;  // PCN: lanes 8.. of DV / AV carry c_p^T dz / c_p^T dza
+        o.x0 = upd ? x0 : 0.0; o.x1 = (upd && vl) ? x1 : 0.0; o.x2 = upd ? x2 : 0.0; o.x3 = (upd && vl) ? x3 : 0.0;
+        if constexpr (PCN) { o.pcd = from_up<8>(x1); o.pca = from_up<8>(x3); }  // lane p <- lane 8 + p
     };
     auto load_fwd = [&](int k, In& o, bool corr) {
         load_common(k, o);
 #pragma unroll
         for (int m = 0; m < 8; m++) o.m[m] = *ws(k, WF_KR + m);  // zero at k = N (factor sweep)
         o.m[8] = from_up<8>(*ws(k, WF_GVK));  // lane i <- kff_i (lanes 8..15: 0)
-        if (corr) { o.x0 = *ws(k, WF_AX); o.x1 = *ws(k, WF_AV); } else { o.x0 = o.x1 = 0.0; }  // corr: constant
+        if (corr) {  // corr: constant
+            o.x0 = *ws(k, WF_AX);
+            const double av = *ws(k, WF_AV);
+            o.x1 = (!PCN || t < 8) ? av : 0.0;
+            if constexpr (PCN) o.pca = from_up<8>(av);
+        } else {
+            o.x0 = o.x1 = 0.0;
+        }
     };
     auto load_bwd = [&](int k, In& o) {
         load_common(k, o);
-        o.x0 = *ws(k, WF_AX); o.x1 = *ws(k, WF_AV); o.x2 = *ws(k, WF_GX);
+        o.x0 = *ws(k, WF_AX); o.x2 = *ws(k, WF_GX);
+        const double av = *ws(k, WF_AV);
+        o.x1 = (!PCN || t < 8) ? av : 0.0;
+        if constexpr (PCN) o.pca = from_up<8>(av);
         const double gvk = *ws(k, WF_GVK);
         o.x3 = (t < 8) ? gvk : 0.0;
 #pragma unroll
@@ -611,6 +634,7 @@ __device__ __forceinline__ void ipm_group(const DevConst& c, const DevBuffers& d
         if constexpr (PACKP) {
             o.sP = from_up<8>(zraw);   // lane p <- lane 8 + p
             o.lP = from_up<12>(zraw);  // lane p <- lane 12 + p
+            if constexpr (PCN) o.pz = from_up<10>(zraw);
             o.zv = (t < 8) ? zraw : 0.0;
         } else {
             o.sP = f(WF_SP); o.lP = f(WF_LP);
@@ -623,11 +647,21 @@ __device__ __forceinline__ void ipm_group(const DevConst& c, const DevBuffers& d
 #pragma unroll
         for (int m = 0; m < 8; m++) o.m[m] = fld(im, WF_KR + m);
         o.m[8] = from_up<8>(fld(im, WF_GVK));
-        if (corr) { o.x0 = fld(im, WF_AX); o.x1 = fld(im, WF_AV); } else { o.x0 = o.x1 = 0.0; }
+        if (corr) {
+            o.x0 = fld(im, WF_AX);
+            const double av = fld(im, WF_AV);
+            o.x1 = (!PCN || t < 8) ? av : 0.0;
+            if constexpr (PCN) o.pca = from_up<8>(av);
+        } else {
+            o.x0 = o.x1 = 0.0;
+        }
     };
     auto lds_bwd = [&](const double* im, In& o) {
         lds_common(im, o);
-        o.x0 = fld(im, WF_AX); o.x1 = fld(im, WF_AV); o.x2 = fld(im, WF_GX);
+        o.x0 = fld(im, WF_AX); o.x2 = fld(im, WF_GX);
+        const double av = fld(im, WF_AV);
+        o.x1 = (!PCN || t < 8) ? av : 0.0;
+        if constexpr (PCN) o.pca = from_up<8>(av);
         const double gvk = fld(im, WF_GVK);
         o.x3 = (t < 8) ? gvk : 0.0;
 #pragma unroll
@@ -764,7 +798,7 @@ __device__ __forceinline__ void ipm_group(const DevConst& c, const DevBuffers& d
             if (aU) { sU = fmax(-(sgnU * cz - sgnU * cur.ub), s_floor); lU = (lam_scale > 0) ? lam_scale / sU : 1.0; }
             if (aP) { sP = fmax(-(sgnU * pcz - sgnU * cur.pub), s_floor); lP = (lam_scale > 0) ? lam_scale / sP : 1.0; }
             mcount += (aL ? 1.0 : 0.0) + (aU ? 1.0 : 0.0) + (aP ? 1.0 : 0.0);
-            store_slots(k, sL, lL, sU, lU, sP, lP, yx, 0.0);
+            store_slots(k, sL, lL, sU, lU, sP, lP, yx, 0.0, pcz);
             // y_{k+1} = M y_k + b_k (oracle order: sum_b M[a][b] y_b, then + b_a)
             const double y8 = from_up<1>(y);  // lane 7 <- y_8
             const double yn = (t == 7) ? m77 * y + m78 * y8 : mt * y;
@@ -810,7 +844,7 @@ __device__ __forceinline__ void ipm_group(const DevConst& c, const DevBuffers& d
                     const double dx = cur.x0, dv = cur.x1, ax = cur.x2, av = cur.x3;
                     const double cz = row_cz(k, zx, zv), cd = row_cz(k, dx, dv), ca = row_cz(k, ax, av);
                     double pcz, pcd, pca;
-                    if constexpr (PCACHE) {
+                    if constexpr (PCV) {
                         pcz = cur.pz; pcd = cur.pcd; pca = cur.pca;
                     } else {
                         pcz = poly_cz(cur, k, zx, zv); pcd = poly_cz(cur, k, dx, dv); pca = poly_cz(cur, k, ax, av);
@@ -821,7 +855,9 @@ __device__ __forceinline__ void ipm_group(const DevConst& c, const DevBuffers& d
                     if (aP) { const SlotStep st = slot_corr(sgnU, cur.pub, pcz, pca, pcd, sP, lP, sigma_mu, &rpd); sP += alpha * st.ds; lP += alpha * st.dl; }
                     zx += alpha * dx;
                     zv += alpha * dv;
-                    if (run) store_slots(k, sL, lL, sU, lU, sP, lP, zx, zv);
+                    if constexpr (!PCN) {
+                        if (run) store_slots(k, sL, lL, sU, lU, sP, lP, zx, zv, 0.0);
+                    }
                 }
                 PMARK(8);
                 // ---- slots: barrier weights and predictor coefficients (rc = s l)
@@ -829,6 +865,9 @@ __device__ __forceinline__ void ipm_group(const DevConst& c, const DevBuffers& d
                 const double pcz = poly_cz(cur, k, zx, zv);
                 if constexpr (PCACHE) {
                     if (run) *ws(k, WF_PZ) = pcz;
+                }
+                if constexpr (PCN) {  // the updated iterate with its c_p^T z (unchanged iterate: stored as it is)
+                    if (run && pending) store_slots(k, sL, lL, sU, lU, sP, lP, zx, zv, pcz);
                 }
                 double WL = 0, WU = 0, WP = 0, cL = 0, cU = 0, cP = 0;
                 if (aL) { const double rp = slot_rp(sgnL, cz, lb, sL); const double ri = rcp(sL); WL = lL * ri; cL = slot_coef(ri, lL, rp, sL * lL); }
@@ -1108,10 +1147,15 @@ __device__ __forceinline__ void ipm_group(const DevConst& c, const DevBuffers& d
                 if (k < N) fwd_step(cur, xt, v, xn);
                 const double dvv = (t < 8 && k < N) ? v : 0.0;
                 *ws(k, WF_AX) = xt;
-                *ws(k, WF_AV) = dvv;
                 const double cz = row_cz(k, cur.zx, cur.zv), ca = row_cz(k, xt, dvv);
-                const double pcz = PCACHE ? cur.pz : poly_cz(cur, k, cur.zx, cur.zv), pca = poly_cz(cur, k, xt, dvv);
+                const double pcz = PCV ? cur.pz : poly_cz(cur, k, cur.zx, cur.zv), pca = poly_cz(cur, k, xt, dvv);
                 if constexpr (PCACHE) *ws(k, WF_PA) = pca;
+                if constexpr (PCN) {
+                    const double pa8 = from_down<8>(pca);  // lane 8 + p <- c_p^T dza
+                    *ws(k, WF_AV) = (t < 8) ? dvv : pa8;
+                } else {
+                    *ws(k, WF_AV) = dvv;
+                }
                 auto rec = [&](bool a, double sgn, double bnd, double czz, double caa, double s, double l) {
                     if (!a) return;
                     const double rp = slot_rp(sgn, czz, bnd, s);
@@ -1144,8 +1188,8 @@ __device__ __forceinline__ void ipm_group(const DevConst& c, const DevBuffers& d
                         [&](const double* im, In& o) { lds_bwd(im, o); }, [&](int k, const In& cur) {
                 const bool aL = row_active(k, cur.lb), aU = row_active(k, cur.ub), aP = poly_slot_active(cur, k);
                 const double cz = row_cz(k, cur.zx, cur.zv), ca = row_cz(k, cur.x0, cur.x1);
-                const double pcz = PCACHE ? cur.pz : poly_cz(cur, k, cur.zx, cur.zv);
-                const double pca = PCACHE ? cur.pca : poly_cz(cur, k, cur.x0, cur.x1);
+                const double pcz = PCV ? cur.pz : poly_cz(cur, k, cur.zx, cur.zv);
+                const double pca = PCV ? cur.pca : poly_cz(cur, k, cur.x0, cur.x1);
                 auto coef = [&](bool a, double sgn, double bnd, double czz, double caa, double s, double l) -> double {
                     if (!a) return 0.0;
                     const double rp = slot_rp(sgn, czz, bnd, s);
@@ -1214,12 +1258,17 @@ __device__ __forceinline__ void ipm_group(const DevConst& c, const DevBuffers& d
                 if (k < N) fwd_step(cur, xt, v, xn);
                 const double dvv = (t < 8 && k < N) ? v : 0.0;
                 *ws(k, WF_DX) = xt;
-                *ws(k, WF_DV) = dvv;
                 dzm = fmax(dzm, fmax(fabs(xt), fabs(dvv)));
                 const double cz = row_cz(k, cur.zx, cur.zv), cd = row_cz(k, xt, dvv), ca = row_cz(k, cur.x0, cur.x1);
-                const double pcz = PCACHE ? cur.pz : poly_cz(cur, k, cur.zx, cur.zv), pcd = poly_cz(cur, k, xt, dvv);
-                const double pca = PCACHE ? cur.pca : poly_cz(cur, k, cur.x0, cur.x1);
+                const double pcz = PCV ? cur.pz : poly_cz(cur, k, cur.zx, cur.zv), pcd = poly_cz(cur, k, xt, dvv);
+                const double pca = PCV ? cur.pca : poly_cz(cur, k, cur.x0, cur.x1);
                 if constexpr (PCACHE) *ws(k, WF_PD) = pcd;
+                if constexpr (PCN) {
+                    const double pd8 = from_down<8>(pcd);  // lane 8 + p <- c_p^T dz
+                    *ws(k, WF_DV) = (t < 8) ? dvv : pd8;
+                } else {
+                    *ws(k, WF_DV) = dvv;
+                }
                 auto rec = [&](bool a, double sgn, double bnd, double czz, double caa, double cdd, double s, double l) {
                     if (!a) return;
                     double rp;
