@@ -270,28 +270,73 @@ __device__ __forceinline__ void sample_input(const DevConst& c, const DevBuffers
 
 }  // namespace
 
-// self network 21 -> 256 -> 64 -> 1 (osqp_interface.cpp:35-38) on the Panda joints
+// self network 21 -> 256 -> 64 -> 1 (osqp_interface.cpp:35-38) on the Panda joints.  The input layer's 16-row
+// output tiles are consumed as they are made: tile t (after bias + ReLU gating) is k-tile t of the 256 -> 64
+// layer, so the 256-wide hidden activation never exists as a whole — a fraction of the registers of the
+// layer-by-layer form (336), several waves per SIMD, and the weights are read straight from L2 (the wave count
+// hides their latency; no LDS, no barriers).  A wave carries SELF_CT 16-column tiles (2 samples each), so every
+// weight fragment it loads feeds SELF_CT MFMAs.  Per output the same fragments in the same ascending k order:
+// bitwise the layer-by-layer form.
+#ifndef MPCC_SELF_CT
+#define MPCC_SELF_CT 2
+#endif
+constexpr int SELF_CT = MPCC_SELF_CT;
 __global__ void __launch_bounds__(256) k_mlp_self(DevConst c, DevBuffers d, NNDesc nd, const double* __restrict__ W, int M,
                                                   const double* __restrict__ qin, const double* __restrict__ obsin,
                                                   double* __restrict__ rec, int S) {
     const int lane = threadIdx.x & 63;
     const int wave = blockIdx.x * 4 + (threadIdx.x >> 6);
-    const int m = 2 * wave + ((lane >> 3) & 1);
-    // no early exit: the input layer synchronizes the block (see k_mlp_env)
-    __shared__ __attribute__((aligned(16))) double wl[RING_SLOTS * 16 * 256];
-    double q[DOF], obs[3];
-    sample_input(c, d, m, M, qin, obsin, q, obs);
-    double x[7];
+    int m[SELF_CT];
+    d4 a0[SELF_CT][2], a2[SELF_CT][4], o[SELF_CT][1];
 #pragma unroll
-    for (int i = 0; i < 7; i++) x[i] = q[NBASE + i];
-    d4 a0[2], a1[16], a2[4], o[1];
-    nerf_input<7>(x, a0, lane);
-    mfma_layer_ring<2, 16>(W + nd.offW[0], a0, a1, lane, wl);
-    relu_gate<16>(a1, W + nd.offb[0], lane);
-    mfma_layer_ring<16, 4>(W + nd.offW[1], a1, a2, lane, wl);
-    relu_gate<4>(a2, W + nd.offb[1], lane);
-    mfma_layer<4, 1>(W + nd.offW[2], a2, o, lane);
-    write_out<1>(o[0], W + nd.offb[2], lane, m, M, rec, S, R_SEL, R_DSEL);
+    for (int ct = 0; ct < SELF_CT; ct++) {
+        m[ct] = 2 * (SELF_CT * wave + ct) + ((lane >> 3) & 1);
+        double q[DOF], obs[3];
+        sample_input(c, d, m[ct], M, qin, obsin, q, obs);
+        double x[7];
+#pragma unroll
+        for (int i = 0; i < 7; i++) x[i] = q[NBASE + i];
+        nerf_input<7>(x, a0[ct], lane);
+#pragma unroll
+        for (int u = 0; u < 4; u++) a2[ct][u] = d4{0.0, 0.0, 0.0, 0.0};
+    }
+    const double* __restrict__ W1 = W + nd.offW[0];  // [16 row tiles][8 k-steps][64]
+    const double* __restrict__ W2 = W + nd.offW[1];  // [4 row tiles][64 k-steps][64]
+#ifndef MPCC_SELF_UNROLL
+#define MPCC_SELF_UNROLL 1
+#endif
+#pragma unroll MPCC_SELF_UNROLL
+    for (int t = 0; t < 16; t++) {
+        d4 z[SELF_CT][1];
+#pragma unroll
+        for (int ct = 0; ct < SELF_CT; ct++) z[ct][0] = d4{0.0, 0.0, 0.0, 0.0};
+        // k-steps 6 and 7 of the input layer hold the zero padding of the 21 NeRF rows to 32 (weights and inputs
+        // both zero): skipped, an fma with two zero factors leaves the accumulator as it is
+#pragma unroll
+        for (int s = 0; s < 6; s++) {
+            const double w = W1[((size_t)t * 8 + s) * 64 + lane];
+#pragma unroll
+            for (int ct = 0; ct < SELF_CT; ct++)
+                z[ct][0] = __builtin_amdgcn_mfma_f64_16x16x4f64(w, a0[ct][s >> 2][s & 3], z[ct][0], 0, 0, 0);
+        }
+#pragma unroll
+        for (int ct = 0; ct < SELF_CT; ct++) relu_gate<1>(z[ct], W + nd.offb[0] + 16 * t, lane);
+#pragma unroll
+        for (int r = 0; r < 4; r++)
+#pragma unroll
+            for (int u = 0; u < 4; u++) {
+                const double w = W2[((size_t)u * 64 + 4 * t + r) * 64 + lane];
+#pragma unroll
+                for (int ct = 0; ct < SELF_CT; ct++)
+                    a2[ct][u] = __builtin_amdgcn_mfma_f64_16x16x4f64(w, z[ct][0][r], a2[ct][u], 0, 0, 0);
+            }
+    }
+#pragma unroll
+    for (int ct = 0; ct < SELF_CT; ct++) {
+        relu_gate<4>(a2[ct], W + nd.offb[1], lane);
+        mfma_layer<4, 1>(W + nd.offW[2], a2[ct], o[ct], lane);
+        write_out<1>(o[ct][0], W + nd.offb[2], lane, m[ct], M, rec, S, R_SEL, R_DSEL);
+    }
 }
 
 // env network 30 -> 256 -> 256 -> 256 -> 256 -> 9 (osqp_interface.cpp:40-43).  Panda: 2 samples per wave,
@@ -347,8 +392,9 @@ __global__ void __launch_bounds__(256) k_mlp_env(DevConst c, DevBuffers d, NNDes
 void launch_nn(const DevConst& c, const DevBuffers& d, const NNDesc& nd, const double* W, int which, int M,
                const double* q, const double* obs, double* rec, int rec_stride, hipStream_t s) {
     if (M <= 0) return;
-    if (which == 0)  // 4 waves x 2 samples
-        hipLaunchKernelGGL(k_mlp_self, dim3((M + 7) / 8), dim3(256), 0, s, c, d, nd, W, M, q, obs, rec, rec_stride);
+    if (which == 0)  // 4 waves x SELF_CT tiles x 2 samples
+        hipLaunchKernelGGL(k_mlp_self, dim3((M + 8 * SELF_CT - 1) / (8 * SELF_CT)), dim3(256), 0, s, c, d, nd, W, M, q, obs,
+                           rec, rec_stride);
     else
         hipLaunchKernelGGL(k_mlp_env, dim3((M + 4 * ENV_SPW - 1) / (4 * ENV_SPW)), dim3(256), 0, s, c, d, nd, W, M, q, obs,
                            rec, rec_stride);

@@ -9,6 +9,6 @@ for r in $(seq 1 ${ROUNDS:-3}); do
   for n in "$@"; do
     MPCC_ENGINE_LIB=mpcc_manipulator_amd/_ab/$n/libmpcc_engine.so timeout -k 10 200 python bench.py --no-cpu-baseline $ARGS \
         > "$OUT/${n}_$r.json" 2> "$OUT/${n}_$r.err"
-    python -c "import json,sys; d=json.load(open('$OUT/${n}_$r.json')); r=d['roofline']; print('$n', $r, round(d['value']), round(r['avg_launch_ms'], 4), flush=True)"
+    python -c "import json,sys; d=json.load(open('$OUT/${n}_$r.json')); r=d['roofline']; m = r.get('mlp') or {}; print('$n', $r, round(d['value']), round(r['avg_launch_ms'], 4), {k: round(v['avg_launch_ms'], 3) for k, v in m.items()}, flush=True)"
   done
 done
