@@ -88,6 +88,12 @@ static_assert(QS_POLY + 2 * 15 <= QS_YLB + 16 * QLINES, "bound block of <= 2 pol
 // The wide-poly variants (NPM >= 9, MPCC_WIDE_RING): a 2-slot ring (one stage in flight) of a 14-line
 // bound block (11 poly rows) and the fields up to the unpacked poly slot state; 19 KiB per slot, so 4 waves
 // of 38 KiB fit a CU's 160 KiB.
+#ifndef MPCC_PIN
+#define MPCC_PIN 0  // 1: settle the prefetched stage before the late stores: 3.43 ms against 3.31 (r03ae_ab_pin.log)
+#endif
+#ifndef MPCC_KR_EARLY
+#define MPCC_KR_EARLY 1
+#endif
 #ifndef MPCC_PCN
 #define MPCC_PCN 0  // 1: cached c_p^T (z, dza, dz) in spare lanes for 1 or 2 poly rows: 1% slower (profiles/r03w_ab_pcn.log)
 #endif
@@ -314,10 +320,10 @@ __device__ __forceinline__ void sweep(int N, bool backward, In& b0, In& b1, Load
     }
     for (int i = 0; i <= N; i += 2) {
         load(s(i + 1 <= N ? i + 1 : N), b1);
-        body(s(i), b0);
+        body(s(i), b0, b1);  // the body may settle the prefetched buffer (pin) before its late stores
         if (i + 1 > N) break;
         load(s(i + 2 <= N ? i + 2 : N), b0);
-        body(s(i + 1), b1);
+        body(s(i + 1), b1, b0);
     }
 }
 
@@ -832,7 +838,19 @@ __device__ __forceinline__ void ipm_group(const DevConst& c, const DevBuffers& d
                 else if constexpr (MPCC_WIDE_FACTOR_PF) sweep<false>(N, true, cur, nxt, load, body);
                 else sweep_noprefetch(N, true, cur, load, body);
             };
-            factor_sweep([&](int k, In& o) { load_factor(run ? k : N, o, pending); }, [&](int k, const In& cur) {
+            // pin(nx): the next stage's prefetched fields, settled in registers before the body's late stores.  A
+            // load's first use waits (vmcnt) for every store issued before it as well (gfx9 counts stores in
+            // vmcnt); settled here, a body's stores no longer delay the next body's start.
+            auto pin = [&](In& x) {
+                asm volatile("" : "+v"(x.lb), "+v"(x.ub), "+v"(x.np), "+v"(x.pub), "+v"(x.zx), "+v"(x.zv));
+                asm volatile("" : "+v"(x.sL), "+v"(x.lL), "+v"(x.sU), "+v"(x.lU), "+v"(x.sP), "+v"(x.lP));
+                asm volatile("" : "+v"(x.x0), "+v"(x.x1), "+v"(x.x2), "+v"(x.x3));
+#pragma unroll
+                for (int q = 0; q < 12; q++) asm volatile("" : "+v"(x.m[q]));
+#pragma unroll
+                for (int q = 0; q < NPE; q++) asm volatile("" : "+v"(x.pa[q]), "+v"(x.pb[q]));
+            };
+            factor_sweep([&](int k, In& o) { load_factor(run ? k : N, o, pending); }, [&](int k, const In& cur, auto&... nx) {
                 const double lb = cur.lb, ub = cur.ub;
                 const double* Qr = cur.m;
                 const double qt = cur.m[9], Rt = cur.m[10], rt = cur.m[11];
@@ -1035,6 +1053,26 @@ __device__ __forceinline__ void ipm_group(const DevConst& c, const DevBuffers& d
 #endif
 #pragma unroll
                 for (int i = 0; i < 8; i++) S[L_K + i * 16 + t] = kc[i];
+                if constexpr (MPCC_PIN) (pin(nx), ...);
+                // K row halves to the workspace (LDS transpose), early: a store's completion is waited for by the
+                // next vmcnt wait on a load (gfx9 counts stores in vmcnt), and the next stage's first use of its
+                // prefetched fields comes right at the top of the next body; issued here, the P update below
+                // covers their latency
+                if constexpr (MPCC_KR_EARLY) {
+                lds_sync();
+                {
+                    const int ri = t & 7, hoff = (t < 8) ? 0 : 8;
+                    const double2* row = reinterpret_cast<const double2*>(S + L_K + ri * 16 + hoff);
+#pragma unroll
+                    for (int q2 = 0; q2 < 4; q2++) {
+                        const double2 w = row[q2];
+                        if (run) {
+                            *ws(k, WF_KR + 2 * q2) = w.x;
+                            *ws(k, WF_KR + 2 * q2 + 1) = w.y;
+                        }
+                    }
+                }
+                }
                 {
                     const double kffd = from_down<8>(kff);  // lane 8+i <- kff_i
                     if (run) *ws(k, WF_GVK) = (t < 8) ? g0v : kffd;
@@ -1109,6 +1147,7 @@ __device__ __forceinline__ void ipm_group(const DevConst& c, const DevBuffers& d
 #pragma unroll
                         for (int r = 0; r < 4; r++) Pc[g + 4 * r] = x[g][r];
                 }
+                if constexpr (!MPCC_KR_EARLY) {
                 lds_sync();
                 {
                     const int ri = t & 7, hoff = (t < 8) ? 0 : 8;
@@ -1121,6 +1160,7 @@ __device__ __forceinline__ void ipm_group(const DevConst& c, const DevBuffers& d
                             *ws(k, WF_KR + 2 * q2 + 1) = w.y;
                         }
                     }
+                }
                 }
                 pv = pnew;
                 lds_sync();
