@@ -56,7 +56,8 @@ enum : int {
     WF_KFJ = WF_FI + NU,                          // LRM fields: kff of the low-rank solves Q_j (BFGS)
     WF_QX = WF_KFJ + LRM,                         // LRM fields: Q_j = M u_j, x~ part
     WF_QV = WF_QX + LRM,                          // LRM fields: Q_j, v part
-    NWF = WF_QV + LRM
+    WF_PZ = WF_QV + LRM, WF_PA, WF_PD,            // PCACHE: lane p -> c_p^T z, c_p^T dza, c_p^T dz of poly row p
+    NWF
 };
 static_assert(NWF * GW <= ISW, "IPM workspace must fit the per-stage ISW allocation");
 
@@ -263,6 +264,7 @@ struct StageIn {
     double pa[NPE], pb[NPE];      // poly rows p: a_p[t], bv_p[t] (t < DOF)
     double pub;                   // upper bound of poly row t (t < npmax)
     double sL, lL, sU, lU, sP, lP, zx, zv;
+    double pz, pca, pcd;          // PCACHE: c_p^T z, c_p^T dza, c_p^T dz of poly row t
     double x0, x1, x2, x3;        // sweep-specific pairs (dz, dza, g0)
     double m[2 * NU];             // sweep-specific: Q row (NX) + q, R, r | K column (NU) + kff | K column + F^-1 row
 };
@@ -409,6 +411,10 @@ __device__ __forceinline__ void ipm_group(const DevConst& c, const DevBuffers& d
 #pragma unroll
     for (int j = 0; j < LRM; j++) uz[j] = 0.0;
 
+    // Many poly rows (without the low-rank terms): c_p^T z, c_p^T dza and c_p^T dz are formed once per iteration
+    // where z, dza and dz are made and kept in the workspace (WF_PZ, WF_PA, WF_PD) for the other sweeps, which
+    // recomputed them from the same stored vectors (ipm.hip PCACHE)
+    constexpr bool PCACHE = NPM >= 9 && !LR;
     // ---- stage loaders (unconditional loads, lane/stage conditions as selects)
     auto load_common = [&](int k, In& o) {
         const gdouble* q = qs_stage(k);
@@ -429,6 +435,7 @@ __device__ __forceinline__ void ipm_group(const DevConst& c, const DevBuffers& d
         o.sL = *ws(k, WF_SL); o.lL = *ws(k, WF_LL); o.sU = *ws(k, WF_SU); o.lU = *ws(k, WF_LU);
         o.sP = *ws(k, WF_SP); o.lP = *ws(k, WF_LP);
         o.zx = *ws(k, WF_ZX); o.zv = *ws(k, WF_ZV);
+        if constexpr (PCACHE) { o.pz = *ws(k, WF_PZ); o.pca = *ws(k, WF_PA); o.pcd = *ws(k, WF_PD); }
     };
     auto load_factor = [&](int k, In& o, bool upd) {
         load_common(k, o);
@@ -568,6 +575,7 @@ __device__ __forceinline__ void ipm_group(const DevConst& c, const DevBuffers& d
                 const double yx = rowY ? y : 0.0;
                 const double cz = row_cz(k, yx, 0.0);
                 const double pcz = poly_cz(cur, k, yx, 0.0);
+                if constexpr (PCACHE) *ws(k, WF_PZ) = pcz;
                 const bool aL = row_active(k, cur.lb), aU = row_active(k, cur.ub), aP = poly_slot_active(cur, k);
                 double sL = 1, lL = 0, sU = 1, lU = 0, sP = 1, lP = 0;
                 if (aL) { sL = fmax(-(sgnL * cz - sgnL * cur.lb), s_floor); lL = (lam_scale > 0) ? lam_scale / sL : 1.0; }
@@ -623,7 +631,12 @@ __device__ __forceinline__ void ipm_group(const DevConst& c, const DevBuffers& d
                     if (pending) {
                         const double dx = cur.x0, dv = cur.x1, ax = cur.x2, av = cur.x3;
                         const double cz = row_cz(k, zx, zv), cd = row_cz(k, dx, dv), ca = row_cz(k, ax, av);
-                        const double pcz = poly_cz(cur, k, zx, zv), pcd = poly_cz(cur, k, dx, dv), pca = poly_cz(cur, k, ax, av);
+                        double pcz, pcd, pca;
+                        if constexpr (PCACHE) {
+                            pcz = cur.pz; pcd = cur.pcd; pca = cur.pca;
+                        } else {
+                            pcz = poly_cz(cur, k, zx, zv); pcd = poly_cz(cur, k, dx, dv); pca = poly_cz(cur, k, ax, av);
+                        }
                         double rpd;
                         if (aL) { const SlotStep st = slot_corr(sgnL, lb, cz, ca, cd, sL, lL, sigma_mu, &rpd); sL += alpha * st.ds; lL += alpha * st.dl; }
                         if (aU) { const SlotStep st = slot_corr(sgnU, ub, cz, ca, cd, sU, lU, sigma_mu, &rpd); sU += alpha * st.ds; lU += alpha * st.dl; }
@@ -637,6 +650,7 @@ __device__ __forceinline__ void ipm_group(const DevConst& c, const DevBuffers& d
                     // ---- slots: barrier weights and predictor coefficients (rc = s l)
                     const double cz = row_cz(k, zx, zv);
                     const double pcz = poly_cz(cur, k, zx, zv);
+                    if constexpr (PCACHE) *ws(k, WF_PZ) = pcz;
                     double WL = 0, WU = 0, WP = 0, cL = 0, cU = 0, cP = 0;
                     if (aL) { const double rp = slot_rp(sgnL, cz, lb, sL); const double ri = rcp(sL); WL = lL * ri; cL = slot_coef(ri, lL, rp, sL * lL); }
                     if (aU) { const double rp = slot_rp(sgnU, cz, ub, sU); const double ri = rcp(sU); WU = lU * ri; cU = slot_coef(ri, lU, rp, sU * lU); }
@@ -897,7 +911,8 @@ __device__ __forceinline__ void ipm_group(const DevConst& c, const DevBuffers& d
                     *ws(k, WF_AX) = xs;
                     *ws(k, WF_AV) = dvv;
                     const double cz = row_cz(k, cur.zx, cur.zv), ca = row_cz(k, xs, dvv);
-                    const double pcz = poly_cz(cur, k, cur.zx, cur.zv), pca = poly_cz(cur, k, xs, dvv);
+                    const double pcz = PCACHE ? cur.pz : poly_cz(cur, k, cur.zx, cur.zv), pca = poly_cz(cur, k, xs, dvv);
+                    if constexpr (PCACHE) *ws(k, WF_PA) = pca;
                     auto rec = [&](bool a, double sgn, double bnd, double czz, double caa, double s, double l) {
                         if (!a) return;
                         const double rp = slot_rp(sgn, czz, bnd, s);
@@ -1002,7 +1017,8 @@ __device__ __forceinline__ void ipm_group(const DevConst& c, const DevBuffers& d
                 light_sweep(true, [&](int k, In& o) { load_bwd(k, o); }, [&](int k, const In& cur) {
                     const bool aL = row_active(k, cur.lb), aU = row_active(k, cur.ub), aP = poly_slot_active(cur, k);
                     const double cz = row_cz(k, cur.zx, cur.zv), ca = row_cz(k, cur.x0, cur.x1);
-                    const double pcz = poly_cz(cur, k, cur.zx, cur.zv), pca = poly_cz(cur, k, cur.x0, cur.x1);
+                    const double pcz = PCACHE ? cur.pz : poly_cz(cur, k, cur.zx, cur.zv);
+                    const double pca = PCACHE ? cur.pca : poly_cz(cur, k, cur.x0, cur.x1);
                     auto coef = [&](bool a, double sgn, double bnd, double czz, double caa, double s, double l) -> double {
                         if (!a) return 0.0;
                         const double rp = slot_rp(sgn, czz, bnd, s);
@@ -1052,8 +1068,9 @@ __device__ __forceinline__ void ipm_group(const DevConst& c, const DevBuffers& d
                     *ws(k, WF_DV) = dvv;
                     dzm = fmax(dzm, fmax(fabs(xtt), fabs(dvv)));
                     const double cz = row_cz(k, cur.zx, cur.zv), cd = row_cz(k, xtt, dvv), ca = row_cz(k, ax, av);
-                    const double pcz = poly_cz(cur, k, cur.zx, cur.zv), pcd = poly_cz(cur, k, xtt, dvv);
-                    const double pca = poly_cz(cur, k, ax, av);
+                    const double pcz = PCACHE ? cur.pz : poly_cz(cur, k, cur.zx, cur.zv), pcd = poly_cz(cur, k, xtt, dvv);
+                    const double pca = PCACHE ? cur.pca : poly_cz(cur, k, ax, av);
+                    if constexpr (PCACHE) *ws(k, WF_PD) = pcd;
                     auto rec = [&](bool a, double sgn, double bnd, double czz, double caa, double cdd, double s, double l) {
                         if (!a) return;
                         double rp;
