@@ -110,7 +110,7 @@ static_assert(LF_CBWD + 1 <= NWF, "the odd last line of a ring slot reads one fi
 size_t ipm_lds_bytes(int /*N*/, int npmax) {
     const size_t uk = (size_t)IPW * GRP_LDS * sizeof(double);
     const size_t ring = (npmax <= 2)          ? (size_t)LRING * LG(LF_CBWD) * 1024
-                        : use_ring(npmax)       ? (size_t)LRING_W * LG(WF_PD + 1, QLINES_W) * 1024
+                        : use_ring(npmax)       ? (size_t)LRING_W * LG(WF_PD, QLINES_W) * 1024  // longest wide run: 26 fields
                                                 : 0;
     return ring > uk ? ring : uk;
 }
@@ -378,6 +378,19 @@ __device__ __forceinline__ void sweep_ring(int N, bool backward, In (&b)[D], Loa
 // idle through it.  Writes the step (d.step), QP status and IPM iteration count (d.sqi).
 template <int NPM>
 __device__ __forceinline__ void ipm_group(const DevConst& c, const DevBuffers& d, double* smem) {
+    // Workspace field indices of this variant.  The wide-poly variants (NPM >= 9) order their fields so that each
+    // light sweep's LDS-ring image is the shortest run from field 0: the poly slot state and c_p^T z right after
+    // the iterate, then K and kff (predictor forward), the predictor step and c_p^T dza (corrector forward), the
+    // gradient and F^-1 (corrector backward); c_p^T dz and the corrector step are read by the factorization only.
+    // The narrow variants keep the enum order (their poly slot state is packed into WF_ZV).
+    constexpr bool WLAY = NPM >= 9;
+    constexpr int F_SL = WF_SL, F_LL = WF_LL, F_SU = WF_SU, F_LU = WF_LU, F_ZX = WF_ZX, F_ZV = WF_ZV;
+    constexpr int F_SP = WLAY ? 6 : WF_SP, F_LP = WLAY ? 7 : WF_LP, F_PZ = WLAY ? 8 : WF_PZ;
+    constexpr int F_KR = WLAY ? 9 : WF_KR, F_GVK = F_KR + 8, F_AX = F_GVK + 1, F_AV = F_AX + 1;
+    constexpr int F_PA = WLAY ? F_AV + 1 : WF_PA, F_GX = WLAY ? F_PA + 1 : WF_GX, F_FI = F_GX + 1;
+    constexpr int F_PD = WLAY ? F_FI + 4 : WF_PD, F_DX = WF_DX, F_DV = WF_DV;
+    static_assert(WLAY || (F_GVK == WF_GVK && F_AX == WF_AX && F_AV == WF_AV && F_FI == WF_FI), "narrow layout = enum");
+    static_assert(!WLAY || (F_PD == WF_PD && F_PD + 1 == F_DX), "wide layout: a permutation of the enum's fields");
     constexpr int NPE = NPM > 0 ? NPM : 1;
     using In = StageIn<NPE>;
     const int lane = threadIdx.x;
@@ -475,12 +488,12 @@ __device__ __forceinline__ void ipm_group(const DevConst& c, const DevBuffers& d
     // 6 workspace lines of slot and iterate state per stage instead of 8.
     constexpr bool PACKP = NPM <= 4;
     // Wide-poly variants: c_p^T z, c_p^T dza and c_p^T dz (11 reductions over the row's 16 lanes each) are formed
-    // once per iteration where z, dza, dz are made, kept in the workspace (WF_PZ, WF_PA, WF_PD) and read by the
+    // once per iteration where z, dza, dz are made, kept in the workspace (F_PZ, F_PA, F_PD) and read by the
     // other sweeps, which recomputed them from the same stored vectors (the same values: 3 evaluations per stage
     // and iteration instead of 11)
     constexpr bool PCACHE = NPM >= 9;
-    // The same for 1 or 2 poly rows at no extra traffic: c_p^T z rides in the free lanes 10 + p of the packed WF_ZV,
-    // c_p^T dza and c_p^T dz in lanes 8 + p of WF_AV and WF_DV (whose v occupies lanes 0..7; readers mask them)
+    // The same for 1 or 2 poly rows at no extra traffic: c_p^T z rides in the free lanes 10 + p of the packed F_ZV,
+    // c_p^T dza and c_p^T dz in lanes 8 + p of F_AV and F_DV (whose v occupies lanes 0..7; readers mask them)
     constexpr bool PCN = MPCC_PCN && NPM >= 1 && NPM <= 2;
     constexpr bool PCV = PCACHE || PCN;
     auto zv_pack = [&](double zv, double sP, double lP, double pz) -> double {
@@ -496,10 +509,10 @@ __device__ __forceinline__ void ipm_group(const DevConst& c, const DevBuffers& d
     };
     auto store_slots = [&](int k, double sL, double lL, double sU, double lU, double sP, double lP, double zx,
                            double zv, double pz) {
-        *ws(k, WF_SL) = sL; *ws(k, WF_LL) = lL; *ws(k, WF_SU) = sU; *ws(k, WF_LU) = lU;
-        if constexpr (!PACKP) { *ws(k, WF_SP) = sP; *ws(k, WF_LP) = lP; }
-        *ws(k, WF_ZX) = zx;
-        *ws(k, WF_ZV) = zv_pack(zv, sP, lP, pz);
+        *ws(k, F_SL) = sL; *ws(k, F_LL) = lL; *ws(k, F_SU) = sU; *ws(k, F_LU) = lU;
+        if constexpr (!PACKP) { *ws(k, F_SP) = sP; *ws(k, F_LP) = lP; }
+        *ws(k, F_ZX) = zx;
+        *ws(k, F_ZV) = zv_pack(zv, sP, lP, pz);
     };
 
     // ---- stage loaders: every load unconditional (addresses clamped inside the stage record), the
@@ -518,17 +531,17 @@ __device__ __forceinline__ void ipm_group(const DevConst& c, const DevBuffers& d
         }
         const double pu = q[QS_POLY + 15 * (t < NPE ? t : 0) + 14];
         o.pub = (t < NPM) ? pu : INF;
-        o.sL = *ws(k, WF_SL); o.lL = *ws(k, WF_LL); o.sU = *ws(k, WF_SU); o.lU = *ws(k, WF_LU);
-        o.zx = *ws(k, WF_ZX);
-        if constexpr (PCACHE) { o.pz = *ws(k, WF_PZ); o.pca = *ws(k, WF_PA); o.pcd = *ws(k, WF_PD); }
-        const double zraw = *ws(k, WF_ZV);
+        o.sL = *ws(k, F_SL); o.lL = *ws(k, F_LL); o.sU = *ws(k, F_SU); o.lU = *ws(k, F_LU);
+        o.zx = *ws(k, F_ZX);
+        if constexpr (PCACHE) { o.pz = *ws(k, F_PZ); o.pca = *ws(k, F_PA); o.pcd = *ws(k, F_PD); }
+        const double zraw = *ws(k, F_ZV);
         if constexpr (PACKP) {
             o.sP = from_up<8>(zraw);   // lane p <- lane 8 + p
             o.lP = from_up<12>(zraw);  // lane p <- lane 12 + p
             if constexpr (PCN) o.pz = from_up<10>(zraw);  // lane p <- lane 10 + p
             o.zv = (t < 8) ? zraw : 0.0;
         } else {
-            o.sP = *ws(k, WF_SP); o.lP = *ws(k, WF_LP);
+            o.sP = *ws(k, F_SP); o.lP = *ws(k, F_LP);
             o.zv = zraw;
         }
     };
@@ -544,7 +557,7 @@ __device__ __forceinline__ void ipm_group(const DevConst& c, const DevBuffers& d
         o.m[9] = (t < 9) ? qv : 0.0;
         o.m[10] = (t < 8 && k < N) ? rv : 0.0;
         o.m[11] = (t < 8 && k < N) ? rr : 0.0;
-        const double x0 = *ws(k, WF_DX), x1 = *ws(k, WF_DV), x2 = *ws(k, WF_AX), x3 = *ws(k, WF_AV);
+        const double x0 = *ws(k, F_DX), x1 = *ws(k, F_DV), x2 = *ws(k, F_AX), x3 = *ws(k, F_AV);
         const bool vl = !PCN || t < 8;  // PCN: lanes 8.. of DV / AV carry c_p^T dz / c_p^T dza
         o.x0 = upd ? x0 : 0.0; o.x1 = (upd && vl) ? x1 : 0.0; o.x2 = upd ? x2 : 0.0; o.x3 = (upd && vl) ? x3 : 0.0;
         if constexpr (PCN) { o.pcd = from_up<8>(x1); o.pca = from_up<8>(x3); }  // lane p <- lane 8 + p
@@ -552,11 +565,11 @@ __device__ __forceinline__ void ipm_group(const DevConst& c, const DevBuffers& d
     auto load_fwd = [&](int k, In& o, bool corr) {
         load_common(k, o);
 #pragma unroll
-        for (int m = 0; m < 8; m++) o.m[m] = *ws(k, WF_KR + m);  // zero at k = N (factor sweep)
-        o.m[8] = from_up<8>(*ws(k, WF_GVK));  // lane i <- kff_i (lanes 8..15: 0)
+        for (int m = 0; m < 8; m++) o.m[m] = *ws(k, F_KR + m);  // zero at k = N (factor sweep)
+        o.m[8] = from_up<8>(*ws(k, F_GVK));  // lane i <- kff_i (lanes 8..15: 0)
         if (corr) {  // corr: constant
-            o.x0 = *ws(k, WF_AX);
-            const double av = *ws(k, WF_AV);
+            o.x0 = *ws(k, F_AX);
+            const double av = *ws(k, F_AV);
             o.x1 = (!PCN || t < 8) ? av : 0.0;
             if constexpr (PCN) o.pca = from_up<8>(av);
         } else {
@@ -565,20 +578,20 @@ __device__ __forceinline__ void ipm_group(const DevConst& c, const DevBuffers& d
     };
     auto load_bwd = [&](int k, In& o) {
         load_common(k, o);
-        o.x0 = *ws(k, WF_AX); o.x2 = *ws(k, WF_GX);
-        const double av = *ws(k, WF_AV);
+        o.x0 = *ws(k, F_AX); o.x2 = *ws(k, F_GX);
+        const double av = *ws(k, F_AV);
         o.x1 = (!PCN || t < 8) ? av : 0.0;
         if constexpr (PCN) o.pca = from_up<8>(av);
-        const double gvk = *ws(k, WF_GVK);
+        const double gvk = *ws(k, F_GVK);
         o.x3 = (t < 8) ? gvk : 0.0;
 #pragma unroll
-        for (int m = 0; m < 8; m++) o.m[m] = *ws(k, WF_KR + m);  // zero at k = N (factor sweep)
+        for (int m = 0; m < 8; m++) o.m[m] = *ws(k, F_KR + m);  // zero at k = N (factor sweep)
 #pragma unroll
-        for (int m = 0; m < 4; m++) o.m[8 + m] = *ws(k, WF_FI + m);
+        for (int m = 0; m < 4; m++) o.m[8 + m] = *ws(k, F_FI + m);
     };
 
     // ---- the light sweeps of NPM <= 2 (and of NPM >= 9 with MPCC_WIDE_RING: 2 slots, 14 record lines from
-    //      QS_YLB - 16, fields 0..WF_LP) read their stages from an LDS ring filled by global_load_lds:
+    //      QS_YLB - 16, fields 0..F_LP) read their stages from an LDS ring filled by global_load_lds:
     //      LRING - 1 = 2 stages in flight at no register cost (a register ring that deep spilled, and
     //      every scratch reload waited for all loads in flight).  Slot image of one instance: line j at
     //      (j >> 1) * 128 + (j & 1) * 16 doubles from the instance's base (grp * 32), lines 0..3 = the QP
@@ -602,7 +615,12 @@ __device__ __forceinline__ void ipm_group(const DevConst& c, const DevBuffers& d
         o_pb[p] = qoff(QS_POLY + 15 * p + 7 + (t < 7 ? t : 0));
     }
     // fields in a slot image: the sweep's run; the wide ring also needs the unpacked poly slot state
-    auto ring_nf = [](auto nfc) { return (NPM <= 2) ? decltype(nfc)::value : WF_PD + 1; };
+    // fields in a slot image: the sweep's run (the wide layout's runs: through kff, through c_p^T dza, through F^-1)
+    auto ring_nf = [](auto nfc) {
+        constexpr int nf = decltype(nfc)::value;
+        if constexpr (NPM <= 2) return nf;
+        else return nf == LF_PRED ? F_GVK + 1 : (nf == LF_CFWD ? F_PA + 1 : F_FI + 4);
+    };
     auto glds_stage = [&](int k, int slot, auto nfc) {
         constexpr int G = LG(ring_nf(nfc), QL);
         // the image's last record line and workspace line stay inside the stage (static), the stage inside the
@@ -633,17 +651,17 @@ __device__ __forceinline__ void ipm_group(const DevConst& c, const DevBuffers& d
         const double pu = im[o_pub];
         o.pub = (t < NPM) ? pu : INF;
         auto f = [&](int field) { return im[img_at(QL + field) + t]; };
-        o.sL = f(WF_SL); o.lL = f(WF_LL); o.sU = f(WF_SU); o.lU = f(WF_LU);
-        o.zx = f(WF_ZX);
-        if constexpr (PCACHE) { o.pz = f(WF_PZ); o.pca = f(WF_PA); o.pcd = f(WF_PD); }
-        const double zraw = f(WF_ZV);
+        o.sL = f(F_SL); o.lL = f(F_LL); o.sU = f(F_SU); o.lU = f(F_LU);
+        o.zx = f(F_ZX);
+        if constexpr (PCACHE) { o.pz = f(F_PZ); o.pca = f(F_PA); o.pcd = f(F_PD); }
+        const double zraw = f(F_ZV);
         if constexpr (PACKP) {
             o.sP = from_up<8>(zraw);   // lane p <- lane 8 + p
             o.lP = from_up<12>(zraw);  // lane p <- lane 12 + p
             if constexpr (PCN) o.pz = from_up<10>(zraw);
             o.zv = (t < 8) ? zraw : 0.0;
         } else {
-            o.sP = f(WF_SP); o.lP = f(WF_LP);
+            o.sP = f(F_SP); o.lP = f(F_LP);
             o.zv = zraw;
         }
     };
@@ -651,11 +669,11 @@ __device__ __forceinline__ void ipm_group(const DevConst& c, const DevBuffers& d
     auto lds_fwd = [&](const double* im, In& o, bool corr) {
         lds_common(im, o);
 #pragma unroll
-        for (int m = 0; m < 8; m++) o.m[m] = fld(im, WF_KR + m);
-        o.m[8] = from_up<8>(fld(im, WF_GVK));
+        for (int m = 0; m < 8; m++) o.m[m] = fld(im, F_KR + m);
+        o.m[8] = from_up<8>(fld(im, F_GVK));
         if (corr) {
-            o.x0 = fld(im, WF_AX);
-            const double av = fld(im, WF_AV);
+            o.x0 = fld(im, F_AX);
+            const double av = fld(im, F_AV);
             o.x1 = (!PCN || t < 8) ? av : 0.0;
             if constexpr (PCN) o.pca = from_up<8>(av);
         } else {
@@ -664,16 +682,16 @@ __device__ __forceinline__ void ipm_group(const DevConst& c, const DevBuffers& d
     };
     auto lds_bwd = [&](const double* im, In& o) {
         lds_common(im, o);
-        o.x0 = fld(im, WF_AX); o.x2 = fld(im, WF_GX);
-        const double av = fld(im, WF_AV);
+        o.x0 = fld(im, F_AX); o.x2 = fld(im, F_GX);
+        const double av = fld(im, F_AV);
         o.x1 = (!PCN || t < 8) ? av : 0.0;
         if constexpr (PCN) o.pca = from_up<8>(av);
-        const double gvk = fld(im, WF_GVK);
+        const double gvk = fld(im, F_GVK);
         o.x3 = (t < 8) ? gvk : 0.0;
 #pragma unroll
-        for (int m = 0; m < 8; m++) o.m[m] = fld(im, WF_KR + m);
+        for (int m = 0; m < 8; m++) o.m[m] = fld(im, F_KR + m);
 #pragma unroll
-        for (int m = 0; m < 4; m++) o.m[8 + m] = fld(im, WF_FI + m);
+        for (int m = 0; m < 4; m++) o.m[8 + m] = fld(im, F_FI + m);
     };
     // stage sweep over the ring: stage s(i + 2) is issued while s(i) is read and processed; every issue
     // is unconditional (the stages past the end re-read s(N)), so the wait count is fixed: after issuing
@@ -797,7 +815,7 @@ __device__ __forceinline__ void ipm_group(const DevConst& c, const DevBuffers& d
             const double yx = rowY ? y : 0.0;
             const double cz = row_cz(k, yx, 0.0);
             const double pcz = poly_cz(cur, k, yx, 0.0);
-            if constexpr (PCACHE) *ws(k, WF_PZ) = pcz;
+            if constexpr (PCACHE) *ws(k, F_PZ) = pcz;
             const bool aL = row_active(k, cur.lb), aU = row_active(k, cur.ub), aP = poly_slot_active(cur, k);
             double sL = 1, lL = 0, sU = 1, lU = 0, sP = 1, lP = 0;
             if (aL) { sL = fmax(-(sgnL * cz - sgnL * cur.lb), s_floor); lL = (lam_scale > 0) ? lam_scale / sL : 1.0; }
@@ -882,7 +900,7 @@ __device__ __forceinline__ void ipm_group(const DevConst& c, const DevBuffers& d
                 const double cz = row_cz(k, zx, zv);
                 const double pcz = poly_cz(cur, k, zx, zv);
                 if constexpr (PCACHE) {
-                    if (run) *ws(k, WF_PZ) = pcz;
+                    if (run) *ws(k, F_PZ) = pcz;
                 }
                 if constexpr (PCN) {  // the updated iterate with its c_p^T z (unchanged iterate: stored as it is)
                     if (run && pending) store_slots(k, sL, lL, sU, lU, sP, lP, zx, zv, pcz);
@@ -915,7 +933,7 @@ __device__ __forceinline__ void ipm_group(const DevConst& c, const DevBuffers& d
                         g0v = s + rt;
                     }
                 }
-                if (run) *ws(k, WF_GX) = g0x;
+                if (run) *ws(k, F_GX) = g0x;
                 double gx, gv;
                 assemble_grad(cur, k, g0x, g0v, dvr, cP, gx, gv);
                 PMARK(9);
@@ -934,10 +952,10 @@ __device__ __forceinline__ void ipm_group(const DevConst& c, const DevBuffers& d
                     // no gains at the terminal stage: zeros, so the light sweeps' loads need no stage select
                     if (run) {
 #pragma unroll
-                        for (int m = 0; m < 8; m++) *ws(k, WF_KR + m) = 0.0;
-                        *ws(k, WF_GVK) = (t < 8) ? g0v : 0.0;
+                        for (int m = 0; m < 8; m++) *ws(k, F_KR + m) = 0.0;
+                        *ws(k, F_GVK) = (t < 8) ? g0v : 0.0;
 #pragma unroll
-                        for (int m = 0; m < 4; m++) *ws(k, WF_FI + m) = 0.0;
+                        for (int m = 0; m < 4; m++) *ws(k, F_FI + m) = 0.0;
                     }
                     return;
                 }
@@ -1067,19 +1085,19 @@ __device__ __forceinline__ void ipm_group(const DevConst& c, const DevBuffers& d
                     for (int q2 = 0; q2 < 4; q2++) {
                         const double2 w = row[q2];
                         if (run) {
-                            *ws(k, WF_KR + 2 * q2) = w.x;
-                            *ws(k, WF_KR + 2 * q2 + 1) = w.y;
+                            *ws(k, F_KR + 2 * q2) = w.x;
+                            *ws(k, F_KR + 2 * q2 + 1) = w.y;
                         }
                     }
                 }
                 }
                 {
                     const double kffd = from_down<8>(kff);  // lane 8+i <- kff_i
-                    if (run) *ws(k, WF_GVK) = (t < 8) ? g0v : kffd;
+                    if (run) *ws(k, F_GVK) = (t < 8) ? g0v : kffd;
                 }
                 if (run) {
 #pragma unroll
-                    for (int m = 0; m < 4; m++) *ws(k, WF_FI + m) = (t < 8) ? fi[m] : fi[4 + m];
+                    for (int m = 0; m < 4; m++) *ws(k, F_FI + m) = (t < 8) ? fi[m] : fi[4 + m];
                 }
                 // ---- (4) Hb column t and P = Hb - U^T U (column t)
                 double hb[16];
@@ -1156,8 +1174,8 @@ __device__ __forceinline__ void ipm_group(const DevConst& c, const DevBuffers& d
                     for (int q2 = 0; q2 < 4; q2++) {
                         const double2 w = row[q2];
                         if (run) {
-                            *ws(k, WF_KR + 2 * q2) = w.x;
-                            *ws(k, WF_KR + 2 * q2 + 1) = w.y;
+                            *ws(k, F_KR + 2 * q2) = w.x;
+                            *ws(k, F_KR + 2 * q2 + 1) = w.y;
                         }
                     }
                 }
@@ -1186,15 +1204,15 @@ __device__ __forceinline__ void ipm_group(const DevConst& c, const DevBuffers& d
                 double v = 0.0, xn = 0.0;
                 if (k < N) fwd_step(cur, xt, v, xn);
                 const double dvv = (t < 8 && k < N) ? v : 0.0;
-                *ws(k, WF_AX) = xt;
+                *ws(k, F_AX) = xt;
                 const double cz = row_cz(k, cur.zx, cur.zv), ca = row_cz(k, xt, dvv);
                 const double pcz = PCV ? cur.pz : poly_cz(cur, k, cur.zx, cur.zv), pca = poly_cz(cur, k, xt, dvv);
-                if constexpr (PCACHE) *ws(k, WF_PA) = pca;
+                if constexpr (PCACHE) *ws(k, F_PA) = pca;
                 if constexpr (PCN) {
                     const double pa8 = from_down<8>(pca);  // lane 8 + p <- c_p^T dza
-                    *ws(k, WF_AV) = (t < 8) ? dvv : pa8;
+                    *ws(k, F_AV) = (t < 8) ? dvv : pa8;
                 } else {
-                    *ws(k, WF_AV) = dvv;
+                    *ws(k, F_AV) = dvv;
                 }
                 auto rec = [&](bool a, double sgn, double bnd, double czz, double caa, double s, double l) {
                     if (!a) return;
@@ -1258,7 +1276,7 @@ __device__ __forceinline__ void ipm_group(const DevConst& c, const DevBuffers& d
                 for (int m = 0; m < 4; m++) part -= cur.m[8 + m] * ((t < 8) ? fb[m] : fb[4 + m]);
                 const double kff = part + from_up<8>(part);
                 const double kffd = from_down<8>(kff);  // lane 8+i <- kff_i
-                if (t >= 8) *ws(k, WF_GVK) = kffd;
+                if (t >= 8) *ws(k, F_GVK) = kffd;
                 double atp = 0.0;
                 const double p7 = from_down<1>(pv);
                 if (t < 9) {
@@ -1297,17 +1315,17 @@ __device__ __forceinline__ void ipm_group(const DevConst& c, const DevBuffers& d
                 double v = 0.0, xn = 0.0;
                 if (k < N) fwd_step(cur, xt, v, xn);
                 const double dvv = (t < 8 && k < N) ? v : 0.0;
-                *ws(k, WF_DX) = xt;
+                *ws(k, F_DX) = xt;
                 dzm = fmax(dzm, fmax(fabs(xt), fabs(dvv)));
                 const double cz = row_cz(k, cur.zx, cur.zv), cd = row_cz(k, xt, dvv), ca = row_cz(k, cur.x0, cur.x1);
                 const double pcz = PCV ? cur.pz : poly_cz(cur, k, cur.zx, cur.zv), pcd = poly_cz(cur, k, xt, dvv);
                 const double pca = PCV ? cur.pca : poly_cz(cur, k, cur.x0, cur.x1);
-                if constexpr (PCACHE) *ws(k, WF_PD) = pcd;
+                if constexpr (PCACHE) *ws(k, F_PD) = pcd;
                 if constexpr (PCN) {
                     const double pd8 = from_down<8>(pcd);  // lane 8 + p <- c_p^T dz
-                    *ws(k, WF_DV) = (t < 8) ? dvv : pd8;
+                    *ws(k, F_DV) = (t < 8) ? dvv : pd8;
                 } else {
-                    *ws(k, WF_DV) = dvv;
+                    *ws(k, F_DV) = dvv;
                 }
                 auto rec = [&](bool a, double sgn, double bnd, double czz, double caa, double cdd, double s, double l) {
                     if (!a) return;
@@ -1375,8 +1393,8 @@ __device__ __forceinline__ void ipm_group(const DevConst& c, const DevBuffers& d
     if (t == 0) si[SQ_QPSTAT] = 0;
     gdouble* stp = (gdouble*)(d.step + (size_t)b * NS * 17);
     for (int k = 0; k <= N; k++) {
-        const double zx = *ws(k, WF_ZX) + alpha * *ws(k, WF_DX);
-        const double zv = *ws(k, WF_ZV) + alpha * *ws(k, WF_DV);  // lanes < 8
+        const double zx = *ws(k, F_ZX) + alpha * *ws(k, F_DX);
+        const double zv = *ws(k, F_ZV) + alpha * *ws(k, F_DV);  // lanes < 8
         if (t < 9) stp[k * 17 + t] = zx;
         if (t < 8) stp[k * 17 + 9 + t] = (k < N) ? zv : 0.0;
     }
