@@ -817,10 +817,10 @@ int mpcc_set_warmstart_device(mpcc_engine* e, int B, const double* d_guess, cons
         hipStream_t st = stream ? (hipStream_t)stream : e->stream;
         if (st != e->stream) e->ext_async = true;
         const size_t NS = e->N + 1;
-        if (d_guess)
-            HIPCHK(hipMemcpyAsync(e->d.guess, d_guess, (size_t)B * NS * NXU * sizeof(double), hipMemcpyDeviceToDevice, st));
-        if (d_valid) HIPCHK(hipMemcpyAsync(e->d.valid, d_valid, (size_t)B * sizeof(int32_t), hipMemcpyDeviceToDevice, st));
-        if (d_fails) HIPCHK(hipMemcpyAsync(e->d.fails, d_fails, (size_t)B * sizeof(int32_t), hipMemcpyDeviceToDevice, st));
+        // one launch for the three arrays (three blits were three launches and their gaps on the step's chain)
+        launch_warmstart_copy(d_guess ? (long)B * NS * NXU : 0, d_guess, e->d.guess, B, d_valid, e->d.valid, d_fails,
+                              e->d.fails, st);
+        HIPCHK(hipGetLastError());
     } catch (const HipError& x) {
         return fail(MPCC_E_HIP, x.what());
     }

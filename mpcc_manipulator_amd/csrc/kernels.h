@@ -97,6 +97,9 @@ void launch_accept(const DevConst& c, const DevBuffers& d, hipStream_t s);
 void launch_apply(const DevConst& c, const DevBuffers& d, hipStream_t s);
 void launch_finalize(const DevConst& c, const DevBuffers& d, hipStream_t s);
 void launch_sim_step(int B, const double* x, const double* u, double ts, double* xn, hipStream_t s);
+// device-to-device warm start (guess, valid, fails) in one launch; null sources are skipped
+void launch_warmstart_copy(long ng, const double* g, double* gd, int B, const int32_t* v, int32_t* vd, const int32_t* f,
+                           int32_t* fd, hipStream_t s);
 void launch_loop_pre(int B, const double* x, double* xtraj, const int* kstep, hipStream_t s);
 void launch_loop_post(int B, double ts, double* x, double* u, const double* xtraj, const double* u0out,
                       const int32_t* status, const int32_t* ok, int32_t* alive, double* utraj, int32_t* straj,

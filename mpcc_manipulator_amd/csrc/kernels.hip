@@ -11,6 +11,8 @@
 //     k_trial      thread / (instance,stage) filter line-search trial at alpha = 1 (objective, violation)
 //     k_accept     thread / instance         filter, step, termination
 //   k_finalize     thread / horizon element  Status -> warm start / outputs (osqp_interface.cpp:575-589, mpc.cpp:140-189)
+#include <algorithm>
+
 #include "dev_sqp.h"
 
 namespace mpcc {
@@ -131,21 +133,44 @@ __device__ inline void robot_record(const DevConst& c, const double* q, double o
 // RPT threads per (instance, stage) record: thread 0 the FK, Jacobian and manipulability, thread 1 + i the
 // central difference of joint i (robot_model.cpp:436-447), so a record costs the latency of two FK evaluations
 // instead of 1 + 2 DOF.  Same arithmetic per term as robot_record.
-constexpr int RPT = (DOF + 1 <= 8) ? 8 : 16;
+// The Panda (2 DOF + 1 <= 16): 16 lanes, lane 1 + i evaluates mu(q + delta e_i), lane 1 + DOF + i
+// mu(q - delta e_i), and lane 1 + i forms the difference with its partner's value (one manipulability evaluation
+// of latency per lane).  The mobile build (10 DOF): lane 1 + i evaluates both of joint i.
+constexpr bool FD_SPLIT = 2 * DOF + 1 <= 16;
+constexpr int RPT = FD_SPLIT ? 16 : ((DOF + 1 <= 8) ? 8 : 16);
 static_assert(DOF + 1 <= RPT, "one thread per gradient term");
 __global__ void __launch_bounds__(64) k_records(DevConst c, DevBuffers d) {
     const long g_t = (long)blockIdx.x * blockDim.x + threadIdx.x;
     const int S = c.S;
-    const int t = (int)(g_t / RPT), u = (int)(g_t % RPT);
-    if (t >= S || u > DOF) return;
+    const int t0 = (int)(g_t / RPT), u = (int)(g_t % RPT);
+    const bool live = t0 < S;
+    const int t = live ? t0 : S - 1;  // every lane of a record group evaluates (the split form exchanges values)
     const int N = c.N;
     const int b = t / (N + 1), k = t - b * (N + 1);
     const double* g = d.guess + ((size_t)b * (N + 1) + k) * NXU;
     double q[DOF];
 #pragma unroll
     for (int j = 0; j < DOF; j++) q[j] = g[j];
-    if (u == 0) robot_record(c, q, d.obs[4 * b + 3], d.rec + t, (size_t)S, false);
-    else d.rec[(size_t)(R_DMU + u - 1) * S + t] = manip_fd(q, u - 1);
+    if constexpr (FD_SPLIT) {
+        const double delta = 1e-4;  // robot_model.cpp:439 (manip_fd)
+        double mu = 0.0;
+        if (u >= 1 && u <= 2 * DOF) {
+            const bool plus = u <= DOF;
+            const int i = plus ? u - 1 : u - 1 - DOF;
+            double qq[DOF];
+#pragma unroll
+            for (int j = 0; j < DOF; j++) qq[j] = plus ? q[j] + (j == i ? delta : 0.0) : q[j] - (j == i ? delta : 0.0);
+            mu = manipulability(qq);
+        }
+        const double mm = __shfl_down(mu, DOF, 16);  // lane 1 + i <- mu(q - delta e_i)
+        if (!live) return;
+        if (u == 0) robot_record(c, q, d.obs[4 * b + 3], d.rec + t, (size_t)S, false);
+        else if (u <= DOF) d.rec[(size_t)(R_DMU + u - 1) * S + t] = (mu - mm) / (2 * delta);
+    } else {
+        if (!live || u > DOF) return;
+        if (u == 0) robot_record(c, q, d.obs[4 * b + 3], d.rec + t, (size_t)S, false);
+        else d.rec[(size_t)(R_DMU + u - 1) * S + t] = manip_fd(q, u - 1);
+    }
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -379,6 +404,26 @@ void launch_debug_records(const DevConst& c, int M, const double* q, const doubl
 }
 void launch_finalize(const DevConst& c, const DevBuffers& d, hipStream_t s) {
     hipLaunchKernelGGL(k_finalize, dim3(nblk((long)c.Bn * (c.N + 1) * NXU, 256)), dim3(256), 0, s, c, d);
+}
+__global__ void __launch_bounds__(256) k_warmstart_copy(long ng, const double* __restrict__ g, double* __restrict__ gd, int B,
+                                                         const int32_t* __restrict__ v, int32_t* __restrict__ vd,
+                                                         const int32_t* __restrict__ f, int32_t* __restrict__ fd) {
+    const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (g)
+        for (long e = i; e < ng; e += (long)gridDim.x * blockDim.x) gd[e] = g[e];
+    if (i < B) {
+        if (v) vd[i] = v[i];
+        if (f) fd[i] = f[i];
+    }
+}
+void launch_warmstart_copy(long ng, const double* g, double* gd, int B, const int32_t* v, int32_t* vd, const int32_t* f,
+                           int32_t* fd, hipStream_t s) {
+    const long n = ng > B ? ng : B;
+    if (n <= 0) return;
+    // grid-stride over the guess; valid / fails one element per thread, so at least ceil(B / 256) blocks
+    const long cap = std::max(4096L, ((long)B + 255) / 256);
+    const long blocks = std::min((n + 255) / 256, cap);
+    hipLaunchKernelGGL(k_warmstart_copy, dim3((int)blocks), dim3(256), 0, s, ng, g, gd, B, v, vd, f, fd);
 }
 void launch_sim_step(int B, const double* x, const double* u, double ts, double* xn, hipStream_t s) {
     hipLaunchKernelGGL(k_sim_step, dim3(nblk(B, 64)), dim3(64), 0, s, B, x, u, ts, xn);
