@@ -246,7 +246,7 @@ __global__ void __launch_bounds__(64) k_apply(DevConst c, DevBuffers d) {
 // result.  x_0 itself (k = 0, a < NX) is never rewritten, so the threads that read it do not race.  One launch per solve: thread (instance b, element r of the opt_sol / zero_guess horizon).  The element
 // threads of stage 0's inputs also write u0 (the value they store); thread r = 0 writes the status and the MPC
 // bookkeeping (mpc.cpp:143-189).
-__global__ void __launch_bounds__(256) k_finalize(DevConst c, DevBuffers d) {
+__global__ void __launch_bounds__(64) k_finalize(DevConst c, DevBuffers d) {
     const long e = (long)blockIdx.x * blockDim.x + threadIdx.x;
     const int W = (c.N + 1) * NXU;
     if (e >= (long)c.Bn * W) return;
@@ -403,9 +403,12 @@ void launch_debug_records(const DevConst& c, int M, const double* q, const doubl
     hipLaunchKernelGGL(k_debug_records, dim3(nblk(M, 64)), dim3(64), 0, s, c, M, q, obs, rec);
 }
 void launch_finalize(const DevConst& c, const DevBuffers& d, hipStream_t s) {
-    hipLaunchKernelGGL(k_finalize, dim3(nblk((long)c.Bn * (c.N + 1) * NXU, 256)), dim3(256), 0, s, c, d);
+    // one-wave workgroups: a multi-wave workgroup waits for room on every SIMD of a CU, which the concurrent
+    // controller groups' k_sqp waves (a whole SIMD's registers each) do not leave until they finish: 256-thread
+    // blocks of this kernel ran 0.5-1.3 ms behind another group's interior point (profiles/r03aj trace)
+    hipLaunchKernelGGL(k_finalize, dim3(nblk((long)c.Bn * (c.N + 1) * NXU, 64)), dim3(64), 0, s, c, d);
 }
-__global__ void __launch_bounds__(256) k_warmstart_copy(long ng, const double* __restrict__ g, double* __restrict__ gd, int B,
+__global__ void __launch_bounds__(64) k_warmstart_copy(long ng, const double* __restrict__ g, double* __restrict__ gd, int B,
                                                          const int32_t* __restrict__ v, int32_t* __restrict__ vd,
                                                          const int32_t* __restrict__ f, int32_t* __restrict__ fd) {
     const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
@@ -420,10 +423,10 @@ void launch_warmstart_copy(long ng, const double* g, double* gd, int B, const in
                            int32_t* fd, hipStream_t s) {
     const long n = ng > B ? ng : B;
     if (n <= 0) return;
-    // grid-stride over the guess; valid / fails one element per thread, so at least ceil(B / 256) blocks
-    const long cap = std::max(4096L, ((long)B + 255) / 256);
-    const long blocks = std::min((n + 255) / 256, cap);
-    hipLaunchKernelGGL(k_warmstart_copy, dim3((int)blocks), dim3(256), 0, s, ng, g, gd, B, v, vd, f, fd);
+    // grid-stride over the guess; valid / fails one element per thread, so at least ceil(B / 64) one-wave blocks
+    const long cap = std::max(16384L, ((long)B + 63) / 64);
+    const long blocks = std::min((n + 63) / 64, cap);
+    hipLaunchKernelGGL(k_warmstart_copy, dim3((int)blocks), dim3(64), 0, s, ng, g, gd, B, v, vd, f, fd);
 }
 void launch_sim_step(int B, const double* x, const double* u, double ts, double* xn, hipStream_t s) {
     hipLaunchKernelGGL(k_sim_step, dim3(nblk(B, 64)), dim3(64), 0, s, B, x, u, ts, xn);
