@@ -88,6 +88,9 @@ static_assert(QS_POLY + 2 * 15 <= QS_YLB + 16 * QLINES, "bound block of <= 2 pol
 // The wide-poly variants (NPM >= 9, MPCC_WIDE_RING): a 2-slot ring (one stage in flight) of a 14-line
 // bound block (11 poly rows) and the fields up to the unpacked poly slot state; 19 KiB per slot, so 4 waves
 // of 38 KiB fit a CU's 160 KiB.
+#ifndef MPCC_GRAM_MFMA
+#define MPCC_GRAM_MFMA 1
+#endif
 #ifndef MPCC_PIN
 #define MPCC_PIN 0  // 1: settle the prefetched stage before the late stores: 3.43 ms against 3.31 (r03ae_ab_pin.log)
 #endif
@@ -496,6 +499,7 @@ __device__ __forceinline__ void ipm_group(const DevConst& c, const DevBuffers& d
     // c_p^T dza and c_p^T dz in lanes 8 + p of F_AV and F_DV (whose v occupies lanes 0..7; readers mask them)
     constexpr bool PCN = MPCC_PCN && NPM >= 1 && NPM <= 2;
     constexpr bool PCV = PCACHE || PCN;
+    constexpr bool GRAM_MFMA = MPCC_GRAM_MFMA && NPM >= 9;  // poly Gram terms of the factorization on MFMA
     auto zv_pack = [&](double zv, double sP, double lP, double pz) -> double {
         if constexpr (PCN) {
             const double s8 = from_down<8>(sP), l12 = from_down<12>(lP), z10 = from_down<10>(pz);  // whole row active
@@ -971,14 +975,82 @@ __device__ __forceinline__ void ipm_group(const DevConst& c, const DevBuffers& d
                 // soon as it is made (DPP results are pinned in program order, so broadcasting every
                 // bv_p[i] first kept 8 NPM values live; at NPM = 11 that spilled).  Per accumulator the
                 // operations and their order are those of the oracle's sum over p.
-                double Wb[NPE];
                 const double wdv = from_up<9>(wd);  // lane j <- ddq row j weight
                 double hF[8], hG[8];
+                double hq[7];
 #pragma unroll
                 for (int i = 0; i < 8; i++) {
                     hF[i] = (i == t) ? Rt + ((t < 7) ? wdv : 0.0) : 0.0;
                     hG[i] = 0.0;
                 }
+                auto hq_base = [&]() {
+#pragma unroll
+                    for (int a = 0; a < 7; a++) {
+                        hq[a] = Qr[a];
+                        if (a == t) hq[a] += wd;
+                    }
+                };
+                if constexpr (GRAM_MFMA) {
+                    // Wide-poly variants: the three rank-NPM blocks as one Gram matrix on the matrix cores.  With
+                    // r_p = [bv_p (lanes 0..6), 0, a_p (lanes 8..14), 0] and w_p the barrier weight of live poly row
+                    // p, D = sum_p w_p r_p r_p^T holds sum_p W_p bv_p bv_p^T (rows, columns 0..6), W_p bv_p a_p^T
+                    // (rows 0..6, columns 8..14) and W_p a_p a_p^T (rows, columns 8..14): per instance
+                    // ceil(NPM / 4) v_mfma_f64_16x16x4f64 over k = p, operands and products moved between the
+                    // instance layout and the MFMA layout by the 16-lane-group transposes of (4).  Replaced ~100
+                    // broadcasts and multiply-adds per poly row and stage.
+                    constexpr int KS = (NPM + 3) / 4;
+                    double xs[KS][4][1], as[KS][4][1];
+#pragma unroll
+                    for (int q = 0; q < KS; q++)
+#pragma unroll
+                        for (int g = 0; g < 4; g++) {
+                            const int pp = 4 * q + g;
+                            double x = 0.0, w = 0.0;
+                            if (pp < NPM) {
+                                const double a8 = from_down<8>(cur.pa[pp]);  // lane 8 + i <- a_p[i]
+                                x = (t < 8) ? cur.pb[pp] : a8;
+                                const bool live = (double)pp < cur.np && k < N;
+                                const double wp = bcn(WP, pp);
+                                w = live ? wp : 0.0;
+                            }
+                            xs[q][g][0] = x;
+                            as[q][g][0] = w * x;
+                        }
+#pragma unroll
+                    for (int q = 0; q < KS; q++) {
+                        group_transpose(xs[q]);
+                        group_transpose(as[q]);
+                    }
+                    double dg[4][4];
+#pragma unroll
+                    for (int j = 0; j < 4; j++) {
+                        d4 acc = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+                        for (int q = 0; q < KS; q++) acc = __builtin_amdgcn_mfma_f64_16x16x4f64(as[q][j][0], xs[q][j][0], acc, 0, 0, 0);
+#pragma unroll
+                        for (int r = 0; r < 4; r++) dg[j][r] = acc[r];
+                    }
+                    group_transpose(dg);  // lane (j, t): column t of D_j, row g + 4 r in dg[g][r]
+                    const bool q7 = t < 7;
+#pragma unroll
+                    for (int i = 0; i < 7; i++) {
+                        const double dF = dg[i & 3][i >> 2];                       // D[i][t]
+                        const double dG = from_up<8>(dg[i & 3][i >> 2]);           // D[i][8 + t]
+                        hF[i] += q7 ? dF : 0.0;
+                        hG[i] += q7 ? dG : 0.0;
+                    }
+                    hq_base();
+#pragma unroll
+                    for (int a = 0; a < 7; a++) {
+                        const double dq = from_up<8>(dg[(8 + a) & 3][(8 + a) >> 2]);  // D[8 + a][8 + t]
+                        hq[a] += q7 ? dq : 0.0;
+                    }
+                } else {
+                // The rank-NPM poly terms accumulate row p by row p: each broadcast bv_p[i] is consumed as
+                // soon as it is made (DPP results are pinned in program order, so broadcasting every
+                // bv_p[i] first kept 8 NPM values live; at NPM = 11 that spilled).  Per accumulator the
+                // operations and their order are those of the oracle's sum over p.
+                double Wb[NPE];
 #pragma unroll
                 for (int p = 0; p < NPM; p++) {
                     const bool live = (double)p < cur.np && k < N;
@@ -991,26 +1063,26 @@ __device__ __forceinline__ void ipm_group(const DevConst& c, const DevBuffers& d
                         hG[i] += Wb[p] * (bv * cur.pa[p]);  // a_p[t]: zero for lanes >= 7
                     }
                 }
-                // Hb's poly terms (q block, rows a < 7), row p by row p as for F above.  The wide-poly variants form
-                // them here, so that a_p (NPM values per lane) dies before the Cholesky instead of living through
-                // it into the Hb section (it spilled there); <= 2 rows keep the late placement, where the 7 sums
-                // would be the longer live range.  Same terms in the same order either way.
-                double hq[7];
+                }
+                // Hb's poly terms (q block, rows a < 7), row p by row p as for F above.  The wide-poly variants
+                // without the Gram MFMA form them here, so that a_p (NPM values per lane) dies before the Cholesky
+                // instead of living through it into the Hb section (it spilled there); <= 2 rows keep the late
+                // placement, where the 7 sums would be the longer live range.  Same terms in the same order.
                 auto poly_hq = [&]() {
+                    hq_base();
 #pragma unroll
-                    for (int a = 0; a < 7; a++) {
-                        hq[a] = Qr[a];
-                        if (a == t) hq[a] += wd;
-                    }
-#pragma unroll
-                    for (int p = 0; p < NPM; p++)
+                    for (int p = 0; p < NPM; p++) {
+                        const bool live = (double)p < cur.np && k < N;
+                        const double wp = bcn(WP, p);
+                        const double wb = live ? wp : 0.0;
 #pragma unroll
                         for (int a = 0; a < 7; a++) {
                             const double pa_ = bcn(cur.pa[p], a);
-                            hq[a] += Wb[p] * (pa_ * cur.pa[p]);
+                            hq[a] += wb * (pa_ * cur.pa[p]);
                         }
+                    }
                 };
-                if constexpr (NPM > 2) poly_hq();
+                if constexpr (!GRAM_MFMA && NPM > 2) poly_hq();
                 double Fc[8], gm[8];
 #pragma unroll
                 for (int i = 0; i < 8; i++) {
