@@ -302,6 +302,13 @@ __global__ void __launch_bounds__(256) k_mlp_self(DevConst c, DevBuffers d, NNDe
     }
     const double* __restrict__ W1 = W + nd.offW[0];  // [16 row tiles][8 k-steps][64]
     const double* __restrict__ W2 = W + nd.offW[1];  // [4 row tiles][64 k-steps][64]
+    // the biases in LDS: the epilogues read 64 of them per lane in a lane-dependent order, which as global loads
+    // the allocator could only issue one at a time (one register pair free, a full wait each)
+    __shared__ double sb[256 + 64 + 16];
+    for (int i = threadIdx.x; i < 256; i += 256) sb[i] = W[nd.offb[0] + i];
+    if (threadIdx.x < 64) sb[256 + threadIdx.x] = W[nd.offb[1] + threadIdx.x];
+    if (threadIdx.x < 1) sb[320] = W[nd.offb[2]];
+    __syncthreads();
 #ifndef MPCC_SELF_UNROLL
 #define MPCC_SELF_UNROLL 1
 #endif
@@ -320,7 +327,7 @@ __global__ void __launch_bounds__(256) k_mlp_self(DevConst c, DevBuffers d, NNDe
                 z[ct][0] = __builtin_amdgcn_mfma_f64_16x16x4f64(w, a0[ct][s >> 2][s & 3], z[ct][0], 0, 0, 0);
         }
 #pragma unroll
-        for (int ct = 0; ct < SELF_CT; ct++) relu_gate<1>(z[ct], W + nd.offb[0] + 16 * t, lane);
+        for (int ct = 0; ct < SELF_CT; ct++) relu_gate<1>(z[ct], sb + 16 * t, lane);
 #pragma unroll
         for (int r = 0; r < 4; r++)
 #pragma unroll
@@ -333,9 +340,9 @@ __global__ void __launch_bounds__(256) k_mlp_self(DevConst c, DevBuffers d, NNDe
     }
 #pragma unroll
     for (int ct = 0; ct < SELF_CT; ct++) {
-        relu_gate<4>(a2[ct], W + nd.offb[1], lane);
+        relu_gate<4>(a2[ct], sb + 256, lane);
         mfma_layer<4, 1>(W + nd.offW[2], a2[ct], o[ct], lane);
-        write_out<1>(o[ct][0], W + nd.offb[2], lane, m[ct], M, rec, S, R_SEL, R_DSEL);
+        write_out<1>(o[ct][0], sb + 320, lane, m[ct], M, rec, S, R_SEL, R_DSEL);
     }
 }
 
@@ -345,7 +352,7 @@ __global__ void __launch_bounds__(256) k_mlp_self(DevConst c, DevBuffers d, NNDe
 template <int CPS>
 __device__ __forceinline__ void mlp_env_body(const DevConst& c, const DevBuffers& d, const NNDesc& nd, const double* __restrict__ W,
                                              int M, const double* __restrict__ qin, const double* __restrict__ obsin,
-                                             double* __restrict__ rec, int S, double* wl) {
+                                             double* __restrict__ rec, int S, double* wl, double* bl) {
     const int lane = threadIdx.x & 63;
     const int wave = blockIdx.x * 4 + (threadIdx.x >> 6);
     const int m = (CPS == 8) ? 2 * wave + ((lane >> 3) & 1) : wave;
@@ -362,19 +369,22 @@ __device__ __forceinline__ void mlp_env_body(const DevConst& c, const DevBuffers
     } else {
         x[7] = obs[0]; x[8] = obs[1]; x[9] = obs[2];
     }
+    // the biases in LDS (see k_mlp_self); the first ring barrier publishes them
+    for (int l = 0; l < 4; l++) bl[l * 256 + threadIdx.x] = W[nd.offb[l] + threadIdx.x];
+    if (threadIdx.x < 9) bl[1024 + threadIdx.x] = W[nd.offb[4] + threadIdx.x];
     d4 a0[2], a[16], h[16], o[1];
     nerf_input<10, CPS>(x, a0, lane);
     mfma_layer_ring<2, 16>(W + nd.offW[0], a0, a, lane, wl);
-    relu_gate<16, CPS>(a, W + nd.offb[0], lane);
+    relu_gate<16, CPS>(a, bl, lane);
     for (int l = 1; l <= 3; l++) {  // three 256 x 256 hidden layers share one unrolled body
         mfma_layer_ring<16, 16>(W + nd.offW[l], a, h, lane, wl);
-        relu_gate<16, CPS>(h, W + nd.offb[l], lane);
+        relu_gate<16, CPS>(h, bl + 256 * l, lane);
 #pragma unroll
         for (int t = 0; t < 16; t++) a[t] = h[t];
     }
     mfma_layer<16, 1>(W + nd.offW[4], a, o, lane);
-    if constexpr (CPS == 8) write_out<9>(o[0], W + nd.offb[4], lane, m, M, rec, S, R_ENV, R_DENV);
-    else write_out_mobile<9>(o[0], W + nd.offb[4], lane, m, M, rec, S, dO);
+    if constexpr (CPS == 8) write_out<9>(o[0], bl + 1024, lane, m, M, rec, S, R_ENV, R_DENV);
+    else write_out_mobile<9>(o[0], bl + 1024, lane, m, M, rec, S, dO);
 }
 
 constexpr int ENV_CPS = (NBASE > 0) ? 16 : 8;  // columns per sample of k_mlp_env
@@ -386,7 +396,8 @@ __global__ void __launch_bounds__(256) k_mlp_env(DevConst c, DevBuffers d, NNDes
     // no early exit: the hidden layers synchronize the block (a wave past M computes on a clamped
     // sample and write_out drops its result)
     __shared__ __attribute__((aligned(16))) double wl[RING_SLOTS * 16 * 256];
-    mlp_env_body<ENV_CPS>(c, d, nd, W, M, qin, obsin, rec, S, wl);
+    __shared__ double bl[4 * 256 + 16];
+    mlp_env_body<ENV_CPS>(c, d, nd, W, M, qin, obsin, rec, S, wl, bl);
 }
 
 void launch_nn(const DevConst& c, const DevBuffers& d, const NNDesc& nd, const double* W, int which, int M,
