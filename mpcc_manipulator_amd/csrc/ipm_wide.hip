@@ -37,6 +37,7 @@ constexpr double IPM_S0 = 0.02, IPM_L0 = 0.002;
 constexpr int IPM_MAX_IT_SCALED = 30;
 constexpr double IPM_TAU = 0.995;
 typedef __attribute__((address_space(1))) double gdouble;
+typedef double d4 __attribute__((ext_vector_type(4)));
 
 constexpr int GW = 32;               // lanes per instance
 constexpr int IPW = 64 / GW;         // instances per wavefront
@@ -65,7 +66,19 @@ static_assert(NWF * GW <= ISW, "IPM workspace must fit the per-stage ISW allocat
 constexpr int L_F = 0, L_U = 16 * 16, L_C = L_U + NU * GW;
 constexpr int GRP_LDS = L_C + 32 + 16;  // + 16 doubles: the two instances of a wave start 16 banks apart
 
-size_t ipm_wide_lds_bytes() { return (size_t)IPW * GRP_LDS * sizeof(double); }
+// Many-poly-row variants (NPM >= 9): the factorization's rank-NPM poly blocks sum_p W_p bv_p bv_p^T,
+// sum_p W_p bv_p a_p^T and sum_p W_p a_p a_p^T of both instances on v_mfma_f64_16x16x4f64 (ipm.hip's Gram form;
+// here bv_p and a_p have DOF = 10 entries each, so the three blocks are separate 16x16 products).  Per wavefront
+// after the per-instance blocks: the operands [inst][24 rows: bv_p (p < 12, zero past NPM), a_p][16 lanes] and
+// the weights [inst][16], then, in the same place, the 6 products [3 inst + {bb, ba, aa}][16][16].
+#ifndef MPCC_WIDE_GRAM
+#define MPCC_WIDE_GRAM 1
+#endif
+constexpr int G_ROWS = 24, G_OPW = IPW * G_ROWS * 16, GRAM_LDS = 6 * 256;
+static_assert(G_OPW + IPW * 16 <= GRAM_LDS, "Gram operands inside the product area");
+__host__ __device__ constexpr bool wide_gram(int npm) { return MPCC_WIDE_GRAM && npm >= 9; }
+
+size_t ipm_wide_lds_bytes(int npm) { return (size_t)(IPW * GRP_LDS + (wide_gram(npm) ? GRAM_LDS : 0)) * sizeof(double); }
 
 namespace {
 
@@ -415,6 +428,10 @@ __device__ __forceinline__ void ipm_group(const DevConst& c, const DevBuffers& d
     // where z, dza and dz are made and kept in the workspace (WF_PZ, WF_PA, WF_PD) for the other sweeps, which
     // recomputed them from the same stored vectors (ipm.hip PCACHE)
     constexpr bool PCACHE = NPM >= 9 && !LR;
+    // Gram variants: the factorization sweep runs on the whole wave (the matrix cores need every lane); lanes of an
+    // instance that is done re-read stage N and store nothing
+    constexpr bool GRAM = wide_gram(NPM);
+    double* const GM = smem + IPW * GRP_LDS;
     // ---- stage loaders (unconditional loads, lane/stage conditions as selects)
     auto load_common = [&](int k, In& o) {
         const gdouble* q = qs_stage(k);
@@ -606,7 +623,7 @@ __device__ __forceinline__ void ipm_group(const DevConst& c, const DevBuffers& d
         if (run) alpha = 0.0;
         while (true) {
             if (__ballot(run) == 0) break;
-            if (run) {
+            if (run || GRAM) {
                 // ================= factorization sweep k = N..0 (lazy update, g0, predictor backward solve)
                 double Pc[NXA];  // column t of P_{k+1}
                 double pv = 0.0; // p_{k+1}, component t
@@ -621,7 +638,50 @@ __device__ __forceinline__ void ipm_group(const DevConst& c, const DevBuffers& d
                     if constexpr (NPM > 2) sweep_noprefetch(N, true, cur, load, body);
                     else sweep(N, true, cur, nxt, load, body);
                 };
-                factor_sweep([&](int k, In& o) { load_factor(k, o, pending); }, [&](int k, const In& cur) {
+                // global stores of the sweep: only a running instance's (the Gram variants run it on the whole wave)
+                auto wst = [&](int k, int f, double v) {
+                    if (!GRAM || run) *ws(k, f) = v;
+                };
+                // the Gram products of this stage (GRAM): operands through the wave's LDS area into the MFMA layouts
+                // (A lane l -> A[l & 15][l >> 4], B lane l -> B[l >> 4][l & 15], k = poly row 4 q + (l >> 4)), the
+                // products back into it (C lane l, reg r -> C[(l >> 4) + 4 r][l & 15]), read there by column
+                auto gram = [&](const In& in, double wp) {
+                    if constexpr (GRAM) {
+                        double* const O = GM + grp * (G_ROWS * 16);
+                        if (t < 16) {
+#pragma unroll
+                            for (int p = 0; p < 12; p++) {
+                                O[p * 16 + t] = (p < NPM) ? in.pb[p] : 0.0;          // bv_p[t] (zero for t >= DOF)
+                                O[(12 + p) * 16 + t] = (p < NPM) ? in.pa[p] : 0.0;   // a_p[t]
+                            }
+                            if (t < 12) GM[G_OPW + grp * 16 + t] = (t < NPM) ? wp : 0.0;  // W_p (zero unless live)
+                        }
+                        lds_sync();
+                        const int g = lane >> 4, cc = lane & 15;
+                        d4 acc[6];
+#pragma unroll
+                        for (int m = 0; m < 6; m++) acc[m] = d4{0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+                        for (int q = 0; q < (NPM + 3) / 4; q++)
+#pragma unroll
+                            for (int j = 0; j < IPW; j++) {
+                                const double* Oj = GM + j * (G_ROWS * 16);
+                                const double bv = Oj[(4 * q + g) * 16 + cc], a = Oj[(12 + 4 * q + g) * 16 + cc];
+                                const double w = GM[G_OPW + j * 16 + 4 * q + g];
+                                const double wb = w * bv, wa = w * a;
+                                acc[3 * j] = __builtin_amdgcn_mfma_f64_16x16x4f64(wb, bv, acc[3 * j], 0, 0, 0);
+                                acc[3 * j + 1] = __builtin_amdgcn_mfma_f64_16x16x4f64(wb, a, acc[3 * j + 1], 0, 0, 0);
+                                acc[3 * j + 2] = __builtin_amdgcn_mfma_f64_16x16x4f64(wa, a, acc[3 * j + 2], 0, 0, 0);
+                            }
+                        // the products overwrite the operands: LDS executes a wave's operations in program order
+#pragma unroll
+                        for (int m = 0; m < 6; m++)
+#pragma unroll
+                            for (int r = 0; r < 4; r++) GM[m * 256 + (g + 4 * r) * 16 + cc] = acc[m][r];
+                        lds_sync();
+                    }
+                };
+                factor_sweep([&](int k, In& o) { load_factor((GRAM && !run) ? N : k, o, pending); }, [&](int k, const In& cur) {
                     const double lb = cur.lb, ub = cur.ub;
                     const double* Qr = cur.m;
                     const double qt = cur.m[NX], Rt = cur.m[NX + 1], rt = cur.m[NX + 2];
@@ -643,14 +703,14 @@ __device__ __forceinline__ void ipm_group(const DevConst& c, const DevBuffers& d
                         if (aP) { const SlotStep st = slot_corr(sgnU, cur.pub, pcz, pca, pcd, sP, lP, sigma_mu, &rpd); sP += alpha * st.ds; lP += alpha * st.dl; }
                         zx += alpha * dx;
                         zv += alpha * dv;
-                        *ws(k, WF_SL) = sL; *ws(k, WF_LL) = lL; *ws(k, WF_SU) = sU; *ws(k, WF_LU) = lU;
-                        *ws(k, WF_SP) = sP; *ws(k, WF_LP) = lP;
-                        *ws(k, WF_ZX) = zx; *ws(k, WF_ZV) = zv;
+                        wst(k, WF_SL, sL); wst(k, WF_LL, lL); wst(k, WF_SU, sU); wst(k, WF_LU, lU);
+                        wst(k, WF_SP, sP); wst(k, WF_LP, lP);
+                        wst(k, WF_ZX, zx); wst(k, WF_ZV, zv);
                     }
                     // ---- slots: barrier weights and predictor coefficients (rc = s l)
                     const double cz = row_cz(k, zx, zv);
                     const double pcz = poly_cz(cur, k, zx, zv);
-                    if constexpr (PCACHE) *ws(k, WF_PZ) = pcz;
+                    if constexpr (PCACHE) wst(k, WF_PZ, pcz);
                     double WL = 0, WU = 0, WP = 0, cL = 0, cU = 0, cP = 0;
                     if (aL) { const double rp = slot_rp(sgnL, cz, lb, sL); const double ri = rcp(sL); WL = lL * ri; cL = slot_coef(ri, lL, rp, sL * lL); }
                     if (aU) { const double rp = slot_rp(sgnU, cz, ub, sU); const double ri = rcp(sU); WU = lU * ri; cU = slot_coef(ri, lU, rp, sU * lU); }
@@ -684,8 +744,8 @@ __device__ __forceinline__ void ipm_group(const DevConst& c, const DevBuffers& d
                             g0x += f * u_y(j, k);
                             g0v += f * u_v(j, k);
                         }
-                    *ws(k, WF_GX) = g0x;
-                    *ws(k, WF_GV) = g0v;
+                    wst(k, WF_GX, g0x);
+                    wst(k, WF_GV, g0v);
                     double gx, gvv;
                     assemble_grad(cur, k, g0x, g0v, dvr, cP, gx, gvv);
                     if (k == N) {
@@ -716,15 +776,25 @@ __device__ __forceinline__ void ipm_group(const DevConst& c, const DevBuffers& d
                     // ---- (2) F column t (t < NU), Gm column t (t < NX); poly terms W_p bv_p bv_p^T, W_p bv_p a_p^T
                     //          (accumulated over p ascending per entry, as ipm.hip)
                     const double wdv = up_nx(wd, t);  // lane j <- ddq row j weight
-                    const Halves hw = halves(WP);
+                    const Halves hw = GRAM ? Halves{0.0, 0.0} : halves(WP);  // the VALU poly terms' broadcasts
                     double Fc[NU], gm[NU];
 #pragma unroll
                     for (int i = 0; i < NU; i++) {
                         Fc[i] = (i == t) ? Rt + ((t < DOF) ? wdv : 0.0) : 0.0;
                         gm[i] = 0.0;
                     }
+                    gram(cur, WP);
+                    const double* const Dg = GM + (3 * grp) * 256 + (t & 15);  // column t of this instance's products
+                    if constexpr (GRAM) {
 #pragma unroll
-                    for (int p = 0; p < NPM; p++) {
+                        for (int i = 0; i < DOF; i++) {
+                            const double dbb = Dg[i * 16], dba = Dg[256 + i * 16];
+                            Fc[i] += (t < DOF) ? dbb : 0.0;
+                            gm[i] += (t < DOF) ? dba : 0.0;
+                        }
+                    }
+#pragma unroll
+                    for (int p = 0; p < (GRAM ? 0 : NPM); p++) {
                         const bool live = (double)p < cur.np && k < N;
                         const double wp = bch(hw, p);
                         const double Wp = live ? wp : 0.0;
@@ -762,7 +832,8 @@ __device__ __forceinline__ void ipm_group(const DevConst& c, const DevBuffers& d
                             if (2 * q2 + 1 <= i) LF[i * (i + 1) / 2 + 2 * q2 + 1] = w.y;
                         }
                     }
-                    chol_ok = cholN(LF, dinv) && chol_ok;
+                    const bool cok = cholN(LF, dinv);
+                    chol_ok = (cok || (GRAM && !run)) && chol_ok;
                     double u[NU];
                     const double gw = (k >= 1) ? Hct - wd : 0.0;
 #pragma unroll
@@ -802,10 +873,10 @@ __device__ __forceinline__ void ipm_group(const DevConst& c, const DevBuffers& d
 #pragma unroll
                     for (int i = 0; i < NU; i++) {
                         S[MPCC_BCHK(c.bchk, L_U + i * GW + t, L_C, BC_LDS)] = u[i];
-                        *ws(k, WF_KC + i) = kc[i];
-                        *ws(k, WF_FI + i) = fi[i];
+                        wst(k, WF_KC + i, kc[i]);
+                        wst(k, WF_FI + i, fi[i]);
                     }
-                    *ws(k, WF_KFF) = (t < NU) ? kff : 0.0;
+                    wst(k, WF_KFF, (t < NU) ? kff : 0.0);
                     if (lrw)  // backward recursion of the low-rank solves, gradient u_j (y and v parts)
 #pragma unroll
                         for (int j = 0; j < LRM; j++) {
@@ -821,7 +892,7 @@ __device__ __forceinline__ void ipm_group(const DevConst& c, const DevBuffers& d
                                 kffj -= fi[m] * fbm;
                                 ktfj += kc[m] * fbm;
                             }
-                            *ws(k, WF_KFJ + j) = (t < NU) ? kffj : 0.0;
+                            wst(k, WF_KFJ + j, (t < NU) ? kffj : 0.0);
                             double atpj = 0.0;
                             const double pq7 = down32<1>(pj[j], hq, t);
                             if (rowY) {
@@ -850,8 +921,15 @@ __device__ __forceinline__ void ipm_group(const DevConst& c, const DevBuffers& d
                             }
                             hbv[a] = v;
                         }
+                        if constexpr (GRAM) {
 #pragma unroll
-                        for (int p = 0; p < NPM; p++) {
+                            for (int a = 0; a < DOF; a++) {
+                                const double daa = Dg[512 + a * 16];
+                                hbv[a] += (t < DOF) ? daa : 0.0;
+                            }
+                        }
+#pragma unroll
+                        for (int p = 0; p < (GRAM ? 0 : NPM); p++) {
                             const bool live = (double)p < cur.np && k < N;
                             const double wpb = bch(hw, p);  // DPP outside the select
                             const double Wp = live ? wpb : zero;
@@ -895,7 +973,7 @@ __device__ __forceinline__ void ipm_group(const DevConst& c, const DevBuffers& d
                     pv = pnew;
                     lds_sync();
                 });
-                if (!chol_ok) {
+                if (run && !chol_ok) {
                     conv = it > 0 && mu_cur < IPM_TOL_FB && rp_cur < IPM_TOL_FB;  // P2
                     alpha = 0.0;
                     run = false;
@@ -1185,7 +1263,7 @@ __global__ void __launch_bounds__(64) k_ipm(DevConst c, DevBuffers d) {
 }
 template <int NPM, bool LR>
 static void launch_ipm_t(const DevConst& c, const DevBuffers& d, hipStream_t s) {
-    hipLaunchKernelGGL((k_ipm<NPM, LR>), dim3((c.Bn + IPW - 1) / IPW), dim3(64), ipm_wide_lds_bytes(), s, c, d);
+    hipLaunchKernelGGL((k_ipm<NPM, LR>), dim3((c.Bn + IPW - 1) / IPW), dim3(64), ipm_wide_lds_bytes(NPM), s, c, d);
 }
 // one QP solve per active instance on the 32-lane interior point (lr: with the instances' low-rank terms)
 void launch_ipm_wide(const DevConst& c, const DevBuffers& d, int npmax, int lr, hipStream_t s) {
@@ -1435,7 +1513,7 @@ __global__ void __launch_bounds__(64) k_sqp(DevConst, DevBuffers, const double* 
 
 template <int NPM, bool LR>
 static void launch_sqp_t(const DevConst& c, const DevBuffers& d, const double* u_cur, hipStream_t s) {
-    hipLaunchKernelGGL((k_sqp<NPM, LR>), dim3((c.Bn + IPW - 1) / IPW), dim3(64), ipm_wide_lds_bytes(), s, c, d, u_cur);
+    hipLaunchKernelGGL((k_sqp<NPM, LR>), dim3((c.Bn + IPW - 1) / IPW), dim3(64), ipm_wide_lds_bytes(NPM), s, c, d, u_cur);
 }
 
 void launch_sqp_wide(const DevConst& c, const DevBuffers& d, const double* u_cur, int npmax, int bfgs, hipStream_t s) {
@@ -1458,7 +1536,7 @@ void launch_sqp_wide(const DevConst& c, const DevBuffers& d, const double* u_cur
 
 #if MPCC_DOF != 7
 // the mobile build's QP solver (the Panda build's is ipm.hip)
-size_t ipm_lds_bytes(int /*N*/, int /*npmax*/) { return ipm_wide_lds_bytes(); }
+size_t ipm_lds_bytes(int /*N*/, int npmax) { return ipm_wide_lds_bytes(npmax > 2 ? 11 : npmax); }
 void launch_ipm(const DevConst& c, const DevBuffers& d, int npmax, hipStream_t s) { launch_ipm_wide(c, d, npmax, 0, s); }
 void launch_sqp(const DevConst& c, const DevBuffers& d, const double* u_cur, int npmax, hipStream_t s) {
     launch_sqp_wide(c, d, u_cur, npmax, c.p.use_BFGS, s);

@@ -86,7 +86,7 @@ void launch_soc(const DevConst& c, const DevBuffers& d, const double* u_cur, hip
 void launch_sqp(const DevConst& c, const DevBuffers& d, const double* u_cur, int npmax, hipStream_t s);
 // the fused SQP loop on the 32-lane interior point (ipm_wide.hip); bfgs = 1: damped BFGS Hessian updates
 void launch_sqp_wide(const DevConst& c, const DevBuffers& d, const double* u_cur, int npmax, int bfgs, hipStream_t s);
-size_t ipm_wide_lds_bytes();
+size_t ipm_wide_lds_bytes(int npmax);
 void launch_ipm_wide(const DevConst& c, const DevBuffers& d, int npmax, int lr, hipStream_t s);
 size_t ipm_lds_bytes(int N, int npmax);
 inline int poly_rows_max(int mask) {
