@@ -20,8 +20,14 @@ namespace mpcc {
 // ------------------------------------------------------------------------------------------------
 // k_prepare
 // ------------------------------------------------------------------------------------------------
-// MPC::runMPC_ before solveOCP (mpc.cpp:104-124, 54-89): projection, vs estimate, guess shift
-__device__ inline void prepare_mpc(const DevConst& c, const DevBuffers& d, int b) {
+// MPC::runMPC_ before solveOCP (mpc.cpp:104-124, 54-89): projection, vs estimate, guess shift.  PL lanes per
+// instance: every lane of the group evaluates the projection and the vs estimate (the same values), then the group
+// writes the new guess element-parallel.  One lane per instance spent most of the kernel on dependent memory round
+// trips: the stage-by-stage shift (a load, wait and store per stage) and the unwrap re-reading what the shift had
+// just stored.
+constexpr int PL = 16;          // lanes per instance (one DPP row, in lockstep within the wave)
+constexpr int PREP_BATCH = 16;  // guess elements per lane loaded before any is stored
+__device__ inline void prepare_mpc(const DevConst& c, const DevBuffers& d, int b, int j) {
     const int N = c.N;
     double x[NX], u[NU];
 #pragma unroll
@@ -38,7 +44,7 @@ __device__ inline void prepare_mpc(const DevConst& c, const DevBuffers& d, int b
     for (int i = 0; i < 3; i++) {
         double s = 0;
 #pragma unroll
-        for (int j = 0; j < DOF; j++) s += J[DOF * i + j] * u[j];
+        for (int jj = 0; jj < DOF; jj++) s += J[DOF * i + jj] * u[jj];
         ev[i] = s;
     }
     double dir[3];
@@ -47,42 +53,80 @@ __device__ inline void prepare_mpc(const DevConst& c, const DevBuffers& d, int b
     int valid = d.valid[b], fails = d.fails[b];
     if (fabs(last_s - x[XS]) > c.p.guess_max_dist) { valid = 0; fails++; }
     double* g = d.guess + (size_t)b * (N + 1) * NXU;
-    if (valid) {  // updateInitialGuess (mpc.cpp:54-68)
-        for (int i = 1; i < N; i++)
-            for (int a = 0; a < NXU; a++) g[NXU * (i - 1) + a] = g[NXU * i + a];
-        for (int a = 0; a < NX; a++) g[a] = x[a];
-        for (int a = 0; a < NXU; a++) g[NXU * (N - 1) + a] = g[NXU * (N - 2) + a];
-        rk4_step(g + NXU * (N - 1), g + NXU * (N - 1) + NX, c.p.Ts, g + NXU * N);
-        for (int a = 0; a < NU; a++) g[NXU * N + NX + a] = 0.0;
-    } else {  // generateNewInitialGuess (mpc.cpp:79-89)
-        for (int i = 0; i <= N; i++) {
-            for (int a = 0; a < NX; a++) g[NXU * i + a] = x[a];
-            for (int a = 0; a < NU; a++) g[NXU * i + NX + a] = 0.0;
-        }
-        valid = 1;
-    }
-    for (int i = 1; i <= N; i++) g[NXU * i + XS] = fmin(g[NXU * i + XS], sp.L);  // unwrapInitialGuess
+    // updateInitialGuess (mpc.cpp:54-68) element by element: stage i < N takes old stage min(i, N - 2) + 1 (the shift,
+    // then g[N-1] = g[N-2]) with the state of stage 0 replaced by x; stage N is RK4 of the new stage N - 1 with a zero
+    // input.  generateNewInitialGuess (:79-89): every stage [x, 0].  unwrapInitialGuess: s of stages >= 1 clamped to
+    // the track length.  N = 1 keeps stage 0's input (the reference's g[N-1] = g[N-2] reads g[-1] there).
+    double xN[NX];
+    {
+        double gN[NXU];  // the new stage N - 1, read before any store
 #pragma unroll
-    for (int i = 0; i < NX; i++) d.x0[NX * b + i] = x[i];
-    d.valid[b] = valid;
-    d.fails[b] = fails;
+        for (int a = 0; a < NXU; a++) gN[a] = g[NXU * (N - 1) + a];
+        if (N <= 2) {
+#pragma unroll
+            for (int a = 0; a < NX; a++) gN[a] = x[a];
+        }
+        rk4_step(gN, gN + NX, c.p.Ts, xN);
+    }
+    const int NE = (N + 1) * NXU;
+    for (int e0 = 0; e0 < NE; e0 += PL * PREP_BATCH) {
+        double v[PREP_BATCH];
+#pragma unroll
+        for (int r = 0; r < PREP_BATCH; r++) {
+            const int e = e0 + PL * r + j;
+            const int i = e / NXU, a = e - i * NXU;
+            const int ii = i < N - 2 ? i : N - 2;  // source stage - 1 (-1 when N = 1)
+            const int src = (e < NE && i < N) ? (ii + 1) * NXU + a : 0;
+            double w = g[src];
+            double xa = 0.0;
+#pragma unroll
+            for (int q = 0; q < NX; q++) xa = (a == q) ? x[q] : xa;
+            double xna = 0.0;
+#pragma unroll
+            for (int q = 0; q < NX; q++) xna = (a == q) ? xN[q] : xna;
+            if (valid) {
+                if (i == N) w = (a < NX) ? xna : 0.0;
+                else if (ii <= 0 && a < NX) w = xa;
+            } else {
+                w = (a < NX) ? xa : 0.0;
+            }
+            if (i >= 1 && a == XS) w = fmin(w, sp.L);
+            v[r] = w;
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every old element of the batch read before the stores
+#pragma unroll
+        for (int r = 0; r < PREP_BATCH; r++) {
+            const int e = e0 + PL * r + j;
+            if (e < NE) g[e] = v[r];
+        }
+    }
+    if (!valid) valid = 1;
+    if (j == 0) {
+#pragma unroll
+        for (int i = 0; i < NX; i++) d.x0[NX * b + i] = x[i];
+        d.valid[b] = valid;
+        d.fails[b] = fails;
+    }
 }
 
 __global__ void __launch_bounds__(64) k_prepare(DevConst c, DevBuffers d) {
-    const int b = blockIdx.x * blockDim.x + threadIdx.x;
-    if (b >= c.Bn) return;
+    const int gt = blockIdx.x * blockDim.x + threadIdx.x;
+    const int b = gt / PL, j = gt % PL;
+    if (b >= c.Bn) return;  // whole groups
     const int N = c.N;
-    if (!c.ocp) prepare_mpc(c, d, b);
+    if (!c.ocp) prepare_mpc(c, d, b, j);
     int32_t* si = d.sqi + (size_t)b * SQI;
-    si[SQ_STATUS] = MPCC_MAX_ITER_EXCEEDED;
-    si[SQ_ACTIVE] = 1;
-    si[SQ_ITER] = 0;
-    si[SQ_NFILT] = 0;
-    si[SQ_QPSTAT] = 0;
-    si[SQ_IPMIT] = 0;
-    si[SQ_NLR] = 0;
+    if (j == 0) {
+        si[SQ_STATUS] = MPCC_MAX_ITER_EXCEEDED;
+        si[SQ_ACTIVE] = 1;
+        si[SQ_ITER] = 0;
+        si[SQ_NFILT] = 0;
+        si[SQ_QPSTAT] = 0;
+        si[SQ_IPMIT] = 0;
+        si[SQ_NLR] = 0;
+    }
     double* st = d.step + (size_t)b * (N + 1) * NXU;
-    for (int i = 0; i < (N + 1) * NXU; i++) st[i] = 0.0;  // step_.setZero (osqp_interface.cpp:404)
+    for (int i = j; i < (N + 1) * NXU; i += PL) st[i] = 0.0;  // step_.setZero (osqp_interface.cpp:404)
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -379,7 +423,7 @@ __global__ void k_debug_cost(DevConst c, int M, const double* __restrict__ x, co
 static inline int nblk(long n, int t) { return (int)((n + t - 1) / t); }
 
 void launch_prepare(const DevConst& c, const DevBuffers& d, hipStream_t s) {
-    hipLaunchKernelGGL(k_prepare, dim3(nblk(c.Bn, 64)), dim3(64), 0, s, c, d);
+    hipLaunchKernelGGL(k_prepare, dim3(nblk((long)c.Bn * PL, 64)), dim3(64), 0, s, c, d);
 }
 void launch_stage_records(const DevConst& c, const DevBuffers& d, hipStream_t s) {
     hipLaunchKernelGGL(k_records, dim3(nblk((long)c.S * RPT, 64)), dim3(64), 0, s, c, d);

@@ -2266,7 +2266,7 @@ static void prepare_one(const Oracle& o, double* x0, const double* u0, const dou
     if (*valid) {  // updateInitialGuess :54-68
         for (int i = 1; i < N; i++) std::memcpy(guess + NXU * (i - 1), guess + NXU * i, sizeof(double) * NXU);
         std::memcpy(guess, x0, sizeof(double) * NX);
-        std::memcpy(guess + NXU * (N - 1), guess + NXU * (N - 2), sizeof(double) * NXU);
+        if (N >= 2) std::memcpy(guess + NXU * (N - 1), guess + NXU * (N - 2), sizeof(double) * NXU);  // N = 1: g[-1] in the reference
         rk4(guess + NXU * (N - 1), guess + NXU * (N - 1) + NX, p.Ts, guess + NXU * N);
         for (int b = 0; b < NU; b++) guess[NXU * N + NX + b] = 0.0;
     } else {  // generateNewInitialGuess :79-89
