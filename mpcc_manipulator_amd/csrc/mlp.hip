@@ -144,8 +144,8 @@ __device__ __forceinline__ void mfma_layer_ring(const double* __restrict__ Wp, c
 }
 
 // hidden-layer epilogue: value columns h = relu(z + b); tangent columns dh = (z + b > 0) ? dz : 0.
-// CPS = columns per sample: 8 (value + 7 tangents, 2 samples per 16-column tile) or 16 (value + up to 15
-// tangents, one sample per tile: the mobile env network's 10 input directions).
+// CPS = columns per sample: 8 (value + 7 tangents, 2 samples per 16-column tile), 4 (value + 3 tangents, 4 samples
+// per tile: the mobile env network's obstacle directions) or 16 (value + up to 15 tangents, one sample per tile).
 template <int RT, int CPS = 8>
 __device__ __forceinline__ void relu_gate(d4 (&a)[RT], const double* __restrict__ bias, int lane) {
     const bool isv = (lane & (CPS - 1)) == 0;
@@ -155,15 +155,21 @@ __device__ __forceinline__ void relu_gate(d4 (&a)[RT], const double* __restrict_
 #pragma unroll
         for (int r = 0; r < 4; r++) {
             const double z = a[t][r] + bias[16 * t + (lane >> 4) + 4 * r];
-            const double z0 = bc<0>(z), z8 = bc<8>(z);  // this row's value of sample 0 / sample 1
-            const bool on = (hi ? z8 : z0) > 0.0;
+            double zs;  // the value of this lane's sample in this row
+            if constexpr (CPS == 4) {
+                zs = dpp_d<0x00>(z);  // quad_perm [0,0,0,0]: the quad's lane 0
+            } else {
+                const double z0 = bc<0>(z), z8 = bc<8>(z);  // this row's value of sample 0 / sample 1
+                zs = hi ? z8 : z0;
+            }
+            const bool on = zs > 0.0;
             a[t][r] = isv ? (z > 0.0 ? z : 0.0) : (on ? a[t][r] : 0.0);  // std::max(0., h) of the oracle
         }
 }
 
 // NeRF input [x, sin x, cos x] (3 NIN rows, zero-padded to 32) with its Jacobian columns for the input
-// directions 0..CPS-2 (nerf_jac = [I; diag(cos x); diag(-sin x)], SelfCollisionModel.cpp:143-151, 177-188)
-template <int NIN, int CPS = 8>
+// directions D0..D0+CPS-2 (nerf_jac = [I; diag(cos x); diag(-sin x)], SelfCollisionModel.cpp:143-151, 177-188)
+template <int NIN, int CPS = 8, int D0 = 0>
 __device__ __forceinline__ void nerf_input(const double (&x)[NIN], d4 (&in)[2], int lane) {
     double sx[NIN], cx[NIN];
 #pragma unroll
@@ -171,8 +177,8 @@ __device__ __forceinline__ void nerf_input(const double (&x)[NIN], d4 (&in)[2], 
         sx[i] = sin(x[i]);
         cx[i] = cos(x[i]);
     }
-    const int j = lane & (CPS - 1);  // 0: value column, 1 + d: tangent of input d
-    const int d = j - 1;
+    const int j = lane & (CPS - 1);  // 0: value column, 1 + d - D0: tangent of input d
+    const int d = j - 1 + D0;
 #pragma unroll
     for (int kt = 0; kt < 2; kt++)
 #pragma unroll
@@ -246,6 +252,26 @@ __device__ __forceinline__ void write_out_mobile(const d4& o, const double* __re
         if (j == 0) rec[(size_t)(R_ENV + i) * S + m] = o[r] + bias[i];
         else if (j <= NARM) rec[(size_t)(R_DENV + DOF * i + NBASE + (j - 1)) * S + m] = o[r];
         else if (bb >= 0 && bb < NBASE) rec[(size_t)(R_DENV + DOF * i + bb) * S + m] = j8 * d0 + j9 * d1 + j10 * d2;
+    }
+}
+
+// mobile env network, obstacle pass (CPS = 4, 4 samples per tile): tangents of the 3 arm-frame obstacle coordinates
+// on lanes 1..3 of each quad; the record's base columns are the chain rule sum_a J[i][7 + a] dO[a][b] (the
+// oracle's order), formed on lane 1 + b from quad broadcasts.  The value and arm columns come from the arm pass.
+template <int NOUT>
+__device__ __forceinline__ void write_out_obs(const d4& o, int lane, int m, int M, double* __restrict__ rec, int S,
+                                              const double (&dO)[3][3]) {
+    const int bb = (lane & 3) - 1;  // base column of lanes 1..3 of a quad
+    double d0 = 0.0, d1 = 0.0, d2 = 0.0;
+#pragma unroll
+    for (int b = 0; b < 3; b++)
+        if (bb == b) { d0 = dO[0][b]; d1 = dO[1][b]; d2 = dO[2][b]; }
+#pragma unroll
+    for (int r = 0; r < 4; r++) {
+        const double j7 = dpp_d<0x55>(o[r]), j8 = dpp_d<0xAA>(o[r]), j9 = dpp_d<0xFF>(o[r]);  // whole row active
+        const int i = (lane >> 4) + 4 * r;
+        if (m >= M || i >= NOUT || bb < 0 || bb >= NBASE) continue;
+        rec[(size_t)(R_DENV + DOF * i + bb) * S + m] = j7 * d0 + j8 * d1 + j9 * d2;
     }
 }
 
@@ -347,15 +373,18 @@ __global__ void __launch_bounds__(256) k_mlp_self(DevConst c, DevBuffers d, NNDe
 }
 
 // env network 30 -> 256 -> 256 -> 256 -> 256 -> 9 (osqp_interface.cpp:40-43).  Panda: 2 samples per wave,
-// tangents of q_0..q_6.  Mobile manipulator: 1 sample per wave, tangents of the 7 arm joints and the 3
-// arm-frame obstacle coordinates (the base columns follow by the chain rule, write_out_mobile).
-template <int CPS>
+// tangents of q_0..q_6.  Mobile manipulator (input directions: 7 arm joints + 3 arm-frame obstacle coordinates, the
+// base columns by the chain rule): two passes, the Panda's (CPS = 8, the arm tangents, D0 = 0) and an obstacle pass
+// (CPS = 4, D0 = 7: 4 samples per tile), 12 columns per sample instead of one 16-column tile with 11 used
+// (MPCC_ENV_SPLIT = 0: that form, CPS = 16).  A column's MFMA chain does not depend on the other columns of its
+// tile, so every output is bitwise that of the one-tile form.
+template <int CPS, int D0 = 0>
 __device__ __forceinline__ void mlp_env_body(const DevConst& c, const DevBuffers& d, const NNDesc& nd, const double* __restrict__ W,
                                              int M, const double* __restrict__ qin, const double* __restrict__ obsin,
                                              double* __restrict__ rec, int S, double* wl, double* bl) {
     const int lane = threadIdx.x & 63;
     const int wave = blockIdx.x * 4 + (threadIdx.x >> 6);
-    const int m = (CPS == 8) ? 2 * wave + ((lane >> 3) & 1) : wave;
+    const int m = (16 / CPS) * wave + (lane & 15) / CPS;
     double q[DOF], obs[3];
     sample_input(c, d, m, M, qin, obsin, q, obs);
     double x[10];
@@ -373,7 +402,7 @@ __device__ __forceinline__ void mlp_env_body(const DevConst& c, const DevBuffers
     for (int l = 0; l < 4; l++) bl[l * 256 + threadIdx.x] = W[nd.offb[l] + threadIdx.x];
     if (threadIdx.x < 9) bl[1024 + threadIdx.x] = W[nd.offb[4] + threadIdx.x];
     d4 a0[2], a[16], h[16], o[1];
-    nerf_input<10, CPS>(x, a0, lane);
+    nerf_input<10, CPS, D0>(x, a0, lane);
     mfma_layer_ring<2, 16>(W + nd.offW[0], a0, a, lane, wl);
     relu_gate<16, CPS>(a, bl, lane);
     for (int l = 1; l <= 3; l++) {  // three 256 x 256 hidden layers share one unrolled body
@@ -384,11 +413,16 @@ __device__ __forceinline__ void mlp_env_body(const DevConst& c, const DevBuffers
     }
     mfma_layer<16, 1>(W + nd.offW[4], a, o, lane);
     if constexpr (CPS == 8) write_out<9>(o[0], bl + 1024, lane, m, M, rec, S, R_ENV, R_DENV);
+    else if constexpr (CPS == 4) write_out_obs<9>(o[0], lane, m, M, rec, S, dO);
     else write_out_mobile<9>(o[0], bl + 1024, lane, m, M, rec, S, dO);
 }
 
-constexpr int ENV_CPS = (NBASE > 0) ? 16 : 8;  // columns per sample of k_mlp_env
-constexpr int ENV_SPW = 16 / ENV_CPS;          // samples per wave
+#ifndef MPCC_ENV_SPLIT
+#define MPCC_ENV_SPLIT 1
+#endif
+constexpr bool ENV_SPLIT = MPCC_ENV_SPLIT && NBASE > 0;      // the mobile build's two passes
+constexpr int ENV_CPS = (NBASE > 0 && !ENV_SPLIT) ? 16 : 8;  // columns per sample of k_mlp_env
+constexpr int ENV_SPW = 16 / ENV_CPS;                        // samples per wave
 
 __global__ void __launch_bounds__(256) k_mlp_env(DevConst c, DevBuffers d, NNDesc nd, const double* __restrict__ W, int M,
                                                  const double* __restrict__ qin, const double* __restrict__ obsin,
@@ -399,6 +433,16 @@ __global__ void __launch_bounds__(256) k_mlp_env(DevConst c, DevBuffers d, NNDes
     __shared__ double bl[4 * 256 + 16];
     mlp_env_body<ENV_CPS>(c, d, nd, W, M, qin, obsin, rec, S, wl, bl);
 }
+#if MPCC_DOF != 7
+// the mobile build's obstacle pass (ENV_SPLIT)
+__global__ void __launch_bounds__(256) k_mlp_env_obs(DevConst c, DevBuffers d, NNDesc nd, const double* __restrict__ W, int M,
+                                                     const double* __restrict__ qin, const double* __restrict__ obsin,
+                                                     double* __restrict__ rec, int S) {
+    __shared__ __attribute__((aligned(16))) double wl[RING_SLOTS * 16 * 256];
+    __shared__ double bl[4 * 256 + 16];
+    mlp_env_body<4, 7>(c, d, nd, W, M, qin, obsin, rec, S, wl, bl);
+}
+#endif
 
 void launch_nn(const DevConst& c, const DevBuffers& d, const NNDesc& nd, const double* W, int which, int M,
                const double* q, const double* obs, double* rec, int rec_stride, hipStream_t s) {
@@ -406,9 +450,14 @@ void launch_nn(const DevConst& c, const DevBuffers& d, const NNDesc& nd, const d
     if (which == 0)  // 4 waves x SELF_CT tiles x 2 samples
         hipLaunchKernelGGL(k_mlp_self, dim3((M + 8 * SELF_CT - 1) / (8 * SELF_CT)), dim3(256), 0, s, c, d, nd, W, M, q, obs,
                            rec, rec_stride);
-    else
+    else {
         hipLaunchKernelGGL(k_mlp_env, dim3((M + 4 * ENV_SPW - 1) / (4 * ENV_SPW)), dim3(256), 0, s, c, d, nd, W, M, q, obs,
                            rec, rec_stride);
+#if MPCC_DOF != 7
+        if constexpr (ENV_SPLIT)  // 4 waves x 4 samples
+            hipLaunchKernelGGL(k_mlp_env_obs, dim3((M + 15) / 16), dim3(256), 0, s, c, d, nd, W, M, q, obs, rec, rec_stride);
+#endif
+    }
 }
 
 }  // namespace mpcc
