@@ -359,6 +359,9 @@ __device__ __forceinline__ void sweep_noprefetch(int N, bool backward, In& b0, L
 #ifndef MPCC_LIGHT_DEPTH
 #define MPCC_LIGHT_DEPTH 2
 #endif
+#ifndef MPCC_LIGHT_UNROLL  // unroll factor of the LDS-ring light sweeps (A/B switch)
+#define MPCC_LIGHT_UNROLL 1
+#endif
 template <int D, class In, class LoadF, class BodyF>
 __device__ __forceinline__ void sweep_ring(int N, bool backward, In (&b)[D], LoadF load, BodyF body) {
     auto s = [&](int i) { return backward ? N - i : i; };
@@ -708,6 +711,7 @@ __device__ __forceinline__ void ipm_group(const DevConst& c, const DevBuffers& d
 #pragma unroll
         for (int j = 0; j < RD - 1; j++) glds_stage(cl(j), j, nfc);
         int slot = 0;
+#pragma unroll MPCC_LIGHT_UNROLL
         for (int i = 0; i <= N; i++) {
             glds_stage(cl(i + RD - 1), slot == 0 ? RD - 1 : slot - 1, nfc);
             asm volatile("s_waitcnt vmcnt(%0)" ::"n"((RD - 1) * G) : "memory");
