@@ -52,7 +52,8 @@ def main():
     merged = collections.defaultdict(dict)
     for p in ("p1", "p2", "p3", "p4"):
         for k, v in load_pmc(args.dir, p).items():
-            if v["grid"] == grid and v["kernel"].startswith(f"void {args.ns}::{args.kernel}<"):
+            if v["grid"] == grid and (v["kernel"].startswith(f"void {args.ns}::{args.kernel}<")  # template kernels
+                                      or v["kernel"].startswith(f"{args.ns}::{args.kernel}(")):
                 merged[p + ":" + str(k)] = v
     per = collections.defaultdict(list)
     for key, v in merged.items():
