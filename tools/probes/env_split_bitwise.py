@@ -3,6 +3,15 @@ records (both MLPs, value and every Jacobian column) of the same seeded samples 
 from a variant built with -DMPCC_ENV_SPLIT=0 (mpcc_manipulator_amd/_ab/envsplit0), each in its own process.
 
     python tools/probes/env_split_bitwise.py            # runs both and compares
+
+The variant library (built in this container, it travels to the GPU box with the tree):
+
+    cd mpcc_manipulator_amd && mkdir -p _ab/envsplit0 && \\
+    hipcc -O3 -std=c++17 -fPIC --offload-arch=gfx950 -I ../include -I csrc -ffp-contract=off -DMPCC_DOF=10 \\
+          -Dmpcc=mpcc_m10 -DMPCC_ENV_SPLIT=0 -c csrc/mlp.hip -o _ab/envsplit0/mlp_mobile.o && \\
+    hipcc --offload-arch=gfx950 -shared -fPIC -o _ab/envsplit0/libmpcc_engine_mobile.so _build/kernels_mobile.o \\
+          _build/ipm_wide_mobile.o _ab/envsplit0/mlp_mobile.o _build/nn_generic_mobile.o _build/engine_mobile.o \\
+          _build/host_params_mobile.o _build/host_spline_mobile.o
 """
 import os
 import subprocess
