@@ -319,6 +319,9 @@ int mpcc_debug_trace_get(mpcc_engine* e, int B, double* out /* [B*4*8] */);
  * recorded since the last clear (0 = every computed workspace / record / ring / LDS / spline index in range;
  * bits: csrc/dev_common.h BC_*); MPCC_E_INVALID on a normal build */
 int mpcc_debug_bounds(mpcc_engine* e, uint32_t* flags, int clear);
+/* QP solves the fused kernels finished in tail mode (the wave's last running instance on all four 16-lane groups,
+ * csrc/ipm_tail.h) since the last reset, over all engines of the process; Panda library, <= 2 polytopic rows */
+int mpcc_debug_tail_solves(long long* out, int reset);
 
 /* Build provenance (no reference counterpart): a hash of the sources the library was compiled from
  * (csrc/ and include/, mpcc_manipulator_amd/_build.py source_hash) and the build's variant bits. */

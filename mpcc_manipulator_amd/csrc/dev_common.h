@@ -109,6 +109,7 @@ struct DevConst {
     int Bn;                          // batch size of this call
     int faithful_dead_trials;
     int ocp;                         // 1: SolverInterface::solveOCP only (mpcc_solve_ocp), no MPC bookkeeping
+    int tail;                        // 1: k_sqp's interior point runs a wave's last active instance in tail mode
     uint32_t* bchk;                  // bounds-checked build: per-lane violation bits (null otherwise)
 };
 

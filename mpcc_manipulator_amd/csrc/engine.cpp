@@ -59,6 +59,7 @@ struct mpcc_engine {
     // (MPCC_STAGED_SQP=1; same arithmetic, kept for A/B timing and debugging)
     bool staged_sqp = false;
     bool wide_sqp = false;  // MPCC_WIDE_SQP=1: the 32-lane fused kernel for the Panda build too (experiment)
+    int tail_mode = 1;      // MPCC_TAIL=0: no tail mode in k_sqp (A/B switch; results are bitwise the same)
     bool last_wide = DOF != 7;  // the last solve's interior point ran on the 32-lane workspace (d.isw)
     uint32_t* bchk = nullptr;  // bounds-checked build: per-lane violation bits (dev_common.h MPCC_BCHK)
     mpcc_params params{};
@@ -168,6 +169,7 @@ struct mpcc_engine {
         c.Bn = Bn;
         c.S = Bn * (N + 1);
         c.faithful_dead_trials = cfg.faithful_dead_trials;
+        c.tail = tail_mode;
         return c;
     }
 
@@ -500,6 +502,13 @@ int mpcc_so3_exp(const double* S9, double* R9) {
     return MPCC_OK;
 }
 const char* mpcc_last_error(void) { return g_last_error.c_str(); }
+#if MPCC_DOF != 7
+// the mobile build's interior point (ipm_wide.hip) has no tail mode (ipm_tail.h is the Panda's 16-lane form)
+int mpcc_debug_tail_solves(long long* out, int /*reset*/) {
+    if (out) *out = 0;
+    return MPCC_OK;
+}
+#endif
 
 int mpcc_create(const mpcc_config* cfg, const mpcc_params* params, const char* nn_dir, mpcc_engine** out) {
     if (!cfg || !params || !out) return fail(MPCC_E_INVALID, "mpcc_create: null argument");
@@ -510,6 +519,8 @@ int mpcc_create(const mpcc_config* cfg, const mpcc_params* params, const char* n
         e->staged_sqp = st && st[0] == '1';
         const char* wd = std::getenv("MPCC_WIDE_SQP");
         e->wide_sqp = wd && wd[0] == '1';
+        const char* tl = std::getenv("MPCC_TAIL");
+        e->tail_mode = (tl && tl[0] == '0') ? 0 : 1;
         e->params = *params;
         e->params.N = cfg->N;
         e->params.Ts = cfg->Ts;

@@ -46,7 +46,11 @@ constexpr double IPM_TOL_MU = 1e-13, IPM_TOL_P = 1e-11, IPM_TOL_STEP = 1e-11;
 constexpr double IPM_TOL_FB = 1e-9;  // P2: a converged iterate is accepted when the Riccati factor breaks down
 constexpr double IPM_DIV = 1e6;      // P3: mu > IPM_DIV * mu_0 -> primal infeasible (divergent multipliers)
 constexpr double IPM_S0 = 0.02, IPM_L0 = 0.002;  // scaled start point (oracle: solve_struct_ipm)
-constexpr int IPM_MAX_IT_SCALED = 30;
+#ifdef MPCC_DBG_IPM_STOP  // debug builds (tools/tail_ws_diff.py): stop every QP after that many iterations, no restart
+constexpr int IPM_MAX_IT_SCALED = MPCC_DBG_IPM_STOP, IPM_ATTEMPTS = 1;
+#else
+constexpr int IPM_MAX_IT_SCALED = 30, IPM_ATTEMPTS = 2;
+#endif
 constexpr double IPM_TAU = 0.995;    // fraction-to-boundary floor: tau = max(IPM_TAU, 1 - sqrt(mu))
 typedef __attribute__((address_space(1))) double gdouble;  // global-memory double (global_* loads/stores)
 constexpr int IPW = 4;               // instances per wavefront (16 lanes each)
@@ -121,8 +125,16 @@ size_t ipm_lds_bytes(int /*N*/, int npmax) {
 #ifdef MPCC_IPM_PROF
 // cycle accounting per k_ipm section (profiling build only, see _build.py / tools/ipm_prof.py)
 __device__ unsigned long long g_ipm_prof[16];
+// per-wave start / end of the last k_sqp launch (s_memrealtime, 100 MHz), indexed by workgroup (one wave each),
+// and the IPM iterations of all QPs of each instance (tools/wave_times.py)
+constexpr int PROF_WAVES = 1 << 16;
+__device__ unsigned long long g_wave_t[2 * PROF_WAVES];
+__device__ int g_inst_its[4 * PROF_WAVES];
+__device__ unsigned long long g_tail_prof[16];  // tail mode: factor A, B, C, D, predictor fwd, corrector bwd, fwd; iterations; B sub-sections
+#define TMARK(i) do { const long long t_ = clock64(); tprof[i] += t_ - tprof_t; tprof_t = t_; } while (0)
 #define PMARK(i) do { const long long t_ = clock64(); prof_acc[i] += t_ - prof_t; prof_t = t_; } while (0)
 #else
+#define TMARK(i) do { } while (0)
 #define PMARK(i) do { } while (0)
 #endif
 
@@ -193,6 +205,14 @@ __device__ __forceinline__ double rcp(double x) {
     double r = __builtin_amdgcn_rcp(x);
     r = fma(fma(-x, r, 1.0), r, r);
     return fma(fma(-x, r, 1.0), r, r);
+}
+// mu(alpha) sums of one slot, S0 += s l, S1 += s dl + l ds, S2 += ds dl, with the fused forms written out: the
+// contraction the compiler would choose depends on whether s l is also used elsewhere, and tail mode (ipm_tail.h)
+// accumulates the same terms in another function, which must come out bitwise the same
+__device__ __forceinline__ void mu_acc(double& S0, double& S1, double& S2, double s, double l, double ds, double dl) {
+    S0 = fma(s, l, S0);
+    S1 = S1 + fma(s, dl, l * ds);
+    S2 = fma(ds, dl, S2);
 }
 // corrector step of a slot given the iterate (cz), the predictor step (ca) and the corrector step (cd)
 __device__ __forceinline__ SlotStep slot_corr(double sgn, double bnd, double cz, double ca, double cd, double s, double l,
@@ -378,12 +398,14 @@ __device__ __forceinline__ void sweep_ring(int N, bool backward, In (&b)[D], Loa
     }
 }
 
+#include "ipm_tail.h"
+
 }  // namespace
 
 // The QP solve of the 4 instances of this wavefront (16 lanes each); instances whose SQP is inactive
 // idle through it.  Writes the step (d.step), QP status and IPM iteration count (d.sqi).
 template <int NPM>
-__device__ __forceinline__ void ipm_group(const DevConst& c, const DevBuffers& d, double* smem) {
+__device__ __forceinline__ bool ipm_group(const DevConst& c, const DevBuffers& d, double* smem) {
     // Workspace field indices of this variant.  The wide-poly variants (NPM >= 9) order their fields so that each
     // light sweep's LDS-ring image is the shortest run from field 0: the poly slot state and c_p^T z right after
     // the iterate, then K and kff (predictor forward), the predictor step and c_p^T dza (corrector forward), the
@@ -414,7 +436,7 @@ __device__ __forceinline__ void ipm_group(const DevConst& c, const DevBuffers& d
     const bool valid = b < c.Bn;
     int32_t* si = d.sqi + (size_t)(valid ? b : 0) * SQI;
     bool run = valid && si[SQ_ACTIVE] != 0;
-    if (__ballot(run) == 0) return;
+    if (__ballot(run) == 0) return false;
 
     // QP records and the workspace through global-address-space pointers: their loads and stores compile
     // to global_* instructions, which count only in vmcnt.  Through the generic pointers of DevBuffers they
@@ -798,9 +820,11 @@ __device__ __forceinline__ void ipm_group(const DevConst& c, const DevBuffers& d
     };
     int it = 0, it_total = 0;
     bool conv = false, diverged = false;
+    bool tail_req = false;  // tail mode requested for instance tail_gs of this wave (NPM <= 2)
+    int tail_gs = 0;
     double alpha = 0.0;  // step length of the last iteration (the final iterate is z + alpha dz)
 #pragma unroll 1
-    for (int attempt = 0; attempt < 2; attempt++) {
+    for (int attempt = 0; attempt < IPM_ATTEMPTS; attempt++) {
     const double s_floor = (attempt == 0) ? IPM_S0 : 1.0;
     const double lam_scale = (attempt == 0) ? IPM_L0 : 0.0;
     const int max_it = (attempt == 0) ? IPM_MAX_IT_SCALED : IPM_MAX_IT;
@@ -851,6 +875,25 @@ __device__ __forceinline__ void ipm_group(const DevConst& c, const DevBuffers& d
     if (run) alpha = 0.0;
     while (true) {
         if (__ballot(run) == 0) break;
+        if constexpr (NPM <= 2) {
+            // Tail mode (ipm_tail.h): the wave's last running instance takes all four groups for the rest of its
+            // solve.  Its iteration state goes to LDS and the solve continues in ipm_tail_solve after this function
+            // returns (a call from here would change this function's register allocation); the wave's other
+            // instances are done with this QP, and none of them waits for the restart of attempt 1.
+            const unsigned long long lead = __ballot(run && t == 0);
+            if (c.tail && __popcll(lead) == 1 && __ballot(t == 0 && !run && entered && !conv && attempt == 0) == 0) {
+                tail_gs = (__ffsll((long long)lead) - 1) >> 4;
+                tail_req = true;
+                if (lane == tail_gs * 16) {
+                    double* st = smem + TL_STATE;
+                    st[0] = it; st[1] = max_it; st[2] = pending ? 1.0 : 0.0; st[3] = attempt; st[4] = it_total;
+                    st[5] = mu0; st[6] = dz_prev; st[7] = sigma_mu; st[8] = mu_cur; st[9] = rp_cur; st[10] = alpha;
+                    st[11] = mcount; st[12] = tail_gs;
+                }
+                run = false;
+                break;
+            }
+        }
         {
             // ================= factorization sweep k = N..0 with the lazy update of the previous step,
             // the objective gradient g0 = H z + h and the predictor backward solve.  The whole wave runs it,
@@ -1143,7 +1186,8 @@ __device__ __forceinline__ void ipm_group(const DevConst& c, const DevBuffers& d
                 PMARK(11);
 #ifdef MPCC_IPM_DBGF
                 if (run) { *ws(k, 35) = gx; *ws(k, 36) = gv; *ws(k, 37) = pv; *ws(k, 38) = fv; *ws(k, 39) = dvr; *ws(k, 40) = cP;
-                *ws(k, 41) = wd; *ws(k, 42) = pnew; *ws(k, 43) = kff; }
+                *ws(k, 41) = wd; *ws(k, 42) = pnew; *ws(k, 43) = kff; *ws(k, 44) = Pc[0]; *ws(k, 45) = LF[35];
+                *ws(k, 46) = dinv[7]; *ws(k, 47) = u[0]; *ws(k, 48) = kc[0]; *ws(k, 49) = Y[0]; *ws(k, 50) = Fc[0]; }
 #endif
 #pragma unroll
                 for (int i = 0; i < 8; i++) S[L_K + i * 16 + t] = kc[i];
@@ -1295,9 +1339,7 @@ __device__ __forceinline__ void ipm_group(const DevConst& c, const DevBuffers& d
                     const double rp = slot_rp(sgn, czz, bnd, s);
                     const SlotStep st = slot_recover(rcp(s), l, rp, sgn * caa, s * l);
                     step_bound(amr, s, l, st);
-                    S0 += s * l;
-                    S1 += s * st.dl + l * st.ds;
-                    S2 += st.ds * st.dl;
+                    mu_acc(S0, S1, S2, s, l, st.ds, st.dl);
                 };
                 rec(aL, sgnL, cur.lb, cz, ca, cur.sL, cur.lL);
                 rec(aU, sgnU, cur.ub, cz, ca, cur.sU, cur.lU);
@@ -1408,9 +1450,7 @@ __device__ __forceinline__ void ipm_group(const DevConst& c, const DevBuffers& d
                     double rp;
                     const SlotStep st = slot_corr(sgn, bnd, czz, caa, cdd, s, l, smu, &rp);
                     step_bound(amc, s, l, st);
-                    T0 += s * l;
-                    T1 += s * st.dl + l * st.ds;
-                    T2 += st.ds * st.dl;
+                    mu_acc(T0, T1, T2, s, l, st.ds, st.dl);
                     rpm = fmax(rpm, fabs(rp));
                 };
                 rec(aL, sgnL, cur.lb, cz, ca, cd, cur.sL, cur.lL);
@@ -1451,6 +1491,7 @@ __device__ __forceinline__ void ipm_group(const DevConst& c, const DevBuffers& d
         }
     }
     it_total += it;
+    if (tail_req) break;  // no other instance of the wave needs the restart (checked at the hand-over)
     }  // attempt
 
 #ifdef MPCC_IPM_PROF
@@ -1460,11 +1501,14 @@ __device__ __forceinline__ void ipm_group(const DevConst& c, const DevBuffers& d
         atomicAdd(&g_ipm_prof[7], 1ull);
     }
 #endif
-    if (!entered) return;
+    if (!entered || (tail_req && grp == tail_gs)) return tail_req;
+#ifdef MPCC_IPM_PROF
+    if (t == 0 && b < 4 * PROF_WAVES) g_inst_its[b] += it_total;
+#endif
     if (t == 0) si[SQ_IPMIT] = it_total;
     if (!conv) {  // keep the previous step (Q6)
         if (t == 0) si[SQ_QPSTAT] = diverged ? MPCC_QP_PrimalInfeasible : MPCC_QP_MaxIterReached;
-        return;
+        return tail_req;
     }
     if (t == 0) si[SQ_QPSTAT] = 0;
     gdouble* stp = (gdouble*)(d.step + (size_t)b * NS * 17);
@@ -1474,9 +1518,29 @@ __device__ __forceinline__ void ipm_group(const DevConst& c, const DevBuffers& d
         if (t < 9) stp[k * 17 + t] = zx;
         if (t < 8) stp[k * 17 + 9 + t] = (k < N) ? zv : 0.0;
     }
+    return tail_req;
 }
 
 #ifdef MPCC_IPM_PROF
+extern "C" int mpcc_debug_wave_times(unsigned long long* out, int n) {
+    if (n > PROF_WAVES) n = PROF_WAVES;
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_wave_t), sizeof(unsigned long long) * n) != hipSuccess) return -1;
+    if (hipMemcpyFromSymbol(out + n, HIP_SYMBOL(g_wave_t), sizeof(unsigned long long) * n,
+                            sizeof(unsigned long long) * PROF_WAVES) != hipSuccess) return -1;
+    return n;
+}
+extern "C" int mpcc_debug_tail_prof(unsigned long long* out, int reset) {
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_tail_prof), sizeof(unsigned long long) * 16) != hipSuccess) return -1;
+    if (reset) {
+        unsigned long long z[16] = {0};
+        if (hipMemcpyToSymbol(HIP_SYMBOL(g_tail_prof), z, sizeof z) != hipSuccess) return -1;
+    }
+    return 0;
+}
+extern "C" int mpcc_debug_inst_ipm_iters(int* out, int n) {  // IPM iterations of every QP of the last k_sqp launch
+    if (n > 4 * PROF_WAVES) n = 4 * PROF_WAVES;
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_inst_its), sizeof(int) * n) == hipSuccess ? n : -1;
+}
 extern "C" int mpcc_debug_ipm_prof(unsigned long long* out, int reset) {
     if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_ipm_prof), sizeof(unsigned long long) * 16) != hipSuccess) return -1;
     if (reset) {
@@ -1487,12 +1551,6 @@ extern "C" int mpcc_debug_ipm_prof(unsigned long long* out, int reset) {
 }
 #endif
 
-// k_ipm: one QP solve per active instance (the staged SQP loop of run_batch and the debug QP entry)
-template <int NPM>
-__global__ void __launch_bounds__(64) k_ipm(DevConst c, DevBuffers d) {
-    extern __shared__ __attribute__((aligned(16))) double smem[];
-    ipm_group<NPM>(c, d, smem);
-}
 
 // ------------------------------------------------------------------------------------------------
 // k_sqp: the whole SQP loop of solveOCP (osqp_interface.cpp:431-574) per instance, one 16-lane group
@@ -1534,9 +1592,25 @@ __device__ __attribute__((noinline)) void sqp_soc_phase(const DevConst& c, const
         soc_stage(c, sp, d.guess + o, d.step + o, RecView{d.rec + (size_t)b * NS + k, c.S}, k, ucur,
                   d.qs + ((size_t)b * NS + k) * QS);
 }
+// returns true when the wave's last running instance is handed to tail mode (ipm_tail_solve, called by the kernel:
+// a call inside this function would change the interior point's register allocation)
 template <int NPM>
-__device__ __attribute__((noinline)) void sqp_ipm_phase(const DevConst& c, const DevBuffers& d, double* smem) {
-    ipm_group<NPM>(c, d, smem);
+__device__ __attribute__((noinline)) bool sqp_ipm_phase(const DevConst& c, const DevBuffers& d, double* smem) {
+    return ipm_group<NPM>(c, d, smem);
+}
+template <int NPM>
+__device__ __forceinline__ void sqp_qp_solve(const DevConst& c, const DevBuffers& d, double* smem) {
+    if (sqp_ipm_phase<NPM>(c, d, smem)) {
+        if constexpr (NPM <= 2) ipm_tail_solve<NPM>(c, d, smem);
+    }
+}
+
+// k_ipm: one QP solve per active instance (the staged SQP loop of run_batch and the debug QP entry); its arguments
+// read in place like k_sqp's (kernels.h kernarg_const)
+template <int NPM>
+__global__ void __launch_bounds__(64) k_ipm(DevConst, DevBuffers) {
+    extern __shared__ __attribute__((aligned(16))) double smem[];
+    sqp_qp_solve<NPM>(kernarg_const(), kernarg_buffers(), smem);
 }
 
 template <int NPM>
@@ -1551,6 +1625,10 @@ __global__ void __launch_bounds__(64) k_sqp(DevConst, DevBuffers, const double* 
     const int bb = valid ? b : 0;
     int32_t* si = d.sqi + (size_t)bb * SQI;
     const double* ucur = ucur_all + 8 * bb;
+#ifdef MPCC_IPM_PROF
+    if (threadIdx.x == 0 && blockIdx.x < PROF_WAVES) g_wave_t[blockIdx.x] = __builtin_amdgcn_s_memrealtime();
+    if (t == 0 && b < 4 * PROF_WAVES) g_inst_its[b] = 0;
+#endif
     for (int it = 0; it < c.p.max_iter; it++) {
         bool act = valid && si[SQ_ACTIVE] != 0;
         if (__ballot(act) == 0) break;
@@ -1558,13 +1636,13 @@ __global__ void __launch_bounds__(64) k_sqp(DevConst, DevBuffers, const double* 
             if (act) sqp_setqp_phase(c, d, b, t, ucur);
             __syncthreads();
         }
-        sqp_ipm_phase<NPM>(c, d, smem);
+        sqp_qp_solve<NPM>(c, d, smem);
         __syncthreads();
         if (c.p.do_SOC) {  // SecondOrderCorrection (osqp_interface.cpp:506-535): same P, q, A, shifted bounds
             act = valid && si[SQ_ACTIVE] != 0;
             if (act) sqp_soc_phase(c, d, b, t, ucur);
             __syncthreads();
-            sqp_ipm_phase<NPM>(c, d, smem);  // a failed correction keeps the step (Q6)
+            sqp_qp_solve<NPM>(c, d, smem);  // a failed correction keeps the step (Q6)
             __syncthreads();
         }
         act = valid && si[SQ_ACTIVE] != 0;
@@ -1588,7 +1666,24 @@ __global__ void __launch_bounds__(64) k_sqp(DevConst, DevBuffers, const double* 
         if (act && t == 0) finish_iteration(c, d, b, nrm);
         __syncthreads();
     }
+#ifdef MPCC_IPM_PROF
+    if (threadIdx.x == 0 && blockIdx.x < PROF_WAVES) g_wave_t[PROF_WAVES + blockIdx.x] = __builtin_amdgcn_s_memrealtime();
+#endif
 }
+
+}  // namespace mpcc
+// QP solves finished in tail mode (ipm_tail.h) since the last reset, over all engines of the process
+extern "C" int mpcc_debug_tail_solves(long long* out, int reset) {
+    unsigned long long v = 0;
+    if (hipMemcpyFromSymbol(&v, HIP_SYMBOL(mpcc::g_tail_solves), sizeof v) != hipSuccess) return -1;
+    if (out) *out = (long long)v;
+    if (reset) {
+        const unsigned long long z = 0;
+        if (hipMemcpyToSymbol(HIP_SYMBOL(mpcc::g_tail_solves), &z, sizeof z) != hipSuccess) return -1;
+    }
+    return 0;
+}
+namespace mpcc {
 
 template <int NPM>
 static void launch_ipm_t(const DevConst& c, const DevBuffers& d, hipStream_t s) {

@@ -1,0 +1,983 @@
+// ipm_tail.h — tail mode of the 16-lane interior point (included by ipm.hip inside namespace mpcc, after its
+// stage helpers).  DESIGN.md §3.5.
+//
+// A k_sqp launch lasts as long as its slowest wave, and a wave as long as its slowest instance: at configs[1] the
+// bulk of a 2048-instance launch is done after ~1.9 ms while 1-5 waves with a cold-started instance (two QPs,
+// 16-17 IPM iterations) run on alone to ~3 ms (tools/wave_times.py, profiles/r04a_wave_times.json).  Such a wave
+// has three idle 16-lane groups.  Tail mode gives them to the last instance: the remaining IPM iterations of the
+// QP run with all four groups on the one instance, each sweep over the horizon in blocks of four stages:
+//   A  group g works on stage kb -/+ g: its stage loads and everything of the stage that does not depend on the
+//      sweep's recursion (the lazy update, slot weights and coefficients, gradients, the P-independent parts of
+//      F, Gm and Hb; in the light sweeps the slot algebra);
+//   B  the recursion itself, stage after stage, redundantly on all four groups (P_k from P_{k+1} through chol(F)
+//      and U; the forward rollout x~_{k+1}; the backward costate p_k);
+//   C  again four stages at once: what needs the recursion's output (K, F^-1, the slot steps and bounds);
+//   D  the order-dependent accumulations (p chain of the factorization, the mu(alpha) sums) in stage order.
+// Stage data move between the phases through the wave's LDS (the ring of the light sweeps is idle in tail mode).
+// Every value is computed by the same expressions as in ipm_group, in the same order; the accumulations of D run
+// in stage order, so a tail-mode solve is bitwise the normal one (tests/test_tail_mode.py checks it on the GPU;
+// only a tie of the fraction-to-boundary candidates within product rounding could pick the other candidate).
+//
+// Narrow variants only (NPM <= 2: the poly slot state packed into WF_ZV, no cached poly products).
+
+__device__ unsigned long long g_tail_solves;  // QP solves finished in tail mode since the last reset
+
+struct TailIO {
+    int it, max_it, pending, conv, diverged, restart;
+    double mu0, dz_prev, sigma_mu, mu_cur, rp_cur, alpha, mcount;
+};
+
+// LDS layout of tail mode (doubles from the wave's base): per-stage exchange slots [slot j][lane t][field],
+// row strides = 2 mod 4 doubles so that the 16 lanes' 16-byte accesses fall on distinct bank groups
+constexpr int TL_SA = 30;                       // factorization A -> B, D: 28 + 2 fields
+constexpr int TL_A = 0;                         // 4 * 16 * TL_SA
+constexpr int TL_LF = TL_A + 4 * 16 * TL_SA;    // 4 * 48: L of chol(F) (36) and its reciprocal pivots (8), per stage
+constexpr int TL_U = TL_LF + 4 * 48;            // 4 * 16 * 10: U column (8)
+constexpr int TL_K = TL_U + 4 * 16 * 10;        // 4 * 144: K transpose area per group (8 x 16, +16 pad)
+constexpr int TL_C = TL_K + 4 * 144;            // 4 * 16 * 18: K column (8) and F^-1 column (8)
+constexpr int TL_END = TL_C + 4 * 16 * 18;
+constexpr int TL_STATE = TL_END;                // 16: iteration state handed over by ipm_group
+// light sweeps (alias the factorization's areas)
+constexpr int TL_LA = 0;                        // A -> B: 14 fields, stride 18
+constexpr int TL_LB = TL_LA + 4 * 16 * 18;      // B -> C: x~_k, v_k, stride 2
+constexpr int TL_LC = TL_LB + 4 * 16 * 2;       // C -> D: per slot row (L, U, P): s, l, ds, dl; stride 14
+constexpr int TL_LM = TL_LC + 4 * 16 * 14;      // per-group combine scratch: 64 lanes x 4
+static_assert((TL_STATE + 16) * 8 <= LRING * LG(LF_CBWD) * 1024, "tail-mode LDS inside the narrow variants' ring");
+static_assert((TL_LM + 64 * 4) * 8 <= LRING * LG(LF_CBWD) * 1024, "tail-mode LDS inside the narrow variants' ring");
+
+template <int NPM>
+__device__ __attribute__((noinline)) void ipm_tail(const DevConst& c, const DevBuffers& d, double* smem, int gs, TailIO& io) {
+    static_assert(NPM <= 2, "tail mode: narrow variants");
+    using namespace dpp;
+    constexpr int NPE = NPM > 0 ? NPM : 1;
+    using In = StageIn<NPE>;
+    const int lane = threadIdx.x;
+    const int g = lane >> 4;
+    const int t = lane & 15;
+    const int b = blockIdx.x * IPW + gs;
+    const int N = c.N;
+    const int NS = N + 1;
+
+    const gdouble* QSb = (const gdouble*)(d.qs + (size_t)MPCC_BCHK(c.bchk, b, c.Bn, BC_INSTANCE) * NS * QS);
+    gdouble* WSb = (gdouble*)(d.is + (size_t)b * NS * IS);
+    gdouble* const WSt = WSb + t;
+    auto ws = [&](int k, int f) -> gdouble* {
+        gdouble* wk = WSt + (size_t)MPCC_BCHK(c.bchk, k, NS, BC_WS_STAGE) * IS;
+        asm("" : "+v"(wk));
+        return wk + MPCC_BCHK(c.bchk, f, NWF, BC_WS_FIELD) * 16;
+    };
+    auto qs_stage = [&](int k) -> const gdouble* {
+        const gdouble* qk = QSb + (size_t)MPCC_BCHK(c.bchk, k, NS, BC_QS_STAGE) * QS;
+        asm("" : "+v"(qk));
+        return qk;
+    };
+    auto lds = [&](int off) -> double* { return smem + MPCC_BCHK(c.bchk, off, TL_END > TL_LM + 256 ? TL_END : TL_LM + 256, BC_LDS); };
+
+    // ---- model constants of this lane (as ipm_group)
+    const double m78 = c.M[7 * 9 + 8], m77 = c.M[7 * 10], m88 = c.M[8 * 10];
+    const double g77 = c.G[7 * 8 + 7], g87 = c.G[8 * 8 + 7];
+    double mt = 0.0, gt = 0.0, Hct = 0.0;
+    const double HcB = -2. * c.p.qp_r_ddq;
+    double mdiag[9], gdiag[7];
+#pragma unroll
+    for (int a = 0; a < 9; a++) {
+        mdiag[a] = c.M[a * 10];
+        if (t == a) mt = mdiag[a];
+    }
+#pragma unroll
+    for (int a = 0; a < 7; a++) {
+        gdiag[a] = c.G[a * 9];
+        if (t == a || t == 9 + a) {
+            gt = (t < 7) ? gdiag[a] : 0.0;
+            Hct = c.p.Tu[a] * HcB * c.p.Tu[a];
+        }
+    }
+    if (t == 7) gt = g77;
+    const bool rowY = t < 9;
+    const int j9 = t - 9;
+    constexpr double sgnL = -1.0, sgnU = 1.0;
+    const bool own = g == 0;  // the group that stores what all four groups computed redundantly (phases B, D)
+
+    // ---- stage loaders (ipm_group's, PACKP form)
+    auto load_common = [&](int k, In& o) {
+        const gdouble* q = qs_stage(k);
+        o.lb = q[rowY ? QS_YLB + t : QS_DLB + j9];
+        o.ub = q[rowY ? QS_YUB + t : QS_DUB + j9];
+        o.np = q[QS_NPOLY];
+        const int tp = t < 7 ? t : 0;
+#pragma unroll
+        for (int p = 0; p < NPE; p++) {
+            const double a = q[QS_POLY + 15 * p + tp], bv = q[QS_POLY + 15 * p + 7 + tp];
+            o.pa[p] = (NPM > 0 && t < 7) ? a : 0.0;
+            o.pb[p] = (NPM > 0 && t < 7) ? bv : 0.0;
+        }
+        const double pu = q[QS_POLY + 15 * (t < NPE ? t : 0) + 14];
+        o.pub = (t < NPM) ? pu : INF;
+        o.sL = *ws(k, WF_SL); o.lL = *ws(k, WF_LL); o.sU = *ws(k, WF_SU); o.lU = *ws(k, WF_LU);
+        o.zx = *ws(k, WF_ZX);
+        const double zraw = *ws(k, WF_ZV);
+        o.sP = from_up<8>(zraw);
+        o.lP = from_up<12>(zraw);
+        o.zv = (t < 8) ? zraw : 0.0;
+    };
+    auto load_factor = [&](int k, In& o, bool upd) {
+        load_common(k, o);
+        const gdouble* q = qs_stage(k);
+#pragma unroll
+        for (int m = 0; m < 9; m++) {
+            const double v = q[QS_Q + t * 9 + m];
+            o.m[m] = (t < 9) ? v : 0.0;
+        }
+        const double qv = q[QS_q + t], rv = q[QS_R + t], rr = q[QS_r + t];
+        o.m[9] = (t < 9) ? qv : 0.0;
+        o.m[10] = (t < 8 && k < N) ? rv : 0.0;
+        o.m[11] = (t < 8 && k < N) ? rr : 0.0;
+        const double x0 = *ws(k, WF_DX), x1 = *ws(k, WF_DV), x2 = *ws(k, WF_AX), x3 = *ws(k, WF_AV);
+        o.x0 = upd ? x0 : 0.0; o.x1 = upd ? x1 : 0.0; o.x2 = upd ? x2 : 0.0; o.x3 = upd ? x3 : 0.0;
+    };
+    auto load_fwd = [&](int k, In& o, bool corr) {
+        load_common(k, o);
+#pragma unroll
+        for (int m = 0; m < 8; m++) o.m[m] = *ws(k, WF_KR + m);
+        o.m[8] = from_up<8>(*ws(k, WF_GVK));
+        if (corr) {
+            o.x0 = *ws(k, WF_AX);
+            o.x1 = *ws(k, WF_AV);
+        } else {
+            o.x0 = o.x1 = 0.0;
+        }
+    };
+    auto load_bwd = [&](int k, In& o) {
+        load_common(k, o);
+        o.x0 = *ws(k, WF_AX); o.x2 = *ws(k, WF_GX);
+        o.x1 = *ws(k, WF_AV);
+        const double gvk = *ws(k, WF_GVK);
+        o.x3 = (t < 8) ? gvk : 0.0;
+#pragma unroll
+        for (int m = 0; m < 8; m++) o.m[m] = *ws(k, WF_KR + m);
+#pragma unroll
+        for (int m = 0; m < 4; m++) o.m[8 + m] = *ws(k, WF_FI + m);
+    };
+    auto store_slots = [&](int k, double sL, double lL, double sU, double lU, double sP, double lP, double zx, double zv) {
+        *ws(k, WF_SL) = sL; *ws(k, WF_LL) = lL; *ws(k, WF_SU) = sU; *ws(k, WF_LU) = lU;
+        *ws(k, WF_ZX) = zx;
+        const double s8 = from_down<8>(sP), l12 = from_down<12>(lP);
+        *ws(k, WF_ZV) = (t < 8) ? zv : ((t < 12) ? s8 : l12);
+    };
+
+    // ---- stage-local helpers (ipm_group's)
+    auto row_active = [&](int k, double bnd) { return (rowY ? (k >= 1) : (k < N)) && fabs(bnd) < BIG; };
+    auto row_cz = [&](int k, double x, double v) -> double {
+        const double vj = from_down<9>(v);
+        if (rowY) return x;
+        return (k == 0) ? vj : vj - x;
+    };
+    auto poly_cz = [&](const In& in, int k, double x, double v) -> double {
+        double r = 0.0;
+#pragma unroll
+        for (int p = 0; p < NPM; p++) {
+            const bool live = (double)p < in.np && k < N;
+            const double term = live ? in.pa[p] * x + in.pb[p] * v : 0.0;
+            const double s = g_sum(term);
+            if (t == p) r = s;
+        }
+        return r;
+    };
+    auto poly_slot_active = [&](const In& in, int k) {
+        return t < NPM && (double)t < in.np && k < N && fabs(in.pub) < BIG;
+    };
+    auto assemble_grad = [&](const In& in, int k, double g0x, double g0v, double dvr, double cP, double& gx, double& gv) {
+        gx = g0x;
+        if (t < 9) gx += dvr;
+        else if (k >= 1) gx -= dvr;
+        gv = g0v;
+        const double dv_up = from_up<9>(dvr);
+        if (t < 7 && k < N) gv += dv_up;
+#pragma unroll
+        for (int p = 0; p < NPM; p++) {
+            const double cp = bcn(cP, p);
+            const bool live = (double)p < in.np && k < N;
+            if (live) {
+                gx += cp * in.pa[p];
+                gv += cp * in.pb[p];
+            }
+        }
+    };
+    // forward step of the rollout from the K row halves + kff (m[0..8])
+    auto fwd_step = [&](const double* m, double xt, double& v, double& xn) {
+        double xb[16];
+#pragma unroll
+        for (int q = 0; q < 16; q++) xb[q] = bcn(xt, q);
+        double part = 0.0;
+#pragma unroll
+        for (int q = 0; q < 8; q++) part += m[q] * ((t < 8) ? xb[q] : xb[8 + q]);
+        v = part + from_up<8>(part) + m[8];
+        const double v7 = from_down<1>(v);
+        const double vj = from_down<9>(v);
+        if (t < 7) xn = mt * xt + gt * v;
+        else if (t == 7) xn = (m77 * xt + m78 * xb[8]) + g77 * v;
+        else if (t == 8) xn = m88 * xt + g87 * v7;
+        else xn = vj;
+    };
+    auto sync = [] { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); };
+    // slot j of an exchange area: lane t's fields at base + (j * 16 + t) * stride
+    auto xs = [&](int base, int j, int stride) -> double* { return lds(base + (j * 16 + t) * stride); };
+    // combine per-group values across the 4 groups (every lane gets groups 0..3 of its t, in order)
+    auto gather4 = [&](double v, double (&o)[4]) {
+        sync();
+        *lds(TL_LM + lane) = v;
+        sync();
+#pragma unroll
+        for (int q = 0; q < 4; q++) o[q] = *lds(TL_LM + q * 16 + t);
+        sync();
+    };
+    auto max4 = [&](double v) {
+        double o[4];
+        gather4(v, o);
+        return fmax(fmax(fmax(o[0], o[1]), o[2]), o[3]);
+    };
+
+#ifdef MPCC_IPM_PROF
+    long long tprof[16] = {0};
+    long long tprof_t = clock64();
+    const int it_in = io.it;
+#endif
+    int it = io.it;
+    const int max_it = io.max_it;
+    double mu0 = io.mu0, dz_prev = io.dz_prev, sigma_mu = io.sigma_mu, mu_cur = io.mu_cur, rp_cur = io.rp_cur;
+    double alpha = io.alpha;
+    double mcount = io.mcount;
+    bool pending = io.pending != 0, conv = false, diverged = false;
+    if (io.restart) {
+        // restart from the unit start point (attempt 1 of ipm_group): dynamics rollout with v = 0, s = max(-g, 1),
+        // lambda = 1, on all groups (the stores by one)
+        In cur, nxt;
+        double y = 0.0, bk = 0, bkn = 0;
+        mcount = 0.0;
+        load_common(0, cur);
+        bk = (N > 0 && t < 9) ? QSb[QS_B + t] : 0.0;
+        for (int k = 0; k <= N; k++) {
+            if (k < N) {
+                load_common(k + 1, nxt);
+                bkn = (k + 1 < N && t < 9) ? QSb[(size_t)(k + 1) * QS + QS_B + t] : 0.0;
+            }
+            const double yx = rowY ? y : 0.0;
+            const double cz = row_cz(k, yx, 0.0);
+            const double pcz = poly_cz(cur, k, yx, 0.0);
+            const bool aL = row_active(k, cur.lb), aU = row_active(k, cur.ub), aP = poly_slot_active(cur, k);
+            double sL = 1, lL = 0, sU = 1, lU = 0, sP = 1, lP = 0;
+            if (aL) { sL = fmax(-(sgnL * cz - sgnL * cur.lb), 1.0); lL = 1.0; }
+            if (aU) { sU = fmax(-(sgnU * cz - sgnU * cur.ub), 1.0); lU = 1.0; }
+            if (aP) { sP = fmax(-(sgnU * pcz - sgnU * cur.pub), 1.0); lP = 1.0; }
+            mcount += (aL ? 1.0 : 0.0) + (aU ? 1.0 : 0.0) + (aP ? 1.0 : 0.0);
+            if (own) store_slots(k, sL, lL, sU, lU, sP, lP, yx, 0.0);
+            const double y8 = from_up<1>(y);
+            const double yn = (t == 7) ? m77 * y + m78 * y8 : mt * y;
+            y = (t < 9) ? yn + bk : 0.0;
+            cur = nxt;
+            bk = bkn;
+        }
+        mcount = g_sum(mcount);
+    }
+
+    while (true) {
+        // ================= factorization sweep k = N..0 (blocks of 4 stages: kb, kb - 1, kb - 2, kb - 3)
+        double Pc[16];
+        double pv = 0.0;
+        bool chol_ok = true;
+#pragma unroll
+        for (int a = 0; a < 16; a++) Pc[a] = 0.0;
+        for (int kb = N; kb >= 0; kb -= 4) {
+            // ---- A: group g, stage kb - g: lazy update, slots, gradient, P-independent parts of F, Gm, Hb
+            {
+                const int kg = kb - g;
+                const bool vA = kg >= 0;
+                const int k = vA ? kg : 0;
+                In cur;
+                load_factor(k, cur, pending);
+                const double lb = cur.lb, ub = cur.ub;
+                const double* Qr = cur.m;
+                const double qt = cur.m[9], Rt = cur.m[10], rt = cur.m[11];
+                double sL = cur.sL, lL = cur.lL, sU = cur.sU, lU = cur.lU, sP = cur.sP, lP = cur.lP;
+                double zx = cur.zx, zv = cur.zv;
+                const bool aL = row_active(k, lb), aU = row_active(k, ub), aP = poly_slot_active(cur, k);
+                if (pending) {
+                    const double dx = cur.x0, dv = cur.x1, ax = cur.x2, av = cur.x3;
+                    const double cz = row_cz(k, zx, zv), cd = row_cz(k, dx, dv), ca = row_cz(k, ax, av);
+                    const double pcz = poly_cz(cur, k, zx, zv), pcd = poly_cz(cur, k, dx, dv), pca = poly_cz(cur, k, ax, av);
+                    double rpd;
+                    if (aL) { const SlotStep st = slot_corr(sgnL, lb, cz, ca, cd, sL, lL, sigma_mu, &rpd); sL += alpha * st.ds; lL += alpha * st.dl; }
+                    if (aU) { const SlotStep st = slot_corr(sgnU, ub, cz, ca, cd, sU, lU, sigma_mu, &rpd); sU += alpha * st.ds; lU += alpha * st.dl; }
+                    if (aP) { const SlotStep st = slot_corr(sgnU, cur.pub, pcz, pca, pcd, sP, lP, sigma_mu, &rpd); sP += alpha * st.ds; lP += alpha * st.dl; }
+                    zx += alpha * dx;
+                    zv += alpha * dv;
+                    if (vA) store_slots(k, sL, lL, sU, lU, sP, lP, zx, zv);
+                }
+                const double cz = row_cz(k, zx, zv);
+                const double pcz = poly_cz(cur, k, zx, zv);
+                double WL = 0, WU = 0, WP = 0, cL = 0, cU = 0, cP = 0;
+                if (aL) { const double rp = slot_rp(sgnL, cz, lb, sL); const double ri = rcp(sL); WL = lL * ri; cL = slot_coef(ri, lL, rp, sL * lL); }
+                if (aU) { const double rp = slot_rp(sgnU, cz, ub, sU); const double ri = rcp(sU); WU = lU * ri; cU = slot_coef(ri, lU, rp, sU * lU); }
+                if (aP) { const double rp = slot_rp(sgnU, pcz, cur.pub, sP); const double ri = rcp(sP); WP = lP * ri; cP = slot_coef(ri, lP, rp, sP * lP); }
+                const double wd = WL + WU;
+                const double dvr = sgnL * cL + sgnU * cU;
+                double g0x, g0v = 0.0;
+                {
+                    double zb[9];
+#pragma unroll
+                    for (int m = 0; m < 9; m++) zb[m] = bcn(zx, m);
+                    const double vj = from_down<9>(zv);
+                    const double wj = from_up<9>(zx);
+                    if (t < 9) {
+                        double s = 0;
+#pragma unroll
+                        for (int m = 0; m < 9; m++) s += Qr[m] * zb[m];
+                        g0x = s + qt;
+                    } else {
+                        g0x = (k >= 1 && k < N) ? Hct * vj : 0.0;
+                    }
+                    if (t < 8 && k < N) {
+                        double s = (k >= 1 && t < DOF) ? Hct * wj : 0.0;
+                        s += Rt * zv;
+                        g0v = s + rt;
+                    }
+                }
+                if (vA) *ws(k, WF_GX) = g0x;
+                double gx, gv;
+                assemble_grad(cur, k, g0x, g0v, dvr, cP, gx, gv);
+                const double wdv = from_up<9>(wd);
+                double hF[8], hG[8], hb9[9];
+#pragma unroll
+                for (int i = 0; i < 8; i++) {
+                    hF[i] = (i == t) ? Rt + ((t < 7) ? wdv : 0.0) : 0.0;
+                    hG[i] = 0.0;
+                }
+                double Wb[NPE];
+#pragma unroll
+                for (int p = 0; p < NPM; p++) {
+                    const bool live = (double)p < cur.np && k < N;
+                    const double wp = bcn(WP, p);
+                    Wb[p] = live ? wp : 0.0;
+#pragma unroll
+                    for (int i = 0; i < 7; i++) {
+                        const double bv = bcn(cur.pb[p], i);
+                        hF[i] += Wb[p] * (bv * cur.pb[p]);
+                        hG[i] += Wb[p] * (bv * cur.pa[p]);
+                    }
+                }
+                if (k == N) {
+                    // terminal stage: P = Hb_N (y block; Q row t as column t) into the hb9 slot; no gains
+#pragma unroll
+                    for (int a = 0; a < 9; a++) {
+                        double v = 0.0;
+                        if (t < 9) {
+                            v = Qr[a];
+                            if (a == t) v += wd;
+                        }
+                        hb9[a] = v;
+                    }
+                    if (vA) {
+#pragma unroll
+                        for (int m = 0; m < 8; m++) *ws(k, WF_KR + m) = 0.0;
+                        *ws(k, WF_GVK) = (t < 8) ? g0v : 0.0;
+#pragma unroll
+                        for (int m = 0; m < 4; m++) *ws(k, WF_FI + m) = 0.0;
+                    }
+                } else {
+                    // Hb base of rows a < 9: the q block with its poly terms (poly_hq), Q rows 7, 8 + the diagonal weight
+                    double hq[7];
+#pragma unroll
+                    for (int a = 0; a < 7; a++) {
+                        hq[a] = Qr[a];
+                        if (a == t) hq[a] += wd;
+                    }
+#pragma unroll
+                    for (int p = 0; p < NPM; p++) {
+                        const bool live = (double)p < cur.np && k < N;
+                        const double wp = bcn(WP, p);
+                        const double wb = live ? wp : 0.0;
+#pragma unroll
+                        for (int a = 0; a < 7; a++) {
+                            const double pa_ = bcn(cur.pa[p], a);
+                            hq[a] += wb * (pa_ * cur.pa[p]);
+                        }
+                    }
+#pragma unroll
+                    for (int a = 0; a < 9; a++) {
+                        double v;
+                        if (a < 7) {
+                            v = hq[a];
+                        } else {
+                            v = Qr[a];
+                            if (a == t) v += wd;
+                        }
+                        hb9[a] = v;
+                    }
+                }
+                const double gw = (k >= 1) ? Hct - wd : 0.0;
+#ifdef MPCC_IPM_DBGF
+                if (vA && k < N) { *ws(k, 35) = gx; *ws(k, 36) = gv; *ws(k, 39) = dvr; *ws(k, 40) = cP; *ws(k, 41) = wd; }
+#endif
+                double* o = xs(TL_A, g, TL_SA);
+                double2* o2 = reinterpret_cast<double2*>(o);
+                o2[0] = make_double2(gx, gv);
+                o2[1] = make_double2(g0v, wd);
+                o2[2] = make_double2(gw, hb9[8]);
+#pragma unroll
+                for (int i = 0; i < 4; i++) o2[3 + i] = make_double2(hF[2 * i], hF[2 * i + 1]);
+#pragma unroll
+                for (int i = 0; i < 4; i++) o2[7 + i] = make_double2(hG[2 * i], hG[2 * i + 1]);
+#pragma unroll
+                for (int i = 0; i < 4; i++) o2[11 + i] = make_double2(hb9[2 * i], hb9[2 * i + 1]);
+            }
+            sync();
+            TMARK(0);
+            // ---- B: the P recursion, stage after stage on all groups
+            for (int j = 0; j < 4; j++) {
+                const int k = kb - j;
+                if (k < 0) break;
+                const double2* a2 = reinterpret_cast<const double2*>(xs(TL_A, j, TL_SA));
+                const double2 x01 = a2[0], x23 = a2[1], x45 = a2[2];
+                const double gx = x01.x, wd = x23.y, gw = x45.x;
+                double hF[8], hG[8], hb9[9];
+#pragma unroll
+                for (int i = 0; i < 4; i++) {
+                    const double2 f = a2[3 + i], gg = a2[7 + i], h = a2[11 + i];
+                    hF[2 * i] = f.x; hF[2 * i + 1] = f.y;
+                    hG[2 * i] = gg.x; hG[2 * i + 1] = gg.y;
+                    hb9[2 * i] = h.x; hb9[2 * i + 1] = h.y;
+                }
+                hb9[8] = x45.y;
+                if (k == N) {
+#pragma unroll
+                    for (int a = 0; a < 16; a++) Pc[a] = (t < 9 && a < 9) ? hb9[a < 9 ? a : 0] : 0.0;
+                    pv = gx;
+                    continue;
+                }
+                // (1) Y = B~^T P (column t)
+                double Y[8];
+#pragma unroll
+                for (int i = 0; i < 7; i++) Y[i] = gdiag[i] * Pc[i] + Pc[9 + i];
+                Y[7] = g77 * Pc[7] + g87 * Pc[8];
+                // (2) F column t, Gm column t
+                double Fc[8], gm[8];
+#pragma unroll
+                for (int i = 0; i < 8; i++) {
+                    const double yu9 = from_up<9>(Y[i]);
+                    const double yu1 = from_up<1>(Y[i]);
+                    const double yd = from_down<1>(Y[i]);
+                    Fc[i] = hF[i] + (gt * Y[i] + ((t < 7) ? yu9 : g87 * yu1));
+                    gm[i] = hG[i] + (mt * Y[i] + ((t == 8) ? m78 * yd : 0.0));
+                }
+                TMARK(8);
+                // (3) chol(F), U = LF^-1 Gm
+                double LF[36], dinv[8];
+#pragma unroll
+                for (int i = 0; i < 8; i++)
+#pragma unroll
+                    for (int jj = 0; jj <= i; jj++) LF[i * (i + 1) / 2 + jj] = bcn(Fc[i], jj);
+                chol_ok = chol8(LF, dinv) && chol_ok;
+                TMARK(9);
+                double u[8];
+#pragma unroll
+                for (int i = 0; i < 8; i++) u[i] = (t < 9) ? gm[i] : ((i == j9) ? gw : 0.0);
+                fwd8(LF, dinv, u);
+#ifdef MPCC_IPM_DBGF
+                if (own) { *ws(k, 44) = Pc[0]; *ws(k, 45) = LF[35]; *ws(k, 46) = dinv[7]; *ws(k, 47) = u[0]; *ws(k, 49) = Y[0]; *ws(k, 50) = Fc[0]; }
+#endif
+                // hand L, its pivots and U to phase C
+                if (lane == 0) {
+                    double2* lf = reinterpret_cast<double2*>(lds(TL_LF + j * 48));
+#pragma unroll
+                    for (int q = 0; q < 18; q++) lf[q] = make_double2(LF[2 * q], LF[2 * q + 1]);
+#pragma unroll
+                    for (int q = 0; q < 4; q++) lf[18 + q] = make_double2(dinv[2 * q], dinv[2 * q + 1]);
+                }
+                {
+                    double2* uo = reinterpret_cast<double2*>(xs(TL_U, j, 10));
+#pragma unroll
+                    for (int q = 0; q < 4; q++) uo[q] = make_double2(u[2 * q], u[2 * q + 1]);
+                }
+                TMARK(10);
+                // (4) Hb column t and P = Hb - U^T U (column t), as ipm_group
+                double hb[16];
+                {
+                    double Pc7[9];
+#pragma unroll
+                    for (int a = 0; a < 9; a++) Pc7[a] = from_down<1>(Pc[a]);
+#pragma unroll
+                    for (int a = 0; a < 16; a++) {
+                        double v = 0.0;
+                        if (a < 9) {
+                            if (t < 9) {
+                                v = hb9[a];
+                                double mp = (mdiag[a] * mt) * Pc[a];
+                                if (t == 8) mp += (mdiag[a] * m78) * Pc7[a];
+                                if (a == 8) mp += (m78 * mt) * Pc[7];
+                                if (a == 8 && t == 8) mp += (m78 * m78) * Pc7[7];
+                                v += mp;
+                            }
+                        } else if (a == t) {
+                            v = wd;
+                        }
+                        hb[a] = v;
+                    }
+                }
+                TMARK(11);
+                if (k > 0) {
+                    double x[4][4], ua[4][1], ub[4][1];
+#pragma unroll
+                    for (int q = 0; q < 4; q++) {
+#pragma unroll
+                        for (int r = 0; r < 4; r++) x[q][r] = hb[q + 4 * r];
+                        ua[q][0] = u[q];
+                        ub[q][0] = u[4 + q];
+                    }
+                    group_transpose(x);
+                    group_transpose(ua);
+                    group_transpose(ub);
+#pragma unroll
+                    for (int q = 0; q < 4; q++) {
+                        d4 acc = {x[q][0], x[q][1], x[q][2], x[q][3]};
+                        acc = __builtin_amdgcn_mfma_f64_16x16x4f64(-ua[q][0], ua[q][0], acc, 0, 0, 0);
+                        acc = __builtin_amdgcn_mfma_f64_16x16x4f64(-ub[q][0], ub[q][0], acc, 0, 0, 0);
+#pragma unroll
+                        for (int r = 0; r < 4; r++) x[q][r] = acc[r];
+                    }
+                    group_transpose(x);
+#pragma unroll
+                    for (int q = 0; q < 4; q++)
+#pragma unroll
+                        for (int r = 0; r < 4; r++) Pc[q + 4 * r] = x[q][r];
+                }
+                TMARK(12);
+            }
+            sync();
+            TMARK(1);
+            // ---- C: group g, stage kb - g (< N): K = -LF^-T U, F^-1 column, the gain stores
+            {
+                const int kg = kb - g;
+                const bool vC = kg >= 0 && kg < N;
+                const double2* lf = reinterpret_cast<const double2*>(lds(TL_LF + g * 48));
+                double LF[36], dinv[8];
+#pragma unroll
+                for (int q = 0; q < 18; q++) { const double2 v = lf[q]; LF[2 * q] = v.x; LF[2 * q + 1] = v.y; }
+#pragma unroll
+                for (int q = 0; q < 4; q++) { const double2 v = lf[18 + q]; dinv[2 * q] = v.x; dinv[2 * q + 1] = v.y; }
+                double kc[8];
+                {
+                    const double2* ui = reinterpret_cast<const double2*>(xs(TL_U, g, 10));
+#pragma unroll
+                    for (int q = 0; q < 4; q++) { const double2 v = ui[q]; kc[2 * q] = v.x; kc[2 * q + 1] = v.y; }
+                }
+                bwd8(LF, dinv, kc);
+#pragma unroll
+                for (int i = 0; i < 8; i++) kc[i] = -kc[i];
+#ifdef MPCC_IPM_DBGF
+                if (vC) *ws(kg, 48) = kc[0];
+#endif
+                double fi[8];
+#pragma unroll
+                for (int i = 0; i < 8; i++) fi[i] = (i == (t & 7)) ? 1.0 : 0.0;
+                fwd8(LF, dinv, fi);
+                bwd8(LF, dinv, fi);
+                double* Sk = lds(TL_K + g * 144);
+#pragma unroll
+                for (int i = 0; i < 8; i++) Sk[i * 16 + t] = kc[i];
+                {
+                    double2* co = reinterpret_cast<double2*>(xs(TL_C, g, 18));
+#pragma unroll
+                    for (int q = 0; q < 4; q++) co[q] = make_double2(kc[2 * q], kc[2 * q + 1]);
+#pragma unroll
+                    for (int q = 0; q < 4; q++) co[4 + q] = make_double2(fi[2 * q], fi[2 * q + 1]);
+                }
+                sync();
+                const int ri = t & 7, hoff = (t < 8) ? 0 : 8;
+                const double2* row = reinterpret_cast<const double2*>(Sk + ri * 16 + hoff);
+#pragma unroll
+                for (int q2 = 0; q2 < 4; q2++) {
+                    const double2 w = row[q2];
+                    if (vC) {
+                        *ws(kg, WF_KR + 2 * q2) = w.x;
+                        *ws(kg, WF_KR + 2 * q2 + 1) = w.y;
+                    }
+                }
+                if (vC) {
+#pragma unroll
+                    for (int m = 0; m < 4; m++) *ws(kg, WF_FI + m) = (t < 8) ? fi[m] : fi[4 + m];
+                }
+            }
+            sync();
+            TMARK(2);
+            // ---- D: the p recursion, stage after stage (f = g_v + B~^T p, kff = -F^-1 f, p = g_x~ + A~^T p + K^T f)
+            for (int j = 0; j < 4; j++) {
+                const int k = kb - j;
+                if (k < 0) break;
+                if (k == N) continue;  // p_N = g_x~ (phase B)
+                const double2* a2 = reinterpret_cast<const double2*>(xs(TL_A, j, TL_SA));
+                const double2 x01 = a2[0], x23 = a2[1];
+                const double gx = x01.x, gv = x01.y, g0v = x23.x;
+                const double2* ci = reinterpret_cast<const double2*>(xs(TL_C, j, 18));
+                double kc[8], fi[8];
+#pragma unroll
+                for (int q = 0; q < 4; q++) {
+                    const double2 a = ci[q], f = ci[4 + q];
+                    kc[2 * q] = a.x; kc[2 * q + 1] = a.y;
+                    fi[2 * q] = f.x; fi[2 * q + 1] = f.y;
+                }
+                const double pu9 = from_up<9>(pv), pu1 = from_up<1>(pv);
+                const double fv = gv + gt * pv + ((t < 7) ? pu9 : g87 * pu1);
+                double fb[8];
+#pragma unroll
+                for (int i = 0; i < 8; i++) fb[i] = bcn(fv, i);
+                double kff = 0.0;
+#pragma unroll
+                for (int m = 0; m < 8; m++) kff -= fi[m] * fb[m];
+                double pnew;
+                {
+                    double atp = 0.0;
+                    const double p7 = from_down<1>(pv);
+                    if (t < 9) {
+                        atp = mt * pv;
+                        if (t == 8) atp += m78 * p7;
+                    }
+                    double ktf = 0.0;
+#pragma unroll
+                    for (int i = 0; i < 8; i++) ktf += kc[i] * fb[i];
+                    pnew = gx + atp + ktf;
+                }
+                const double kffd = from_down<8>(kff);
+                if (own) *ws(k, WF_GVK) = (t < 8) ? g0v : kffd;
+#ifdef MPCC_IPM_DBGF
+                if (own) { *ws(k, 37) = pv; *ws(k, 38) = fv; *ws(k, 42) = pnew; *ws(k, 43) = kff; }
+#endif
+                pv = pnew;
+            }
+            sync();
+            TMARK(3);
+        }
+        if (!chol_ok) {
+            conv = it > 0 && mu_cur < IPM_TOL_FB && rp_cur < IPM_TOL_FB;
+            alpha = 0.0;
+            break;
+        }
+
+        // ================= predictor forward: x~_0 = 0; recover dsa, dla; max step; mu(alpha) sums
+        double S0 = 0, S1 = 0, S2 = 0;
+        MinRatio amr(1.0);
+        double xt = 0.0;
+        // forward light sweep in blocks k = kb + j: A loads (and exports the gains), B rolls x~ out, C does the slot
+        // algebra of its stage (body), D accumulates the sums in stage order (acc)
+        auto fwd_sweep = [&](bool corr, auto body, auto acc) {
+            for (int kb = 0; kb <= N; kb += 4) {
+                const int kg = kb + g;
+                const bool vA = kg <= N;
+                const int k = vA ? kg : N;
+                In cur;
+                load_fwd(k, cur, corr);
+                {
+                    double* o = xs(TL_LA, g, 18);
+                    double2* o2 = reinterpret_cast<double2*>(o);
+#pragma unroll
+                    for (int q = 0; q < 4; q++) o2[q] = make_double2(cur.m[2 * q], cur.m[2 * q + 1]);
+                    o[8] = cur.m[8];
+                }
+                sync();
+                if (!corr) TMARK(13);
+                for (int j = 0; j < 4; j++) {
+                    const int kk = kb + j;
+                    if (kk > N) break;
+                    const double* mi = xs(TL_LA, j, 18);
+                    double m[9];
+#pragma unroll
+                    for (int q = 0; q < 9; q++) m[q] = mi[q];
+                    double v = 0.0, xn = 0.0;
+                    if (kk < N) fwd_step(m, xt, v, xn);
+                    const double dvv = (t < 8 && kk < N) ? v : 0.0;
+                    *reinterpret_cast<double2*>(xs(TL_LB, j, 2)) = make_double2(xt, dvv);
+                    xt = xn;
+                }
+                sync();
+                if (!corr) TMARK(14);
+                {
+                    const double2 xv = *reinterpret_cast<const double2*>(xs(TL_LB, g, 2));
+                    double rr[14];
+                    body(k, vA, cur, xv.x, xv.y, rr);
+                    double2* o2 = reinterpret_cast<double2*>(xs(TL_LC, g, 14));
+#pragma unroll
+                    for (int q = 0; q < 7; q++) o2[q] = make_double2(rr[2 * q], rr[2 * q + 1]);
+                }
+                sync();
+                if (!corr) TMARK(15);
+                for (int j = 0; j < 4; j++) {
+                    if (kb + j > N) break;
+                    const double2* r2 = reinterpret_cast<const double2*>(xs(TL_LC, j, 14));
+                    double rr[14];
+#pragma unroll
+                    for (int q = 0; q < 7; q++) { const double2 v = r2[q]; rr[2 * q] = v.x; rr[2 * q + 1] = v.y; }
+                    acc(rr);
+                }
+                sync();
+            }
+        };
+        fwd_sweep(false, [&](int k, bool vA, const In& cur, double xt_k, double dvv, double (&rr)[14]) {
+            const bool aL = row_active(k, cur.lb), aU = row_active(k, cur.ub), aP = poly_slot_active(cur, k);
+            if (vA) { *ws(k, WF_AX) = xt_k; *ws(k, WF_AV) = dvv; }
+            const double cz = row_cz(k, cur.zx, cur.zv), ca = row_cz(k, xt_k, dvv);
+            const double pcz = poly_cz(cur, k, cur.zx, cur.zv), pca = poly_cz(cur, k, xt_k, dvv);
+            MinRatio loc(1.0);  // this stage's candidates; merged in stage order in D (strict <: the sequential scan)
+            auto rec = [&](bool a, double sgn, double bnd, double czz, double caa, double s, double l, int r) {
+                double ds = 0.0, dl = 0.0, sv = 0.0, lv = 0.0;
+                if (a && vA) {
+                    const double rp = slot_rp(sgn, czz, bnd, s);
+                    const SlotStep st = slot_recover(rcp(s), l, rp, sgn * caa, s * l);
+                    step_bound(loc, s, l, st);
+                    sv = s; lv = l; ds = st.ds; dl = st.dl;
+                }
+                rr[4 * r] = sv; rr[4 * r + 1] = lv; rr[4 * r + 2] = ds; rr[4 * r + 3] = dl;
+            };
+            rec(aL, sgnL, cur.lb, cz, ca, cur.sL, cur.lL, 0);
+            rec(aU, sgnU, cur.ub, cz, ca, cur.sU, cur.lU, 1);
+            rec(aP, sgnU, cur.pub, pcz, pca, cur.sP, cur.lP, 2);
+            rr[12] = loc.num;
+            rr[13] = loc.den;
+        }, [&](const double (&rr)[14]) {
+#pragma unroll
+            for (int r = 0; r < 3; r++) {
+                const double s = rr[4 * r], l = rr[4 * r + 1], ds = rr[4 * r + 2], dl = rr[4 * r + 3];
+                mu_acc(S0, S1, S2, s, l, ds, dl);
+            }
+            amr.add(rr[12], -rr[13]);
+        });
+        const double amax = g_min(amr.value());
+        S0 = g_sum(S0); S1 = g_sum(S1); S2 = g_sum(S2);
+        const double mu = (mcount > 0) ? S0 / mcount : 0.0;
+        if (it == 0) mu0 = mu;
+        double mua = S0 + amax * S1 + amax * amax * S2;
+        mua = (mcount > 0) ? mua / mcount : 0.0;
+        const double ratio = (mu > 0) ? mua / mu : 0.0;
+        const double sigma = (mu > 0) ? ratio * ratio * ratio : 0.0;
+        const double smu = sigma * mu;
+        TMARK(4);
+
+        // ================= corrector backward: A coefficients and gradients (4 stages), B the p recursion
+        {
+            double pvc = 0.0;
+            for (int kb = N; kb >= 0; kb -= 4) {
+                {
+                    const int kg = kb - g;
+                    const bool vA = kg >= 0;
+                    const int k = vA ? kg : 0;
+                    In cur;
+                    load_bwd(k, cur);
+                    const bool aL = row_active(k, cur.lb), aU = row_active(k, cur.ub), aP = poly_slot_active(cur, k);
+                    const double cz = row_cz(k, cur.zx, cur.zv), ca = row_cz(k, cur.x0, cur.x1);
+                    const double pcz = poly_cz(cur, k, cur.zx, cur.zv);
+                    const double pca = poly_cz(cur, k, cur.x0, cur.x1);
+                    auto coef = [&](bool a, double sgn, double bnd, double czz, double caa, double s, double l) -> double {
+                        if (!a) return 0.0;
+                        const double rp = slot_rp(sgn, czz, bnd, s);
+                        const double ri = rcp(s);
+                        const SlotStep pa = slot_recover(ri, l, rp, sgn * caa, s * l);
+                        const double rc = s * l + pa.ds * pa.dl - smu;
+                        return slot_coef(ri, l, rp, rc);
+                    };
+                    const double cL = coef(aL, sgnL, cur.lb, cz, ca, cur.sL, cur.lL);
+                    const double cU = coef(aU, sgnU, cur.ub, cz, ca, cur.sU, cur.lU);
+                    const double cP = coef(aP, sgnU, cur.pub, pcz, pca, cur.sP, cur.lP);
+                    const double dvr = sgnL * cL + sgnU * cU;
+                    double gx, gv;
+                    assemble_grad(cur, k, cur.x2, cur.x3, dvr, cP, gx, gv);
+                    double2* o2 = reinterpret_cast<double2*>(xs(TL_LA, g, 18));
+                    o2[0] = make_double2(gx, gv);
+#pragma unroll
+                    for (int q = 0; q < 6; q++) o2[1 + q] = make_double2(cur.m[2 * q], cur.m[2 * q + 1]);
+                }
+                sync();
+                for (int j = 0; j < 4; j++) {
+                    const int k = kb - j;
+                    if (k < 0) break;
+                    const double2* a2 = reinterpret_cast<const double2*>(xs(TL_LA, j, 18));
+                    const double2 gg = a2[0];
+                    const double gx = gg.x, gv = gg.y;
+                    if (k == N) {
+                        pvc = gx;
+                        continue;
+                    }
+                    double m[12];
+#pragma unroll
+                    for (int q = 0; q < 6; q++) { const double2 v = a2[1 + q]; m[2 * q] = v.x; m[2 * q + 1] = v.y; }
+                    const double pu9 = from_up<9>(pvc), pu1 = from_up<1>(pvc);
+                    const double fv = gv + gt * pvc + ((t < 7) ? pu9 : g87 * pu1);
+                    double fb[8];
+#pragma unroll
+                    for (int i = 0; i < 8; i++) fb[i] = bcn(fv, i);
+                    double part = 0.0;
+#pragma unroll
+                    for (int q = 0; q < 4; q++) part -= m[8 + q] * ((t < 8) ? fb[q] : fb[4 + q]);
+                    const double kff = part + from_up<8>(part);
+                    const double kffd = from_down<8>(kff);
+                    if (own && t >= 8) *ws(k, WF_GVK) = kffd;
+                    double atp = 0.0;
+                    const double p7 = from_down<1>(pvc);
+                    if (t < 9) {
+                        atp = mt * pvc;
+                        if (t == 8) atp += m78 * p7;
+                    }
+                    const double f8 = rot16<8>(fv);
+                    const double fh = (t < 8) ? fv : f8;
+                    double r1[4], r2[2];
+#pragma unroll
+                    for (int q = 0; q < 4; q++) {
+                        const bool lo = (t & 4) == 0;
+                        const double a0 = m[q] * fh, a1 = m[4 + q] * fh;
+                        r1[q] = (lo ? a0 : a1) + half_mirror(lo ? a1 : a0);
+                    }
+#pragma unroll
+                    for (int q = 0; q < 2; q++) {
+                        const bool lo = (t & 2) == 0;
+                        r2[q] = (lo ? r1[q] : r1[2 + q]) + quad_swap2(lo ? r1[2 + q] : r1[q]);
+                    }
+                    const bool lo1 = (t & 1) == 0;
+                    const double ktf = (lo1 ? r2[0] : r2[1]) + quad_swap1(lo1 ? r2[1] : r2[0]);
+                    pvc = gx + atp + ktf;
+                }
+                sync();
+            }
+        }
+
+        TMARK(5);
+        // ================= corrector forward: dz, ds, dl, max step, mu(alpha) sums, max |rp|, max |dz|
+        double T0 = 0, T1 = 0, T2 = 0, rpm = 0, dzm = 0;
+        MinRatio amc(1e30);
+        xt = 0.0;
+        fwd_sweep(true, [&](int k, bool vA, const In& cur, double xt_k, double dvv, double (&rr)[14]) {
+            const bool aL = row_active(k, cur.lb), aU = row_active(k, cur.ub), aP = poly_slot_active(cur, k);
+            if (vA) {
+                *ws(k, WF_DX) = xt_k;
+                *ws(k, WF_DV) = dvv;
+                dzm = fmax(dzm, fmax(fabs(xt_k), fabs(dvv)));
+            }
+            const double cz = row_cz(k, cur.zx, cur.zv), cd = row_cz(k, xt_k, dvv), ca = row_cz(k, cur.x0, cur.x1);
+            const double pcz = poly_cz(cur, k, cur.zx, cur.zv), pcd = poly_cz(cur, k, xt_k, dvv);
+            const double pca = poly_cz(cur, k, cur.x0, cur.x1);
+            MinRatio loc(1e30);
+            auto rec = [&](bool a, double sgn, double bnd, double czz, double caa, double cdd, double s, double l, int r) {
+                double ds = 0.0, dl = 0.0, sv = 0.0, lv = 0.0;
+                if (a && vA) {
+                    double rp;
+                    const SlotStep st = slot_corr(sgn, bnd, czz, caa, cdd, s, l, smu, &rp);
+                    step_bound(loc, s, l, st);
+                    rpm = fmax(rpm, fabs(rp));
+                    sv = s; lv = l; ds = st.ds; dl = st.dl;
+                }
+                rr[4 * r] = sv; rr[4 * r + 1] = lv; rr[4 * r + 2] = ds; rr[4 * r + 3] = dl;
+            };
+            rec(aL, sgnL, cur.lb, cz, ca, cd, cur.sL, cur.lL, 0);
+            rec(aU, sgnU, cur.ub, cz, ca, cd, cur.sU, cur.lU, 1);
+            rec(aP, sgnU, cur.pub, pcz, pca, pcd, cur.sP, cur.lP, 2);
+            rr[12] = loc.num;
+            rr[13] = loc.den;
+        }, [&](const double (&rr)[14]) {
+#pragma unroll
+            for (int r = 0; r < 3; r++) {
+                const double s = rr[4 * r], l = rr[4 * r + 1], ds = rr[4 * r + 2], dl = rr[4 * r + 3];
+                mu_acc(T0, T1, T2, s, l, ds, dl);
+            }
+            amc.add(rr[12], -rr[13]);
+        });
+        rpm = max4(rpm);
+        dzm = max4(dzm);
+        const double amx = g_min(amc.value());
+        T0 = g_sum(T0); T1 = g_sum(T1); T2 = g_sum(T2);
+        rpm = g_max(rpm);
+        dzm = g_max(dzm);
+        alpha = fmin(1.0, fmax(IPM_TAU, 1.0 - sqrt(mu)) * amx);
+        sigma_mu = smu;
+        pending = true;
+        it++;
+        TMARK(6);
+        if (it < max_it) {
+            double mun = T0 + alpha * T1 + alpha * alpha * T2;
+            mun = (mcount > 0) ? mun / mcount : 0.0;
+            const double rpn = (1.0 - alpha) * rpm;
+            mu_cur = mun;
+            rp_cur = rpn;
+            const bool step_ok = dzm < IPM_TOL_STEP || dzm * dzm < IPM_TOL_STEP * dz_prev;
+            dz_prev = dzm;
+            if (mun < IPM_TOL_MU && rpn < IPM_TOL_P && step_ok) {
+                conv = true;
+                break;
+            } else if (mun > IPM_DIV * mu0) {
+                diverged = true;
+                break;
+            }
+        } else {
+            break;
+        }
+    }
+#ifdef MPCC_IPM_PROF
+    if (lane == 0) {
+        for (int i = 0; i < 16; i++) if (i != 7) atomicAdd(&g_tail_prof[i], (unsigned long long)tprof[i]);
+        atomicAdd(&g_tail_prof[7], (unsigned long long)(it - it_in));
+    }
+#endif
+    io.it = it;
+    io.conv = conv ? 1 : 0;
+    io.diverged = diverged ? 1 : 0;
+    io.alpha = alpha;
+}
+
+// The rest of a QP solve handed over by ipm_group (its iteration state in LDS at TL_STATE): the remaining
+// iterations of the current attempt, the restart from the unit start point if that attempt fails, and ipm_group's
+// epilogue (iteration count, QP status, step).
+template <int NPM>
+__device__ __attribute__((noinline)) void ipm_tail_solve(const DevConst& c, const DevBuffers& d, double* smem) {
+    if (threadIdx.x == 0) atomicAdd(&g_tail_solves, 1ull);  // tail-mode hand-overs (mpcc_debug_tail_solves)
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    const double* st = smem + TL_STATE;
+    TailIO io;
+    io.it = (int)st[0];
+    io.max_it = (int)st[1];
+    io.pending = (int)st[2];
+    const int attempt = (int)st[3];
+    int it_total = (int)st[4];
+    io.mu0 = st[5]; io.dz_prev = st[6]; io.sigma_mu = st[7]; io.mu_cur = st[8]; io.rp_cur = st[9]; io.alpha = st[10];
+    io.mcount = st[11];
+    const int gs = (int)st[12];
+    io.conv = io.diverged = io.restart = 0;
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    ipm_tail<NPM>(c, d, smem, gs, io);
+    it_total += io.it;
+    if (!io.conv && attempt == 0 && IPM_ATTEMPTS > 1) {
+        io.it = 0; io.max_it = IPM_MAX_IT; io.pending = 0; io.conv = 0; io.diverged = 0; io.restart = 1;
+        io.mu0 = 0.0; io.dz_prev = 1e30; io.sigma_mu = 0.0; io.mu_cur = 1e30; io.rp_cur = 1e30; io.alpha = 0.0;
+        io.mcount = 0.0;
+        ipm_tail<NPM>(c, d, smem, gs, io);
+        it_total += io.it;
+    }
+    const int lane = threadIdx.x, t = lane & 15;
+    const int b = blockIdx.x * IPW + gs;
+    const int N = c.N, NS = N + 1;
+    int32_t* si = d.sqi + (size_t)b * SQI;
+#ifdef MPCC_IPM_PROF
+    if (lane == 0 && b < 4 * PROF_WAVES) g_inst_its[b] += it_total;
+#endif
+    if (lane == 0) si[SQ_IPMIT] = it_total;
+    if (!io.conv) {  // keep the previous step (Q6)
+        if (lane == 0) si[SQ_QPSTAT] = io.diverged ? MPCC_QP_PrimalInfeasible : MPCC_QP_MaxIterReached;
+        return;
+    }
+    if (lane == 0) si[SQ_QPSTAT] = 0;
+    if (lane >= 16) return;
+    const gdouble* W = (const gdouble*)(d.is + (size_t)b * NS * IS) + t;
+    gdouble* stp = (gdouble*)(d.step + (size_t)b * NS * 17);
+    const double alpha = io.alpha;
+    for (int k = 0; k <= N; k++) {
+        const gdouble* wk = W + (size_t)k * IS;
+        const double zx = wk[WF_ZX * 16] + alpha * wk[WF_DX * 16];
+        const double zv = wk[WF_ZV * 16] + alpha * wk[WF_DV * 16];  // lanes < 8
+        if (t < 9) stp[k * 17 + t] = zx;
+        if (t < 8) stp[k * 17 + 9 + t] = (k < N) ? zv : 0.0;
+    }
+}

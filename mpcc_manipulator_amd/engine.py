@@ -180,6 +180,7 @@ def lib(dof=7):
         "mpcc_mlp_destroy": (None, [V]),
         "mpcc_robot_frames": (C.c_int, [C.c_int, C.c_int, DP, C.c_int, DP, DP, DP, DP, DP]),
         "mpcc_debug_bounds": (C.c_int, [V, C.POINTER(C.c_uint32), C.c_int]),
+        "mpcc_debug_tail_solves": (C.c_int, [C.POINTER(C.c_longlong), C.c_int]),
         "mpcc_build_id": (C.c_char_p, []),
         "mpcc_build_flags": (C.c_int, []),
         "mpcc_timing_mlp": (C.c_int, [V, C.POINTER(D), IP, C.POINTER(D), IP]),
@@ -665,6 +666,12 @@ class Engine:
         out = np.zeros(M)
         self._check(self.L.mpcc_debug_project(self.h, M, _dp(sg), _dp(e), _dp(out)), "mpcc_debug_project")
         return out
+
+    def tail_solves(self, reset=True):
+        """QP solves finished in tail mode (csrc/ipm_tail.h) since the last reset, over the whole process."""
+        v = C.c_longlong()
+        self._check(self.L.mpcc_debug_tail_solves(C.byref(v), 1 if reset else 0), "mpcc_debug_tail_solves")
+        return int(v.value)
 
     def bounds_flags(self, clear=True):
         """Bounds-checked build (MPCC_BOUNDS_CHECK): OR of the index-violation bits recorded by every kernel since

@@ -1,0 +1,98 @@
+"""Tail mode of the fused interior point (csrc/ipm_tail.h): the last running instance of a wave
+takes all four 16-lane groups.  It computes the same expressions in the same order as the normal path, so every
+output must be bitwise the MPCC_TAIL=0 engine's; the runs must also have used it.  Reference: the QP solve it
+belongs to replaces OSQP inside solveOCP (osqp_interface.cpp:398-590)."""
+import os
+
+import numpy as np
+import pytest
+
+from helpers import batch_from_pool, make_oracle
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+SEED = 0x4D504343
+
+
+def _bench_pool():
+    f = np.load(os.path.join(ROOT, "mpcc_manipulator_amd", "data", "bench_pool_n20_mask2.npz"), allow_pickle=False)
+    return {k: f[k] for k in f.files}
+
+
+def _solve(monkeypatch, tail, params, mask, track, batch, staged=False):
+    import mpcc_manipulator_amd as m
+    monkeypatch.setenv("MPCC_TAIL", "1" if tail else "0")
+    if staged:
+        monkeypatch.setenv("MPCC_STAGED_SQP", "1")
+    x0, u0, obs, guess, valid, fails = batch
+    B = x0.shape[0]
+    eng = m.Engine(params, max_batch=B, constraint_mask=mask)
+    eng.set_track(*track)
+    eng.tail_solves(reset=True)
+    eng.set_warmstart(guess, valid, fails)
+    x = x0.copy()
+    out = eng.solve(x, u0, obs)
+    n_tail = eng.tail_solves(reset=True)
+    ws = eng.get_warmstart(B)
+    st = eng.solve_stats(B)
+    eng.close()
+    return x, out, ws, st, n_tail
+
+
+def _assert_bitwise(a, b):
+    xa, oa, wa, sa, _ = a
+    xb, ob, wb, sb, _ = b
+    assert np.array_equal(xa.view(np.int64), xb.view(np.int64))
+    for k in oa:
+        assert np.array_equal(np.asarray(oa[k]).view(np.uint8), np.asarray(ob[k]).view(np.uint8)), k
+    for u, v in zip(wa, wb):
+        assert np.array_equal(np.asarray(u).view(np.uint8), np.asarray(v).view(np.uint8))
+    for k in sa:
+        assert np.array_equal(sa[k], sb[k]), k
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("mask,B,qnoise,soc,staged", [
+    (2, 4096, 0.005, 0, False),   # configs[1], the bench pool and noise
+    (2, 1024, 0.02, 0, False),    # filter rejections, restarts
+    (2, 512, 0.005, 1, False),    # second-order correction: two QPs per SQP iteration
+    (2, 512, 0.005, 0, True),     # staged path (k_ipm)
+    (0, 512, 0.005, 0, False),    # no polytopic row
+    (3, 512, 0.005, 0, False),    # self collision + singularity: two polytopic rows
+])
+def test_tail_mode_bitwise(built_lib, monkeypatch, mask, B, qnoise, soc, staged):
+    import mpcc_manipulator_amd as m
+    ov = {"sqp": {"max_iter": 2, "do_SOC": soc}}
+    params = m.load_params(N=20, overrides=ov)
+    eng = m.Engine(params, max_batch=1, constraint_mask=mask)
+    X, Y, Z, q = m.load_default_track()
+    ee = eng.robot_records(np.array([[0, 0, 0, -np.pi / 2, 0, np.pi / 2, np.pi / 4]]), np.array([[3.0, 3.0, 3.0, 0.0]]))[0, :3]
+    eng.close()
+    track = m.track_from_points(X, Y, Z, q, ee)
+    rng = np.random.default_rng(SEED + 41)
+    batch = batch_from_pool(_bench_pool(), B, rng, qnoise=qnoise)
+    on = _solve(monkeypatch, True, params, mask, track, batch, staged)
+    off = _solve(monkeypatch, False, params, mask, track, batch, staged)
+    assert off[4] == 0
+    assert on[4] > 0, "tail mode was not used"
+    _assert_bitwise(on, off)
+
+
+@pytest.mark.gpu
+def test_tail_mode_against_oracle(built_lib, oracle_lib, monkeypatch):
+    """The instances that finished in tail mode (the cold-started ones of the bench pool, two QPs) against the
+    oracle: status exact, inputs <= 1e-6 (north star), x0 update <= 1e-9."""
+    import mpcc_manipulator_amd as m
+    o, P, track = make_oracle(N=20, max_iter=2, mask=2, nthreads=16)
+    params = m.load_params(N=20, overrides={"sqp": {"max_iter": 2}})
+    pool = _bench_pool()
+    rng = np.random.default_rng(SEED + 43)
+    x0, u0, obs, guess, valid, fails = batch_from_pool(pool, 2048, rng, qnoise=0.005)
+    xg, outg, (gg, vg, fg), st, n_tail = _solve(monkeypatch, True, params, 2, track, (x0, u0, obs, guess, valid, fails))
+    assert n_tail > 0
+    xo, go, vo, fo = x0.copy(), guess.copy(), valid.copy(), fails.copy()
+    outo = o.run_mpc(xo, u0, obs, go, vo, fo)
+    assert np.array_equal(outg["status"], outo["status"])
+    assert np.abs(outg["horizon"][:, :-1, 9:] - outo["horizon"][:, :-1, 9:]).max() <= 1e-6
+    assert np.abs(xg - xo).max() <= 1e-9
+    assert np.array_equal(vg, vo) and np.array_equal(fg, fo)
+    o.close()

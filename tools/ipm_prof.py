@@ -45,6 +45,8 @@ def main():
             if rep == 2 and prof:
                 buf = (C.c_ulonglong * 16)()
                 prof(buf, 1)
+                if getattr(L, "mpcc_debug_tail_prof", None):
+                    L.mpcc_debug_tail_prof((C.c_ulonglong * 16)(), 1)
             eng.timing_begin()
             out = eng.solve(*[a.copy() for a in args_])
             tm, ncalls, nipm = eng.timing_end()
@@ -56,6 +58,15 @@ def main():
             res["instances"] = n_inst
             res["ipm_iters"] = n_it
             res["kcycles_per_iter"] = {s: round(buf[i] / max(1, n_it) / 1e3, 2) for i, s in enumerate(SECTIONS) if s != "-"}
+        tp = getattr(L, "mpcc_debug_tail_prof", None)
+        if tp:
+            tb = (C.c_ulonglong * 16)()
+            tp(tb, 1)
+            nt = max(1, tb[7])
+            res["tail_iters"] = int(tb[7])
+            res["tail_kcycles_per_iter"] = {s: round(tb[i] / nt / 1e3, 2) for i, s in enumerate(
+                ["f_A", "f_B_rest", "f_C", "f_D", "pred_fwd", "corr_bwd", "corr_fwd", "-", "fB_Y_F_Gm", "fB_chol",
+                 "fB_u_export", "fB_hb", "fB_P"]) if s != "-"}
         print(json.dumps(res), flush=True)
         eng.close()
 

@@ -125,6 +125,7 @@ class Track:
         R = [[list(map(float, r[3 * i:3 * i + 3])) for i in range(3)] if len(np.shape(r)) == 1 else
              [list(map(float, row)) for row in r] for r in R]
         path, self.fin = sr.gen6d(list(map(float, X)), list(map(float, Y)), list(map(float, Z)), R)
+        self.path = path  # the final regular path data (s, X, Y, Z, R): projectOnSpline's far branch reads it
         self.length = path[0][-1]
 
     def ref(self, s):
@@ -441,21 +442,44 @@ def solve_dense(H, q, A, lo, hi, tol=1e-13, max_it=100):
         a = min(1.0, 0.995 * _max_step(w, dw), 0.995 * _max_step(z, dz))
         s, y, w, z = s + a * ds, y + a * dy, w + a * dw, z + a * dz
     info = dict(ipm_iters=it, mu=float(w.dot(z) / m), polished=False)
-    # polish: the equality-constrained QP of the active set (z > w), accepted if it satisfies the KKT conditions
+    # polish: the equality-constrained QP of the active set (z > w), accepted if it satisfies the KKT conditions;
+    # when it does not (an interior point that stalled before identifying the active set), primal-dual active-set
+    # steps from there (act <- {z + (G s - h) > 0}, the semismooth Newton iteration of the complementarity
+    # conditions) until the KKT conditions hold
     act = z > w
-    Ea = np.vstack([E, G[act]])
-    ea = np.concatenate([e, h[act]])
-    ka = Ea.shape[0]
-    K = np.zeros((n + ka, n + ka))
-    K[:n, :n] = H; K[:n, n:] = Ea.T; K[n:, :n] = Ea
-    sol = np.linalg.lstsq(K, np.concatenate([-q, ea]), rcond=None)[0]
-    sp, lam = sol[:n], sol[n:]
-    za = lam[me:]
-    feas = (G @ sp - h).max() if m else 0.0
-    stat = np.abs(H @ sp + q + Ea.T @ lam).max()
-    if feas <= 1e-11 and (za.min() if za.size else 0.0) >= -1e-11 and stat <= 1e-10:
-        info.update(polished=True, max_step_change=float(np.abs(sp - s).max()))
-        s = sp
+
+    def eqp(act):
+        Ea = np.vstack([E, G[act]])
+        ea = np.concatenate([e, h[act]])
+        ka = Ea.shape[0]
+        K = np.zeros((n + ka, n + ka))
+        K[:n, :n] = H; K[:n, n:] = Ea.T; K[n:, :n] = Ea
+        rhs = np.concatenate([-q, ea])
+        sol = np.linalg.lstsq(K, rhs, rcond=None)[0]
+        for _ in range(2):  # iterative refinement of the (ill-conditioned) KKT solve
+            sol = sol + np.linalg.lstsq(K, rhs - K @ sol, rcond=None)[0]
+        sp, lam = sol[:n], sol[n:]
+        return sp, lam, Ea
+    stat = None
+    hs = 1.0 + (np.abs(h).max() if m else 0.0)      # scales of the feasibility and stationarity tests
+    ss = 1.0 + np.abs(q).max() + np.abs(H).max()
+    for pd in range(40):
+        sp, lam, Ea = eqp(act)
+        za = lam[me:]
+        feas = (G @ sp - h).max() if m else 0.0
+        stat = np.abs(H @ sp + q + Ea.T @ lam).max()
+        if os.environ.get("QPR_DEBUG"):
+            print("pdas", pd, int(act.sum()), feas, za.min() if za.size else 0.0, stat)
+        if feas <= 1e-11 * hs and (za.min() if za.size else 0.0) >= -1e-11 and stat <= 1e-12 * ss:
+            info.update(polished=True, max_step_change=float(np.abs(sp - s).max()), active_set_steps=pd)
+            s = sp
+            break
+        zf = np.zeros(m)
+        zf[act] = za
+        nxt = (zf + (G @ sp - h)) > 0
+        if np.array_equal(nxt, act):
+            break
+        act = nxt
     info.update(kkt_stationarity=float(np.abs(H @ s + q + E.T @ y + G.T @ z).max()) if not info["polished"] else float(stat),
                 primal_violation=float(max((G @ s - h).max() if m else 0.0, np.abs(E @ s - e).max() if me else 0.0)),
                 active=int(act.sum()))
