@@ -62,12 +62,14 @@ def find_traffic(kname, B, N, mask, dof, override=None, prof_dir=None):
 
 
 def pmc_fp64_flops(counters):
-    """FP64 flops per launch from the VALU instruction counters: 64 lanes x (ADD + MUL + 2 FMA) wave
-    instructions (an upper bound: lanes masked off inside a 16-lane group are counted), or None."""
+    """FP64 flops per launch from the PMC counters: 64 lanes x (ADD + MUL + 2 FMA) VALU wave instructions (an upper
+    bound: lanes masked off inside a 16-lane group are counted) plus, when the profile has it, the FP64 matrix-core
+    work (SQ_INSTS_VALU_MFMA_MOPS_F64, in units of 512 flops: 4 per v_mfma_f64_16x16x4f64 of 2048); or None."""
     if not counters or "SQ_INSTS_VALU_FMA_F64" not in counters:
         return None
-    return 64.0 * (counters["SQ_INSTS_VALU_ADD_F64"] + counters["SQ_INSTS_VALU_MUL_F64"] +
+    valu = 64.0 * (counters["SQ_INSTS_VALU_ADD_F64"] + counters["SQ_INSTS_VALU_MUL_F64"] +
                    2.0 * counters["SQ_INSTS_VALU_FMA_F64"])
+    return valu + 512.0 * counters.get("SQ_INSTS_VALU_MFMA_MOPS_F64", 0.0)
 
 
 def union_length(starts, ends):
@@ -418,7 +420,8 @@ def main():
     tmlps = [e.timing_mlp() for e in engs]
     # the QP-solve launches of all groups, as intervals on engine 0's clock (its window's first event, recorded
     # before any group's first kernel of the timed region): their union is the time the kernel family ran
-    ivs = [e.timing_intervals("qp", anchor=engs[0], max_n=4 * args.steps + 8) for e in engs]
+    nq = max(x[2] for x in tms)  # QP-solve launches of the timed steps per engine (the staged loop: one per SQP iteration)
+    ivs = [e.timing_intervals("qp", anchor=engs[0], max_n=nq + 8) for e in engs]
     ivs_env = [e.timing_intervals("k_mlp_env", anchor=engs[0], max_n=4 * args.steps + 8) for e in engs]
     if world > 1:
         elapsed = max_over_ranks(elapsed, device=dev)
@@ -451,10 +454,12 @@ def main():
     pmc = find_pmc(kname, Bs, N, args.mask, dof, args.traffic)
     traffic = pmc.get("hbm_bytes_per_launch") if pmc else None
     pflops = pmc_fp64_flops(pmc.get("counters")) if pmc else None
-    # k_sqp is a latency-bound FP64 VALU + DPP kernel (no MFMA in it): its roof is the FP64 vector peak, its
-    # work the SURVEY's condensed-dense F_qp per QP actually solved; the PMC-counted FP64 flops it executed and
-    # its HBM fraction (PMC traffic of all launches / the time they ran / 8 TB/s) are reported beside it
-    roof = {"kernel": kname, "bound": "valu", "achieved": achieved, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
+    # k_sqp is a latency-bound FP64 kernel: VALU + DPP for the stage recursions, the matrix cores for P = Hb - U^T U
+    # (and the poly Gram blocks of the wide variants); its roof is the FP64 peak (78.6 TFLOP/s for vector and matrix
+    # alike on MI355X), its work the SURVEY's condensed-dense F_qp per QP actually solved; the PMC-counted FP64 flops
+    # it executed (VALU and MFMA) and its HBM fraction (PMC traffic of all launches / the time they ran / 8 TB/s) are
+    # reported beside it
+    roof = {"kernel": kname, "bound": "valu+mfma", "achieved": achieved, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
             "frac": achieved / FP64_PEAK_TFLOPS, "traffic": traffic,
             "hbm_frac": (traffic * nipm / busy / HBM_PEAK_BPS) if traffic and busy > 0 else None,
             "pmc_fp64_flops_per_launch": pflops,
@@ -519,8 +524,14 @@ def main():
             args.cpu_threads = threads
             v, n, passes, dt, lat = cpu_baseline(pd, track, x0, u0, obs, guess, valid, fails, threads,
                                                  args.cpu_sample, args.cpu_seconds, dof=dof)
+            # the machine's other cores: the GPU box gives one GPU's job a CPU share (OMP_NUM_THREADS; gpurun:
+            # 16 of nproc), so the all-core figure is the measured per-thread rate times nproc, stated as an estimate
+            allc = {"value": v / threads * ci["nproc"], "cores": ci["nproc"], "kind": "estimate",
+                    "basis": f"measured {threads}-thread rate x {ci['nproc']}/{threads} (linear; instances are "
+                             f"independent, one per thread); single-thread rate from the latency run: "
+                             f"{1e3 / lat['mean_ms']:.1f} solves/s"}
             cpu = {"value": v, "unit": "solves/s", "cores": threads, "kind": "port", "host": ci,
-                   "latency_1thread": lat,
+                   "all_cores": allc, "latency_1thread": lat,
                    "sample": f"{passes} passes over the first {n} instances of the same workload "
                              f"({passes * n} runMPC_ solves, {dt:.1f} s; oracle = CPU restatement of the "
                              f"reference algorithm with OSQP replaced by an exact IPM, OpenMP {args.cpu_threads} threads)"}
@@ -528,9 +539,11 @@ def main():
             print(f"cpu baseline failed: {e}", file=sys.stderr)
 
     if rank == 0:
-        phases = {k: round(v / max(1, ncalls) * 1e3, 4) for k, v in tm.items()}
-        phases.update({k: round(v[0] / max(1, ncalls) * 1e3, 4) for k, v in tmlp.items() if v[1]})
-        print(json.dumps({"phase_ms_per_step": phases, "solved_frac": solved,
+        # per controller group and step: the S groups' phases run concurrently, so the sum over groups would
+        # exceed the wall time per step
+        phases = {k: round(v / max(1, ncalls) / S * 1e3, 4) for k, v in tm.items()}
+        phases.update({k: round(v[0] / max(1, ncalls) / S * 1e3, 4) for k, v in tmlp.items() if v[1]})
+        print(json.dumps({"phase_ms_per_group_step": phases, "groups": S, "solved_frac": solved,
                           "sqp_iter_hist": np.bincount(stats["sqp_iter"], minlength=3).tolist(),
                           "ipm_iters_mean": float(stats["ipm_iters"].mean()),
                           "pcie_inclusive_solves_per_s": pcie}), file=sys.stderr)

@@ -210,7 +210,8 @@ int mpcc_timing_mlp(mpcc_engine* e, double* self_s, int32_t* self_n, double* env
 /* the launches of one kernel of e's last timing window (kind: MPCC_TIMING_QP = the QP solve, k_sqp or k_ipm in
  * the staged path; MPCC_TIMING_MLP_SELF / _MLP_ENV = the collision networks) as [start, end] in ms after the
  * first event of `anchor`'s window (anchor = e, or another engine on the same device): several engines stepping
- * on their own streams measure the union of their kernels' busy time */
+ * on their own streams measure the union of their kernels' busy time.  *n = the number of intervals recorded,
+ * of which the first min(*n, max) are written (*n > max: the buffers were too small) */
 #define MPCC_TIMING_QP 0
 #define MPCC_TIMING_MLP_SELF 1
 #define MPCC_TIMING_MLP_ENV 2

@@ -409,6 +409,7 @@ void run_batch(mpcc_engine* e, int B, hipStream_t st, mpcc_timing* timing, bool 
             solve_qp.push_back({a1, b1});
         }
     } else {
+    e->last_wide = DOF != 7;  // the staged loop's k_ipm: 16 lanes for the Panda (a wide debug QP before must not stick)
     for (int it = 0; it < c.p.max_iter; it++) {
         int a0 = -1, a1 = -1, b1 = -1, c1 = -1;
         if (tm) a0 = mark();
@@ -1366,7 +1367,9 @@ int mpcc_timing_intervals(mpcc_engine* e, mpcc_engine* anchor, int kind, int max
             end_ms[k] = t;
             k++;
         }
-        *n = k;
+        // the number of intervals recorded, which may exceed max (only the first max were written): a caller that
+        // sized its buffers too small sees n > max instead of a silently truncated list
+        *n = (int32_t)lv.size();
     } catch (const HipError& x) {
         return fail(MPCC_E_HIP, x.what());
     }

@@ -1184,6 +1184,17 @@ __device__ __forceinline__ bool ipm_group(const DevConst& c, const DevBuffers& d
                     pnew = gx + atp + ktf;
                 }
                 PMARK(11);
+#ifdef MPCC_IPM_DBGF2  // tools/tail_ws_diff.py --dbg2: L, 1/L_jj (lane 0, fields 29..31), U and K columns (32..47)
+                if (run) {
+                    if (t == 0) {
+                        for (int i = 0; i < 36; i++) WSb[(size_t)k * IS + 29 * 16 + i] = LF[i];
+                        for (int i = 0; i < 8; i++) WSb[(size_t)k * IS + 29 * 16 + 36 + i] = dinv[i];
+                    }
+                    double uu[8];
+                    for (int i = 0; i < 8; i++) uu[i] = u[i];
+                    for (int i = 0; i < 8; i++) { *ws(k, 32 + i) = uu[i]; *ws(k, 40 + i) = kc[i]; }
+                }
+#endif
 #ifdef MPCC_IPM_DBGF
                 if (run) { *ws(k, 35) = gx; *ws(k, 36) = gv; *ws(k, 37) = pv; *ws(k, 38) = fv; *ws(k, 39) = dvr; *ws(k, 40) = cP;
                 *ws(k, 41) = wd; *ws(k, 42) = pnew; *ws(k, 43) = kff; *ws(k, 44) = Pc[0]; *ws(k, 45) = LF[35];

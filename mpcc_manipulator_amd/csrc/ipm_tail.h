@@ -482,6 +482,15 @@ __device__ __attribute__((noinline)) void ipm_tail(const DevConst& c, const DevB
 #pragma unroll
                 for (int i = 0; i < 8; i++) u[i] = (t < 9) ? gm[i] : ((i == j9) ? gw : 0.0);
                 fwd8(LF, dinv, u);
+#ifdef MPCC_IPM_DBGF2
+                if (own) {
+                    if (t == 0) {
+                        for (int i = 0; i < 36; i++) WSb[(size_t)k * IS + 29 * 16 + i] = LF[i];
+                        for (int i = 0; i < 8; i++) WSb[(size_t)k * IS + 29 * 16 + 36 + i] = dinv[i];
+                    }
+                    for (int i = 0; i < 8; i++) *ws(k, 32 + i) = u[i];
+                }
+#endif
 #ifdef MPCC_IPM_DBGF
                 if (own) { *ws(k, 44) = Pc[0]; *ws(k, 45) = LF[35]; *ws(k, 46) = dinv[7]; *ws(k, 47) = u[0]; *ws(k, 49) = Y[0]; *ws(k, 50) = Fc[0]; }
 #endif
@@ -575,6 +584,9 @@ __device__ __attribute__((noinline)) void ipm_tail(const DevConst& c, const DevB
                 for (int i = 0; i < 8; i++) kc[i] = -kc[i];
 #ifdef MPCC_IPM_DBGF
                 if (vC) *ws(kg, 48) = kc[0];
+#endif
+#ifdef MPCC_IPM_DBGF2
+                if (vC) for (int i = 0; i < 8; i++) *ws(kg, 40 + i) = kc[i];
 #endif
                 double fi[8];
 #pragma unroll

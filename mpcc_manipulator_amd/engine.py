@@ -579,12 +579,15 @@ class Engine:
     def timing_intervals(self, kind="qp", anchor=None, max_n=4096):
         """After timing_end: (start_ms, end_ms) arrays of one kernel's launches in the window ("qp": the QP solve,
         "k_mlp_self", "k_mlp_env"), relative to the first event of `anchor`'s window (default: this engine)."""
-        s, t = np.zeros(max_n), np.zeros(max_n)
-        n = C.c_int32()
         a = (anchor or self).h
-        self._check(self.L.mpcc_timing_intervals(self.h, a, self.TIMING_KINDS[kind], int(max_n), _dp(s), _dp(t),
-                                                 C.byref(n)), "mpcc_timing_intervals")
-        return s[:n.value], t[:n.value]
+        while True:
+            s, t = np.zeros(max_n), np.zeros(max_n)
+            n = C.c_int32()
+            self._check(self.L.mpcc_timing_intervals(self.h, a, self.TIMING_KINDS[kind], int(max_n), _dp(s), _dp(t),
+                                                     C.byref(n)), "mpcc_timing_intervals")
+            if n.value <= max_n:
+                return s[:n.value], t[:n.value]
+            max_n = n.value  # more launches than the buffer held (e.g. the staged loop: one per SQP iteration)
 
     def solve_stats(self, B):
         a, b, c = np.zeros(B, np.int32), np.zeros(B, np.int32), np.zeros(B, np.int32)

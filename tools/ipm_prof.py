@@ -65,8 +65,8 @@ def main():
             nt = max(1, tb[7])
             res["tail_iters"] = int(tb[7])
             res["tail_kcycles_per_iter"] = {s: round(tb[i] / nt / 1e3, 2) for i, s in enumerate(
-                ["f_A", "f_B_rest", "f_C", "f_D", "pred_fwd", "corr_bwd", "corr_fwd", "-", "fB_Y_F_Gm", "fB_chol",
-                 "fB_u_export", "fB_hb", "fB_P"]) if s != "-"}
+                ["f_A", "f_B_rest", "f_C", "f_D", "pred_D", "corr_bwd", "corr_fwd", "-", "fB_Y_F_Gm", "fB_chol",
+                 "fB_u_export", "fB_hb", "fB_P", "pred_A_loads", "pred_B_chain", "pred_C_slots"]) if s != "-"}
         print(json.dumps(res), flush=True)
         eng.close()
 

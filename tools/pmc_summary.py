@@ -50,7 +50,7 @@ def main():
         shutil.copy(stats[0], os.path.join(prof, f"{args.round}_kernel_stats.csv"))
     grid = (args.batch + args.ipw - 1) // args.ipw * 64
     merged = collections.defaultdict(dict)
-    for p in ("p1", "p2", "p3", "p4"):
+    for p in ("p1", "p2", "p3", "p4", "p5"):
         for k, v in load_pmc(args.dir, p).items():
             if v["grid"] == grid and (v["kernel"].startswith(f"void {args.ns}::{args.kernel}<")  # template kernels
                                       or v["kernel"].startswith(f"{args.ns}::{args.kernel}(")):
