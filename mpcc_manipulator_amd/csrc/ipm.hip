@@ -178,7 +178,7 @@ __device__ __forceinline__ double slot_rp(double sgn, double cz, double bnd, dou
 // ri = 1/s is formed once per slot and sweep (W = l/s, rc/s become products)
 __device__ __forceinline__ SlotStep slot_recover(double ri, double l, double rp, double cd, double rc) {
     const double W = l * ri;
-    return {-rp - cd, W * (cd + rp) - rc * ri};
+    return {-rp - cd, fma(W, cd + rp, -(rc * ri))};
 }
 __device__ __forceinline__ double slot_coef(double ri, double l, double rp, double rc) { return l + (l * ri) * rp - rc * ri; }
 // Fraction-to-boundary ratio test min(a, -s/ds, -l/dl) without a division per slot: the running
@@ -214,13 +214,17 @@ __device__ __forceinline__ void mu_acc(double& S0, double& S1, double& S2, doubl
     S1 = S1 + fma(s, dl, l * ds);
     S2 = fma(ds, dl, S2);
 }
+// a b + c d with the product a b fused: every two-product form of the recursions and the dynamics is written out for
+// the reason of mu_acc (which product the compiler fuses depends on the surrounding code, and tail mode evaluates the
+// same expressions in another function)
+__device__ __forceinline__ double fma2(double a, double b, double c, double d) { return fma(a, b, c * d); }
 // corrector step of a slot given the iterate (cz), the predictor step (ca) and the corrector step (cd)
 __device__ __forceinline__ SlotStep slot_corr(double sgn, double bnd, double cz, double ca, double cd, double s, double l,
                                               double smu, double* rp_out) {
     const double ri = rcp(s);
     const double rp = slot_rp(sgn, cz, bnd, s);
     const SlotStep pa = slot_recover(ri, l, rp, sgn * ca, s * l);
-    const double rc = s * l + pa.ds * pa.dl - smu;
+    const double rc = fma(s, l, pa.ds * pa.dl) - smu;
     *rp_out = rp;
     return slot_recover(ri, l, rp, sgn * cd, rc);
 }
@@ -483,6 +487,14 @@ __device__ __forceinline__ bool ipm_group(const DevConst& c, const DevBuffers& d
     const bool rowY = t < 9;
     const int j9 = t - 9;
     constexpr double sgnL = -1.0, sgnU = 1.0;
+    // Hb[a][t] (a, t < 9) = base + (A~^T P A~)[a][t] for the sparse A~ (diagonal + the (7, 8) entry); Pc7: lane 8 <- P[a][7]
+    auto hb_mp = [&](double v, int a, const double (&Pc)[16], const double (&Pc7)[9]) -> double {
+        v = fma(mdiag[a] * mt, Pc[a], v);
+        if (t == 8) v = fma(mdiag[a] * m78, Pc7[a], v);
+        if (a == 8) v = fma(m78 * mt, Pc[7], v);
+        if (a == 8 && t == 8) v = fma(m78 * m78, Pc7[7], v);
+        return v;
+    };
 
     // ---- Hessian checks (osqp_interface.cpp:454-473): stage flags from k_setqp + tridiagonal input blocks
     int fl = 0;
@@ -761,7 +773,7 @@ __device__ __forceinline__ bool ipm_group(const DevConst& c, const DevBuffers& d
 #pragma unroll
         for (int p = 0; p < NPM; p++) {
             const bool live = (double)p < in.np && k < N;
-            const double term = live ? in.pa[p] * x + in.pb[p] * v : 0.0;
+            const double term = live ? fma2(in.pa[p], x, in.pb[p], v) : 0.0;
             const double s = g_sum(term);
             if (t == p) r = s;
         }
@@ -800,9 +812,9 @@ __device__ __forceinline__ bool ipm_group(const DevConst& c, const DevBuffers& d
         v = part + from_up<8>(part) + in.m[8];
         const double v7 = from_down<1>(v);
         const double vj = from_down<9>(v);
-        if (t < 7) xn = mt * xt + gt * v;
-        else if (t == 7) xn = (m77 * xt + m78 * xb[8]) + g77 * v;
-        else if (t == 8) xn = m88 * xt + g87 * v7;
+        if (t < 7) xn = fma2(mt, xt, gt, v);
+        else if (t == 7) xn = fma(g77, v, fma2(m77, xt, m78, xb[8]));
+        else if (t == 8) xn = fma2(m88, xt, g87, v7);
         else xn = vj;
     };
 
@@ -857,8 +869,8 @@ __device__ __forceinline__ bool ipm_group(const DevConst& c, const DevBuffers& d
             store_slots(k, sL, lL, sU, lU, sP, lP, yx, 0.0, pcz);
             // y_{k+1} = M y_k + b_k (oracle order: sum_b M[a][b] y_b, then + b_a)
             const double y8 = from_up<1>(y);  // lane 7 <- y_8
-            const double yn = (t == 7) ? m77 * y + m78 * y8 : mt * y;
-            y = (t < 9) ? yn + bk : 0.0;
+            const double yn = (t == 7) ? fma2(m77, y, m78, y8) + bk : fma(mt, y, bk);
+            y = (t < 9) ? yn : 0.0;
             cur = nxt;
             bk = bkn;
         }
@@ -1014,9 +1026,10 @@ __device__ __forceinline__ bool ipm_group(const DevConst& c, const DevBuffers& d
                 double Y[8];
 #pragma unroll
                 for (int i = 0; i < 7; i++) Y[i] = gdiag[i] * Pc[i] + Pc[9 + i];
-                Y[7] = g77 * Pc[7] + g87 * Pc[8];
+                Y[7] = fma2(g77, Pc[7], g87, Pc[8]);
                 const double pu9 = from_up<9>(pv), pu1 = from_up<1>(pv);  // DPP in uniform control flow
-                const double fv = gv + gt * pv + ((t < 7) ? pu9 : g87 * pu1);
+                const double fg = fma(gt, pv, gv);
+                const double fv = (t < 7) ? fg + pu9 : fma(g87, pu1, fg);
                 // ---- (2) F column t (t < 8), Gm column t (t < 9); poly terms W_p bv_p bv_p^T, W_p bv_p a_p^T
                 // The rank-NPM poly terms accumulate row p by row p: each broadcast bv_p[i] is consumed as
                 // soon as it is made (DPP results are pinned in program order, so broadcasting every
@@ -1136,8 +1149,8 @@ __device__ __forceinline__ bool ipm_group(const DevConst& c, const DevBuffers& d
                     const double yu9 = from_up<9>(Y[i]);
                     const double yu1 = from_up<1>(Y[i]);
                     const double yd = from_down<1>(Y[i]);
-                    Fc[i] = hF[i] + (gt * Y[i] + ((t < 7) ? yu9 : g87 * yu1));
-                    gm[i] = hG[i] + (mt * Y[i] + ((t == 8) ? m78 * yd : 0.0));
+                    Fc[i] = hF[i] + fma(gt, Y[i], (t < 7) ? yu9 : g87 * yu1);
+                    gm[i] = hG[i] + fma(mt, Y[i], (t == 8) ? m78 * yd : 0.0);
                 }
                 PMARK(10);
                 // ---- (3) chol(F) from the broadcast columns; U = LF^-1 Gm; K = -LF^-T U; Finv column (t & 7);
@@ -1172,16 +1185,14 @@ __device__ __forceinline__ bool ipm_group(const DevConst& c, const DevBuffers& d
                 for (int m = 0; m < 8; m++) kff -= fi[m] * fb[m];
                 double pnew;
                 {
-                    double atp = 0.0;
                     const double p7 = from_down<1>(pv);
-                    if (t < 9) {
-                        atp = mt * pv;
-                        if (t == 8) atp += m78 * p7;
-                    }
+                    double gxa = gx;  // g_x~ + A~^T p
+                    if (t < 9) gxa = fma(mt, pv, gxa);
+                    if (t == 8) gxa = fma(m78, p7, gxa);
                     double ktf = 0.0;
 #pragma unroll
                     for (int i = 0; i < 8; i++) ktf += kc[i] * fb[i];
-                    pnew = gx + atp + ktf;
+                    pnew = gxa + ktf;
                 }
                 PMARK(11);
 #ifdef MPCC_IPM_DBGF2  // tools/tail_ws_diff.py --dbg2: L, 1/L_jj (lane 0, fields 29..31), U and K columns (32..47)
@@ -1248,11 +1259,7 @@ __device__ __forceinline__ bool ipm_group(const DevConst& c, const DevBuffers& d
                                     v = Qr[a];
                                     if (a == t) v += wd;
                                 }
-                                double mp = (mdiag[a] * mt) * Pc[a];
-                                if (t == 8) mp += (mdiag[a] * m78) * Pc7[a];
-                                if (a == 8) mp += (m78 * mt) * Pc[7];
-                                if (a == 8 && t == 8) mp += (m78 * m78) * Pc7[7];
-                                v += mp;
+                                v = hb_mp(v, a, Pc, Pc7);
                             }
                         } else if (a == t) {
                             v = wd;
@@ -1382,7 +1389,7 @@ __device__ __forceinline__ bool ipm_group(const DevConst& c, const DevBuffers& d
                     const double rp = slot_rp(sgn, czz, bnd, s);
                     const double ri = rcp(s);
                     const SlotStep pa = slot_recover(ri, l, rp, sgn * caa, s * l);
-                    const double rc = s * l + pa.ds * pa.dl - smu;
+                    const double rc = fma(s, l, pa.ds * pa.dl) - smu;
                     return slot_coef(ri, l, rp, rc);
                 };
                 const double cL = coef(aL, sgnL, cur.lb, cz, ca, cur.sL, cur.lL);
@@ -1396,7 +1403,8 @@ __device__ __forceinline__ bool ipm_group(const DevConst& c, const DevBuffers& d
                     return;
                 }
                 const double pu9 = from_up<9>(pv), pu1 = from_up<1>(pv);  // DPP in uniform control flow
-                const double fv = gv + gt * pv + ((t < 7) ? pu9 : g87 * pu1);
+                const double fg = fma(gt, pv, gv);
+                const double fv = (t < 7) ? fg + pu9 : fma(g87, pu1, fg);
                 double fb[8];
 #pragma unroll
                 for (int i = 0; i < 8; i++) fb[i] = bcn(fv, i);
@@ -1406,12 +1414,10 @@ __device__ __forceinline__ bool ipm_group(const DevConst& c, const DevBuffers& d
                 const double kff = part + from_up<8>(part);
                 const double kffd = from_down<8>(kff);  // lane 8+i <- kff_i
                 if (t >= 8) *ws(k, F_GVK) = kffd;
-                double atp = 0.0;
                 const double p7 = from_down<1>(pv);
-                if (t < 9) {
-                    atp = mt * pv;
-                    if (t == 8) atp += m78 * p7;
-                }
+                double gxa = gx;  // g_x~ + A~^T p
+                if (t < 9) gxa = fma(mt, pv, gxa);
+                if (t == 8) gxa = fma(m78, p7, gxa);
                 // K^T f from the K row halves: column sums over each 8-lane half by a transpose-reduce
                 // butterfly (lane j <-> 7-j, j^2, j^1); lane c ends with column c (c < 8) or 8 + (c & 7)
                 const double f8 = rot16<8>(fv);  // lane 8+i <- f_i (unconditional: DPP in uniform control flow)
@@ -1420,8 +1426,8 @@ __device__ __forceinline__ bool ipm_group(const DevConst& c, const DevBuffers& d
 #pragma unroll
                 for (int q = 0; q < 4; q++) {
                     const bool lo = (t & 4) == 0;
-                    const double a0 = cur.m[q] * fh, a1 = cur.m[4 + q] * fh;
-                    r1[q] = (lo ? a0 : a1) + half_mirror(lo ? a1 : a0);
+                    const double mk = lo ? cur.m[q] : cur.m[4 + q], mo = lo ? cur.m[4 + q] : cur.m[q];
+                    r1[q] = fma(mk, fh, half_mirror(mo * fh));
                 }
 #pragma unroll
                 for (int q = 0; q < 2; q++) {
@@ -1430,7 +1436,7 @@ __device__ __forceinline__ bool ipm_group(const DevConst& c, const DevBuffers& d
                 }
                 const bool lo1 = (t & 1) == 0;
                 const double ktf = (lo1 ? r2[0] : r2[1]) + quad_swap1(lo1 ? r2[1] : r2[0]);
-                pv = gx + atp + ktf;
+                pv = gxa + ktf;
             });
             PMARK(4);
 

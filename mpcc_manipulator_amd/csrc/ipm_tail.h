@@ -20,6 +20,10 @@
 //
 // Narrow variants only (NPM <= 2: the poly slot state packed into WF_ZV, no cached poly products).
 
+#ifndef MPCC_TAIL_P1
+#define MPCC_TAIL_P1 1  // phase B's P update without the instance transposes (0: ipm_group's form)
+#endif
+
 __device__ unsigned long long g_tail_solves;  // QP solves finished in tail mode since the last reset
 
 struct TailIO {
@@ -33,7 +37,7 @@ constexpr int TL_SA = 30;                       // factorization A -> B, D: 28 +
 constexpr int TL_A = 0;                         // 4 * 16 * TL_SA
 constexpr int TL_LF = TL_A + 4 * 16 * TL_SA;    // 4 * 48: L of chol(F) (36) and its reciprocal pivots (8), per stage
 constexpr int TL_U = TL_LF + 4 * 48;            // 4 * 16 * 10: U column (8)
-constexpr int TL_K = TL_U + 4 * 16 * 10;        // 4 * 144: K transpose area per group (8 x 16, +16 pad)
+constexpr int TL_K = TL_U + 4 * 16 * 10;        // 4 * 144: K transpose area per group (8 x 16, +16 pad); in B the P exchange
 constexpr int TL_C = TL_K + 4 * 144;            // 4 * 16 * 18: K column (8) and F^-1 column (8)
 constexpr int TL_END = TL_C + 4 * 16 * 18;
 constexpr int TL_STATE = TL_END;                // 16: iteration state handed over by ipm_group
@@ -96,6 +100,13 @@ __device__ __attribute__((noinline)) void ipm_tail(const DevConst& c, const DevB
     const bool rowY = t < 9;
     const int j9 = t - 9;
     constexpr double sgnL = -1.0, sgnU = 1.0;
+    auto hb_mp = [&](double v, int a, const double (&Pc)[16], const double (&Pc7)[9]) -> double {  // as ipm_group
+        v = fma(mdiag[a] * mt, Pc[a], v);
+        if (t == 8) v = fma(mdiag[a] * m78, Pc7[a], v);
+        if (a == 8) v = fma(m78 * mt, Pc[7], v);
+        if (a == 8 && t == 8) v = fma(m78 * m78, Pc7[7], v);
+        return v;
+    };
     const bool own = g == 0;  // the group that stores what all four groups computed redundantly (phases B, D)
 
     // ---- stage loaders (ipm_group's, PACKP form)
@@ -177,7 +188,7 @@ __device__ __attribute__((noinline)) void ipm_tail(const DevConst& c, const DevB
 #pragma unroll
         for (int p = 0; p < NPM; p++) {
             const bool live = (double)p < in.np && k < N;
-            const double term = live ? in.pa[p] * x + in.pb[p] * v : 0.0;
+            const double term = live ? fma2(in.pa[p], x, in.pb[p], v) : 0.0;
             const double s = g_sum(term);
             if (t == p) r = s;
         }
@@ -214,9 +225,9 @@ __device__ __attribute__((noinline)) void ipm_tail(const DevConst& c, const DevB
         v = part + from_up<8>(part) + m[8];
         const double v7 = from_down<1>(v);
         const double vj = from_down<9>(v);
-        if (t < 7) xn = mt * xt + gt * v;
-        else if (t == 7) xn = (m77 * xt + m78 * xb[8]) + g77 * v;
-        else if (t == 8) xn = m88 * xt + g87 * v7;
+        if (t < 7) xn = fma2(mt, xt, gt, v);
+        else if (t == 7) xn = fma(g77, v, fma2(m77, xt, m78, xb[8]));
+        else if (t == 8) xn = fma2(m88, xt, g87, v7);
         else xn = vj;
     };
     auto sync = [] { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); };
@@ -272,8 +283,8 @@ __device__ __attribute__((noinline)) void ipm_tail(const DevConst& c, const DevB
             mcount += (aL ? 1.0 : 0.0) + (aU ? 1.0 : 0.0) + (aP ? 1.0 : 0.0);
             if (own) store_slots(k, sL, lL, sU, lU, sP, lP, yx, 0.0);
             const double y8 = from_up<1>(y);
-            const double yn = (t == 7) ? m77 * y + m78 * y8 : mt * y;
-            y = (t < 9) ? yn + bk : 0.0;
+            const double yn = (t == 7) ? fma2(m77, y, m78, y8) + bk : fma(mt, y, bk);
+            y = (t < 9) ? yn : 0.0;
             cur = nxt;
             bk = bkn;
         }
@@ -458,7 +469,7 @@ __device__ __attribute__((noinline)) void ipm_tail(const DevConst& c, const DevB
                 double Y[8];
 #pragma unroll
                 for (int i = 0; i < 7; i++) Y[i] = gdiag[i] * Pc[i] + Pc[9 + i];
-                Y[7] = g77 * Pc[7] + g87 * Pc[8];
+                Y[7] = fma2(g77, Pc[7], g87, Pc[8]);
                 // (2) F column t, Gm column t
                 double Fc[8], gm[8];
 #pragma unroll
@@ -466,8 +477,8 @@ __device__ __attribute__((noinline)) void ipm_tail(const DevConst& c, const DevB
                     const double yu9 = from_up<9>(Y[i]);
                     const double yu1 = from_up<1>(Y[i]);
                     const double yd = from_down<1>(Y[i]);
-                    Fc[i] = hF[i] + (gt * Y[i] + ((t < 7) ? yu9 : g87 * yu1));
-                    gm[i] = hG[i] + (mt * Y[i] + ((t == 8) ? m78 * yd : 0.0));
+                    Fc[i] = hF[i] + fma(gt, Y[i], (t < 7) ? yu9 : g87 * yu1);
+                    gm[i] = hG[i] + fma(mt, Y[i], (t == 8) ? m78 * yd : 0.0);
                 }
                 TMARK(8);
                 // (3) chol(F), U = LF^-1 Gm
@@ -520,11 +531,7 @@ __device__ __attribute__((noinline)) void ipm_tail(const DevConst& c, const DevB
                         if (a < 9) {
                             if (t < 9) {
                                 v = hb9[a];
-                                double mp = (mdiag[a] * mt) * Pc[a];
-                                if (t == 8) mp += (mdiag[a] * m78) * Pc7[a];
-                                if (a == 8) mp += (m78 * mt) * Pc[7];
-                                if (a == 8 && t == 8) mp += (m78 * m78) * Pc7[7];
-                                v += mp;
+                                v = hb_mp(v, a, Pc, Pc7);
                             }
                         } else if (a == t) {
                             v = wd;
@@ -534,6 +541,34 @@ __device__ __attribute__((noinline)) void ipm_tail(const DevConst& c, const DevB
                 }
                 TMARK(11);
                 if (k > 0) {
+#if MPCC_TAIL_P1
+                    // One instance on all four groups: the operands of its two MFMAs are already in every lane (lane
+                    // (g, t) holds U[g][t], U[4 + g][t] and Hb[g + 4r][t]: selects by g instead of ipm_group's
+                    // transposes between instances), and the products P[g + 4r][t] go back to the column layout
+                    // (every group: P[a][t]) through LDS.  Same MFMAs on the same operands: bitwise ipm_group's P.
+                    double ua = u[0], ub = u[4];
+                    d4 acc = {hb[0], hb[4], hb[8], hb[12]};
+#pragma unroll
+                    for (int q = 1; q < 4; q++)
+                        if (g == q) {
+                            ua = u[q];
+                            ub = u[4 + q];
+                            acc = d4{hb[q], hb[q + 4], hb[q + 8], hb[q + 12]};
+                        }
+                    acc = __builtin_amdgcn_mfma_f64_16x16x4f64(-ua, ua, acc, 0, 0, 0);
+                    acc = __builtin_amdgcn_mfma_f64_16x16x4f64(-ub, ub, acc, 0, 0, 0);
+                    double* Sp = lds(TL_K + t * 18);  // row t: P[0..15][t] (stride 18: conflict-free, 16-byte aligned)
+#pragma unroll
+                    for (int r = 0; r < 4; r++) Sp[g + 4 * r] = acc[r];
+                    sync();
+#pragma unroll
+                    for (int q = 0; q < 8; q++) {
+                        const double2 v = reinterpret_cast<const double2*>(Sp)[q];
+                        Pc[2 * q] = v.x;
+                        Pc[2 * q + 1] = v.y;
+                    }
+                    sync();
+#else
                     double x[4][4], ua[4][1], ub[4][1];
 #pragma unroll
                     for (int q = 0; q < 4; q++) {
@@ -558,6 +593,7 @@ __device__ __attribute__((noinline)) void ipm_tail(const DevConst& c, const DevB
                     for (int q = 0; q < 4; q++)
 #pragma unroll
                         for (int r = 0; r < 4; r++) Pc[q + 4 * r] = x[q][r];
+#endif
                 }
                 TMARK(12);
             }
@@ -638,7 +674,8 @@ __device__ __attribute__((noinline)) void ipm_tail(const DevConst& c, const DevB
                     fi[2 * q] = f.x; fi[2 * q + 1] = f.y;
                 }
                 const double pu9 = from_up<9>(pv), pu1 = from_up<1>(pv);
-                const double fv = gv + gt * pv + ((t < 7) ? pu9 : g87 * pu1);
+                const double fg = fma(gt, pv, gv);
+                const double fv = (t < 7) ? fg + pu9 : fma(g87, pu1, fg);
                 double fb[8];
 #pragma unroll
                 for (int i = 0; i < 8; i++) fb[i] = bcn(fv, i);
@@ -647,16 +684,14 @@ __device__ __attribute__((noinline)) void ipm_tail(const DevConst& c, const DevB
                 for (int m = 0; m < 8; m++) kff -= fi[m] * fb[m];
                 double pnew;
                 {
-                    double atp = 0.0;
                     const double p7 = from_down<1>(pv);
-                    if (t < 9) {
-                        atp = mt * pv;
-                        if (t == 8) atp += m78 * p7;
-                    }
+                    double gxa = gx;  // g_x~ + A~^T p
+                    if (t < 9) gxa = fma(mt, pv, gxa);
+                    if (t == 8) gxa = fma(m78, p7, gxa);
                     double ktf = 0.0;
 #pragma unroll
                     for (int i = 0; i < 8; i++) ktf += kc[i] * fb[i];
-                    pnew = gx + atp + ktf;
+                    pnew = gxa + ktf;
                 }
                 const double kffd = from_down<8>(kff);
                 if (own) *ws(k, WF_GVK) = (t < 8) ? g0v : kffd;
@@ -791,7 +826,7 @@ __device__ __attribute__((noinline)) void ipm_tail(const DevConst& c, const DevB
                         const double rp = slot_rp(sgn, czz, bnd, s);
                         const double ri = rcp(s);
                         const SlotStep pa = slot_recover(ri, l, rp, sgn * caa, s * l);
-                        const double rc = s * l + pa.ds * pa.dl - smu;
+                        const double rc = fma(s, l, pa.ds * pa.dl) - smu;
                         return slot_coef(ri, l, rp, rc);
                     };
                     const double cL = coef(aL, sgnL, cur.lb, cz, ca, cur.sL, cur.lL);
@@ -820,7 +855,8 @@ __device__ __attribute__((noinline)) void ipm_tail(const DevConst& c, const DevB
 #pragma unroll
                     for (int q = 0; q < 6; q++) { const double2 v = a2[1 + q]; m[2 * q] = v.x; m[2 * q + 1] = v.y; }
                     const double pu9 = from_up<9>(pvc), pu1 = from_up<1>(pvc);
-                    const double fv = gv + gt * pvc + ((t < 7) ? pu9 : g87 * pu1);
+                    const double fg = fma(gt, pvc, gv);
+                    const double fv = (t < 7) ? fg + pu9 : fma(g87, pu1, fg);
                     double fb[8];
 #pragma unroll
                     for (int i = 0; i < 8; i++) fb[i] = bcn(fv, i);
@@ -830,20 +866,18 @@ __device__ __attribute__((noinline)) void ipm_tail(const DevConst& c, const DevB
                     const double kff = part + from_up<8>(part);
                     const double kffd = from_down<8>(kff);
                     if (own && t >= 8) *ws(k, WF_GVK) = kffd;
-                    double atp = 0.0;
                     const double p7 = from_down<1>(pvc);
-                    if (t < 9) {
-                        atp = mt * pvc;
-                        if (t == 8) atp += m78 * p7;
-                    }
+                    double gxa = gx;  // g_x~ + A~^T p
+                    if (t < 9) gxa = fma(mt, pvc, gxa);
+                    if (t == 8) gxa = fma(m78, p7, gxa);
                     const double f8 = rot16<8>(fv);
                     const double fh = (t < 8) ? fv : f8;
                     double r1[4], r2[2];
 #pragma unroll
                     for (int q = 0; q < 4; q++) {
                         const bool lo = (t & 4) == 0;
-                        const double a0 = m[q] * fh, a1 = m[4 + q] * fh;
-                        r1[q] = (lo ? a0 : a1) + half_mirror(lo ? a1 : a0);
+                        const double mk = lo ? m[q] : m[4 + q], mo = lo ? m[4 + q] : m[q];
+                        r1[q] = fma(mk, fh, half_mirror(mo * fh));
                     }
 #pragma unroll
                     for (int q = 0; q < 2; q++) {
@@ -852,7 +886,7 @@ __device__ __attribute__((noinline)) void ipm_tail(const DevConst& c, const DevB
                     }
                     const bool lo1 = (t & 1) == 0;
                     const double ktf = (lo1 ? r2[0] : r2[1]) + quad_swap1(lo1 ? r2[1] : r2[0]);
-                    pvc = gx + atp + ktf;
+                    pvc = gxa + ktf;
                 }
                 sync();
             }
