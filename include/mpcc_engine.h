@@ -298,8 +298,8 @@ int mpcc_debug_solve_qp(mpcc_engine* e, int B, const double* guess, const double
                         double* step, int32_t* qp_status, int32_t* ipm_iters);
 
 /* the same QP with low-rank Hessian terms sum_j lrc_j u_j u_j^T (the damped-BFGS QP form): lr [nlr*(N+1)*NXU]
- * (per stage [x | u], u_N = 0), lrc [nlr], nlr <= 4, solved by the 32-lane interior point with the Woodbury
- * correction */
+ * (per stage [x | u], u_N = 0), lrc [nlr], nlr <= 28, solved by the 32-lane interior point with the Woodbury
+ * correction (nlr > 4: the extended path, Woodbury columns and capacitance matrix in memory) */
 int mpcc_debug_solve_qp_lr(mpcc_engine* e, int B, const double* guess, const double* rec, const double* u_cur, int nlr,
                            const double* lr, const double* lrc, double* step, int32_t* qp_status, int32_t* ipm_iters);
 

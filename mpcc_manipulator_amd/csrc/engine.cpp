@@ -101,7 +101,7 @@ struct mpcc_engine {
         f(d_spl);
         f(d.guess); f(d.valid); f(d.fails); f(d.rec); f(d.qs); f(d.is); f(d.step); f(d.trial); f(d.sqi); f(d.sqd);
         if (d.isw != d.is) f(d.isw);
-        f(d.lr); f(d.lrc); f(d.glam); f(d.gprev); f(d.aty); f(d.sp);
+        f(d.lr); f(d.lrc); f(d.glam); f(d.gprev); f(d.aty); f(d.sp); f(d.lrq);
         f(d.dbg_trace);
         f(bchk);
         f(s_x0); f(s_u0); f(s_obs); f(s_u0out); f(s_hor); f(s_status); f(s_ok);
@@ -139,17 +139,19 @@ struct mpcc_engine {
 
     // Buffers of the damped-BFGS option (use_BFGS): the 32-lane interior point's workspace (the mobile build's
     // regular one) and the per-instance BFGS state, allocated when the option is first enabled.
-    void ensure_bfgs_buffers() {
+    // nterms: low-rank terms the solves may hold (2 per BFGS update); above LRM the Woodbury columns go to memory.
+    void ensure_bfgs_buffers(int nterms) {
         const size_t B = (size_t)maxB, NE = ((size_t)N + 1) * NXU;
         if (!d.isw) d.isw = dmalloc<double>(B * (N + 1) * ISW);
         if (!d.lr) {
-            d.lr = dmalloc<double>(B * LRM * NE);
-            d.lrc = dmalloc<double>(B * LRM);
+            d.lr = dmalloc<double>(B * LRX * NE);
+            d.lrc = dmalloc<double>(B * LRX);
             d.glam = dmalloc<double>(B * NE);
             d.gprev = dmalloc<double>(B * NE);
             d.aty = dmalloc<double>(B * NE);
             d.sp = dmalloc<double>(B * NE);
         }
+        if (nterms > LRM && !d.lrq) d.lrq = dmalloc<double>(B * LRX * (N + 1) * 3 * 32);
     }
 
     DevConst make_const(int Bn) const {
@@ -275,9 +277,9 @@ void validate_params(const mpcc_params& p) {
     if (p.max_iter < 0 || p.line_search_max_iter < 0) throw std::invalid_argument("negative iteration limit");
     // Damped BFGS (osqp_interface.cpp:683-715): the QP Hessian is the structured Hessian of SQP iteration 0 plus
     // 2 low-rank terms per update, solved with the Woodbury identity around the Riccati recursion (DESIGN.md
-    // §4.2); at most LRM terms are held, i.e. max_iter <= 1 + LRM / 2.
-    if (p.use_BFGS && p.max_iter > 1 + LRM / 2)
-        throw std::invalid_argument("use_BFGS supports max_iter <= " + std::to_string(1 + LRM / 2) +
+    // §4.2); at most LRX terms are held, i.e. max_iter <= 1 + LRX / 2.
+    if (p.use_BFGS && p.max_iter > 1 + LRX / 2)
+        throw std::invalid_argument("use_BFGS supports max_iter <= " + std::to_string(1 + LRX / 2) +
                                     " (low-rank terms of the damped BFGS Hessian)");
 }
 
@@ -556,7 +558,7 @@ int mpcc_create(const mpcc_config* cfg, const mpcc_params* params, const char* n
         e->bchk = dmalloc<uint32_t>(64);
         HIPCHK(hipMemset(e->bchk, 0, 64 * sizeof(uint32_t)));
 #endif
-        if (e->params.use_BFGS || e->wide_sqp) e->ensure_bfgs_buffers();
+        if (e->params.use_BFGS || e->wide_sqp) e->ensure_bfgs_buffers(e->params.use_BFGS ? 2 * (e->params.max_iter - 1) : 0);
         e->s_x0 = dmalloc<double>(B * NX);
         e->s_u0 = dmalloc<double>(B * NU);
         e->s_obs = dmalloc<double>(B * 4);
@@ -606,7 +608,7 @@ int mpcc_set_params(mpcc_engine* e, const mpcc_params* p) {
         validate_params(np);
         e->params = np;
         e->set_model();
-        if (np.use_BFGS) e->ensure_bfgs_buffers();
+        if (np.use_BFGS) e->ensure_bfgs_buffers(2 * (np.max_iter - 1));
     } catch (const std::exception& x) {
         e->params = old;
         e->set_model();
@@ -1189,7 +1191,7 @@ int mpcc_debug_solve_qp(mpcc_engine* e, int B, const double* guess, const double
 
 int mpcc_debug_solve_qp_lr(mpcc_engine* e, int B, const double* guess, const double* rec, const double* u_cur, int nlr,
                            const double* lr, const double* lrc, double* step, int32_t* qp_status, int32_t* ipm_iters) {
-    if (nlr < 0 || nlr > LRM || (nlr && (!lr || !lrc))) return fail(MPCC_E_INVALID, "mpcc_debug_solve_qp_lr: invalid argument");
+    if (nlr < 0 || nlr > LRX || (nlr && (!lr || !lrc))) return fail(MPCC_E_INVALID, "mpcc_debug_solve_qp_lr: invalid argument");
     return debug_solve_qp(e, B, guess, rec, u_cur, nlr, lr, lrc, step, qp_status, ipm_iters);
 }
 
@@ -1220,13 +1222,13 @@ static int debug_solve_qp(mpcc_engine* e, int B, const double* guess, const doub
         HIPCHK(hipMemcpy(e->d.sqi, sqi.data(), sqi.size() * sizeof(int32_t), hipMemcpyHostToDevice));
         HIPCHK(hipMemset(e->d.step, 0, S * NXU * sizeof(double)));
         if (nlr >= 0) {  // low-rank terms of every instance, then the 32-lane solver
-            e->ensure_bfgs_buffers();
+            e->ensure_bfgs_buffers(nlr);
             const size_t NE = S * NXU / B;
-            std::vector<double> l((size_t)B * LRM * NE, 0.0), lc((size_t)B * LRM, 0.0);
+            std::vector<double> l((size_t)B * LRX * NE, 0.0), lc((size_t)B * LRX, 0.0);
             for (int b = 0; b < B; b++)
                 for (int j = 0; j < nlr; j++) {
-                    std::memcpy(&l[((size_t)b * LRM + j) * NE], lr + (size_t)j * NE, NE * sizeof(double));
-                    lc[(size_t)b * LRM + j] = lrc[j];
+                    std::memcpy(&l[((size_t)b * LRX + j) * NE], lr + (size_t)j * NE, NE * sizeof(double));
+                    lc[(size_t)b * LRX + j] = lrc[j];
                 }
             HIPCHK(hipMemcpy(e->d.lr, l.data(), l.size() * sizeof(double), hipMemcpyHostToDevice));
             HIPCHK(hipMemcpy(e->d.lrc, lc.data(), lc.size() * sizeof(double), hipMemcpyHostToDevice));

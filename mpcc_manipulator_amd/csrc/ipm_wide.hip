@@ -78,7 +78,14 @@ constexpr int G_ROWS = 24, G_OPW = IPW * G_ROWS * 16, GRAM_LDS = 6 * 256;
 static_assert(G_OPW + IPW * 16 <= GRAM_LDS, "Gram operands inside the product area");
 __host__ __device__ constexpr bool wide_gram(int npm) { return MPCC_WIDE_GRAM && npm >= 9; }
 
-size_t ipm_wide_lds_bytes(int npm) { return (size_t)(IPW * GRP_LDS + (wide_gram(npm) ? GRAM_LDS : 0)) * sizeof(double); }
+// extended low-rank path (nlr > LRM): per instance the capacitance matrix S = C^-1 + U^T Q (LU in place) and
+// the per-term scalars u_j^T z, t = S^-1 U^T dz_s, u_j^T dz, the row pivots and c_j (doubles)
+constexpr int XL_S = 0, XL_UZ = LRX * LRX, XL_TT = XL_UZ + LRX, XL_UD = XL_TT + LRX, XL_PIV = XL_UD + LRX,
+              XL_C = XL_PIV + LRX, XL_LDS = XL_C + LRX;
+static_assert(LRX <= GW && LRX % 4 == 0, "extended low-rank path: one lane per term, terms in chunks of 4");
+size_t ipm_wide_lds_bytes(int npm, bool lr) {
+    return (size_t)(IPW * GRP_LDS + (wide_gram(npm) ? GRAM_LDS : 0) + (lr ? IPW * XL_LDS : 0)) * sizeof(double);
+}
 
 namespace {
 
@@ -408,21 +415,53 @@ __device__ __forceinline__ void ipm_group(const DevConst& c, const DevBuffers& d
     if constexpr (LR) {
         nlr = si[SQ_NLR];
 #pragma unroll
-        for (int j = 0; j < LRM; j++) lrc[j] = (j < nlr) ? d.lrc[(size_t)(valid ? b : 0) * LRM + j] : 0.0;
-        LRb = (const gdouble*)(d.lr + (size_t)(valid ? b : 0) * LRM * NS * NXU);
+        for (int j = 0; j < LRM; j++) lrc[j] = (j < nlr) ? d.lrc[(size_t)(valid ? b : 0) * LRX + j] : 0.0;
+        LRb = (const gdouble*)(d.lr + (size_t)(valid ? b : 0) * LRX * NS * NXU);
     }
-    const bool lrw = LR && __ballot(entered && nlr > 0) != 0;  // this wave runs the split (Woodbury) sweeps
+    // more terms than the fused sweeps carry: the wave runs the extended path (both instances; nlr_w = the larger
+    // count, the other instance's extra terms are zero vectors with unit capacitance)
+    const bool xlw = LR && __ballot(entered && nlr > LRM) != 0;
+    const int nlr_w = xlw ? max(__shfl(entered ? nlr : 0, 0), __shfl(entered ? nlr : 0, GW)) : 0;
+    const bool lrw = LR && !xlw && __ballot(entered && nlr > 0) != 0;  // this wave runs the split (Woodbury) sweeps
     auto u_y = [&](int j, int k) -> double {  // u_j, y part of stage k (lanes < NX)
-        const double v = LRb[((size_t)MPCC_BCHK(c.bchk, j, LRM, BC_LR) * NS + MPCC_BCHK(c.bchk, k, NS, BC_LR)) * NXU + (rowY ? t : 0)];
+        const double v = LRb[((size_t)MPCC_BCHK(c.bchk, j, LRX, BC_LR) * NS + MPCC_BCHK(c.bchk, k, NS, BC_LR)) * NXU + (rowY ? t : 0)];
         return (LR && rowY && j < nlr) ? v : 0.0;
     };
     auto u_v = [&](int j, int k) -> double {  // u_j, v part of stage k (lanes < NU, k < N)
-        const double v = LRb[((size_t)MPCC_BCHK(c.bchk, j, LRM, BC_LR) * NS + MPCC_BCHK(c.bchk, k, NS, BC_LR)) * NXU + NX + (t < NU ? t : 0)];
+        const double v = LRb[((size_t)MPCC_BCHK(c.bchk, j, LRX, BC_LR) * NS + MPCC_BCHK(c.bchk, k, NS, BC_LR)) * NXU + NX + (t < NU ? t : 0)];
         return (LR && t < NU && k < N && j < nlr) ? v : 0.0;
     };
     double uz[LRM];  // u_j^T z of the current iterate
 #pragma unroll
     for (int j = 0; j < LRM; j++) uz[j] = 0.0;
+
+    // ---- extended low-rank path (xlw): the Woodbury correction of the fused sweeps for any nlr <= LRX, with the
+    //      columns Q_j in memory (d.lrq, per lane) and S, its LU and the per-term scalars in the instance's LDS
+    //      (XL_*), the terms taken 4 at a time.  Same formulas as the fused path and the oracle's lr_solve.
+    double* const XL = smem + IPW * GRP_LDS + (wide_gram(NPM) ? GRAM_LDS : 0) + grp * XL_LDS;
+    gdouble* const XQb = (gdouble*)(d.lrq ? d.lrq + (size_t)(valid ? b : 0) * LRX * NS * 3 * GW : d.step);
+    auto xq = [&](int j, int k, int f) -> gdouble* {  // f: 0 Q_j x~ part, 1 Q_j v part, 2 kff of the solve of u_j
+        return XQb + (((size_t)MPCC_BCHK(c.bchk, j, LRX, BC_LR) * NS + MPCC_BCHK(c.bchk, k, NS, BC_LR)) * 3 + f) * GW + t;
+    };
+    const int xlt = t < LRX ? t : LRX - 1;  // this lane's term / row of S (clamped address)
+    if (xlw && t < LRX) XL[XL_C + t] = (t < nlr) ? d.lrc[(size_t)(valid ? b : 0) * LRX + t] : 0.0;
+    // dst[j] = u_j^T [ws fx | ws fv] over the horizon, all j < nlr_w
+    auto xl_dots = [&](int dst, int fx, int fv) {
+        for (int j0 = 0; j0 < nlr_w; j0 += 4) {
+            double pq[4] = {0.0, 0.0, 0.0, 0.0};
+            for (int k = 0; k <= N; k++) {
+                const double x = *ws(k, fx), v = *ws(k, fv);
+#pragma unroll
+                for (int q = 0; q < 4; q++) pq[q] += u_y(j0 + q, k) * x + u_v(j0 + q, k) * v;
+            }
+#pragma unroll
+            for (int q = 0; q < 4; q++) {
+                const double sm = g_sum32(pq[q]);
+                if (t == 0) XL[dst + j0 + q] = sm;
+            }
+        }
+        lds_sync();
+    };
 
     // Many poly rows (without the low-rank terms): c_p^T z, c_p^T dza and c_p^T dz are formed once per iteration
     // where z, dza and dz are made and kept in the workspace (WF_PZ, WF_PA, WF_PD) for the other sweeps, which
@@ -560,6 +599,154 @@ __device__ __forceinline__ void ipm_group(const DevConst& c, const DevBuffers& d
     };
     auto fwd_step = [&](const In& in, double xt, double& v, double& xn) { fwd_step_k(in, xt, in.m[NU], v, xn); };
 
+    // ---- extended low-rank path: Q_j = M u_j = -solve(u_j) from the stored gains, 4 terms per backward +
+    //      forward pass (the fused path's recursions, ipm_group factorization / predictor sweeps)
+    auto xl_q = [&]() {
+        for (int j0 = 0; j0 < nlr_w; j0 += 4) {
+            double pj[4];
+            for (int k = N; k >= 0; k--) {
+                if (k == N) {
+#pragma unroll
+                    for (int q = 0; q < 4; q++) pj[q] = u_y(j0 + q, k);
+                    continue;
+                }
+                double kc[NU], fi[NU];
+#pragma unroll
+                for (int i = 0; i < NU; i++) { kc[i] = *ws(k, WF_KC + i); fi[i] = *ws(k, WF_FI + i); }
+#pragma unroll
+                for (int q = 0; q < 4; q++) {
+                    const Halves hq = halves(pj[q]);
+                    const double qu = up32<NX>(pj[q], hq, t), qu1 = up32<1>(pj[q], hq, t);
+                    const double fvj = u_v(j0 + q, k) + gt * pj[q] + ((t < DOF) ? qu : gv * qu1);
+                    const Halves hfj = halves(fvj);
+                    double kffj = 0.0, ktfj = 0.0;
+#pragma unroll
+                    for (int m = 0; m < NU; m++) {
+                        const double fbm = bch(hfj, m);
+                        kffj -= fi[m] * fbm;
+                        ktfj += kc[m] * fbm;
+                    }
+                    *xq(j0 + q, k, 2) = (t < NU) ? kffj : 0.0;
+                    double atpj = 0.0;
+                    const double pq7 = down32<1>(pj[q], hq, t);
+                    if (rowY) {
+                        atpj = mt * pj[q];
+                        if (t == XVS) atpj += msv * pq7;
+                    }
+                    pj[q] = u_y(j0 + q, k) + atpj + ktfj;
+                }
+            }
+            double xqv[4] = {0.0, 0.0, 0.0, 0.0};
+            for (int k = 0; k <= N; k++) {
+                In kin;
+#pragma unroll
+                for (int i = 0; i < NU; i++) {
+                    const double v = *ws(k, WF_KC + i);
+                    kin.m[i] = (k < N) ? v : 0.0;
+                }
+#pragma unroll
+                for (int q = 0; q < 4; q++) {
+                    const double kfj = *xq(j0 + q, k, 2);
+                    double vq = 0.0, xqn = 0.0;
+                    fwd_step_k(kin, xqv[q], (k < N) ? kfj : 0.0, vq, xqn);
+                    *xq(j0 + q, k, 0) = (t < NXA) ? -xqv[q] : 0.0;
+                    *xq(j0 + q, k, 1) = (t < NU && k < N) ? -vq : 0.0;
+                    xqv[q] = (k < N) ? xqn : 0.0;
+                }
+            }
+        }
+    };
+    // S = C^-1 + U^T Q over 4 x 4 blocks of terms (the upper blocks, mirrored), then its LU with partial pivoting
+    // in place: lane c works on column c (< nlr_w), row swaps as the oracle's lu_solve_small (the first largest
+    // |pivot| candidate), multipliers below the diagonal, pivot rows in XL_PIV
+    auto xl_smat_lu = [&]() {
+        double* const Sm = XL + XL_S;
+        for (int i0 = 0; i0 < nlr_w; i0 += 4)
+            for (int j0 = i0; j0 < nlr_w; j0 += 4) {
+                double pq[4][4];
+#pragma unroll
+                for (int q = 0; q < 4; q++)
+#pragma unroll
+                    for (int r = 0; r < 4; r++) pq[q][r] = 0.0;
+                for (int k = 0; k <= N; k++) {
+                    double qx[4], qv[4];
+#pragma unroll
+                    for (int r = 0; r < 4; r++) { qx[r] = *xq(j0 + r, k, 0); qv[r] = *xq(j0 + r, k, 1); }
+#pragma unroll
+                    for (int q = 0; q < 4; q++) {
+                        const double uy = u_y(i0 + q, k), uv = u_v(i0 + q, k);
+#pragma unroll
+                        for (int r = 0; r < 4; r++) pq[q][r] += uy * qx[r] + uv * qv[r];
+                    }
+                }
+#pragma unroll
+                for (int q = 0; q < 4; q++)
+#pragma unroll
+                    for (int r = 0; r < 4; r++) {
+                        const int i = i0 + q, j = j0 + r;
+                        const double uq = g_sum32(pq[q][r]);
+                        if (t == 0) {
+                            const double ci = (i < nlr) ? 1.0 / XL[XL_C + i] : 1.0;
+                            Sm[i * LRX + j] = (i == j ? ci : 0.0) + uq;
+                            if (j0 > i0) Sm[j * LRX + i] = uq;
+                        }
+                    }
+            }
+        lds_sync();
+        for (int kk = 0; kk < nlr_w; kk++) {
+            const double a = (t >= kk && t < nlr_w) ? fabs(Sm[xlt * LRX + kk]) : -1.0;
+            const double mx = g_max32(a);
+            const unsigned gb = (unsigned)(__ballot(a == mx) >> (grp * GW));
+            const int p = gb ? __ffs(gb) - 1 : kk;
+            if (t == 0) XL[XL_PIV + kk] = (double)p;
+            if (p != kk && t < nlr_w) {
+                const double x = Sm[kk * LRX + xlt], y = Sm[p * LRX + xlt];
+                Sm[kk * LRX + xlt] = y;
+                Sm[p * LRX + xlt] = x;
+            }
+            lds_sync();
+            const double rp = 1.0 / Sm[kk * LRX + kk];
+            const double ukt = Sm[kk * LRX + xlt];
+            for (int i = kk + 1; i < nlr_w; i++) {
+                const double l = Sm[i * LRX + kk] * rp;  // read by every lane before lane kk stores it (in order)
+                if (t > kk && t < nlr_w) Sm[i * LRX + xlt] -= l * ukt;
+                if (t == kk) Sm[i * LRX + kk] = l;
+            }
+            lds_sync();
+        }
+    };
+    // XL[slot + j] <- S^-1 XL[slot + j]: the row swaps in order (the multipliers were swapped with their rows),
+    // the unit lower solve, the upper solve; lane j holds entry j, the pivot entry is broadcast by a lane shuffle
+    auto xl_solve = [&](int slot) {
+        const double* const Sm = XL + XL_S;
+        const int base = grp * GW;
+        double v = (t < nlr_w) ? XL[slot + xlt] : 0.0;
+        for (int kk = 0; kk < nlr_w; kk++) {
+            const int p = (int)XL[XL_PIV + kk];
+            const int src = (t == kk) ? p : ((t == p) ? kk : t);
+            v = __shfl(v, base + src);
+        }
+        for (int kk = 0; kk < nlr_w; kk++) {
+            const double vk = __shfl(v, base + kk);
+            if (t > kk && t < nlr_w) v -= Sm[xlt * LRX + kk] * vk;
+        }
+        for (int kk = nlr_w - 1; kk >= 0; kk--) {
+            if (t == kk) v = v / Sm[kk * LRX + kk];
+            const double xk = __shfl(v, base + kk);
+            if (t < kk) v -= Sm[xlt * LRX + kk] * xk;
+        }
+        if (t < nlr_w) XL[slot + t] = v;
+        lds_sync();
+    };
+    // dz = dz_s - sum_j t_j Q_j of stage k (t = XL_TT)
+    auto xl_fix = [&](int k, double& x, double& v) {
+        for (int j = 0; j < nlr_w; j++) {
+            const double tj = XL[XL_TT + j];
+            x -= tj * *xq(j, k, 0);
+            v -= tj * *xq(j, k, 1);
+        }
+    };
+
     In cur, nxt;
     // light sweeps (no factorization), optionally without the prefetch buffer (MPCC_WIDE_LIGHT_NOPF)
     auto light_sweep = [&](bool backward, auto load, auto body) {
@@ -616,6 +803,7 @@ __device__ __forceinline__ void ipm_group(const DevConst& c, const DevBuffers& d
         if (lrw)
 #pragma unroll
             for (int j = 0; j < LRM; j++) uz[j] = g_sum32(uzp[j]);
+        if (xlw && run) xl_dots(XL_UZ, WF_ZX, WF_ZV);  // u_j^T z of the start point (v = 0)
 
         it = 0;
         double mu0 = 0.0, dz_prev = 1e30, sigma_mu = 0.0, mu_cur = 1e30, rp_cur = 1e30;
@@ -741,6 +929,12 @@ __device__ __forceinline__ void ipm_group(const DevConst& c, const DevBuffers& d
 #pragma unroll
                         for (int j = 0; j < LRM; j++) {
                             const double f = lrc[j] * uz[j];
+                            g0x += f * u_y(j, k);
+                            g0v += f * u_v(j, k);
+                        }
+                    if (xlw)
+                        for (int j = 0; j < nlr_w; j++) {
+                            const double f = XL[XL_C + j] * XL[XL_UZ + j];
                             g0x += f * u_y(j, k);
                             g0v += f * u_v(j, k);
                         }
@@ -1016,7 +1210,35 @@ __device__ __forceinline__ void ipm_group(const DevConst& c, const DevBuffers& d
 #pragma unroll
                     for (int j = 0; j < LRM; j++) { o.m[j] = *ws(k, WF_QX + j); o.m[LRM + j] = *ws(k, WF_QV + j); }
                 };
-                if (!lrw) {
+                auto load_xfix = [&](int k, In& o, bool corr) {  // the stored dz_s (and predictor step)
+                    load_common(k, o);
+                    o.x0 = *ws(k, WF_AX); o.x1 = *ws(k, WF_AV);
+                    o.x2 = corr ? *ws(k, WF_DX) : 0.0; o.x3 = corr ? *ws(k, WF_DV) : 0.0;
+                };
+                if (xlw) {
+                    xl_q();
+                    xl_smat_lu();
+#ifdef MPCC_IPM_TRACE
+                    trc_S0 = XL[XL_S];  // U[0][0] after the pivoting
+#endif
+                    light_sweep(false, [&](int k, In& o) { load_fwd(k, o, false); }, [&](int k, const In& cur) {
+                        double v = 0.0, xn = 0.0;
+                        fwd_step(cur, xt, v, xn);
+                        *ws(k, WF_AX) = xt;  // dz_s
+                        *ws(k, WF_AV) = (t < NU && k < N) ? v : 0.0;
+                        xt = (k < N) ? xn : 0.0;
+                    });
+                    xl_dots(XL_TT, WF_AX, WF_AV);
+                    xl_solve(XL_TT);
+#ifdef MPCC_IPM_TRACE
+                    trc_t0 = XL[XL_TT];
+#endif
+                    light_sweep(false, [&](int k, In& o) { load_xfix(k, o, false); }, [&](int k, const In& cur) {
+                        double xs = cur.x0, dvv = cur.x1;
+                        xl_fix(k, xs, dvv);
+                        pred_rec(k, cur, xs, dvv);
+                    });
+                } else if (!lrw) {
                     light_sweep(false, [&](int k, In& o) { load_fwd(k, o, false); }, [&](int k, const In& cur) {
                         double v = 0.0, xn = 0.0;
                         fwd_step(cur, xt, v, xn);
@@ -1164,7 +1386,23 @@ __device__ __forceinline__ void ipm_group(const DevConst& c, const DevBuffers& d
                     rec(aP, sgnU, cur.pub, pcz, pca, pcd, cur.sP, cur.lP);
                 };
                 xt = 0.0;
-                if (!lrw) {
+                if (xlw) {
+                    light_sweep(false, [&](int k, In& o) { load_fwd(k, o, false); }, [&](int k, const In& cur) {
+                        double v = 0.0, xn = 0.0;
+                        fwd_step(cur, xt, v, xn);
+                        *ws(k, WF_DX) = (t < NXA) ? xt : 0.0;  // dz_s
+                        *ws(k, WF_DV) = (t < NU && k < N) ? v : 0.0;
+                        xt = (k < N) ? xn : 0.0;
+                    });
+                    xl_dots(XL_TT, WF_DX, WF_DV);
+                    xl_solve(XL_TT);
+                    light_sweep(false, [&](int k, In& o) { load_xfix(k, o, true); }, [&](int k, const In& cur) {
+                        double xtt = cur.x2, dvv = cur.x3;
+                        xl_fix(k, xtt, dvv);
+                        corr_rec(k, cur, xtt, dvv, cur.x0, cur.x1);
+                    });
+                    xl_dots(XL_UD, WF_DX, WF_DV);  // u_j^T dz of the corrector step
+                } else if (!lrw) {
                     light_sweep(false, [&](int k, In& o) { load_fwd(k, o, true); }, [&](int k, const In& cur) {
                         double v = 0.0, xn = 0.0;
                         fwd_step(cur, xt, v, xn);
@@ -1210,9 +1448,16 @@ __device__ __forceinline__ void ipm_group(const DevConst& c, const DevBuffers& d
 #pragma unroll
                 for (int j = 0; j < LRM; j++) uz[j] += alpha * uzd[j];  // u_j^T z of the next iterate
 #ifdef MPCC_IPM_TRACE
+                const double trc_uz0 = xlw ? XL[XL_UZ] : uz[0] - alpha * uzd[0];
+#endif
+                if (xlw) {
+                    if (t < nlr_w) XL[XL_UZ + t] += alpha * XL[XL_UD + t];
+                    lds_sync();
+                }
+#ifdef MPCC_IPM_TRACE
                 if (b == 0 && t == 0)
                     printf("gpu it %2d mu %.6e amax %.6e sig %.6e amx %.6e alpha %.6e rp %.6e dz %.6e uz0 %.9e t0 %.9e S0 %.9e\n",
-                           it, mu, amax, sigma, amx, alpha, rpm, dzm, uz[0], trc_t0, trc_S0);
+                           it, mu, amax, sigma, amx, alpha, rpm, dzm, trc_uz0, trc_t0, trc_S0);
 #endif
                 sigma_mu = smu;
                 pending = true;
@@ -1263,7 +1508,7 @@ __global__ void __launch_bounds__(64) k_ipm(DevConst c, DevBuffers d) {
 }
 template <int NPM, bool LR>
 static void launch_ipm_t(const DevConst& c, const DevBuffers& d, hipStream_t s) {
-    hipLaunchKernelGGL((k_ipm<NPM, LR>), dim3((c.Bn + IPW - 1) / IPW), dim3(64), ipm_wide_lds_bytes(NPM), s, c, d);
+    hipLaunchKernelGGL((k_ipm<NPM, LR>), dim3((c.Bn + IPW - 1) / IPW), dim3(64), ipm_wide_lds_bytes(NPM, LR), s, c, d);
 }
 // one QP solve per active instance on the 32-lane interior point (lr: with the instances' low-rank terms)
 void launch_ipm_wide(const DevConst& c, const DevBuffers& d, int npmax, int lr, hipStream_t s) {
@@ -1346,7 +1591,9 @@ __device__ __forceinline__ double bfgs_hmul_elem(const DevConst& c, const double
             if (k + 1 <= N - 1) v += hct * sv[e + NXU];
         }
     }
-    for (int j = 0; j < nlr; j++) v += (lrcb[j] * us[j]) * lrb[(size_t)j * NS * NXU + e];
+#pragma unroll
+    for (int j = 0; j < LRX; j++)
+        if (j < nlr) v += (lrcb[j] * us[j]) * lrb[(size_t)j * NS * NXU + e];
     return v;
 }
 // the QP gradient (normalized grad_obj) of element e: Tx f_x / Tu f_u + ddq gradient (QS_q / QS_r)
@@ -1357,9 +1604,9 @@ __device__ __forceinline__ double bfgs_q_elem(const double* __restrict__ qsb, in
 }
 // u_j^T s over the horizon for the instance's low-rank terms (group reductions)
 __device__ __forceinline__ void bfgs_us(const double* __restrict__ lrb, const double* __restrict__ sv, int nlr, int NE, int t,
-                                        double (&us)[LRM]) {
+                                        double (&us)[LRX]) {
 #pragma unroll
-    for (int j = 0; j < LRM; j++) {
+    for (int j = 0; j < LRX; j++) {
         double p = 0.0;
         if (j < nlr)
             for (int e = t; e < NE; e += GW) p += lrb[(size_t)j * NE + e] * sv[e];
@@ -1374,8 +1621,8 @@ __device__ __attribute__((noinline)) bool bfgs_pre(const DevConst& c, const DevB
     int32_t* si = d.sqi + (size_t)b * SQI;
     const int nlr = si[SQ_NLR];
     const double* qsb = d.qs + (size_t)b * NS * QS;
-    double* lrb = d.lr + (size_t)b * LRM * NE;
-    const double* lrcb = d.lrc + (size_t)b * LRM;
+    double* lrb = d.lr + (size_t)b * LRX * NE;
+    const double* lrcb = d.lrc + (size_t)b * LRX;
     double* glam = d.glam + (size_t)b * NE;
     double* gprev = d.gprev + (size_t)b * NE;
     const double* sp = d.sp + (size_t)b * NE;
@@ -1386,7 +1633,7 @@ __device__ __attribute__((noinline)) bool bfgs_pre(const DevConst& c, const DevB
     // dgrad_L into slot nlr + 1, B step_prev into slot nlr (B of the previous iteration)
     double* bsv = lrb + (size_t)nlr * NE;
     double* dgv = lrb + (size_t)(nlr + 1) * NE;
-    double us[LRM];
+    double us[LRX];
     bfgs_us(lrb, sp, nlr, NE, t, us);
     double sbs = 0.0, sy = 0.0;
     for (int e = t; e < NE; e += GW) {
@@ -1414,7 +1661,7 @@ __device__ __attribute__((noinline)) bool bfgs_pre(const DevConst& c, const DevB
         dgv[e] = damp ? theta * dg + (1 - theta) * bsv[e] : dg;  // r
     }
     if (t == 0) {
-        double* lc = d.lrc + (size_t)b * LRM;
+        double* lc = d.lrc + (size_t)b * LRX;
         lc[nlr] = -1.0 / sbs;
         lc[nlr + 1] = 1.0 / sr;
         si[SQ_NLR] = nlr + 2;
@@ -1426,11 +1673,11 @@ __device__ __attribute__((noinline)) void bfgs_post_qp(const DevConst& c, const 
     const int N = c.N, NS = N + 1, NE = NS * NXU;
     const int nlr = d.sqi[(size_t)b * SQI + SQ_NLR];
     const double* qsb = d.qs + (size_t)b * NS * QS;
-    const double* lrb = d.lr + (size_t)b * LRM * NE;
-    const double* lrcb = d.lrc + (size_t)b * LRM;
+    const double* lrb = d.lr + (size_t)b * LRX * NE;
+    const double* lrcb = d.lrc + (size_t)b * LRX;
     const double* stp = d.step + (size_t)b * NE;
     double* aty = d.aty + (size_t)b * NE;
-    double us[LRM];
+    double us[LRX];
     bfgs_us(lrb, stp, nlr, NE, t, us);
     for (int e = t; e < NE; e += GW) aty[e] = -(bfgs_hmul_elem(c, qsb, stp, lrb, lrcb, us, nlr, N, e) + bfgs_q_elem(qsb, N, e));
 }
@@ -1513,7 +1760,7 @@ __global__ void __launch_bounds__(64) k_sqp(DevConst, DevBuffers, const double* 
 
 template <int NPM, bool LR>
 static void launch_sqp_t(const DevConst& c, const DevBuffers& d, const double* u_cur, hipStream_t s) {
-    hipLaunchKernelGGL((k_sqp<NPM, LR>), dim3((c.Bn + IPW - 1) / IPW), dim3(64), ipm_wide_lds_bytes(NPM), s, c, d, u_cur);
+    hipLaunchKernelGGL((k_sqp<NPM, LR>), dim3((c.Bn + IPW - 1) / IPW), dim3(64), ipm_wide_lds_bytes(NPM, LR), s, c, d, u_cur);
 }
 
 void launch_sqp_wide(const DevConst& c, const DevBuffers& d, const double* u_cur, int npmax, int bfgs, hipStream_t s) {
@@ -1536,7 +1783,7 @@ void launch_sqp_wide(const DevConst& c, const DevBuffers& d, const double* u_cur
 
 #if MPCC_DOF != 7
 // the mobile build's QP solver (the Panda build's is ipm.hip)
-size_t ipm_lds_bytes(int /*N*/, int npmax) { return ipm_wide_lds_bytes(npmax > 2 ? 11 : npmax); }
+size_t ipm_lds_bytes(int /*N*/, int npmax) { return ipm_wide_lds_bytes(npmax > 2 ? 11 : npmax, true); }
 void launch_ipm(const DevConst& c, const DevBuffers& d, int npmax, hipStream_t s) { launch_ipm_wide(c, d, npmax, 0, s); }
 void launch_sqp(const DevConst& c, const DevBuffers& d, const double* u_cur, int npmax, hipStream_t s) {
     launch_sqp_wide(c, d, u_cur, npmax, c.p.use_BFGS, s);

@@ -43,9 +43,12 @@ struct DevBuffers {
     // damped-BFGS option of either build
     double* isw;
     // damped BFGS (use_BFGS, osqp_interface.cpp:437-453, 683-715), per instance, horizon layout [(N+1)][NXU]:
-    // low-rank vectors lr [LRM][(N+1)*NXU] and coefficients lrc [LRM], A^T lambda (glam), grad_L of the previous
+    // low-rank vectors lr [LRX][(N+1)*NXU] and coefficients lrc [LRX], A^T lambda (glam), grad_L of the previous
     // iteration (gprev), A^T y of the last QP (aty), step_prev = alpha * step (sp)
     double *lr, *lrc, *glam, *gprev, *aty, *sp;
+    // more than LRM low-rank terms (max_iter > 1 + LRM / 2): per term and stage the Woodbury column Q_j = M u_j (x~
+    // and v parts) and the kff of its backward solve, [LRX][(N+1)][3][32 lanes]; null until such a max_iter is set
+    double* lrq;
 };
 // The fused SQP kernels (k_sqp of ipm.hip / ipm_wide.hip) are declared (DevConst c, DevBuffers d, const double*)
 // and hand c and d to their non-inlined phases by reference into the kernel-argument segment: a reference to the
@@ -64,7 +67,8 @@ constexpr int TRACE_W = 8, TRACE_IT = 4;  // qp status, ipm iters, obj, vio, acc
 constexpr int SQI = 8;  // int bookkeeping per instance: status, active, iter, nfilt, qp_status, ipm_iters, reject, nlr
 constexpr int SQ_REJECT = 6;
 constexpr int SQ_NLR = 7;  // low-rank BFGS terms held (2 per update)
-constexpr int LRM = 4;     // at most LRM low-rank terms: use_BFGS with max_iter <= 1 + LRM / 2
+constexpr int LRM = 4;     // low-rank terms carried in registers through the fused sweeps (use_BFGS, max_iter <= 3)
+constexpr int LRX = 28;    // low-rank terms held at most: use_BFGS with max_iter <= 1 + LRX / 2 (ipm_wide.hip xl_*)
 constexpr int ISW = 2048;  // doubles per stage of the 32-lane interior point's workspace (64 fields x 32 lanes)
 
 struct NNDesc {
@@ -86,7 +90,7 @@ void launch_soc(const DevConst& c, const DevBuffers& d, const double* u_cur, hip
 void launch_sqp(const DevConst& c, const DevBuffers& d, const double* u_cur, int npmax, hipStream_t s);
 // the fused SQP loop on the 32-lane interior point (ipm_wide.hip); bfgs = 1: damped BFGS Hessian updates
 void launch_sqp_wide(const DevConst& c, const DevBuffers& d, const double* u_cur, int npmax, int bfgs, hipStream_t s);
-size_t ipm_wide_lds_bytes(int npmax);
+size_t ipm_wide_lds_bytes(int npmax, bool lr);
 void launch_ipm_wide(const DevConst& c, const DevBuffers& d, int npmax, int lr, hipStream_t s);
 size_t ipm_lds_bytes(int N, int npmax);
 inline int poly_rows_max(int mask) {

@@ -37,10 +37,11 @@ def _lowrank_terms(o, rng, nlr):
     return lr, lrc
 
 
-@pytest.mark.parametrize("nlr", [1, 2, 4])
+@pytest.mark.parametrize("nlr", [1, 2, 4, 6, 12, 28])
 def test_lowrank_qp_step(built_lib, oracle_lib, nlr):
     """One QP with low-rank Hessian terms (the BFGS QP form) on the 32-lane interior point with the Woodbury
-    correction, against the oracle's structured (Riccati + Woodbury) and dense-Hessian solves."""
+    correction, against the oracle's structured (Riccati + Woodbury) and dense-Hessian solves.  nlr > 4: the
+    extended path (Woodbury columns and the capacitance LU in memory), up to LRX = 28 terms (max_iter 15)."""
     import mpcc_manipulator_amd as m
     o, P, track = make_oracle(N=20, max_iter=2, mask=7, nthreads=16)
     pool = oracle_pool(o, 40, obs=(0.48, 0.218, 0.521, 5.0))
@@ -158,6 +159,31 @@ def test_bfgs_with_soc_parity(built_lib, oracle_lib):
     eng = m.Engine(m.load_params(N=20, overrides=ov), max_batch=B, constraint_mask=2)
     eng.set_track(*track)
     xg, outg, stats, outo = _run(m, eng, o, x0, u0, obs, guess, valid, fails)
+    assert np.array_equal(outg["status"], outo["status"])
+    assert np.array_equal(stats["sqp_iter"], outo["sqp_iters"])
+    assert np.abs(outg["horizon"] - outo["horizon"]).max() <= 1e-6
+    eng.close()
+
+
+@pytest.mark.parametrize("mask,B", [(2, 256), (7, 128)])
+def test_bfgs_max_iter_10_parity(built_lib, oracle_lib, mask, B):
+    """use_BFGS at max_iter 10: with eps_prim 1e-4 many controllers run 4+ SQP iterations, so
+    their QPs hold 6..18 low-rank terms and go through the extended Woodbury path; status, SQP iterations and
+    the horizon as in test_bfgs_batch_parity."""
+    import mpcc_manipulator_amd as m
+    ov = {"sqp": {"max_iter": 10, "use_BFGS": 1, "eps_prim": 1e-4}}
+    o, P, track = make_oracle(N=20, max_iter=10, mask=mask, overrides=ov, nthreads=16)
+    assert P["use_BFGS"] == 1 and P["max_iter"] == 10
+    ob = (0.48, 0.218, 0.521, 5.0)
+    pool = oracle_pool(o, 100, obs=ob if mask == 7 else (3.0, 3.0, 3.0, 0.0))
+    rng = np.random.default_rng(SEED + 750 + mask)
+    obs = np.tile(ob, (B, 1)) if mask == 7 else None
+    x0, u0, obs, guess, valid, fails = batch_from_pool(pool, B, rng, obs=obs)
+    valid[::4] = 0
+    eng = m.Engine(m.load_params(N=20, overrides=ov), max_batch=B, constraint_mask=mask)
+    eng.set_track(*track)
+    xg, outg, stats, outo = _run(m, eng, o, x0, u0, obs, guess, valid, fails)
+    assert np.sum(outo["sqp_iters"] >= 4) >= B // 16, np.bincount(outo["sqp_iters"])  # > LRM terms in play
     assert np.array_equal(outg["status"], outo["status"])
     assert np.array_equal(stats["sqp_iter"], outo["sqp_iters"])
     assert np.abs(outg["horizon"] - outo["horizon"]).max() <= 1e-6
