@@ -143,6 +143,71 @@ __device__ __forceinline__ void mfma_layer_ring(const double* __restrict__ Wp, c
     __syncthreads();  // the ring is free for the next layer's first copies
 }
 
+// mfma_layer_ring with the A fragments read one k-step ahead: the fragment of row tile t is reloaded right after
+// its MFMA issues, with the next k-step's, so each LDS read has the other RT - 1 MFMAs of the k-step to land
+// (mfma_layer_ring read each fragment just before its MFMA: with one wave per SIMD the matrix core waited on the
+// LDS latency, profiles/r03bg_cfg2_env_k_mlp_env_pmc.json 65% SQ_WAIT_INST_ANY).  The next tile's first
+// fragments are read during the tile's last k-step, so its barrier (own copies landed, tile visible to the
+// block) moves to that k-step; the copy two tiles ahead is issued right after it, into the slot of the tile
+// every wave has finished reading.  Same MFMAs in the same order per row tile: bitwise mfma_layer.
+#ifndef MPCC_MLP_PF
+#define MPCC_MLP_PF 1
+#endif
+template <int KT, int RT>
+__device__ __forceinline__ void mfma_layer_ring_pf(const double* __restrict__ Wp, const d4 (&in)[KT], d4 (&out)[RT],
+                                                   int lane, double* __restrict__ ring /* RING_SLOTS x RT*256 */) {
+    constexpr int KS = 4 * KT;
+    constexpr int CH = RT * 256;
+    constexpr int PT = CH / 2 / 256;
+    static_assert(CH % 512 == 0, "mfma_layer_ring_pf: whole 16-byte copies per thread");
+    const int tid = threadIdx.x, w = tid >> 6;
+    const unsigned base = (unsigned)(uintptr_t)(__attribute__((address_space(3))) char*)(char*)ring;
+    auto issue = [&](int kt) {
+        const unsigned slot = base + (unsigned)((kt % RING_SLOTS) * CH * 8);
+#pragma unroll
+        for (int j = 0; j < PT; j++) {
+            const int e = tid + 256 * j;
+            const int t = e >> 7;
+            glds16_to(Wp + ((size_t)t * KS + 4 * kt) * 64 + 2 * (e & 127),
+                      __builtin_amdgcn_readfirstlane(slot + 4096u * j + 1024u * w));
+        }
+    };
+#pragma unroll
+    for (int t = 0; t < RT; t++) out[t] = d4{0.0, 0.0, 0.0, 0.0};
+    issue(0);
+    if (KT > 1) {
+        issue(1);
+        asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PT) : "memory");
+    } else {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    __syncthreads();
+    double fr[RT];
+#pragma unroll
+    for (int t = 0; t < RT; t++) fr[t] = ring[(t * 4) * 64 + lane];
+#pragma unroll
+    for (int kt = 0; kt < KT; kt++) {
+        const double* L = ring + (kt % RING_SLOTS) * CH;
+#pragma unroll
+        for (int r = 0; r < 4; r++) {
+            if (r == 3 && kt + 1 < KT) {
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's copies of tile kt + 1
+                __syncthreads();
+                if (kt + 2 < KT) issue(kt + 2);
+            }
+            const bool nxt = r < 3 || kt + 1 < KT;
+            const double* Ln = (r < 3) ? L : ring + ((kt + 1) % RING_SLOTS) * CH;
+            const int rn = (r < 3) ? r + 1 : 0;
+#pragma unroll
+            for (int t = 0; t < RT; t++) {
+                out[t] = __builtin_amdgcn_mfma_f64_16x16x4f64(fr[t], in[kt][r], out[t], 0, 0, 0);
+                if (nxt) fr[t] = Ln[(t * 4 + rn) * 64 + lane];
+            }
+        }
+    }
+    __syncthreads();  // the ring is free for the next layer's first copies
+}
+
 // hidden-layer epilogue: value columns h = relu(z + b); tangent columns dh = (z + b > 0) ? dz : 0.
 // CPS = columns per sample: 8 (value + 7 tangents, 2 samples per 16-column tile), 4 (value + 3 tangents, 4 samples
 // per tile: the mobile env network's obstacle directions) or 16 (value + up to 15 tangents, one sample per tile).
@@ -403,10 +468,18 @@ __device__ __forceinline__ void mlp_env_body(const DevConst& c, const DevBuffers
     if (threadIdx.x < 9) bl[1024 + threadIdx.x] = W[nd.offb[4] + threadIdx.x];
     d4 a0[2], a[16], h[16], o[1];
     nerf_input<10, CPS, D0>(x, a0, lane);
+#if MPCC_MLP_PF
+    mfma_layer_ring_pf<2, 16>(W + nd.offW[0], a0, a, lane, wl);
+#else
     mfma_layer_ring<2, 16>(W + nd.offW[0], a0, a, lane, wl);
+#endif
     relu_gate<16, CPS>(a, bl, lane);
     for (int l = 1; l <= 3; l++) {  // three 256 x 256 hidden layers share one unrolled body
+#if MPCC_MLP_PF
+        mfma_layer_ring_pf<16, 16>(W + nd.offW[l], a, h, lane, wl);
+#else
         mfma_layer_ring<16, 16>(W + nd.offW[l], a, h, lane, wl);
+#endif
         relu_gate<16, CPS>(h, bl + 256 * l, lane);
 #pragma unroll
         for (int t = 0; t < 16; t++) a[t] = h[t];
