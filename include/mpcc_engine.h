@@ -323,6 +323,11 @@ int mpcc_debug_bounds(mpcc_engine* e, uint32_t* flags, int clear);
 /* QP solves the fused kernels finished in tail mode (the wave's last running instance on all four 16-lane groups,
  * csrc/ipm_tail.h) since the last reset, over all engines of the process; Panda library, <= 2 polytopic rows */
 int mpcc_debug_tail_solves(long long* out, int reset);
+/* k_sqp's group slots of the last fused solve (csrc/kernels.hip k_order): out[i] = instance of 16-lane group slot i
+ * (wave i / 4), -1 empty, for 4 * (ceil(B / 4) + 64) slots, then k_prepare's cold-start flag of each instance [B];
+ * returns the number copied.  Cold-started instances get a wave of their own (solo waves); with solo waves off
+ * (MPCC_SOLO=0) k_order does not run and the slots are stale. */
+int mpcc_debug_order(mpcc_engine* e, int32_t* out, int n);
 
 /* Build provenance (no reference counterpart): a hash of the sources the library was compiled from
  * (csrc/ and include/, mpcc_manipulator_amd/_build.py source_hash) and the build's variant bits. */

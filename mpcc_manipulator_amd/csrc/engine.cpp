@@ -60,6 +60,7 @@ struct mpcc_engine {
     bool staged_sqp = false;
     bool wide_sqp = false;  // MPCC_WIDE_SQP=1: the 32-lane fused kernel for the Panda build too (experiment)
     int tail_mode = 1;      // MPCC_TAIL=0: no tail mode in k_sqp (A/B switch; results are bitwise the same)
+    int solo_mode = 1;      // MPCC_SOLO=0: no solo waves for cold starts in k_sqp (A/B switch; bitwise the same)
     bool last_wide = DOF != 7;  // the last solve's interior point ran on the 32-lane workspace (d.isw)
     uint32_t* bchk = nullptr;  // bounds-checked build: per-lane violation bits (dev_common.h MPCC_BCHK)
     mpcc_params params{};
@@ -99,7 +100,7 @@ struct mpcc_engine {
     ~mpcc_engine() {
         auto f = [](void* p) { if (p) (void)hipFree(p); };
         f(d_spl);
-        f(d.guess); f(d.valid); f(d.fails); f(d.rec); f(d.qs); f(d.is); f(d.step); f(d.trial); f(d.sqi); f(d.sqd);
+        f(d.guess); f(d.valid); f(d.fails); f(d.rec); f(d.qs); f(d.is); f(d.step); f(d.trial); f(d.sqi); f(d.sqd); f(d.order);
         if (d.isw != d.is) f(d.isw);
         f(d.lr); f(d.lrc); f(d.glam); f(d.gprev); f(d.aty); f(d.sp); f(d.lrq);
         f(d.dbg_trace);
@@ -403,7 +404,14 @@ void run_batch(mpcc_engine* e, int B, hipStream_t st, mpcc_timing* timing, bool 
         if (tm) a1 = mark();
         e->last_wide = DOF != 7 || c.p.use_BFGS || e->wide_sqp;
         if (c.p.use_BFGS || e->wide_sqp) launch_sqp_wide(c, d, ucur, poly_rows_max(c.p.constraint_mask), c.p.use_BFGS ? 1 : 0, st);
-        else launch_sqp(c, d, ucur, poly_rows_max(c.p.constraint_mask), st);
+        else if (e->solo_mode && e->tail_mode && !c.ocp) {  // cold starts alone in a wave (k_prepare flags them)
+            DevConst cs = c;
+            cs.solo = 1;
+            launch_order(cs, d, st);
+            launch_sqp(cs, d, ucur, poly_rows_max(c.p.constraint_mask), st);
+        } else {
+            launch_sqp(c, d, ucur, poly_rows_max(c.p.constraint_mask), st);
+        }
         launched = true;
         if (tm) {
             b1 = mark();
@@ -513,6 +521,18 @@ int mpcc_debug_tail_solves(long long* out, int /*reset*/) {
 }
 #endif
 
+int mpcc_debug_order(mpcc_engine* e, int32_t* out, int n) {
+    if (!e || !out || n < 0) return fail(MPCC_E_INVALID, "mpcc_debug_order: invalid argument");
+    n = std::min(n, order_slots(e->maxB) + e->maxB);
+    try {
+        HIPCHK(hipStreamSynchronize(e->stream));
+        HIPCHK(hipMemcpy(out, e->d.order, (size_t)n * sizeof(int32_t), hipMemcpyDeviceToHost));
+    } catch (const std::exception& x) {
+        return fail(MPCC_E_HIP, std::string("mpcc_debug_order: ") + x.what());
+    }
+    return n;
+}
+
 int mpcc_create(const mpcc_config* cfg, const mpcc_params* params, const char* nn_dir, mpcc_engine** out) {
     if (!cfg || !params || !out) return fail(MPCC_E_INVALID, "mpcc_create: null argument");
     std::unique_ptr<mpcc_engine> e(new mpcc_engine());
@@ -524,6 +544,8 @@ int mpcc_create(const mpcc_config* cfg, const mpcc_params* params, const char* n
         e->wide_sqp = wd && wd[0] == '1';
         const char* tl = std::getenv("MPCC_TAIL");
         e->tail_mode = (tl && tl[0] == '0') ? 0 : 1;
+        const char* so = std::getenv("MPCC_SOLO");
+        e->solo_mode = (so && so[0] == '0') ? 0 : 1;
         e->params = *params;
         e->params.N = cfg->N;
         e->params.Ts = cfg->Ts;
@@ -549,6 +571,7 @@ int mpcc_create(const mpcc_config* cfg, const mpcc_params* params, const char* n
         d.trial = dmalloc<double>(B * NS * 4);
         d.sqi = dmalloc<int32_t>(B * SQI);
         d.sqd = dmalloc<double>(B * SQ);
+        d.order = dmalloc<int32_t>((size_t)order_slots((int)B) + B);
         HIPCHK(hipMemset(d.guess, 0, B * NS * NXU * sizeof(double)));
         HIPCHK(hipMemset(d.valid, 0, B * sizeof(int32_t)));
         HIPCHK(hipMemset(d.fails, 0, B * sizeof(int32_t)));

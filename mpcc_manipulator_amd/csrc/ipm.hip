@@ -218,6 +218,13 @@ __device__ __forceinline__ void mu_acc(double& S0, double& S1, double& S2, doubl
 // the reason of mu_acc (which product the compiler fuses depends on the surrounding code, and tail mode evaluates the
 // same expressions in another function)
 __device__ __forceinline__ double fma2(double a, double b, double c, double d) { return fma(a, b, c * d); }
+// instance of 16-lane group slot `slot` of the launch: k_sqp with solo waves maps slots through d.order (k_order),
+// every other launch is the identity; an empty slot is c.Bn (not valid)
+__device__ __forceinline__ int inst_of(const DevConst& c, const DevBuffers& d, int slot) {
+    if (!c.solo) return slot;
+    const int v = d.order[slot];
+    return v < 0 ? c.Bn : v;
+}
 // corrector step of a slot given the iterate (cz), the predictor step (ca) and the corrector step (cd)
 __device__ __forceinline__ SlotStep slot_corr(double sgn, double bnd, double cz, double ca, double cd, double s, double l,
                                               double smu, double* rp_out) {
@@ -428,7 +435,7 @@ __device__ __forceinline__ bool ipm_group(const DevConst& c, const DevBuffers& d
     const int lane = threadIdx.x;
     const int grp = lane >> 4;
     const int t = lane & 15;
-    const int b = blockIdx.x * IPW + grp;
+    const int b = inst_of(c, d, blockIdx.x * IPW + grp);
     const int N = c.N;
     const int NS = N + 1;
     double* const S = smem + grp * GRP_LDS;
@@ -1636,7 +1643,7 @@ __global__ void __launch_bounds__(64) k_sqp(DevConst, DevBuffers, const double* 
     const DevConst& c = kernarg_const();     // the arguments in place (kernels.h kernarg_const)
     const DevBuffers& d = kernarg_buffers();
     const int t = threadIdx.x & 15;
-    const int b = blockIdx.x * IPW + (threadIdx.x >> 4);
+    const int b = inst_of(c, d, blockIdx.x * IPW + (threadIdx.x >> 4));
     const bool valid = b < c.Bn;
     const int N = c.N, NS = N + 1;
     const int bb = valid ? b : 0;
@@ -1708,7 +1715,8 @@ static void launch_ipm_t(const DevConst& c, const DevBuffers& d, hipStream_t s) 
 }
 template <int NPM>
 static void launch_sqp_t(const DevConst& c, const DevBuffers& d, const double* u_cur, hipStream_t s) {
-    hipLaunchKernelGGL(k_sqp<NPM>, dim3((c.Bn + IPW - 1) / IPW), dim3(64), ipm_lds_bytes(c.N, NPM), s, c, d, u_cur);
+    const int waves = c.solo ? order_slots(c.Bn) / IPW : (c.Bn + IPW - 1) / IPW;
+    hipLaunchKernelGGL(k_sqp<NPM>, dim3(waves), dim3(64), ipm_lds_bytes(c.N, NPM), s, c, d, u_cur);
 }
 
 void launch_ipm(const DevConst& c, const DevBuffers& d, int npmax, hipStream_t s) {

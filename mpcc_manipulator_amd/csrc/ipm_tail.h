@@ -58,7 +58,7 @@ __device__ __attribute__((noinline)) void ipm_tail(const DevConst& c, const DevB
     const int lane = threadIdx.x;
     const int g = lane >> 4;
     const int t = lane & 15;
-    const int b = blockIdx.x * IPW + gs;
+    const int b = inst_of(c, d, blockIdx.x * IPW + gs);
     const int N = c.N;
     const int NS = N + 1;
 
@@ -1003,7 +1003,7 @@ __device__ __attribute__((noinline)) void ipm_tail_solve(const DevConst& c, cons
         it_total += io.it;
     }
     const int lane = threadIdx.x, t = lane & 15;
-    const int b = blockIdx.x * IPW + gs;
+    const int b = inst_of(c, d, blockIdx.x * IPW + gs);
     const int N = c.N, NS = N + 1;
     int32_t* si = d.sqi + (size_t)b * SQI;
 #ifdef MPCC_IPM_PROF

@@ -49,7 +49,15 @@ struct DevBuffers {
     // more than LRM low-rank terms (max_iter > 1 + LRM / 2): per term and stage the Woodbury column Q_j = M u_j (x~
     // and v parts) and the kff of its backward solve, [LRX][(N+1)][3][32 lanes]; null until such a max_iter is set
     double* lrq;
+    // k_sqp's instance of each 16-lane group slot ([4 * (ceil(Bn / 4) + NSOLO)], -1: none) followed by the per-instance
+    // cold-start flags of this step ([Bn], written by k_prepare); k_order builds the slots (solo waves)
+    int32_t* order;
 };
+// Cold-started controllers (a regenerated initial guess) are the ones that take a second SQP iteration; k_sqp
+// gives each of the first NSOLO of them a wave of its own (tail mode from its first IPM iteration), so that they do
+// not set the launch's length from inside a 4-instance wave
+constexpr int NSOLO = 64;
+__host__ __device__ inline int order_slots(int Bn) { return 4 * ((Bn + 3) / 4 + NSOLO); }
 // The fused SQP kernels (k_sqp of ipm.hip / ipm_wide.hip) are declared (DevConst c, DevBuffers d, const double*)
 // and hand c and d to their non-inlined phases by reference into the kernel-argument segment: a reference to the
 // by-value parameter itself makes the compiler copy the 5.4 KB DevConst into every lane's private segment (a
@@ -79,6 +87,8 @@ struct NNDesc {
 };
 
 void launch_prepare(const DevConst& c, const DevBuffers& d, hipStream_t s);
+// k_sqp's slot -> instance map from k_prepare's cold-start flags (c.solo launches)
+void launch_order(const DevConst& c, const DevBuffers& d, hipStream_t s);
 void launch_stage_records(const DevConst& c, const DevBuffers& d, hipStream_t s);
 void launch_nn(const DevConst& c, const DevBuffers& d, const NNDesc& nd, const double* W, int which, int M,
                const double* q, const double* obs, double* rec, int rec_stride, hipStream_t s);

@@ -52,6 +52,7 @@ __device__ inline void prepare_mpc(const DevConst& c, const DevBuffers& d, int b
     x[XVS] = ev[0] * dir[0] + ev[1] * dir[1] + ev[2] * dir[2];
     int valid = d.valid[b], fails = d.fails[b];
     if (fabs(last_s - x[XS]) > c.p.guess_max_dist) { valid = 0; fails++; }
+    if (j == 0 && d.order) d.order[order_slots(c.Bn) + b] = valid ? 0 : 1;  // cold start this step (k_order)
     double* g = d.guess + (size_t)b * (N + 1) * NXU;
     // updateInitialGuess (mpc.cpp:54-68) element by element: stage i < N takes old stage min(i, N - 2) + 1 (the shift,
     // then g[N-1] = g[N-2]) with the state of stage 0 replaced by x; stage N is RK4 of the new stage N - 1 with a zero
@@ -418,12 +419,46 @@ __global__ void k_debug_cost(DevConst c, int M, const double* __restrict__ x, co
 }
 
 // ------------------------------------------------------------------------------------------------
+// k_order: k_sqp's group slots.  The first NSOLO cold-started instances (ascending) get slot 4 r of wave r, alone in
+// it; every other instance (ascending) is packed 4 per wave after them; unused slots hold -1.  One block.
+// ------------------------------------------------------------------------------------------------
+__global__ void __launch_bounds__(1024) k_order(DevConst c, DevBuffers d) {
+    const int Bn = c.Bn, NSL = order_slots(Bn);
+    int32_t* slot = d.order;
+    const int32_t* cold = d.order + NSL;
+    const int tid = threadIdx.x;
+    for (int i = tid; i < NSL; i += 1024) slot[i] = -1;
+    const int per = (Bn + 1023) / 1024, lo = tid * per, hi = min(Bn, lo + per);
+    int n = 0;
+    for (int b = lo; b < hi; b++) n += cold[b] != 0;
+    __shared__ int sc[1024];
+    sc[tid] = n;
+    __syncthreads();
+    for (int off = 1; off < 1024; off <<= 1) {  // inclusive scan
+        const int v = tid >= off ? sc[tid - off] : 0;
+        __syncthreads();
+        sc[tid] += v;
+        __syncthreads();
+    }
+    int cb = sc[tid] - n;  // cold instances before lo
+    for (int b = lo; b < hi; b++) {
+        const bool cd = cold[b] != 0;
+        if (cd && cb < NSOLO) slot[4 * cb] = b;
+        else slot[4 * NSOLO + b - min(cb, NSOLO)] = b;
+        if (cd) cb++;
+    }
+}
+
+// ------------------------------------------------------------------------------------------------
 // launch wrappers
 // ------------------------------------------------------------------------------------------------
 static inline int nblk(long n, int t) { return (int)((n + t - 1) / t); }
 
 void launch_prepare(const DevConst& c, const DevBuffers& d, hipStream_t s) {
     hipLaunchKernelGGL(k_prepare, dim3(nblk((long)c.Bn * PL, 64)), dim3(64), 0, s, c, d);
+}
+void launch_order(const DevConst& c, const DevBuffers& d, hipStream_t s) {
+    hipLaunchKernelGGL(k_order, dim3(1), dim3(1024), 0, s, c, d);
 }
 void launch_stage_records(const DevConst& c, const DevBuffers& d, hipStream_t s) {
     hipLaunchKernelGGL(k_records, dim3(nblk((long)c.S * RPT, 64)), dim3(64), 0, s, c, d);

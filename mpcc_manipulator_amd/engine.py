@@ -181,6 +181,7 @@ def lib(dof=7):
         "mpcc_robot_frames": (C.c_int, [C.c_int, C.c_int, DP, C.c_int, DP, DP, DP, DP, DP]),
         "mpcc_debug_bounds": (C.c_int, [V, C.POINTER(C.c_uint32), C.c_int]),
         "mpcc_debug_tail_solves": (C.c_int, [C.POINTER(C.c_longlong), C.c_int]),
+        "mpcc_debug_order": (C.c_int, [V, IP, C.c_int]),
         "mpcc_build_id": (C.c_char_p, []),
         "mpcc_build_flags": (C.c_int, []),
         "mpcc_timing_mlp": (C.c_int, [V, C.POINTER(D), IP, C.POINTER(D), IP]),
@@ -675,6 +676,14 @@ class Engine:
         v = C.c_longlong()
         self._check(self.L.mpcc_debug_tail_solves(C.byref(v), 1 if reset else 0), "mpcc_debug_tail_solves")
         return int(v.value)
+
+    def order(self, n):
+        """k_sqp's instance per 16-lane group slot of the last fused solve (-1: empty; csrc/kernels.hip k_order)."""
+        out = np.zeros(n, dtype=np.int32)
+        got = self.L.mpcc_debug_order(self.h, out.ctypes.data_as(C.POINTER(C.c_int)), n)
+        if got < 0:
+            self._check(got, "mpcc_debug_order")
+        return out[:got]
 
     def bounds_flags(self, clear=True):
         """Bounds-checked build (MPCC_BOUNDS_CHECK): OR of the index-violation bits recorded by every kernel since

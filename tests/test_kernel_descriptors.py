@@ -13,10 +13,10 @@ import pytest
 
 LLVM = "/opt/rocm/lib/llvm/bin"
 # sizeof(DevConst) at this revision: the kernel-argument segment of k_ipm<9> (DevConst + DevBuffers, then the 256
-# bytes of HIP's hidden arguments) minus DevBuffers' 28 pointers (224 bytes).  Any private segment this large could
+# bytes of HIP's hidden arguments) minus DevBuffers' 29 pointers (232 bytes).  Any private segment this large could
 # hold a copy.
-DEVCONST_BYTES = 3280
-DEVBUFFERS_PTRS = 28
+DEVCONST_BYTES = 3288
+DEVBUFFERS_PTRS = 29
 PANDA_NARROW_MAX = 1740   # 1.7 KB: k_sqp / k_ipm of ipm.hip (16-lane interior point, tail mode included)
 WIDE_MAX = 2400           # 2.3 KB: the 32-lane kernels of ipm_wide.hip (mobile build, damped BFGS incl. the extended low-rank path)
 

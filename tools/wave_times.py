@@ -42,18 +42,25 @@ def main():
         for _ in range(3):
             eng.set_warmstart(*ws)
             eng.solve(*[v.copy() for v in a])
-        nw = (B + 3) // 4
+        solo = os.environ.get("MPCC_SOLO", "1") != "0"
+        nw = (B + 3) // 4 + (64 if solo else 0)  # solo waves: the group slots map through eng.order
+        slots = eng.order(4 * nw).reshape(-1, 4) if solo else np.arange(4 * nw).reshape(-1, 4)
+        slots = np.where(slots < B, slots, -1)
         buf = (C.c_ulonglong * (2 * nw))()
         assert wt(buf, nw) == nw
         t = np.frombuffer(buf, dtype=np.uint64).astype(np.int64)
-        st, en = t[:nw], t[nw:]
+        live = (slots >= 0).any(axis=1)  # waves with an instance (empty ones exit at once)
+        st, en = t[:nw][live], t[nw:][live]
+        slots = slots[live]
         t0 = st.min()
         st_us, en_us = (st - t0) / 100.0, (en - t0) / 100.0  # 100 MHz -> us
         stats = eng.solve_stats(B)
         ib = (C.c_int * B)()
         assert L.mpcc_debug_inst_ipm_iters(ib, B) == B
-        it = np.frombuffer(ib, dtype=np.int32).reshape(-1, 4)  # IPM iterations summed over the instance's QPs
-        sq = stats["sqp_iter"].reshape(-1, 4)
+        its = np.frombuffer(ib, dtype=np.int32)  # IPM iterations summed over the instance's QPs
+        it = np.where(slots >= 0, its[np.maximum(slots, 0)], 0)
+        sq = np.where(slots >= 0, stats["sqp_iter"][np.maximum(slots, 0)], 0)
+        nw = len(slots)
         wmax = it.max(axis=1)
         res = {"batch": B, "waves": nw, "launch_us": float(en_us.max()), "start_spread_us": float(st_us.max()),
                "end_quantiles_us": {q: float(np.percentile(en_us, q)) for q in (10, 50, 90, 99, 99.9, 100)},
