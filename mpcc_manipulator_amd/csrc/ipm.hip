@@ -131,6 +131,7 @@ constexpr int PROF_WAVES = 1 << 16;
 __device__ unsigned long long g_wave_t[2 * PROF_WAVES];
 __device__ int g_inst_its[4 * PROF_WAVES];
 __device__ unsigned long long g_tail_prof[16];  // tail mode: factor A, B, C, D, predictor fwd, corrector bwd, fwd; iterations; B sub-sections
+__device__ unsigned long long g_solo_prof[8];   // solo waves of k_sqp: cycles in setqp, QP solve, trial, accept, step; waves, SQP iterations
 #define TMARK(i) do { const long long t_ = clock64(); tprof[i] += t_ - tprof_t; tprof_t = t_; } while (0)
 #define PMARK(i) do { const long long t_ = clock64(); prof_acc[i] += t_ - prof_t; prof_t = t_; } while (0)
 #else
@@ -1565,6 +1566,14 @@ extern "C" int mpcc_debug_inst_ipm_iters(int* out, int n) {  // IPM iterations o
     if (n > 4 * PROF_WAVES) n = 4 * PROF_WAVES;
     return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_inst_its), sizeof(int) * n) == hipSuccess ? n : -1;
 }
+extern "C" int mpcc_debug_solo_prof(unsigned long long* out, int reset) {
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_solo_prof), sizeof(unsigned long long) * 8) != hipSuccess) return -1;
+    if (reset) {
+        unsigned long long z[8] = {0};
+        if (hipMemcpyToSymbol(HIP_SYMBOL(g_solo_prof), z, sizeof z) != hipSuccess) return -1;
+    }
+    return 0;
+}
 extern "C" int mpcc_debug_ipm_prof(unsigned long long* out, int reset) {
     if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_ipm_prof), sizeof(unsigned long long) * 16) != hipSuccess) return -1;
     if (reset) {
@@ -1587,18 +1596,19 @@ extern "C" int mpcc_debug_ipm_prof(unsigned long long* out, int reset) {
 // ------------------------------------------------------------------------------------------------
 // Phases of k_sqp as separate (non-inlined) functions: each has its own register allocation, so the
 // QP assembly and trial code does not add live ranges to the register-resident interior point.
-__device__ __attribute__((noinline)) void sqp_setqp_phase(const DevConst& c, const DevBuffers& d, int b, int t,
+// the per-stage phases of k_sqp: lane t of st lanes works on stages t, t + st, ... (st = 16, a solo wave: 64)
+__device__ __attribute__((noinline)) void sqp_setqp_phase(const DevConst& c, const DevBuffers& d, int b, int t, int st,
                                                           const double* __restrict__ ucur) {
     const int N = c.N, NS = N + 1;
     const SplineView sp = spl_of(c.spl, b);
     const double* gb = d.guess + (size_t)b * NS * 17;
-    for (int k = t; k <= N; k += 16)
+    for (int k = t; k <= N; k += st)
         setqp_stage(c, sp, gb, RecView{d.rec + (size_t)b * NS + k, c.S}, k, ucur, d.qs + ((size_t)b * NS + k) * QS);
 }
-__device__ __attribute__((noinline)) void sqp_trial_phase(const DevConst& c, const DevBuffers& d, int b, int t,
+__device__ __attribute__((noinline)) void sqp_trial_phase(const DevConst& c, const DevBuffers& d, int b, int t, int st,
                                                           const double* __restrict__ ucur, double alpha, bool keep) {
     const int N = c.N, NS = N + 1;
-    for (int k = t; k <= N; k += 16) {
+    for (int k = t; k <= N; k += st) {
         double out[4];
         trial_stage(c, d, b, k, alpha, ucur, out);
         if (keep) {
@@ -1607,12 +1617,12 @@ __device__ __attribute__((noinline)) void sqp_trial_phase(const DevConst& c, con
         }
     }
 }
-__device__ __attribute__((noinline)) void sqp_soc_phase(const DevConst& c, const DevBuffers& d, int b, int t,
+__device__ __attribute__((noinline)) void sqp_soc_phase(const DevConst& c, const DevBuffers& d, int b, int t, int st,
                                                         const double* __restrict__ ucur) {
     const int N = c.N, NS = N + 1;
     const SplineView sp = spl_of(c.spl, b);
     const size_t o = (size_t)b * NS * 17;
-    for (int k = t; k <= N; k += 16)
+    for (int k = t; k <= N; k += st)
         soc_stage(c, sp, d.guess + o, d.step + o, RecView{d.rec + (size_t)b * NS + k, c.S}, k, ucur,
                   d.qs + ((size_t)b * NS + k) * QS);
 }
@@ -1649,36 +1659,59 @@ __global__ void __launch_bounds__(64) k_sqp(DevConst, DevBuffers, const double* 
     const int bb = valid ? b : 0;
     int32_t* si = d.sqi + (size_t)bb * SQI;
     const double* ucur = ucur_all + 8 * bb;
+    // a wave holding one instance (a solo wave, or the batch's last) runs that instance's per-stage phases (QP
+    // assembly, line-search trial, correction bounds) on all 64 lanes, one stage per lane
+    const unsigned long long lead = __ballot(valid && t == 0);
+    const bool one = __popcll(lead) == 1;
+    const int pb = one ? __shfl(b, __ffsll((long long)lead) - 1) : b;  // the instance of this lane's stage phases
+    const int pt = one ? (int)threadIdx.x : t, pst = one ? 64 : 16;
+    const int pbb = pb < c.Bn ? pb : 0;
+    const int32_t* psi = d.sqi + (size_t)pbb * SQI;
+    const double* pucur = ucur_all + 8 * pbb;
 #ifdef MPCC_IPM_PROF
     if (threadIdx.x == 0 && blockIdx.x < PROF_WAVES) g_wave_t[blockIdx.x] = __builtin_amdgcn_s_memrealtime();
     if (t == 0 && b < 4 * PROF_WAVES) g_inst_its[b] = 0;
+    const bool solo_w = __popcll(__ballot(valid && t == 0)) == 1;
+    long long sp_t = clock64(), sp_acc[5] = {0, 0, 0, 0, 0};
+    int sp_it = 0;
+#define SPMARK(i) do { const long long t_ = clock64(); sp_acc[i] += t_ - sp_t; sp_t = t_; } while (0)
+#else
+#define SPMARK(i) do { } while (0)
 #endif
     for (int it = 0; it < c.p.max_iter; it++) {
         bool act = valid && si[SQ_ACTIVE] != 0;
         if (__ballot(act) == 0) break;
+#ifdef MPCC_IPM_PROF
+        sp_it++;
+#endif
+        SPMARK(4);
         if (it > 0) {
-            if (act) sqp_setqp_phase(c, d, b, t, ucur);
+            if (pb < c.Bn && psi[SQ_ACTIVE] != 0) sqp_setqp_phase(c, d, pb, pt, pst, pucur);
             __syncthreads();
         }
+        SPMARK(0);
         sqp_qp_solve<NPM>(c, d, smem);
         __syncthreads();
+        SPMARK(1);
         if (c.p.do_SOC) {  // SecondOrderCorrection (osqp_interface.cpp:506-535): same P, q, A, shifted bounds
-            act = valid && si[SQ_ACTIVE] != 0;
-            if (act) sqp_soc_phase(c, d, b, t, ucur);
+            if (pb < c.Bn && psi[SQ_ACTIVE] != 0) sqp_soc_phase(c, d, pb, pt, pst, pucur);
             __syncthreads();
             sqp_qp_solve<NPM>(c, d, smem);  // a failed correction keeps the step (Q6)
             __syncthreads();
         }
         act = valid && si[SQ_ACTIVE] != 0;
-        if (act) sqp_trial_phase(c, d, b, t, ucur, 1.0, true);
+        const bool pact = pb < c.Bn && psi[SQ_ACTIVE] != 0;
+        if (pact) sqp_trial_phase(c, d, pb, pt, pst, pucur, 1.0, true);
         __syncthreads();
+        SPMARK(2);
         if (act && t == 0) accept_instance(c, d, b);
         __syncthreads();
-        if (act && c.faithful_dead_trials && si[SQ_REJECT]) {  // discarded trials (Q5), evaluated for timing fidelity
+        SPMARK(3);
+        if (pact && c.faithful_dead_trials && psi[SQ_REJECT]) {  // discarded trials (Q5), evaluated for timing fidelity
             double alpha = 1.0;
             for (int l = 1; l < c.p.line_search_max_iter; l++) {
                 alpha *= c.p.line_search_tau;
-                sqp_trial_phase(c, d, b, t, ucur, alpha, false);
+                sqp_trial_phase(c, d, pb, pt, pst, pucur, alpha, false);
             }
         }
         double nrm = 0.0;
@@ -1691,8 +1724,15 @@ __global__ void __launch_bounds__(64) k_sqp(DevConst, DevBuffers, const double* 
         __syncthreads();
     }
 #ifdef MPCC_IPM_PROF
+    SPMARK(4);
     if (threadIdx.x == 0 && blockIdx.x < PROF_WAVES) g_wave_t[PROF_WAVES + blockIdx.x] = __builtin_amdgcn_s_memrealtime();
+    if (solo_w && threadIdx.x == 0) {
+        for (int i = 0; i < 5; i++) atomicAdd(&g_solo_prof[i], (unsigned long long)sp_acc[i]);
+        atomicAdd(&g_solo_prof[5], 1ull);
+        atomicAdd(&g_solo_prof[6], (unsigned long long)sp_it);
+    }
 #endif
+#undef SPMARK
 }
 
 }  // namespace mpcc
