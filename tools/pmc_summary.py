@@ -40,6 +40,9 @@ def main():
     ap.add_argument("--kernel", default="k_sqp")
     ap.add_argument("--ipw", type=int, default=4, help="instances per wavefront (4 Panda, 2 mobile build)")
     ap.add_argument("--ns", default="mpcc", help="kernel namespace (mpcc_m10 for the mobile build)")
+    ap.add_argument("--grid", type=int, default=None,
+                    help="grid size (threads) of the profiled launches (default: batch / ipw waves; k_sqp with solo "
+                         "waves launches 64 more)")
     ap.add_argument("--traffic-name", default=None,
                     help="traffic file name under profiles/ (default pmc_traffic_<kernel>.json, read by bench.py)")
     args = ap.parse_args()
@@ -48,7 +51,7 @@ def main():
     stats = glob.glob(os.path.join(args.dir, "trace", "*kernel_stats.csv"))
     if stats:
         shutil.copy(stats[0], os.path.join(prof, f"{args.round}_kernel_stats.csv"))
-    grid = (args.batch + args.ipw - 1) // args.ipw * 64
+    grid = args.grid or (args.batch + args.ipw - 1) // args.ipw * 64
     merged = collections.defaultdict(dict)
     for p in ("p1", "p2", "p3", "p4", "p5"):
         for k, v in load_pmc(args.dir, p).items():
