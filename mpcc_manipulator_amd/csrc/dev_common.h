@@ -110,7 +110,7 @@ struct DevConst {
     int faithful_dead_trials;
     int ocp;                         // 1: SolverInterface::solveOCP only (mpcc_solve_ocp), no MPC bookkeeping
     int tail;                        // 1: k_sqp's interior point runs a wave's last active instance in tail mode
-    int solo;                        // 1 (k_sqp launches): group slots map to instances through d.order (solo waves)
+    int solo;                        // k_sqp launches: group slots map to instances through d.order: 1 solo waves, 2 solo blocks
     uint32_t* bchk;                  // bounds-checked build: per-lane violation bits (null otherwise)
 };
 

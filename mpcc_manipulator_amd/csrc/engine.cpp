@@ -60,12 +60,15 @@ struct mpcc_engine {
     bool staged_sqp = false;
     bool wide_sqp = false;  // MPCC_WIDE_SQP=1: the 32-lane fused kernel for the Panda build too (experiment)
     int tail_mode = 1;      // MPCC_TAIL=0: no tail mode in k_sqp (A/B switch; results are bitwise the same)
-    int solo_mode = 1;      // MPCC_SOLO=0: no solo waves for cold starts in k_sqp (A/B switch; bitwise the same)
+    int solo_mode = 2;      // MPCC_SOLO: 0 no solo waves for cold starts in k_sqp, 1 solo waves, 2 (default) solo blocks
+                            // (narrow variants; A/B switch, bitwise the same)
     bool last_wide = DOF != 7;  // the last solve's interior point ran on the 32-lane workspace (d.isw)
     uint32_t* bchk = nullptr;  // bounds-checked build: per-lane violation bits (dev_common.h MPCC_BCHK)
     mpcc_params params{};
     int N = 0, maxB = 0;
     hipStream_t stream = nullptr;
+    hipStream_t solo_stream = nullptr;  // k_sqp_solo (solo blocks), forked from and joined to `stream` per launch
+    hipEvent_t solo_fork = nullptr, solo_join = nullptr;
     SplineTables track;
     bool has_track = false;
     double* d_spl = nullptr;
@@ -110,6 +113,9 @@ struct mpcc_engine {
         for (auto ev : events) (void)hipEventDestroy(ev);
         for (auto ev : live_pool) (void)hipEventDestroy(ev);
         if (stream) (void)hipStreamDestroy(stream);
+        if (solo_stream) (void)hipStreamDestroy(solo_stream);
+        if (solo_fork) (void)hipEventDestroy(solo_fork);
+        if (solo_join) (void)hipEventDestroy(solo_join);
     }
 
     void set_model() {
@@ -404,11 +410,24 @@ void run_batch(mpcc_engine* e, int B, hipStream_t st, mpcc_timing* timing, bool 
         if (tm) a1 = mark();
         e->last_wide = DOF != 7 || c.p.use_BFGS || e->wide_sqp;
         if (c.p.use_BFGS || e->wide_sqp) launch_sqp_wide(c, d, ucur, poly_rows_max(c.p.constraint_mask), c.p.use_BFGS ? 1 : 0, st);
-        else if (e->solo_mode && e->tail_mode && !c.ocp) {  // cold starts alone in a wave (k_prepare flags them)
+        else if (e->solo_mode && e->tail_mode && !c.ocp) {  // cold starts alone in a wave / block (k_prepare flags them)
             DevConst cs = c;
+            const int npm = poly_rows_max(c.p.constraint_mask);
             cs.solo = 1;
             launch_order(cs, d, st);
-            launch_sqp(cs, d, ucur, poly_rows_max(c.p.constraint_mask), st);
+            if (e->solo_mode == 2 && DOF == 7 && npm <= 2) {
+                // solo blocks: k_sqp_solo on the side stream beside k_sqp (which leaves the solo waves to it), joined
+                // before anything after k_sqp
+                cs.solo = 2;
+                HIPCHK(hipEventRecord(e->solo_fork, st));
+                HIPCHK(hipStreamWaitEvent(e->solo_stream, e->solo_fork, 0));
+                launch_sqp_solo(cs, d, ucur, npm, e->solo_stream);
+                HIPCHK(hipEventRecord(e->solo_join, e->solo_stream));
+                launch_sqp(cs, d, ucur, npm, st);
+                HIPCHK(hipStreamWaitEvent(st, e->solo_join, 0));
+            } else {
+                launch_sqp(cs, d, ucur, npm, st);
+            }
         } else {
             launch_sqp(c, d, ucur, poly_rows_max(c.p.constraint_mask), st);
         }
@@ -545,7 +564,7 @@ int mpcc_create(const mpcc_config* cfg, const mpcc_params* params, const char* n
         const char* tl = std::getenv("MPCC_TAIL");
         e->tail_mode = (tl && tl[0] == '0') ? 0 : 1;
         const char* so = std::getenv("MPCC_SOLO");
-        e->solo_mode = (so && so[0] == '0') ? 0 : 1;
+        e->solo_mode = (so && so[0] == '0') ? 0 : (so && so[0] == '1') ? 1 : 2;
         e->params = *params;
         e->params.N = cfg->N;
         e->params.Ts = cfg->Ts;
@@ -559,6 +578,9 @@ int mpcc_create(const mpcc_config* cfg, const mpcc_params* params, const char* n
         // stream, or any NULL-stream copy of the inputs) is ordered before and after the engine's
         // kernels, as the ABI's "NULL = engine stream" would otherwise race with it.
         HIPCHK(hipStreamCreateWithFlags(&e->stream, hipStreamDefault));
+        HIPCHK(hipStreamCreateWithFlags(&e->solo_stream, hipStreamNonBlocking));
+        HIPCHK(hipEventCreateWithFlags(&e->solo_fork, hipEventDisableTiming));
+        HIPCHK(hipEventCreateWithFlags(&e->solo_join, hipEventDisableTiming));
         const size_t B = (size_t)e->maxB, NS = (size_t)e->N + 1;
         DevBuffers& d = e->d;
         d.guess = dmalloc<double>(B * NS * NXU);

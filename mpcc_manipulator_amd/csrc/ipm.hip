@@ -114,6 +114,14 @@ __host__ __device__ constexpr int ring_q(int npm) { return npm <= 2 ? QLINES : Q
 __host__ __device__ constexpr int ring_d(int npm) { return npm <= 2 ? LRING : LRING_W; }
 static_assert(LF_CBWD + 1 <= NWF, "the odd last line of a ring slot reads one field past the run");
 
+// doubles of LDS per k_sqp wave
+__host__ __device__ constexpr int ipm_wave_lds(int npmax) {
+    const int uk = IPW * GRP_LDS;
+    const int ring = (npmax <= 2)     ? LRING * LG(LF_CBWD) * 128
+                     : use_ring(npmax) ? LRING_W * LG(WF_PD, QLINES_W) * 128
+                                       : 0;
+    return ring > uk ? ring : uk;
+}
 size_t ipm_lds_bytes(int /*N*/, int npmax) {
     const size_t uk = (size_t)IPW * GRP_LDS * sizeof(double);
     const size_t ring = (npmax <= 2)          ? (size_t)LRING * LG(LF_CBWD) * 1024
@@ -1632,11 +1640,41 @@ template <int NPM>
 __device__ __attribute__((noinline)) bool sqp_ipm_phase(const DevConst& c, const DevBuffers& d, double* smem) {
     return ipm_group<NPM>(c, d, smem);
 }
+// Solo blocks (k_sqp_solo): wave 0 runs a cold-started instance's SQP, wave 1 helps in each of its
+// tail-mode QP solves.  The helper waits at the block barrier for wave 0's post: 1 = a solve (ipm_tail_solve on all
+// SB_GB groups), 0 = the end.  Wave 0 meets the block's barriers only at its posts and inside ipm_tail_solve.
 template <int NPM>
+__device__ __attribute__((noinline)) void solo_helper(const DevConst& c, const DevBuffers& d, double* smem) {
+    while (true) {
+        __syncthreads();
+        const double cmd = smem[SB_CMD];
+        if (cmd == 0.0) break;
+        ipm_tail_solve<NPM, SB_GB>(c, d, smem);
+    }
+}
+__device__ __forceinline__ void solo_post(double* smem, double cmd) {
+    if (threadIdx.x == 0) smem[SB_CMD] = cmd;
+    __syncthreads();
+}
+template <int NPM, bool SB = false>
 __device__ __forceinline__ void sqp_qp_solve(const DevConst& c, const DevBuffers& d, double* smem) {
     if (sqp_ipm_phase<NPM>(c, d, smem)) {
-        if constexpr (NPM <= 2) ipm_tail_solve<NPM>(c, d, smem);
+        if constexpr (NPM <= 2) {
+            if constexpr (SB) {
+                solo_post(smem, 1.0);
+                ipm_tail_solve<NPM, SB_GB>(c, d, smem);
+            } else {
+                ipm_tail_solve<NPM>(c, d, smem);
+            }
+        }
     }
+}
+// wave 0 of a solo block: the ordering of the SQP phases within the wave (some lanes' global stores before other
+// lanes' loads) without the barrier of __syncthreads, which the helper wave does not meet there
+__device__ __forceinline__ void wave_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
 }
 
 // k_ipm: one QP solve per active instance (the staged SQP loop of run_batch and the debug QP entry); its arguments
@@ -1647,11 +1685,14 @@ __global__ void __launch_bounds__(64) k_ipm(DevConst, DevBuffers) {
     sqp_qp_solve<NPM>(kernarg_const(), kernarg_buffers(), smem);
 }
 
-template <int NPM>
-__global__ void __launch_bounds__(64) k_sqp(DevConst, DevBuffers, const double* __restrict__ ucur_all) {
-    extern __shared__ __attribute__((aligned(16))) double smem[];
-    const DevConst& c = kernarg_const();     // the arguments in place (kernels.h kernarg_const)
-    const DevBuffers& d = kernarg_buffers();
+// the SQP loop of one wave (k_sqp: each wave; k_sqp_solo: wave 0 of a solo block, SB)
+template <int NPM, bool SB>
+__device__ __forceinline__ void sqp_waves(const DevConst& c, const DevBuffers& d, const double* __restrict__ ucur_all,
+                                          double* smem) {
+    auto bar = [] {
+        if constexpr (SB) wave_sync();
+        else __syncthreads();
+    };
     const int t = threadIdx.x & 15;
     const int b = inst_of(c, d, blockIdx.x * IPW + (threadIdx.x >> 4));
     const bool valid = b < c.Bn;
@@ -1687,25 +1728,25 @@ __global__ void __launch_bounds__(64) k_sqp(DevConst, DevBuffers, const double* 
         SPMARK(4);
         if (it > 0) {
             if (pb < c.Bn && psi[SQ_ACTIVE] != 0) sqp_setqp_phase(c, d, pb, pt, pst, pucur);
-            __syncthreads();
+            bar();
         }
         SPMARK(0);
-        sqp_qp_solve<NPM>(c, d, smem);
-        __syncthreads();
+        sqp_qp_solve<NPM, SB>(c, d, smem);
+        bar();
         SPMARK(1);
         if (c.p.do_SOC) {  // SecondOrderCorrection (osqp_interface.cpp:506-535): same P, q, A, shifted bounds
             if (pb < c.Bn && psi[SQ_ACTIVE] != 0) sqp_soc_phase(c, d, pb, pt, pst, pucur);
-            __syncthreads();
-            sqp_qp_solve<NPM>(c, d, smem);  // a failed correction keeps the step (Q6)
-            __syncthreads();
+            bar();
+            sqp_qp_solve<NPM, SB>(c, d, smem);  // a failed correction keeps the step (Q6)
+            bar();
         }
         act = valid && si[SQ_ACTIVE] != 0;
         const bool pact = pb < c.Bn && psi[SQ_ACTIVE] != 0;
         if (pact) sqp_trial_phase(c, d, pb, pt, pst, pucur, 1.0, true);
-        __syncthreads();
+        bar();
         SPMARK(2);
         if (act && t == 0) accept_instance(c, d, b);
-        __syncthreads();
+        bar();
         SPMARK(3);
         if (pact && c.faithful_dead_trials && psi[SQ_REJECT]) {  // discarded trials (Q5), evaluated for timing fidelity
             double alpha = 1.0;
@@ -1721,8 +1762,9 @@ __global__ void __launch_bounds__(64) k_sqp(DevConst, DevBuffers, const double* 
         }
         nrm = g_max(nrm);  // DPP: whole row active
         if (act && t == 0) finish_iteration(c, d, b, nrm);
-        __syncthreads();
+        bar();
     }
+    if constexpr (SB) solo_post(smem, 0.0);  // the helper leaves
 #ifdef MPCC_IPM_PROF
     SPMARK(4);
     if (threadIdx.x == 0 && blockIdx.x < PROF_WAVES) g_wave_t[PROF_WAVES + blockIdx.x] = __builtin_amdgcn_s_memrealtime();
@@ -1733,6 +1775,32 @@ __global__ void __launch_bounds__(64) k_sqp(DevConst, DevBuffers, const double* 
     }
 #endif
 #undef SPMARK
+}
+
+// k_sqp: every wave its slots' instances.  With solo blocks (c.solo 2) the first NSOLO waves (k_order's solo waves)
+// are k_sqp_solo's and return at once.
+template <int NPM>
+__global__ void __launch_bounds__(64) k_sqp(DevConst, DevBuffers, const double* __restrict__ ucur_all) {
+    extern __shared__ __attribute__((aligned(16))) double smem[];
+    const DevConst& c = kernarg_const();     // the arguments in place (kernels.h kernarg_const)
+    const DevBuffers& d = kernarg_buffers();
+    if (c.solo == 2 && blockIdx.x < NSOLO) return;
+    sqp_waves<NPM, false>(c, d, ucur_all, smem);
+}
+// k_sqp_solo (c.solo 2, launched beside k_sqp on a second stream): block r holds solo wave r's cold-started instance
+// (k_order's slot 4 r); wave 0 runs its SQP, wave 1 joins its tail-mode QP solves (solo_helper).  A block without a
+// cold instance returns at once.
+template <int NPM>
+__global__ void __launch_bounds__(64 * SB_WAVES) k_sqp_solo(DevConst, DevBuffers, const double* __restrict__ ucur_all) {
+    extern __shared__ __attribute__((aligned(16))) double smem[];
+    const DevConst& c = kernarg_const();
+    const DevBuffers& d = kernarg_buffers();
+    if (d.order[blockIdx.x * IPW] < 0) return;
+    if (threadIdx.x >= 64) {
+        solo_helper<NPM>(c, d, smem);
+        return;
+    }
+    sqp_waves<NPM, true>(c, d, ucur_all, smem);
 }
 
 }  // namespace mpcc
@@ -1758,6 +1826,11 @@ static void launch_sqp_t(const DevConst& c, const DevBuffers& d, const double* u
     const int waves = c.solo ? order_slots(c.Bn) / IPW : (c.Bn + IPW - 1) / IPW;
     hipLaunchKernelGGL(k_sqp<NPM>, dim3(waves), dim3(64), ipm_lds_bytes(c.N, NPM), s, c, d, u_cur);
 }
+template <int NPM>
+static void launch_sqp_solo_t(const DevConst& c, const DevBuffers& d, const double* u_cur, hipStream_t s) {
+    hipLaunchKernelGGL(k_sqp_solo<NPM>, dim3(NSOLO), dim3(64 * SB_WAVES), SB_WAVES * ipm_lds_bytes(c.N, NPM), s, c, d,
+                       u_cur);
+}
 
 void launch_ipm(const DevConst& c, const DevBuffers& d, int npmax, hipStream_t s) {
     switch (npmax) {
@@ -1767,6 +1840,14 @@ void launch_ipm(const DevConst& c, const DevBuffers& d, int npmax, hipStream_t s
         case 9: launch_ipm_t<9>(c, d, s); break;
         case 10: launch_ipm_t<10>(c, d, s); break;
         default: launch_ipm_t<11>(c, d, s); break;
+    }
+}
+bool launch_sqp_solo(const DevConst& c, const DevBuffers& d, const double* u_cur, int npmax, hipStream_t s) {
+    switch (npmax) {
+        case 0: launch_sqp_solo_t<0>(c, d, u_cur, s); return true;
+        case 1: launch_sqp_solo_t<1>(c, d, u_cur, s); return true;
+        case 2: launch_sqp_solo_t<2>(c, d, u_cur, s); return true;
+        default: return false;  // tail mode (and so solo blocks): narrow variants only
     }
 }
 void launch_sqp(const DevConst& c, const DevBuffers& d, const double* u_cur, int npmax, hipStream_t s) {

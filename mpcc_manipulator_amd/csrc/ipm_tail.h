@@ -48,17 +48,40 @@ constexpr int TL_LC = TL_LB + 4 * 16 * 2;       // C -> D: per slot row (L, U, P
 constexpr int TL_LM = TL_LC + 4 * 16 * 14;      // per-group combine scratch: 64 lanes x 4
 static_assert((TL_STATE + 16) * 8 <= LRING * LG(LF_CBWD) * 1024, "tail-mode LDS inside the narrow variants' ring");
 static_assert((TL_LM + 64 * 4) * 8 <= LRING * LG(LF_CBWD) * 1024, "tail-mode LDS inside the narrow variants' ring");
+// The same layout for GB 16-lane groups (GB / 4 waves of one workgroup: solo blocks); GB = 4 is the
+// layout above.  Phase B's P exchange uses the K area of the wave's first group.
+template <int GB>
+struct TailLayout {
+    static constexpr int A = 0, LF = A + GB * 16 * TL_SA, U = LF + GB * 48, K = U + GB * 16 * 10, C = K + GB * 144;
+    static constexpr int END = C + GB * 16 * 18;
+    static constexpr int LA = 0, LB = LA + GB * 16 * 18, LC = LB + GB * 16 * 2, LM = LC + GB * 16 * 14;
+    static constexpr int LEND = LM + GB * 16 * 4;
+    static constexpr int SIZE = END > LEND ? END : LEND;
+};
+static_assert(TailLayout<4>::END == TL_END && TailLayout<4>::LM == TL_LM && TailLayout<4>::K == TL_K, "GB = 4 layout");
+// a solo block: SB_WAVES waves on one instance; the command word (wave 0 -> helper waves) is the last double of the
+// block's ring slices, past the SB_GB-group layout
+constexpr int SB_WAVES = 2, SB_GB = 4 * SB_WAVES;
+constexpr int WAVE_LDS = LRING * LG(LF_CBWD) * 1024 / 8;  // doubles of LDS per k_sqp wave (narrow variants)
+constexpr int SB_CMD = SB_WAVES * WAVE_LDS - 1;
+static_assert(TailLayout<SB_GB>::SIZE <= SB_CMD && TL_STATE + 16 <= SB_CMD, "solo-block LDS");
 
-template <int NPM>
-__device__ __attribute__((noinline)) void ipm_tail(const DevConst& c, const DevBuffers& d, double* smem, int gs, TailIO& io) {
+template <int NPM, int GB>
+__device__ __attribute__((noinline)) void ipm_tail(const DevConst& c, const DevBuffers& d, double* smem, int b, TailIO& io) {
     static_assert(NPM <= 2, "tail mode: narrow variants");
+    static_assert(GB % 4 == 0, "whole waves");
     using namespace dpp;
+    using TLy = TailLayout<GB>;
+    constexpr int NWV = GB / 4;  // waves on the instance
+    constexpr int TL_A = TLy::A, TL_LF = TLy::LF, TL_U = TLy::U, TL_K = TLy::K, TL_C = TLy::C;
+    constexpr int TL_LA = TLy::LA, TL_LB = TLy::LB, TL_LC = TLy::LC, TL_LM = TLy::LM;
     constexpr int NPE = NPM > 0 ? NPM : 1;
     using In = StageIn<NPE>;
-    const int lane = threadIdx.x;
-    const int g = lane >> 4;
+    const int lane = threadIdx.x & 63;
+    const int wv = NWV > 1 ? (int)(threadIdx.x >> 6) : 0;
+    const int g = lane >> 4;      // group in the wave (phase B's MFMA operand selects)
+    const int G = wv * 4 + g;     // group on the instance: its stage in phases A and C
     const int t = lane & 15;
-    const int b = inst_of(c, d, blockIdx.x * IPW + gs);
     const int N = c.N;
     const int NS = N + 1;
 
@@ -75,7 +98,7 @@ __device__ __attribute__((noinline)) void ipm_tail(const DevConst& c, const DevB
         asm("" : "+v"(qk));
         return qk;
     };
-    auto lds = [&](int off) -> double* { return smem + MPCC_BCHK(c.bchk, off, TL_END > TL_LM + 256 ? TL_END : TL_LM + 256, BC_LDS); };
+    auto lds = [&](int off) -> double* { return smem + MPCC_BCHK(c.bchk, off, TLy::SIZE, BC_LDS); };
 
     // ---- model constants of this lane (as ipm_group)
     const double m78 = c.M[7 * 9 + 8], m77 = c.M[7 * 10], m88 = c.M[8 * 10];
@@ -107,7 +130,7 @@ __device__ __attribute__((noinline)) void ipm_tail(const DevConst& c, const DevB
         if (a == 8 && t == 8) v = fma(m78 * m78, Pc7[7], v);
         return v;
     };
-    const bool own = g == 0;  // the group that stores what all four groups computed redundantly (phases B, D)
+    const bool own = G == 0;  // the group that stores what all groups computed redundantly (phases B, D)
 
     // ---- stage loaders (ipm_group's, PACKP form)
     auto load_common = [&](int k, In& o) {
@@ -231,21 +254,27 @@ __device__ __attribute__((noinline)) void ipm_tail(const DevConst& c, const DevB
         else xn = vj;
     };
     auto sync = [] { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); };
+    // between phases: the wave's LDS order, or with more than one wave a workgroup barrier (its fences also order
+    // one wave's workspace stores before the other's loads)
+    auto bsync = [] {
+        if constexpr (NWV == 1) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        else __syncthreads();
+    };
     // slot j of an exchange area: lane t's fields at base + (j * 16 + t) * stride
     auto xs = [&](int base, int j, int stride) -> double* { return lds(base + (j * 16 + t) * stride); };
-    // combine per-group values across the 4 groups (every lane gets groups 0..3 of its t, in order)
-    auto gather4 = [&](double v, double (&o)[4]) {
+    // max of per-group values over the GB groups (every lane gets the max over the groups of its t)
+    auto maxG = [&](double v) {
         sync();
-        *lds(TL_LM + lane) = v;
-        sync();
+        *lds(TL_LM + wv * 64 + lane) = v;
+        bsync();
+        double o[GB];
 #pragma unroll
-        for (int q = 0; q < 4; q++) o[q] = *lds(TL_LM + q * 16 + t);
-        sync();
-    };
-    auto max4 = [&](double v) {
-        double o[4];
-        gather4(v, o);
-        return fmax(fmax(fmax(o[0], o[1]), o[2]), o[3]);
+        for (int q = 0; q < GB; q++) o[q] = *lds(TL_LM + q * 16 + t);
+        bsync();
+        double m = o[0];
+#pragma unroll
+        for (int q = 1; q < GB; q++) m = fmax(m, o[q]);
+        return m;
     };
 
 #ifdef MPCC_IPM_PROF
@@ -289,6 +318,7 @@ __device__ __attribute__((noinline)) void ipm_tail(const DevConst& c, const DevB
             bk = bkn;
         }
         mcount = g_sum(mcount);
+        if constexpr (NWV > 1) bsync();  // the start point's stores before any group's loads
     }
 
     while (true) {
@@ -298,10 +328,10 @@ __device__ __attribute__((noinline)) void ipm_tail(const DevConst& c, const DevB
         bool chol_ok = true;
 #pragma unroll
         for (int a = 0; a < 16; a++) Pc[a] = 0.0;
-        for (int kb = N; kb >= 0; kb -= 4) {
+        for (int kb = N; kb >= 0; kb -= GB) {
             // ---- A: group g, stage kb - g: lazy update, slots, gradient, P-independent parts of F, Gm, Hb
             {
-                const int kg = kb - g;
+                const int kg = kb - G;
                 const bool vA = kg >= 0;
                 const int k = vA ? kg : 0;
                 In cur;
@@ -429,7 +459,7 @@ __device__ __attribute__((noinline)) void ipm_tail(const DevConst& c, const DevB
 #ifdef MPCC_IPM_DBGF
                 if (vA && k < N) { *ws(k, 35) = gx; *ws(k, 36) = gv; *ws(k, 39) = dvr; *ws(k, 40) = cP; *ws(k, 41) = wd; }
 #endif
-                double* o = xs(TL_A, g, TL_SA);
+                double* o = xs(TL_A, G, TL_SA);
                 double2* o2 = reinterpret_cast<double2*>(o);
                 o2[0] = make_double2(gx, gv);
                 o2[1] = make_double2(g0v, wd);
@@ -441,10 +471,10 @@ __device__ __attribute__((noinline)) void ipm_tail(const DevConst& c, const DevB
 #pragma unroll
                 for (int i = 0; i < 4; i++) o2[11 + i] = make_double2(hb9[2 * i], hb9[2 * i + 1]);
             }
-            sync();
+            bsync();
             TMARK(0);
             // ---- B: the P recursion, stage after stage on all groups
-            for (int j = 0; j < 4; j++) {
+            for (int j = 0; j < GB; j++) {
                 const int k = kb - j;
                 if (k < 0) break;
                 const double2* a2 = reinterpret_cast<const double2*>(xs(TL_A, j, TL_SA));
@@ -506,7 +536,7 @@ __device__ __attribute__((noinline)) void ipm_tail(const DevConst& c, const DevB
                 if (own) { *ws(k, 44) = Pc[0]; *ws(k, 45) = LF[35]; *ws(k, 46) = dinv[7]; *ws(k, 47) = u[0]; *ws(k, 49) = Y[0]; *ws(k, 50) = Fc[0]; }
 #endif
                 // hand L, its pivots and U to phase C
-                if (lane == 0) {
+                if (lane == 0 && wv == 0) {
                     double2* lf = reinterpret_cast<double2*>(lds(TL_LF + j * 48));
 #pragma unroll
                     for (int q = 0; q < 18; q++) lf[q] = make_double2(LF[2 * q], LF[2 * q + 1]);
@@ -557,7 +587,7 @@ __device__ __attribute__((noinline)) void ipm_tail(const DevConst& c, const DevB
                         }
                     acc = __builtin_amdgcn_mfma_f64_16x16x4f64(-ua, ua, acc, 0, 0, 0);
                     acc = __builtin_amdgcn_mfma_f64_16x16x4f64(-ub, ub, acc, 0, 0, 0);
-                    double* Sp = lds(TL_K + t * 18);  // row t: P[0..15][t] (stride 18: conflict-free, 16-byte aligned)
+                    double* Sp = lds(TL_K + wv * 576 + t * 18);  // row t: P[0..15][t] (stride 18: conflict-free, 16-byte aligned)
 #pragma unroll
                     for (int r = 0; r < 4; r++) Sp[g + 4 * r] = acc[r];
                     sync();
@@ -597,13 +627,13 @@ __device__ __attribute__((noinline)) void ipm_tail(const DevConst& c, const DevB
                 }
                 TMARK(12);
             }
-            sync();
+            bsync();
             TMARK(1);
             // ---- C: group g, stage kb - g (< N): K = -LF^-T U, F^-1 column, the gain stores
             {
-                const int kg = kb - g;
+                const int kg = kb - G;
                 const bool vC = kg >= 0 && kg < N;
-                const double2* lf = reinterpret_cast<const double2*>(lds(TL_LF + g * 48));
+                const double2* lf = reinterpret_cast<const double2*>(lds(TL_LF + G * 48));
                 double LF[36], dinv[8];
 #pragma unroll
                 for (int q = 0; q < 18; q++) { const double2 v = lf[q]; LF[2 * q] = v.x; LF[2 * q + 1] = v.y; }
@@ -611,7 +641,7 @@ __device__ __attribute__((noinline)) void ipm_tail(const DevConst& c, const DevB
                 for (int q = 0; q < 4; q++) { const double2 v = lf[18 + q]; dinv[2 * q] = v.x; dinv[2 * q + 1] = v.y; }
                 double kc[8];
                 {
-                    const double2* ui = reinterpret_cast<const double2*>(xs(TL_U, g, 10));
+                    const double2* ui = reinterpret_cast<const double2*>(xs(TL_U, G, 10));
 #pragma unroll
                     for (int q = 0; q < 4; q++) { const double2 v = ui[q]; kc[2 * q] = v.x; kc[2 * q + 1] = v.y; }
                 }
@@ -629,11 +659,11 @@ __device__ __attribute__((noinline)) void ipm_tail(const DevConst& c, const DevB
                 for (int i = 0; i < 8; i++) fi[i] = (i == (t & 7)) ? 1.0 : 0.0;
                 fwd8(LF, dinv, fi);
                 bwd8(LF, dinv, fi);
-                double* Sk = lds(TL_K + g * 144);
+                double* Sk = lds(TL_K + G * 144);
 #pragma unroll
                 for (int i = 0; i < 8; i++) Sk[i * 16 + t] = kc[i];
                 {
-                    double2* co = reinterpret_cast<double2*>(xs(TL_C, g, 18));
+                    double2* co = reinterpret_cast<double2*>(xs(TL_C, G, 18));
 #pragma unroll
                     for (int q = 0; q < 4; q++) co[q] = make_double2(kc[2 * q], kc[2 * q + 1]);
 #pragma unroll
@@ -655,10 +685,10 @@ __device__ __attribute__((noinline)) void ipm_tail(const DevConst& c, const DevB
                     for (int m = 0; m < 4; m++) *ws(kg, WF_FI + m) = (t < 8) ? fi[m] : fi[4 + m];
                 }
             }
-            sync();
+            bsync();
             TMARK(2);
             // ---- D: the p recursion, stage after stage (f = g_v + B~^T p, kff = -F^-1 f, p = g_x~ + A~^T p + K^T f)
-            for (int j = 0; j < 4; j++) {
+            for (int j = 0; j < GB; j++) {
                 const int k = kb - j;
                 if (k < 0) break;
                 if (k == N) continue;  // p_N = g_x~ (phase B)
@@ -700,7 +730,7 @@ __device__ __attribute__((noinline)) void ipm_tail(const DevConst& c, const DevB
 #endif
                 pv = pnew;
             }
-            sync();
+            bsync();
             TMARK(3);
         }
         if (!chol_ok) {
@@ -716,22 +746,22 @@ __device__ __attribute__((noinline)) void ipm_tail(const DevConst& c, const DevB
         // forward light sweep in blocks k = kb + j: A loads (and exports the gains), B rolls x~ out, C does the slot
         // algebra of its stage (body), D accumulates the sums in stage order (acc)
         auto fwd_sweep = [&](bool corr, auto body, auto acc) {
-            for (int kb = 0; kb <= N; kb += 4) {
-                const int kg = kb + g;
+            for (int kb = 0; kb <= N; kb += GB) {
+                const int kg = kb + G;
                 const bool vA = kg <= N;
                 const int k = vA ? kg : N;
                 In cur;
                 load_fwd(k, cur, corr);
                 {
-                    double* o = xs(TL_LA, g, 18);
+                    double* o = xs(TL_LA, G, 18);
                     double2* o2 = reinterpret_cast<double2*>(o);
 #pragma unroll
                     for (int q = 0; q < 4; q++) o2[q] = make_double2(cur.m[2 * q], cur.m[2 * q + 1]);
                     o[8] = cur.m[8];
                 }
-                sync();
+                bsync();
                 if (!corr) TMARK(13);
-                for (int j = 0; j < 4; j++) {
+                for (int j = 0; j < GB; j++) {
                     const int kk = kb + j;
                     if (kk > N) break;
                     const double* mi = xs(TL_LA, j, 18);
@@ -744,19 +774,19 @@ __device__ __attribute__((noinline)) void ipm_tail(const DevConst& c, const DevB
                     *reinterpret_cast<double2*>(xs(TL_LB, j, 2)) = make_double2(xt, dvv);
                     xt = xn;
                 }
-                sync();
+                bsync();
                 if (!corr) TMARK(14);
                 {
-                    const double2 xv = *reinterpret_cast<const double2*>(xs(TL_LB, g, 2));
+                    const double2 xv = *reinterpret_cast<const double2*>(xs(TL_LB, G, 2));
                     double rr[14];
                     body(k, vA, cur, xv.x, xv.y, rr);
-                    double2* o2 = reinterpret_cast<double2*>(xs(TL_LC, g, 14));
+                    double2* o2 = reinterpret_cast<double2*>(xs(TL_LC, G, 14));
 #pragma unroll
                     for (int q = 0; q < 7; q++) o2[q] = make_double2(rr[2 * q], rr[2 * q + 1]);
                 }
-                sync();
+                bsync();
                 if (!corr) TMARK(15);
-                for (int j = 0; j < 4; j++) {
+                for (int j = 0; j < GB; j++) {
                     if (kb + j > N) break;
                     const double2* r2 = reinterpret_cast<const double2*>(xs(TL_LC, j, 14));
                     double rr[14];
@@ -764,7 +794,7 @@ __device__ __attribute__((noinline)) void ipm_tail(const DevConst& c, const DevB
                     for (int q = 0; q < 7; q++) { const double2 v = r2[q]; rr[2 * q] = v.x; rr[2 * q + 1] = v.y; }
                     acc(rr);
                 }
-                sync();
+                bsync();
             }
         };
         fwd_sweep(false, [&](int k, bool vA, const In& cur, double xt_k, double dvv, double (&rr)[14]) {
@@ -810,9 +840,9 @@ __device__ __attribute__((noinline)) void ipm_tail(const DevConst& c, const DevB
         // ================= corrector backward: A coefficients and gradients (4 stages), B the p recursion
         {
             double pvc = 0.0;
-            for (int kb = N; kb >= 0; kb -= 4) {
+            for (int kb = N; kb >= 0; kb -= GB) {
                 {
-                    const int kg = kb - g;
+                    const int kg = kb - G;
                     const bool vA = kg >= 0;
                     const int k = vA ? kg : 0;
                     In cur;
@@ -835,13 +865,13 @@ __device__ __attribute__((noinline)) void ipm_tail(const DevConst& c, const DevB
                     const double dvr = sgnL * cL + sgnU * cU;
                     double gx, gv;
                     assemble_grad(cur, k, cur.x2, cur.x3, dvr, cP, gx, gv);
-                    double2* o2 = reinterpret_cast<double2*>(xs(TL_LA, g, 18));
+                    double2* o2 = reinterpret_cast<double2*>(xs(TL_LA, G, 18));
                     o2[0] = make_double2(gx, gv);
 #pragma unroll
                     for (int q = 0; q < 6; q++) o2[1 + q] = make_double2(cur.m[2 * q], cur.m[2 * q + 1]);
                 }
-                sync();
-                for (int j = 0; j < 4; j++) {
+                bsync();
+                for (int j = 0; j < GB; j++) {
                     const int k = kb - j;
                     if (k < 0) break;
                     const double2* a2 = reinterpret_cast<const double2*>(xs(TL_LA, j, 18));
@@ -888,7 +918,7 @@ __device__ __attribute__((noinline)) void ipm_tail(const DevConst& c, const DevB
                     const double ktf = (lo1 ? r2[0] : r2[1]) + quad_swap1(lo1 ? r2[1] : r2[0]);
                     pvc = gxa + ktf;
                 }
-                sync();
+                bsync();
             }
         }
 
@@ -932,8 +962,8 @@ __device__ __attribute__((noinline)) void ipm_tail(const DevConst& c, const DevB
             }
             amc.add(rr[12], -rr[13]);
         });
-        rpm = max4(rpm);
-        dzm = max4(dzm);
+        rpm = maxG(rpm);
+        dzm = maxG(dzm);
         const double amx = g_min(amc.value());
         T0 = g_sum(T0); T1 = g_sum(T1); T2 = g_sum(T2);
         rpm = g_max(rpm);
@@ -963,7 +993,7 @@ __device__ __attribute__((noinline)) void ipm_tail(const DevConst& c, const DevB
         }
     }
 #ifdef MPCC_IPM_PROF
-    if (lane == 0) {
+    if (lane == 0 && wv == 0) {
         for (int i = 0; i < 16; i++) if (i != 7) atomicAdd(&g_tail_prof[i], (unsigned long long)tprof[i]);
         atomicAdd(&g_tail_prof[7], (unsigned long long)(it - it_in));
     }
@@ -976,10 +1006,14 @@ __device__ __attribute__((noinline)) void ipm_tail(const DevConst& c, const DevB
 
 // The rest of a QP solve handed over by ipm_group (its iteration state in LDS at TL_STATE): the remaining
 // iterations of the current attempt, the restart from the unit start point if that attempt fails, and ipm_group's
-// epilogue (iteration count, QP status, step).
-template <int NPM>
+// epilogue (iteration count, QP status, step).  GB = 4: the handing wave alone; GB > 4: every wave of a solo block
+// (wave 0 handed over, the others are its helpers, solo_helper), the instance that of wave 0.
+template <int NPM, int GB = 4>
 __device__ __attribute__((noinline)) void ipm_tail_solve(const DevConst& c, const DevBuffers& d, double* smem) {
-    if (threadIdx.x == 0) atomicAdd(&g_tail_solves, 1ull);  // tail-mode hand-overs (mpcc_debug_tail_solves)
+    constexpr int NWV = GB / 4;
+    const int lane = threadIdx.x & 63, t = lane & 15;
+    const int wv = NWV > 1 ? (int)(threadIdx.x >> 6) : 0;
+    if (lane == 0 && wv == 0) atomicAdd(&g_tail_solves, 1ull);  // tail-mode hand-overs (mpcc_debug_tail_solves)
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     const double* st = smem + TL_STATE;
     TailIO io;
@@ -993,17 +1027,21 @@ __device__ __attribute__((noinline)) void ipm_tail_solve(const DevConst& c, cons
     const int gs = (int)st[12];
     io.conv = io.diverged = io.restart = 0;
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    ipm_tail<NPM>(c, d, smem, gs, io);
+    const int b = inst_of(c, d, blockIdx.x * IPW + gs);
+    if constexpr (NWV > 1) __syncthreads();  // every wave has the state before the layout reuses its LDS
+    ipm_tail<NPM, GB>(c, d, smem, b, io);
     it_total += io.it;
     if (!io.conv && attempt == 0 && IPM_ATTEMPTS > 1) {
         io.it = 0; io.max_it = IPM_MAX_IT; io.pending = 0; io.conv = 0; io.diverged = 0; io.restart = 1;
         io.mu0 = 0.0; io.dz_prev = 1e30; io.sigma_mu = 0.0; io.mu_cur = 1e30; io.rp_cur = 1e30; io.alpha = 0.0;
         io.mcount = 0.0;
-        ipm_tail<NPM>(c, d, smem, gs, io);
+        ipm_tail<NPM, GB>(c, d, smem, b, io);
         it_total += io.it;
     }
-    const int lane = threadIdx.x, t = lane & 15;
-    const int b = inst_of(c, d, blockIdx.x * IPW + gs);
+    if constexpr (NWV > 1) {
+        __syncthreads();  // the helpers are done with the LDS and the workspace
+        if (wv != 0) return;
+    }
     const int N = c.N, NS = N + 1;
     int32_t* si = d.sqi + (size_t)b * SQI;
 #ifdef MPCC_IPM_PROF

@@ -1785,6 +1785,7 @@ void launch_sqp_wide(const DevConst& c, const DevBuffers& d, const double* u_cur
 // the mobile build's QP solver (the Panda build's is ipm.hip)
 size_t ipm_lds_bytes(int /*N*/, int npmax) { return ipm_wide_lds_bytes(npmax > 2 ? 11 : npmax, true); }
 void launch_ipm(const DevConst& c, const DevBuffers& d, int npmax, hipStream_t s) { launch_ipm_wide(c, d, npmax, 0, s); }
+bool launch_sqp_solo(const DevConst&, const DevBuffers&, const double*, int, hipStream_t) { return false; }
 void launch_sqp(const DevConst& c, const DevBuffers& d, const double* u_cur, int npmax, hipStream_t s) {
     launch_sqp_wide(c, d, u_cur, npmax, c.p.use_BFGS, s);
 }

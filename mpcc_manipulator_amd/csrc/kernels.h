@@ -55,7 +55,8 @@ struct DevBuffers {
 };
 // Cold-started controllers (a regenerated initial guess) are the ones that take a second SQP iteration; k_sqp
 // gives each of the first NSOLO of them a wave of its own (tail mode from its first IPM iteration), so that they do
-// not set the launch's length from inside a 4-instance wave
+// not set the launch's length from inside a 4-instance wave; with solo blocks (DevConst::solo 2)
+// k_sqp_solo runs those waves instead, each as a block of two waves (§3.7)
 constexpr int NSOLO = 64;
 __host__ __device__ inline int order_slots(int Bn) { return 4 * ((Bn + 3) / 4 + NSOLO); }
 // The fused SQP kernels (k_sqp of ipm.hip / ipm_wide.hip) are declared (DevConst c, DevBuffers d, const double*)
@@ -98,6 +99,9 @@ void launch_ipm(const DevConst& c, const DevBuffers& d, int npmax, hipStream_t s
 void launch_soc(const DevConst& c, const DevBuffers& d, const double* u_cur, hipStream_t s);
 // the fused SQP loop (QP solve, line search, step, next QP assembly) after the first k_setqp
 void launch_sqp(const DevConst& c, const DevBuffers& d, const double* u_cur, int npmax, hipStream_t s);
+// solo blocks: k_sqp_solo beside a k_sqp launch with c.solo 2; false (nothing launched) where the
+// variant has no tail mode
+bool launch_sqp_solo(const DevConst& c, const DevBuffers& d, const double* u_cur, int npmax, hipStream_t s);
 // the fused SQP loop on the 32-lane interior point (ipm_wide.hip); bfgs = 1: damped BFGS Hessian updates
 void launch_sqp_wide(const DevConst& c, const DevBuffers& d, const double* u_cur, int npmax, int bfgs, hipStream_t s);
 size_t ipm_wide_lds_bytes(int npmax, bool lr);

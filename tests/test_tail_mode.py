@@ -101,9 +101,11 @@ def test_tail_mode_against_oracle(built_lib, oracle_lib, monkeypatch):
 @pytest.mark.gpu
 @pytest.mark.parametrize("mask,B,cold_every", [(2, 4096, 64), (3, 512, 8), (2, 512, 1)])
 def test_solo_waves_bitwise(built_lib, monkeypatch, mask, B, cold_every):
-    """Solo waves (csrc/kernels.hip k_order): k_sqp gives the first 64 cold-started controllers a
-    wave each; the instance -> wave map changes nothing in an instance's arithmetic (tail mode is bitwise the normal
-    path), so every output equals the MPCC_SOLO=0 engine's.  cold_every 1: every controller cold, past the cap."""
+    """Solo waves and solo blocks (csrc/kernels.hip k_order): k_sqp gives the first 64
+    cold-started controllers a wave each (MPCC_SOLO=1) or, in k_sqp_solo, a block of two waves whose second joins the
+    tail-mode solves (MPCC_SOLO=2, the default); the instance -> wave map and the number of groups on a tail-mode solve change
+    nothing in an instance's arithmetic, so every output equals the MPCC_SOLO=0 engine's.  cold_every 1: every
+    controller cold, past the cap."""
     import mpcc_manipulator_amd as m
     params = m.load_params(N=20, overrides={"sqp": {"max_iter": 2}})
     eng = m.Engine(params, max_batch=1, constraint_mask=mask)
@@ -114,8 +116,9 @@ def test_solo_waves_bitwise(built_lib, monkeypatch, mask, B, cold_every):
     rng = np.random.default_rng(SEED + 43)
     x0, u0, obs, guess, valid, fails = batch_from_pool(_bench_pool(), B, rng, qnoise=0.005)
     valid[::cold_every] = 0
+    nsl = 4 * ((B + 3) // 4 + 64)  # kernels.h order_slots: the map, then k_prepare's cold flags
     res, orders = {}, {}
-    for solo in (1, 0):
+    for solo in (2, 1, 0):
         monkeypatch.setenv("MPCC_SOLO", str(solo))
         eng = m.Engine(params, max_batch=B, constraint_mask=mask)
         eng.set_track(*track)
@@ -123,14 +126,15 @@ def test_solo_waves_bitwise(built_lib, monkeypatch, mask, B, cold_every):
         x = x0.copy()
         out = eng.solve(x, u0, obs)
         res[solo] = (x, out, eng.get_warmstart(B), eng.solve_stats(B), 0)
-        orders[solo] = eng.order(4 * ((B + 3) // 4 + 64) + B)
+        orders[solo] = eng.order(nsl + B)
         eng.close()
     _assert_bitwise(res[1], res[0])
-    nsl = 4 * ((B + 3) // 4 + 64)
-    sl, flags = orders[1][:nsl].reshape(-1, 4), orders[1][nsl:]
-    cold = np.nonzero(flags)[0]  # k_prepare's cold starts: the host's plus projection resets
-    assert set(np.nonzero(valid == 0)[0]) <= set(cold)
-    ns = min(len(cold), 64)
-    assert np.array_equal(sl[:ns, 0], cold[:ns]) and np.all(sl[:ns, 1:] == -1)  # the first 64 cold starts alone
-    used = sl[sl >= 0]
-    assert np.array_equal(np.sort(used), np.arange(B))  # every instance exactly once
+    _assert_bitwise(res[2], res[0])
+    for solo in (1, 2):
+        sl, flags = orders[solo][:nsl].reshape(-1, 4), orders[solo][nsl:]
+        cold = np.nonzero(flags)[0]  # k_prepare's cold starts: the host's plus projection resets
+        assert set(np.nonzero(valid == 0)[0]) <= set(cold)
+        ns = min(len(cold), 64)
+        assert np.array_equal(sl[:ns, 0], cold[:ns]) and np.all(sl[:ns, 1:] == -1)  # the first 64 cold starts alone
+        used = sl[sl >= 0]
+        assert np.array_equal(np.sort(used), np.arange(B))  # every instance exactly once
