@@ -61,7 +61,10 @@ struct TailLayout {
 static_assert(TailLayout<4>::END == TL_END && TailLayout<4>::LM == TL_LM && TailLayout<4>::K == TL_K, "GB = 4 layout");
 // a solo block: SB_WAVES waves on one instance; the command word (wave 0 -> helper waves) is the last double of the
 // block's ring slices, past the SB_GB-group layout
-constexpr int SB_WAVES = 2, SB_GB = 4 * SB_WAVES;
+#ifndef MPCC_SB_WAVES
+#define MPCC_SB_WAVES 2
+#endif
+constexpr int SB_WAVES = MPCC_SB_WAVES, SB_GB = 4 * SB_WAVES;
 constexpr int WAVE_LDS = LRING * LG(LF_CBWD) * 1024 / 8;  // doubles of LDS per k_sqp wave (narrow variants)
 constexpr int SB_CMD = SB_WAVES * WAVE_LDS - 1;
 static_assert(TailLayout<SB_GB>::SIZE <= SB_CMD && TL_STATE + 16 <= SB_CMD, "solo-block LDS");
