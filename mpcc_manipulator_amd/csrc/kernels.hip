@@ -420,32 +420,39 @@ __global__ void k_debug_cost(DevConst c, int M, const double* __restrict__ x, co
 
 // ------------------------------------------------------------------------------------------------
 // k_order: k_sqp's group slots.  The first NSOLO cold-started instances (ascending) get slot 4 r of wave r, alone in
-// it; every other instance (ascending) is packed 4 per wave after them; unused slots hold -1.  One block.
+// it; every other instance (ascending) is packed 4 per wave after them; unused slots hold -1.  One wave: it runs
+// between the other controller group's k_sqp waves, which hold every VGPR of their SIMDs (a 1024-thread block had
+// to wait for a whole CU to drain: up to 1.1 ms, profiles/r04z_kernel_stats.csv).  Chunks of 64 instances, the cold
+// count before each lane by ballot, 8 chunks' flags loaded ahead.
 // ------------------------------------------------------------------------------------------------
-__global__ void __launch_bounds__(1024) k_order(DevConst c, DevBuffers d) {
+__global__ void __launch_bounds__(64) k_order(DevConst c, DevBuffers d) {
     const int Bn = c.Bn, NSL = order_slots(Bn);
     int32_t* slot = d.order;
     const int32_t* cold = d.order + NSL;
-    const int tid = threadIdx.x;
-    for (int i = tid; i < NSL; i += 1024) slot[i] = -1;
-    const int per = (Bn + 1023) / 1024, lo = tid * per, hi = min(Bn, lo + per);
-    int n = 0;
-    for (int b = lo; b < hi; b++) n += cold[b] != 0;
-    __shared__ int sc[1024];
-    sc[tid] = n;
-    __syncthreads();
-    for (int off = 1; off < 1024; off <<= 1) {  // inclusive scan
-        const int v = tid >= off ? sc[tid - off] : 0;
-        __syncthreads();
-        sc[tid] += v;
-        __syncthreads();
-    }
-    int cb = sc[tid] - n;  // cold instances before lo
-    for (int b = lo; b < hi; b++) {
-        const bool cd = cold[b] != 0;
-        if (cd && cb < NSOLO) slot[4 * cb] = b;
-        else slot[4 * NSOLO + b - min(cb, NSOLO)] = b;
-        if (cd) cb++;
+    const int lane = threadIdx.x;
+    for (int i = lane; i < NSL; i += 64) slot[i] = -1;
+    __syncthreads();  // the -1 stores land before any slot's instance
+    const unsigned long long below = (1ull << lane) - 1;
+    int cb = 0;  // cold instances before the chunk
+    for (int base = 0; base < Bn; base += 8 * 64) {
+        int fl[8];
+#pragma unroll
+        for (int q = 0; q < 8; q++) {
+            const int b = base + q * 64 + lane;
+            fl[q] = b < Bn ? cold[b] : 0;
+        }
+#pragma unroll
+        for (int q = 0; q < 8; q++) {
+            const int b = base + q * 64 + lane;
+            const bool cd = fl[q] != 0;
+            const unsigned long long m = __ballot(cd);
+            const int before = cb + __popcll(m & below);
+            if (b < Bn) {
+                if (cd && before < NSOLO) slot[4 * before] = b;
+                else slot[4 * NSOLO + b - min(before, NSOLO)] = b;
+            }
+            cb += __popcll(m);
+        }
     }
 }
 
@@ -458,7 +465,7 @@ void launch_prepare(const DevConst& c, const DevBuffers& d, hipStream_t s) {
     hipLaunchKernelGGL(k_prepare, dim3(nblk((long)c.Bn * PL, 64)), dim3(64), 0, s, c, d);
 }
 void launch_order(const DevConst& c, const DevBuffers& d, hipStream_t s) {
-    hipLaunchKernelGGL(k_order, dim3(1), dim3(1024), 0, s, c, d);
+    hipLaunchKernelGGL(k_order, dim3(1), dim3(64), 0, s, c, d);
 }
 void launch_stage_records(const DevConst& c, const DevBuffers& d, hipStream_t s) {
     hipLaunchKernelGGL(k_records, dim3(nblk((long)c.S * RPT, 64)), dim3(64), 0, s, c, d);
