@@ -295,9 +295,9 @@ def main():
     # Every controller group's stream needs a hardware queue of its own, or the groups' kernels run back to back:
     # HIP multiplexes all streams onto GPU_MAX_HW_QUEUES queues (4 by default) and torch's stream pool, created
     # whole at the first torch.cuda.Stream(), lands consecutive pool streams on one queue (measured:
-    # tools/probes/stream_overlap.py, profiles/r03g_stream_overlap.log, r03h_stream_overlap.log).  Each engine also
-    # has the side stream of its solo blocks.  Read by HIP when it initialises, below.
-    hwq = min(32, max(12, 3 * args.sub_batches + 6))
+    # tools/probes/stream_overlap.py, profiles/r03g_stream_overlap.log, r03h_stream_overlap.log).  Read by HIP when it
+    # initialises, below.
+    hwq = min(32, max(8, 2 * args.sub_batches + 4))
     if args.sub_batches > 1 and int(os.environ.get("GPU_MAX_HW_QUEUES", "4")) < hwq:
         os.environ["GPU_MAX_HW_QUEUES"] = str(hwq)
     import torch

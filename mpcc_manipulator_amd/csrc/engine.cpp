@@ -578,7 +578,16 @@ int mpcc_create(const mpcc_config* cfg, const mpcc_params* params, const char* n
         // stream, or any NULL-stream copy of the inputs) is ordered before and after the engine's
         // kernels, as the ABI's "NULL = engine stream" would otherwise race with it.
         HIPCHK(hipStreamCreateWithFlags(&e->stream, hipStreamDefault));
-        HIPCHK(hipStreamCreateWithFlags(&e->solo_stream, hipStreamNonBlocking));
+        {  // the solo blocks' side stream; MPCC_SOLO_PRIO=h / l: created at the highest / lowest stream priority (A/B)
+            const char* sp = std::getenv("MPCC_SOLO_PRIO");
+            if (sp && (sp[0] == 'h' || sp[0] == 'l')) {
+                int least = 0, greatest = 0;
+                HIPCHK(hipDeviceGetStreamPriorityRange(&least, &greatest));
+                HIPCHK(hipStreamCreateWithPriority(&e->solo_stream, hipStreamNonBlocking, sp[0] == 'h' ? greatest : least));
+            } else {
+                HIPCHK(hipStreamCreateWithFlags(&e->solo_stream, hipStreamNonBlocking));
+            }
+        }
         HIPCHK(hipEventCreateWithFlags(&e->solo_fork, hipEventDisableTiming));
         HIPCHK(hipEventCreateWithFlags(&e->solo_join, hipEventDisableTiming));
         const size_t B = (size_t)e->maxB, NS = (size_t)e->N + 1;
