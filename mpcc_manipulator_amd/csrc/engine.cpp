@@ -68,6 +68,7 @@ struct mpcc_engine {
     int N = 0, maxB = 0;
     hipStream_t stream = nullptr;
     hipStream_t solo_stream = nullptr;  // k_sqp_solo (solo blocks), forked from and joined to `stream` per launch
+    int simds = 1024;                   // SIMDs of the device (4 per CU)
     hipEvent_t solo_fork = nullptr, solo_join = nullptr;
     SplineTables track;
     bool has_track = false;
@@ -349,6 +350,7 @@ void quiesce(mpcc_engine* e) {
     }
 }
 
+constexpr int IPW_SQP = 4;  // instances per k_sqp wave (ipm.hip IPW)
 void run_batch(mpcc_engine* e, int B, hipStream_t st, mpcc_timing* timing, bool ocp = false) {
     DevConst c = e->make_const(B);
     c.ocp = ocp ? 1 : 0;
@@ -415,7 +417,9 @@ void run_batch(mpcc_engine* e, int B, hipStream_t st, mpcc_timing* timing, bool 
             const int npm = poly_rows_max(c.p.constraint_mask);
             cs.solo = 1;
             launch_order(cs, d, st);
-            if (e->solo_mode == 2 && DOF == 7 && npm <= 2) {
+            // solo blocks where the packed launch is one round of waves (at most one per SIMD): beyond that the
+            // cold starts' time is spread over several rounds (B = 65,536: 2.078M with, 2.092M without, r04ah)
+            if (e->solo_mode == 2 && DOF == 7 && npm <= 2 && (c.Bn + IPW_SQP - 1) / IPW_SQP <= e->simds) {
                 // solo blocks: k_sqp_solo on the side stream beside k_sqp (which leaves the solo waves to it), joined
                 // before anything after k_sqp
                 cs.solo = 2;
@@ -587,6 +591,11 @@ int mpcc_create(const mpcc_config* cfg, const mpcc_params* params, const char* n
             } else {
                 HIPCHK(hipStreamCreateWithFlags(&e->solo_stream, hipStreamNonBlocking));
             }
+        }
+        {
+            int ncu = 0;
+            if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, cfg->device) == hipSuccess && ncu > 0)
+                e->simds = 4 * ncu;
         }
         HIPCHK(hipEventCreateWithFlags(&e->solo_fork, hipEventDisableTiming));
         HIPCHK(hipEventCreateWithFlags(&e->solo_join, hipEventDisableTiming));
