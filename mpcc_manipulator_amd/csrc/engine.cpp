@@ -422,12 +422,22 @@ void run_batch(mpcc_engine* e, int B, hipStream_t st, mpcc_timing* timing, bool 
             if (e->solo_mode == 2 && DOF == 7 && npm <= 2 && (c.Bn + IPW_SQP - 1) / IPW_SQP <= e->simds) {
                 // solo blocks: k_sqp_solo on the side stream beside k_sqp (which leaves the solo waves to it), joined
                 // before anything after k_sqp
+                // The kernel on the forked stream starts ≈30 µs after the one that follows k_order in its own stream
+                // (the cross-queue wait): k_sqp_solo, which ends last, goes on the group's stream, the packed k_sqp
+                // on the side stream (MPCC_SOLO_SIDE=1: the other way round, A/B).
                 cs.solo = 2;
+                const char* ss = std::getenv("MPCC_SOLO_SIDE");
+                const bool solo_side = ss && ss[0] == '1';
                 HIPCHK(hipEventRecord(e->solo_fork, st));
                 HIPCHK(hipStreamWaitEvent(e->solo_stream, e->solo_fork, 0));
-                launch_sqp_solo(cs, d, ucur, npm, e->solo_stream);
+                if (solo_side) {
+                    launch_sqp_solo(cs, d, ucur, npm, e->solo_stream);
+                    launch_sqp(cs, d, ucur, npm, st);
+                } else {
+                    launch_sqp_solo(cs, d, ucur, npm, st);
+                    launch_sqp(cs, d, ucur, npm, e->solo_stream);
+                }
                 HIPCHK(hipEventRecord(e->solo_join, e->solo_stream));
-                launch_sqp(cs, d, ucur, npm, st);
                 HIPCHK(hipStreamWaitEvent(st, e->solo_join, 0));
             } else {
                 launch_sqp(cs, d, ucur, npm, st);
