@@ -33,6 +33,28 @@ def q_start(dof):
     return Q0 if dof == 7 else np.concatenate([np.zeros(dof - 7), Q0])
 
 
+def batch_inputs(pool, B, dof, obstacles, obs_xyz, start=0, world=1):
+    """The bench's instances: pool step t = (global index) mod T, q += N(0, 0.005); the noise
+    is drawn for the global batch, so instance i gets the same input whatever the number of ranks.  Obstacles:
+    main_w_sim.py:42-45's scenario, xyz = (0.48, 0.218, z), z ~ U[z0 - 0.1, z0 + 0.1], r = 5 cm, or the dummy
+    obstacle of MPC::runMPC (mpc.cpp:97-100).  Returns x0, u0, obs, guess, valid, fails of this rank's block."""
+    rng = np.random.default_rng(SEED)
+    T = len(pool["x0"])
+    idx = (np.arange(B) + start) % T
+    x0 = pool["x0"][idx].copy()
+    x0[:, :dof] += rng.normal(0.0, 0.005, size=(B * world, dof))[start:start + B]
+    u0 = pool["u0"][idx].copy()
+    guess = pool["guess"][idx].copy()
+    valid = pool["valid"][idx].astype(np.int32)
+    fails = pool["fails"][idx].astype(np.int32)
+    if obstacles:
+        z = rng.uniform(obs_xyz[2] - 0.1, obs_xyz[2] + 0.1, B * world)[start:start + B]
+        obs = np.column_stack([np.full(B, obs_xyz[0]), np.full(B, obs_xyz[1]), z, np.full(B, 5.0)])
+    else:
+        obs = np.tile(np.array([3.0, 3.0, 3.0, 0.0]), (B, 1))
+    return x0, u0, obs, guess, valid, fails
+
+
 def find_pmc(kname, B, N, mask, dof, override=None, prof_dir=None):
     """The committed PMC summary of this workload (tools/pmc_summary.py): the first pmc_traffic_<kernel>*.json
     whose kernel, batch, horizon, constraint mask and DOF match, with the per-launch counters of the summary it
@@ -335,23 +357,8 @@ def main():
         e.set_track(*track)
     eng = engs[0]
 
-    # instances: pool step t = (global index) mod T, q += N(0, 0.005); the noise is
-    # drawn for the global batch, so instance i gets the same input whatever the number of ranks
-    rng = np.random.default_rng(SEED)
-    T = len(pool["x0"])
     start, _ = shard_bounds(B * world, rank, world)  # contiguous instance block of this rank
-    idx = (np.arange(B) + start) % T
-    x0 = pool["x0"][idx].copy()
-    x0[:, :dof] += rng.normal(0.0, 0.005, size=(B * world, dof))[start:start + B]
-    u0 = pool["u0"][idx].copy()
-    guess = pool["guess"][idx].copy()
-    valid = pool["valid"][idx].astype(np.int32)
-    fails = pool["fails"][idx].astype(np.int32)
-    if obstacles:  # main_w_sim.py:42-45 scenario: xyz = (0.48, 0.218, z), z ~ U[0.421, 0.621], r = 5 cm
-        z = rng.uniform(obs_xyz[2] - 0.1, obs_xyz[2] + 0.1, B * world)[start:start + B]
-        obs = np.column_stack([np.full(B, obs_xyz[0]), np.full(B, obs_xyz[1]), z, np.full(B, 5.0)])
-    else:  # dummy obstacle of MPC::runMPC (mpc.cpp:97-100)
-        obs = np.tile(np.array([3.0, 3.0, 3.0, 0.0]), (B, 1))
+    x0, u0, obs, guess, valid, fails = batch_inputs(pool, B, dof, obstacles, obs_xyz, start, world)
 
     dev = torch.device("cuda", local)
     t = lambda a, dt=torch.float64: torch.from_numpy(np.ascontiguousarray(a)).to(dev, dt)

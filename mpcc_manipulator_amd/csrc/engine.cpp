@@ -145,21 +145,30 @@ struct mpcc_engine {
         }
     }
 
-    // Buffers of the damped-BFGS option (use_BFGS): the 32-lane interior point's workspace (the mobile build's
-    // regular one) and the per-instance BFGS state, allocated when the option is first enabled.
-    // nterms: low-rank terms the solves may hold (2 per BFGS update); above LRM the Woodbury columns go to memory.
-    void ensure_bfgs_buffers(int nterms) {
+    // Buffers of the 32-lane interior point (use_BFGS, MPCC_WIDE_SQP): its workspace (the mobile build's regular
+    // one) and, with use_BFGS, the per-instance BFGS state for the low-rank terms max_iter can produce
+    // (bfgs_terms: 2 per update, at most LRX; above LRM the Woodbury columns go to memory, d.lrq).  Reallocated
+    // when a larger max_iter needs more terms (the stride d.lrs changes; the state is per solve).
+    void ensure_wide_buffers(bool bfgs, int max_iter) {
         const size_t B = (size_t)maxB, NE = ((size_t)N + 1) * NXU;
         if (!d.isw) d.isw = dmalloc<double>(B * (N + 1) * ISW);
-        if (!d.lr) {
-            d.lr = dmalloc<double>(B * LRX * NE);
-            d.lrc = dmalloc<double>(B * LRX);
+        if (!bfgs) return;
+        if (!d.glam) {
             d.glam = dmalloc<double>(B * NE);
             d.gprev = dmalloc<double>(B * NE);
             d.aty = dmalloc<double>(B * NE);
             d.sp = dmalloc<double>(B * NE);
         }
-        if (nterms > LRM && !d.lrq) d.lrq = dmalloc<double>(B * LRX * (N + 1) * 3 * 32);
+        const int lrs = bfgs_terms(max_iter);
+        if (lrs > d.lrs) {
+            auto f = [](double*& p) { if (p) (void)hipFree(p); p = nullptr; };
+            f(d.lr); f(d.lrc); f(d.lrq);
+            d.lrs = 0;
+            d.lr = dmalloc<double>(B * lrs * NE);
+            d.lrc = dmalloc<double>(B * lrs);
+            if (lrs > LRM) d.lrq = dmalloc<double>(B * lrs * (N + 1) * 3 * 32);
+            d.lrs = lrs;
+        }
     }
 
     DevConst make_const(int Bn) const {
@@ -181,6 +190,21 @@ struct mpcc_engine {
         c.faithful_dead_trials = cfg.faithful_dead_trials;
         c.tail = tail_mode;
         return c;
+    }
+
+    // the solo blocks' side stream, created at their first launch (each stream takes one of the process's few
+    // hardware queues); MPCC_SOLO_PRIO=h / l: at the highest / lowest stream priority (A/B)
+    hipStream_t side_stream() {
+        if (solo_stream) return solo_stream;
+        const char* sp = std::getenv("MPCC_SOLO_PRIO");
+        if (sp && (sp[0] == 'h' || sp[0] == 'l')) {
+            int least = 0, greatest = 0;
+            HIPCHK(hipDeviceGetStreamPriorityRange(&least, &greatest));
+            HIPCHK(hipStreamCreateWithPriority(&solo_stream, hipStreamNonBlocking, sp[0] == 'h' ? greatest : least));
+        } else {
+            HIPCHK(hipStreamCreateWithFlags(&solo_stream, hipStreamNonBlocking));
+        }
+        return solo_stream;
     }
 
     hipEvent_t ev(size_t i) {
@@ -283,12 +307,9 @@ void validate_params(const mpcc_params& p) {
     for (int i = 0; i < NX; i++) if (!(p.Tx[i] > 0)) throw std::invalid_argument("T_x must be > 0");
     for (int i = 0; i < NU; i++) if (!(p.Tu[i] > 0)) throw std::invalid_argument("T_u must be > 0");
     if (p.max_iter < 0 || p.line_search_max_iter < 0) throw std::invalid_argument("negative iteration limit");
-    // Damped BFGS (osqp_interface.cpp:683-715): the QP Hessian is the structured Hessian of SQP iteration 0 plus
-    // 2 low-rank terms per update, solved with the Woodbury identity around the Riccati recursion (DESIGN.md
-    // §4.2); at most LRX terms are held, i.e. max_iter <= 1 + LRX / 2.
-    if (p.use_BFGS && p.max_iter > 1 + LRX / 2)
-        throw std::invalid_argument("use_BFGS supports max_iter <= " + std::to_string(1 + LRX / 2) +
-                                    " (low-rank terms of the damped BFGS Hessian)");
+    // Damped BFGS (osqp_interface.cpp:683-715) takes any max_iter: the QP Hessian is the structured Hessian of
+    // SQP iteration 0 plus 2 low-rank terms per update, solved with the Woodbury identity around the Riccati
+    // recursion; an update past LRX terms restarts from that iteration's exact Hessian.
 }
 
 // one track's tables in the device layout (dev_common.h SplineDev): SPL_STRIDE doubles
@@ -412,7 +433,8 @@ void run_batch(mpcc_engine* e, int B, hipStream_t st, mpcc_timing* timing, bool 
         if (tm) a1 = mark();
         e->last_wide = DOF != 7 || c.p.use_BFGS || e->wide_sqp;
         if (c.p.use_BFGS || e->wide_sqp) launch_sqp_wide(c, d, ucur, poly_rows_max(c.p.constraint_mask), c.p.use_BFGS ? 1 : 0, st);
-        else if (e->solo_mode && e->tail_mode && !c.ocp) {  // cold starts alone in a wave / block (k_prepare flags them)
+        else if (DOF == 7 && e->solo_mode && e->tail_mode && !c.ocp) {  // cold starts alone in a wave / block (k_prepare flags
+                                                                       // them; the 16-lane interior point's tail mode)
             DevConst cs = c;
             const int npm = poly_rows_max(c.p.constraint_mask);
             cs.solo = 1;
@@ -428,16 +450,14 @@ void run_batch(mpcc_engine* e, int B, hipStream_t st, mpcc_timing* timing, bool 
                 cs.solo = 2;
                 const char* ss = std::getenv("MPCC_SOLO_SIDE");
                 const bool solo_side = ss && ss[0] == '1';
+                hipStream_t side = e->side_stream();
                 HIPCHK(hipEventRecord(e->solo_fork, st));
-                HIPCHK(hipStreamWaitEvent(e->solo_stream, e->solo_fork, 0));
-                if (solo_side) {
-                    launch_sqp_solo(cs, d, ucur, npm, e->solo_stream);
-                    launch_sqp(cs, d, ucur, npm, st);
-                } else {
-                    launch_sqp_solo(cs, d, ucur, npm, st);
-                    launch_sqp(cs, d, ucur, npm, e->solo_stream);
-                }
-                HIPCHK(hipEventRecord(e->solo_join, e->solo_stream));
+                HIPCHK(hipStreamWaitEvent(side, e->solo_fork, 0));
+                // k_sqp with solo 2 leaves its first NSOLO waves to k_sqp_solo: if that cannot launch (a variant
+                // without tail mode), k_sqp runs them itself as solo waves (solo 1)
+                if (!launch_sqp_solo(cs, d, ucur, npm, solo_side ? side : st)) cs.solo = 1;
+                launch_sqp(cs, d, ucur, npm, solo_side ? st : side);
+                HIPCHK(hipEventRecord(e->solo_join, side));
                 HIPCHK(hipStreamWaitEvent(st, e->solo_join, 0));
             } else {
                 launch_sqp(cs, d, ucur, npm, st);
@@ -592,16 +612,6 @@ int mpcc_create(const mpcc_config* cfg, const mpcc_params* params, const char* n
         // stream, or any NULL-stream copy of the inputs) is ordered before and after the engine's
         // kernels, as the ABI's "NULL = engine stream" would otherwise race with it.
         HIPCHK(hipStreamCreateWithFlags(&e->stream, hipStreamDefault));
-        {  // the solo blocks' side stream; MPCC_SOLO_PRIO=h / l: created at the highest / lowest stream priority (A/B)
-            const char* sp = std::getenv("MPCC_SOLO_PRIO");
-            if (sp && (sp[0] == 'h' || sp[0] == 'l')) {
-                int least = 0, greatest = 0;
-                HIPCHK(hipDeviceGetStreamPriorityRange(&least, &greatest));
-                HIPCHK(hipStreamCreateWithPriority(&e->solo_stream, hipStreamNonBlocking, sp[0] == 'h' ? greatest : least));
-            } else {
-                HIPCHK(hipStreamCreateWithFlags(&e->solo_stream, hipStreamNonBlocking));
-            }
-        }
         {
             int ncu = 0;
             if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, cfg->device) == hipSuccess && ncu > 0)
@@ -631,7 +641,7 @@ int mpcc_create(const mpcc_config* cfg, const mpcc_params* params, const char* n
         e->bchk = dmalloc<uint32_t>(64);
         HIPCHK(hipMemset(e->bchk, 0, 64 * sizeof(uint32_t)));
 #endif
-        if (e->params.use_BFGS || e->wide_sqp) e->ensure_bfgs_buffers(e->params.use_BFGS ? 2 * (e->params.max_iter - 1) : 0);
+        if (e->params.use_BFGS || e->wide_sqp) e->ensure_wide_buffers(e->params.use_BFGS, e->params.max_iter);
         e->s_x0 = dmalloc<double>(B * NX);
         e->s_u0 = dmalloc<double>(B * NU);
         e->s_obs = dmalloc<double>(B * 4);
@@ -681,7 +691,7 @@ int mpcc_set_params(mpcc_engine* e, const mpcc_params* p) {
         validate_params(np);
         e->params = np;
         e->set_model();
-        if (np.use_BFGS) e->ensure_bfgs_buffers(2 * (np.max_iter - 1));
+        if (np.use_BFGS) e->ensure_wide_buffers(true, np.max_iter);
     } catch (const std::exception& x) {
         e->params = old;
         e->set_model();
@@ -1075,6 +1085,7 @@ int mpcc_closed_loop(mpcc_engine* e, int B, int steps, double* x0, double* u0, c
         };
         if (use_graph && steps > 0) {
             HIPCHK(hipStreamSynchronize(st));
+            if (DOF == 7) (void)e->side_stream();  // created outside the capture (the solo blocks fork onto it)
             HIPCHK(hipStreamBeginCapture(st, hipStreamCaptureModeThreadLocal));
             step();
             HIPCHK(hipStreamEndCapture(st, &graph));
@@ -1295,13 +1306,13 @@ static int debug_solve_qp(mpcc_engine* e, int B, const double* guess, const doub
         HIPCHK(hipMemcpy(e->d.sqi, sqi.data(), sqi.size() * sizeof(int32_t), hipMemcpyHostToDevice));
         HIPCHK(hipMemset(e->d.step, 0, S * NXU * sizeof(double)));
         if (nlr >= 0) {  // low-rank terms of every instance, then the 32-lane solver
-            e->ensure_bfgs_buffers(nlr);
-            const size_t NE = S * NXU / B;
-            std::vector<double> l((size_t)B * LRX * NE, 0.0), lc((size_t)B * LRX, 0.0);
+            e->ensure_wide_buffers(true, (nlr + 1) / 2 + 1);  // room for nlr terms
+            const size_t NE = S * NXU / B, L = (size_t)e->d.lrs;
+            std::vector<double> l((size_t)B * L * NE, 0.0), lc((size_t)B * L, 0.0);
             for (int b = 0; b < B; b++)
                 for (int j = 0; j < nlr; j++) {
-                    std::memcpy(&l[((size_t)b * LRX + j) * NE], lr + (size_t)j * NE, NE * sizeof(double));
-                    lc[(size_t)b * LRX + j] = lrc[j];
+                    std::memcpy(&l[((size_t)b * L + j) * NE], lr + (size_t)j * NE, NE * sizeof(double));
+                    lc[(size_t)b * L + j] = lrc[j];
                 }
             HIPCHK(hipMemcpy(e->d.lr, l.data(), l.size() * sizeof(double), hipMemcpyHostToDevice));
             HIPCHK(hipMemcpy(e->d.lrc, lc.data(), lc.size() * sizeof(double), hipMemcpyHostToDevice));

@@ -401,6 +401,13 @@ __device__ __forceinline__ void ipm_group(const DevConst& c, const DevBuffers& d
     if (run && (fl & 2)) { if (t == 0) { si[SQ_STATUS] = MPCC_NON_PD_HESSIAN; si[SQ_ACTIVE] = 0; } run = false; }
     if (run && (fl & 1)) { if (t == 0) { si[SQ_STATUS] = MPCC_NAN_HESSIAN; si[SQ_ACTIVE] = 0; } run = false; }
     if (run && (fl & 4)) { if (t == 0) si[SQ_QPSTAT] = MPCC_QP_PrimalInfeasible; run = false; }  // keep old step (Q6)
+    if constexpr (LR) {  // more than LRM terms need the extended path's columns (d.lrq, allocated by the engine
+                         // whenever d.lrs > LRM): without them the instance stops with INVALID_SETTINGS, never a stray write
+        if (run && si[SQ_NLR] > LRM && d.lrq == nullptr) {
+            if (t == 0) { si[SQ_STATUS] = MPCC_INVALID_SETTINGS; si[SQ_ACTIVE] = 0; }
+            run = false;
+        }
+    }
     const bool entered = run;
 
     // ---- low-rank Hessian terms of the damped-BFGS option: B = H_0 + sum_j c_j u_j u_j^T, u_j per stage as
@@ -415,8 +422,8 @@ __device__ __forceinline__ void ipm_group(const DevConst& c, const DevBuffers& d
     if constexpr (LR) {
         nlr = si[SQ_NLR];
 #pragma unroll
-        for (int j = 0; j < LRM; j++) lrc[j] = (j < nlr) ? d.lrc[(size_t)(valid ? b : 0) * LRX + j] : 0.0;
-        LRb = (const gdouble*)(d.lr + (size_t)(valid ? b : 0) * LRX * NS * NXU);
+        for (int j = 0; j < LRM; j++) lrc[j] = (j < nlr) ? d.lrc[(size_t)(valid ? b : 0) * d.lrs + j] : 0.0;
+        LRb = (const gdouble*)(d.lr + (size_t)(valid ? b : 0) * d.lrs * NS * NXU);
     }
     // more terms than the fused sweeps carry: the wave runs the extended path (both instances; nlr_w = the larger
     // count, the other instance's extra terms are zero vectors with unit capacitance)
@@ -424,11 +431,11 @@ __device__ __forceinline__ void ipm_group(const DevConst& c, const DevBuffers& d
     const int nlr_w = xlw ? max(__shfl(entered ? nlr : 0, 0), __shfl(entered ? nlr : 0, GW)) : 0;
     const bool lrw = LR && !xlw && __ballot(entered && nlr > 0) != 0;  // this wave runs the split (Woodbury) sweeps
     auto u_y = [&](int j, int k) -> double {  // u_j, y part of stage k (lanes < NX)
-        const double v = LRb[((size_t)MPCC_BCHK(c.bchk, j, LRX, BC_LR) * NS + MPCC_BCHK(c.bchk, k, NS, BC_LR)) * NXU + (rowY ? t : 0)];
+        const double v = LRb[((size_t)MPCC_BCHK(c.bchk, j, d.lrs, BC_LR) * NS + MPCC_BCHK(c.bchk, k, NS, BC_LR)) * NXU + (rowY ? t : 0)];
         return (LR && rowY && j < nlr) ? v : 0.0;
     };
     auto u_v = [&](int j, int k) -> double {  // u_j, v part of stage k (lanes < NU, k < N)
-        const double v = LRb[((size_t)MPCC_BCHK(c.bchk, j, LRX, BC_LR) * NS + MPCC_BCHK(c.bchk, k, NS, BC_LR)) * NXU + NX + (t < NU ? t : 0)];
+        const double v = LRb[((size_t)MPCC_BCHK(c.bchk, j, d.lrs, BC_LR) * NS + MPCC_BCHK(c.bchk, k, NS, BC_LR)) * NXU + NX + (t < NU ? t : 0)];
         return (LR && t < NU && k < N && j < nlr) ? v : 0.0;
     };
     double uz[LRM];  // u_j^T z of the current iterate
@@ -439,12 +446,13 @@ __device__ __forceinline__ void ipm_group(const DevConst& c, const DevBuffers& d
     //      columns Q_j in memory (d.lrq, per lane) and S, its LU and the per-term scalars in the instance's LDS
     //      (XL_*), the terms taken 4 at a time.  Same formulas as the fused path and the oracle's lr_solve.
     double* const XL = smem + IPW * GRP_LDS + (wide_gram(NPM) ? GRAM_LDS : 0) + grp * XL_LDS;
-    gdouble* const XQb = (gdouble*)(d.lrq ? d.lrq + (size_t)(valid ? b : 0) * LRX * NS * 3 * GW : d.step);
+    // xlw implies d.lrq (the INVALID_SETTINGS guard above); the null base is never dereferenced otherwise
+    gdouble* const XQb = (gdouble*)(d.lrq + (d.lrq ? (size_t)(valid ? b : 0) * d.lrs * NS * 3 * GW : 0));
     auto xq = [&](int j, int k, int f) -> gdouble* {  // f: 0 Q_j x~ part, 1 Q_j v part, 2 kff of the solve of u_j
-        return XQb + (((size_t)MPCC_BCHK(c.bchk, j, LRX, BC_LR) * NS + MPCC_BCHK(c.bchk, k, NS, BC_LR)) * 3 + f) * GW + t;
+        return XQb + (((size_t)MPCC_BCHK(c.bchk, j, d.lrs, BC_LR) * NS + MPCC_BCHK(c.bchk, k, NS, BC_LR)) * 3 + f) * GW + t;
     };
     const int xlt = t < LRX ? t : LRX - 1;  // this lane's term / row of S (clamped address)
-    if (xlw && t < LRX) XL[XL_C + t] = (t < nlr) ? d.lrc[(size_t)(valid ? b : 0) * LRX + t] : 0.0;
+    if (xlw && t < LRX) XL[XL_C + t] = (t < nlr) ? d.lrc[(size_t)(valid ? b : 0) * d.lrs + t] : 0.0;
     // dst[j] = u_j^T [ws fx | ws fv] over the horizon, all j < nlr_w
     auto xl_dots = [&](int dst, int fx, int fv) {
         for (int j0 = 0; j0 < nlr_w; j0 += 4) {
@@ -1616,18 +1624,23 @@ __device__ __forceinline__ void bfgs_us(const double* __restrict__ lrb, const do
 // SQP iteration it (after setQP): grad_L = q + A^T lambda; for it > 0, dgrad_L = grad_L - grad_L_prev and
 // Hess_ = BFGSUpdate(Hess_, step_prev, dgrad_L) appends -Bs Bs^T / sBs + r r^T / sr to the low-rank terms.
 // Returns false when the update makes the Hessian NaN (sBs = 0 with sr >= eps): NAN_HESSIAN (:474-477).
-__device__ __attribute__((noinline)) bool bfgs_pre(const DevConst& c, const DevBuffers& d, int b, int t, int it) {
+// restart (the instance holds LRX - 1 or more terms, so the update would not fit): this iteration's exact
+// Hessian (setQP with keep_hess off) becomes the new iteration-0 Hessian and the terms are dropped, as the
+// oracle's solve_ocp (BFGS_MAX_TERMS); grad_L is recorded as in iteration 0.
+__device__ __attribute__((noinline)) bool bfgs_pre(const DevConst& c, const DevBuffers& d, int b, int t, int it,
+                                                   bool restart) {
     const int N = c.N, NS = N + 1, NE = NS * NXU;
     int32_t* si = d.sqi + (size_t)b * SQI;
     const int nlr = si[SQ_NLR];
     const double* qsb = d.qs + (size_t)b * NS * QS;
-    double* lrb = d.lr + (size_t)b * LRX * NE;
-    const double* lrcb = d.lrc + (size_t)b * LRX;
+    double* lrb = d.lr + (size_t)b * d.lrs * NE;
+    const double* lrcb = d.lrc + (size_t)b * d.lrs;
     double* glam = d.glam + (size_t)b * NE;
     double* gprev = d.gprev + (size_t)b * NE;
     const double* sp = d.sp + (size_t)b * NE;
-    if (it == 0) {
+    if (it == 0 || restart) {
         for (int e = t; e < NE; e += GW) gprev[e] = bfgs_q_elem(qsb, N, e) + glam[e];
+        if (restart && t == 0) si[SQ_NLR] = 0;
         return true;
     }
     // dgrad_L into slot nlr + 1, B step_prev into slot nlr (B of the previous iteration)
@@ -1661,7 +1674,7 @@ __device__ __attribute__((noinline)) bool bfgs_pre(const DevConst& c, const DevB
         dgv[e] = damp ? theta * dg + (1 - theta) * bsv[e] : dg;  // r
     }
     if (t == 0) {
-        double* lc = d.lrc + (size_t)b * LRX;
+        double* lc = d.lrc + (size_t)b * d.lrs;
         lc[nlr] = -1.0 / sbs;
         lc[nlr + 1] = 1.0 / sr;
         si[SQ_NLR] = nlr + 2;
@@ -1673,8 +1686,8 @@ __device__ __attribute__((noinline)) void bfgs_post_qp(const DevConst& c, const 
     const int N = c.N, NS = N + 1, NE = NS * NXU;
     const int nlr = d.sqi[(size_t)b * SQI + SQ_NLR];
     const double* qsb = d.qs + (size_t)b * NS * QS;
-    const double* lrb = d.lr + (size_t)b * LRX * NE;
-    const double* lrcb = d.lrc + (size_t)b * LRX;
+    const double* lrb = d.lr + (size_t)b * d.lrs * NE;
+    const double* lrcb = d.lrc + (size_t)b * d.lrs;
     const double* stp = d.step + (size_t)b * NE;
     double* aty = d.aty + (size_t)b * NE;
     double us[LRX];
@@ -1713,12 +1726,14 @@ __global__ void __launch_bounds__(64) k_sqp(DevConst, DevBuffers, const double* 
     for (int it = 0; it < c.p.max_iter; it++) {
         bool act = valid && si[SQ_ACTIVE] != 0;
         if (__ballot(act) == 0) break;
+        // damped BFGS past LRX terms: restart from this iteration's exact Hessian (bfgs_pre)
+        const bool restart = LR && it > 0 && act && si[SQ_NLR] + 2 > LRX;
         if (it > 0) {
-            if (act) sqp_setqp_phase(c, d, b, t, ucur, LR);
+            if (act) sqp_setqp_phase(c, d, b, t, ucur, LR && !restart);
             __syncthreads();
         }
         if constexpr (LR) {
-            if (act && !bfgs_pre(c, d, b, t, it) && t == 0) { si[SQ_STATUS] = MPCC_NAN_HESSIAN; si[SQ_ACTIVE] = 0; }
+            if (act && !bfgs_pre(c, d, b, t, it, restart) && t == 0) { si[SQ_STATUS] = MPCC_NAN_HESSIAN; si[SQ_ACTIVE] = 0; }
             __syncthreads();
         }
         sqp_ipm_phase<NPM, LR>(c, d, smem);

@@ -43,12 +43,15 @@ struct DevBuffers {
     // damped-BFGS option of either build
     double* isw;
     // damped BFGS (use_BFGS, osqp_interface.cpp:437-453, 683-715), per instance, horizon layout [(N+1)][NXU]:
-    // low-rank vectors lr [LRX][(N+1)*NXU] and coefficients lrc [LRX], A^T lambda (glam), grad_L of the previous
+    // low-rank vectors lr [lrs][(N+1)*NXU] and coefficients lrc [lrs], A^T lambda (glam), grad_L of the previous
     // iteration (gprev), A^T y of the last QP (aty), step_prev = alpha * step (sp)
     double *lr, *lrc, *glam, *gprev, *aty, *sp;
     // more than LRM low-rank terms (max_iter > 1 + LRM / 2): per term and stage the Woodbury column Q_j = M u_j (x~
-    // and v parts) and the kff of its backward solve, [LRX][(N+1)][3][32 lanes]; null until such a max_iter is set
+    // and v parts) and the kff of its backward solve, [lrs][(N+1)][3][32 lanes]; null unless lrs > LRM
     double* lrq;
+    // low-rank terms allocated per instance (the stride of lr / lrc / lrq): the terms max_iter can produce,
+    // min(LRX, 2 (max_iter - 1)), rounded up to a multiple of 4 (>= LRM); 0 without use_BFGS
+    int lrs;
     // k_sqp's instance of each 16-lane group slot ([4 * (ceil(Bn / 4) + NSOLO)], -1: none) followed by the per-instance
     // cold-start flags of this step ([Bn], written by k_prepare); k_order builds the slots (solo waves)
     int32_t* order;
@@ -77,7 +80,14 @@ constexpr int SQI = 8;  // int bookkeeping per instance: status, active, iter, n
 constexpr int SQ_REJECT = 6;
 constexpr int SQ_NLR = 7;  // low-rank BFGS terms held (2 per update)
 constexpr int LRM = 4;     // low-rank terms carried in registers through the fused sweeps (use_BFGS, max_iter <= 3)
-constexpr int LRX = 28;    // low-rank terms held at most: use_BFGS with max_iter <= 1 + LRX / 2 (ipm_wide.hip xl_*)
+constexpr int LRX = 28;    // low-rank terms held at most (ipm_wide.hip xl_*); an update past them restarts the
+                           // quasi-Newton matrix from that iteration's exact Hessian (bfgs_pre)
+// low-rank terms an instance can hold with max_iter SQP iterations (2 per update), as allocated (DevBuffers::lrs)
+inline int bfgs_terms(int max_iter) {
+    const int n = max_iter > 1 ? 2 * (max_iter - 1) : 0;
+    const int r = ((n < LRX ? n : LRX) + 3) / 4 * 4;
+    return r < LRM ? LRM : r;
+}
 constexpr int ISW = 2048;  // doubles per stage of the 32-lane interior point's workspace (64 fields x 32 lanes)
 
 struct NNDesc {

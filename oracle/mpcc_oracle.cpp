@@ -1557,6 +1557,7 @@ static void lu_solve_small(std::vector<double>& A, int n, std::vector<double>& b
         b[i] = s2 / A[(size_t)i * n + i];
     }
 }
+constexpr int BFGS_MAX_TERMS = 28;  // low-rank terms held at most (the engine's LRX, kernels.h)
 struct LowRank {
     std::vector<std::vector<double>> u;  // (N+1)*NZ each
     std::vector<double> c;
@@ -2050,6 +2051,11 @@ static int solve_ocp(const Oracle& o, double* guess, const double* recs, const d
     // multiplier update lambda += alpha (y - lambda) is carried as A^T lambda (the constraint Jacobian does
     // not change within a solve: frozen records, Q4) — DESIGN.md §4.2.
     const bool bfgs = p.use_BFGS != 0;
+    // At most BFGS_MAX_TERMS low-rank terms are held (the engine's LRX).  An update that would need more restarts
+    // the quasi-Newton matrix instead: that SQP iteration's Hessian is the exact one of setQP (as in iteration 0,
+    // :440), the terms are dropped, and later iterations update from it.  Below 1 + BFGS_MAX_TERMS / 2 = 15 SQP
+    // iterations no restart can happen, so the reference's update is reproduced verbatim there.
+    bool bfgs_restart = false;
     LowRank lr;
     StructQP S0;
     std::vector<double> P0, grad_L_prev(nv, 0.0), g_lam(nv, 0.0), step_prev(nv, 0.0), qd(nv, 0.0);
@@ -2057,7 +2063,7 @@ static int solve_ocp(const Oracle& o, double* guess, const double* recs, const d
     auto bfgs_grad = [&](int iter) {  // grad_L = q + A^T lambda; Hess_ = BFGSUpdate(Hess_, step_prev, dgrad_L)
         std::vector<double> gl(nv);
         for (int i = 0; i < nv; i++) gl[i] = qd[i] + g_lam[i];
-        if (iter > 0) {
+        if (iter > 0 && !bfgs_restart) {
             std::vector<double> dg(nv);
             for (int i = 0; i < nv; i++) dg[i] = gl[i] - grad_L_prev[i];
             if (!bfgs_update(S0, lr, step_prev, dg)) bfgs_nan = true;
@@ -2067,11 +2073,13 @@ static int solve_ocp(const Oracle& o, double* guess, const double* recs, const d
     for (it = 0; it < p.max_iter; it++) {
         // setQP + PD / NaN checks of the normalized Hessian (:445-473)
         bool nan = false, pd = true;
+        bfgs_restart = bfgs && it > 0 && lr.r() + 2 > BFGS_MAX_TERMS;
+        if (bfgs_restart) { lr.u.clear(); lr.c.clear(); }
         if (o.opt.qp_mode == 1) {
             DenseQP q;
             set_qp(o, guess, recs, ucur, true, q);
             if (bfgs) {  // dense form of the same BFGS matrix: P0 + sum_j c_j u_j u_j^T
-                if (it == 0) { P0 = q.P; build_struct_qp(o, guess, recs, ucur, S0); }
+                if (it == 0 || bfgs_restart) { P0 = q.P; build_struct_qp(o, guess, recs, ucur, S0); }
                 qd = q.g;
                 bfgs_grad(it);
                 q.P = P0;
@@ -2126,7 +2134,7 @@ static int solve_ocp(const Oracle& o, double* guess, const double* recs, const d
             StructQP S;
             build_struct_qp(o, guess, recs, ucur, S);
             if (bfgs) {  // the QP keeps the Hessian of iteration 0 (setQP without Hess_, :441-442)
-                if (it == 0) S0 = S;
+                if (it == 0 || bfgs_restart) S0 = S;
                 else for (int k = 0; k <= N; k++) std::memcpy(S.st[k].H, S0.st[k].H, sizeof S.st[k].H);
                 for (int k = 0; k <= N; k++) {
                     for (int a = 0; a < NX; a++) qd[(size_t)NX * k + a] = S.st[k].h[a];

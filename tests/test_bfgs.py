@@ -73,9 +73,11 @@ def test_lowrank_qp_step(built_lib, oracle_lib, nlr):
 
 @pytest.mark.parametrize("mask,B", [(2, 512), (7, 256)])
 def test_bfgs_batch_parity(built_lib, oracle_lib, mask, B):
+    """The reference's own sqp.json with use_BFGS switched on: max_iter 100, eps_prim 0.1 (sqp.json:2-5)."""
     import mpcc_manipulator_amd as m
-    o, P, track = make_oracle(N=20, max_iter=3, mask=mask, overrides=OV, nthreads=16)
-    assert P["use_BFGS"] == 1
+    OV = {"sqp": {"use_BFGS": 1}}
+    o, P, track = make_oracle(N=20, max_iter=None, mask=mask, overrides=OV, nthreads=16)
+    assert P["use_BFGS"] == 1 and P["max_iter"] == 100 and P["eps_prim"] == 0.1
     ob = (0.48, 0.218, 0.521, 5.0)
     pool = oracle_pool(o, 120, obs=ob if mask == 7 else (3.0, 3.0, 3.0, 0.0))
     rng = np.random.default_rng(SEED + 700 + mask)
@@ -91,7 +93,7 @@ def test_bfgs_batch_parity(built_lib, oracle_lib, mask, B):
     assert np.abs(outg["horizon"][:, :-1, 9:] - outo["horizon"][:, :-1, 9:]).max() <= 1e-6
     assert np.abs(outg["horizon"] - outo["horizon"]).max() <= 1e-6
     # the update is live: the exact-Hessian SQP (use_BFGS = 0) gives different inputs
-    eng2 = m.Engine(m.load_params(N=20, overrides={"sqp": {"max_iter": 3}}), max_batch=B, constraint_mask=mask)
+    eng2 = m.Engine(m.load_params(N=20), max_batch=B, constraint_mask=mask)
     eng2.set_track(*track)
     eng2.set_warmstart(guess, valid, fails)
     out2 = eng2.solve(x0.copy(), u0, obs)
@@ -184,6 +186,33 @@ def test_bfgs_max_iter_10_parity(built_lib, oracle_lib, mask, B):
     eng.set_track(*track)
     xg, outg, stats, outo = _run(m, eng, o, x0, u0, obs, guess, valid, fails)
     assert np.sum(outo["sqp_iters"] >= 4) >= B // 16, np.bincount(outo["sqp_iters"])  # > LRM terms in play
+    assert np.array_equal(outg["status"], outo["status"])
+    assert np.array_equal(stats["sqp_iter"], outo["sqp_iters"])
+    assert np.abs(outg["horizon"] - outo["horizon"]).max() <= 1e-6
+    eng.close()
+
+
+@pytest.mark.parametrize("mask,B", [(2, 64), (7, 32)])
+def test_bfgs_restart_parity(built_lib, oracle_lib, mask, B):
+    """More updates than the LRX = 28 low-rank terms hold: with eps_prim 3e-3 BFGS-SQP runs past 15 iterations, and
+    the update of iteration 15 (and 29) restarts the quasi-Newton matrix from that iteration's exact Hessian (ipm_wide.hip
+    bfgs_pre; the oracle's solve_ocp BFGS_MAX_TERMS).  No error for the batch; status, SQP iterations
+    and the horizon as in test_bfgs_batch_parity."""
+    import mpcc_manipulator_amd as m
+    ov = {"sqp": {"max_iter": 40, "use_BFGS": 1, "eps_prim": 3e-3}}
+    o, P, track = make_oracle(N=20, max_iter=40, mask=mask, overrides=ov, nthreads=16)
+    ob = (0.48, 0.218, 0.521, 5.0)
+    pool = oracle_pool(o, 60, obs=ob if mask == 7 else (3.0, 3.0, 3.0, 0.0))
+    rng = np.random.default_rng(SEED + 760 + mask)
+    obs = np.tile(ob, (B, 1)) if mask == 7 else None
+    x0, u0, obs, guess, valid, fails = batch_from_pool(pool, B, rng, obs=obs, qnoise=0.02)
+    valid[::2] = 0
+    eng = m.Engine(m.load_params(N=20, overrides=ov), max_batch=B, constraint_mask=mask)
+    eng.set_track(*track)
+    xg, outg, stats, outo = _run(m, eng, o, x0, u0, obs, guess, valid, fails)
+    # restarts in play: controllers that converge on a restarted Hessian, others that run into MAX_ITER
+    assert np.sum((outo["sqp_iters"] >= 15) & (outo["status"] == 0)) >= B // 8, np.bincount(outo["sqp_iters"])
+    assert np.any(outo["status"] == 1)
     assert np.array_equal(outg["status"], outo["status"])
     assert np.array_equal(stats["sqp_iter"], outo["sqp_iters"])
     assert np.abs(outg["horizon"] - outo["horizon"]).max() <= 1e-6

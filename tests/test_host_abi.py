@@ -126,19 +126,12 @@ def test_engine_fails_loudly_without_gpu(built_lib):
         m.Engine(params, max_batch=4, constraint_mask=2)
 
 
-def test_bfgs_max_iter_bound(built_lib):
-    """Damped BFGS (osqp_interface.cpp:683-715) is held as the iteration-0 Hessian plus 2 low-rank terms per
-    update, at most LRX = 28 terms: max_iter > 15 with use_BFGS is an error raised before any
-    device work, never a silent fallback to plain SQP."""
-    import mpcc_manipulator_amd as m
-    params = m.load_params(N=20, overrides={"sqp": {"use_BFGS": 1.0, "max_iter": 16}})
-    with pytest.raises(m.MpccError, match="max_iter"):
-        m.Engine(params, max_batch=4, constraint_mask=2)
-
-
 @pytest.mark.skipif(torch.cuda.is_available(), reason="checks the no-GPU failure path")
-@pytest.mark.parametrize("max_iter", [3, 10, 15])
+@pytest.mark.parametrize("max_iter", [3, 10, 15, 16, 100])
 def test_bfgs_passes_validation(built_lib, max_iter):
+    """Damped BFGS (osqp_interface.cpp:683-715) takes any max_iter, the reference sqp.json's 100 included: past
+    LRX = 28 low-rank terms the quasi-Newton matrix restarts from that iteration's exact Hessian,
+    so validation accepts it and without a GPU creation fails only at the device."""
     import mpcc_manipulator_amd as m
     params = m.load_params(N=20, overrides={"sqp": {"use_BFGS": 1.0, "max_iter": max_iter}})
     assert params.use_BFGS == 1

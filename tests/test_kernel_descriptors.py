@@ -13,10 +13,10 @@ import pytest
 
 LLVM = "/opt/rocm/lib/llvm/bin"
 # sizeof(DevConst) at this revision: the kernel-argument segment of k_ipm<9> (DevConst + DevBuffers, then the 256
-# bytes of HIP's hidden arguments) minus DevBuffers' 29 pointers (232 bytes).  Any private segment this large could
-# hold a copy.
+# bytes of HIP's hidden arguments) minus DevBuffers (29 pointers and the low-rank stride, 240 bytes).  Any private
+# segment this large could hold a copy.
 DEVCONST_BYTES = 3288
-DEVBUFFERS_PTRS = 29
+DEVBUFFERS_BYTES = 240
 PANDA_NARROW_MAX = 1740   # 1.7 KB: k_sqp / k_ipm of ipm.hip (16-lane interior point, tail mode included)
 WIDE_MAX = 2400           # 2.3 KB: the 32-lane kernels of ipm_wide.hip (mobile build, damped BFGS incl. the extended low-rank path)
 
@@ -58,7 +58,7 @@ def test_no_private_devconst_copy(built_lib, tmp_path):
         for name, v in kern.items():
             priv = v.get("private_segment_fixed_size", 0)
             assert priv < DEVCONST_BYTES, f"{name}: {priv}-byte private segment could hold a DevConst copy"
-            if "5k_sqp" in name or "5k_ipm" in name:
+            if re.search(r"\d+k_(sqp|sqp_solo|ipm)I", name):  # k_sqp, k_sqp_solo, k_ipm (mangled: <len>k_...I<args>)
                 # ipm_wide.hip's kernels carry a bool template argument (ILb0/ILb1 after the row count)
                 wide = dof == 10 or re.search(r"ILi\d+ELb[01]E", name) is not None
                 lim = WIDE_MAX if wide else PANDA_NARROW_MAX
@@ -67,5 +67,5 @@ def test_no_private_devconst_copy(built_lib, tmp_path):
         # the DevConst size the bound is derived from
         if dof == 7:
             ka = [v["kernarg_segment_size"] for k, v in kern.items() if k.startswith("_ZN4mpcc5k_ipmILi9E")]
-            assert ka and ka[0] - 8 * DEVBUFFERS_PTRS - 256 == DEVCONST_BYTES
+            assert ka and ka[0] - DEVBUFFERS_BYTES - 256 == DEVCONST_BYTES
     assert seen["narrow"] >= 12 and seen["wide"] >= 8

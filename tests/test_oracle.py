@@ -337,6 +337,28 @@ def test_bfgs_layouts_agree(oracle_lib):
     assert np.abs(outs[0]["horizon"] - outs[2]["horizon"]).max() > 1e-6  # BFGS is live
 
 
+def test_bfgs_restart_layouts_agree(oracle_lib):
+    """Past LRX = 28 low-rank terms (15 SQP iterations) the damped-BFGS matrix restarts from that iteration's exact
+    Hessian.  The structured oracle (low-rank terms dropped, the stage Hessians re-assembled) and the
+    dense-layout oracle (Hessian_ replaced by setQP's exact one) take the restart alike: same statuses and SQP
+    iteration counts, inputs equal, and controllers do run past the restart."""
+    from helpers import batch_from_pool, oracle_pool
+    N = 8
+    ov = {"sqp": {"max_iter": 40, "use_BFGS": 1, "eps_prim": 1e-3}}
+    (o0, P, _), (o1, _, _) = (make_oracle(N=N, max_iter=40, mask=7, qp_mode=m, overrides=ov, nthreads=8) for m in (0, 1))
+    ob, _, _ = make_oracle(N=N, max_iter=3, mask=7, overrides={"sqp": {"max_iter": 3}}, nthreads=8)
+    pool = oracle_pool(ob, 40, obs=(0.48, 0.218, 0.521, 5.0))
+    B = 16
+    rng = np.random.default_rng(SEED + 24)
+    x0, u0, obs, g, v, f = batch_from_pool(pool, B, rng, obs=np.tile([0.48, 0.218, 0.521, 5.0], (B, 1)))
+    v[:] = 0
+    outs = [o.run_mpc(x0.copy(), u0, obs, g.copy(), v.copy(), f.copy()) for o in (o0, o1)]
+    assert np.array_equal(outs[0]["status"], outs[1]["status"])
+    assert np.array_equal(outs[0]["sqp_iters"], outs[1]["sqp_iters"])
+    assert np.sum(outs[0]["sqp_iters"] >= 15) >= 4, outs[0]["sqp_iters"]
+    assert np.abs(outs[0]["horizon"] - outs[1]["horizon"]).max() <= 1e-8
+
+
 def test_params_resolution(oracle_lib):
     """Params/*.json with the reference's override semantics: T_x/T_u (normalization.json:3-20)."""
     P = rp.resolve(N=20)

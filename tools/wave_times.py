@@ -22,6 +22,7 @@ def main():
     ap.add_argument("--batch", type=int, nargs="+", default=[2048, 4096])
     ap.add_argument("--N", type=int, default=20)
     ap.add_argument("--mask", type=int, default=2)
+    ap.add_argument("--obstacles", action="store_true", help="bench.py's obstacle scenario (--config 1-all-rows / 2)")
     args = ap.parse_args()
     import mpcc_manipulator_amd as m
     from mpcc_manipulator_amd.engine import lib
@@ -29,16 +30,14 @@ def main():
     wt = L.mpcc_debug_wave_times
     params = m.load_params(args.N, overrides={"sqp": {"max_iter": 2}})
     params.constraint_mask = args.mask
-    pool, track = bench.make_pool(m, params, args.mask, 1000, 0)
+    oxyz = (0.48, 0.218, 0.521)
+    pool, track = bench.make_pool(m, params, args.mask, 1000, 0, (*oxyz, 5.0) if args.obstacles else (3., 3., 3., 0.))
     for B in args.batch:
         eng = m.Engine(params, max_batch=B, device=0, constraint_mask=args.mask)
         eng.set_track(*track)
-        rng = np.random.default_rng(bench.SEED)
-        idx = np.arange(B) % len(pool["x0"])
-        x0 = pool["x0"][idx].copy()
-        x0[:, :7] += rng.normal(0, 0.005, (4096 if B <= 4096 else B, 7))[:B]
-        a = (x0, pool["u0"][idx], np.tile([3., 3., 3., 0.], (B, 1)))
-        ws = (pool["guess"][idx], pool["valid"][idx].astype(np.int32), pool["fails"][idx].astype(np.int32))
+        x0, u0, obs, g, v, f = bench.batch_inputs(pool, B, 7, args.obstacles, oxyz)
+        a = (x0, u0, obs)
+        ws = (g, v, f)
         for _ in range(3):
             eng.set_warmstart(*ws)
             eng.solve(*[v.copy() for v in a])
