@@ -426,6 +426,7 @@ def main():
     last = (nstep[0] - 1) % 2
     tms = [e.timing_end() for e in engs]
     tmlps = [e.timing_mlp() for e in engs]
+    tsqp = [e.timing_sqp() for e in engs]  # the fused kernel's spans (timing_end splits them over set_qp/solve_qp/get_alpha)
     # the QP-solve launches of all groups, as intervals on engine 0's clock (its window's first event, recorded
     # before any group's first kernel of the timed region): their union is the time the kernel family ran
     nq = max(x[2] for x in tms)  # QP-solve launches of the timed steps per engine (the staged loop: one per SQP iteration)
@@ -450,7 +451,9 @@ def main():
     # with the collision networks on (configs[2]), k_mlp_env.  Launch durations are HIP events on the engine
     # stream around those launches alone, over the timed steps.
     kname = "k_ipm" if os.environ.get("MPCC_STAGED_SQP", "0") == "1" else "k_sqp"
-    t_ipm = tm["solve_qp"] / max(1, nipm)  # mean duration of one launch (B/S instances)
+    nsqp = sum(x[1] for x in tsqp)
+    # mean duration of one launch (B/S instances): the fused kernel's span, or the staged path's k_ipm launches
+    t_ipm = sum(x[0] for x in tsqp) / nsqp if nsqp else tm["solve_qp"] / max(1, nipm)
     # QP solves per step: an instance solves min(sqp_iter + 1, max_iter) QPs (a SOLVED exit at SQP
     # iteration i has solved i + 1); the launches are credited with the QPs they actually solved
     qps = int(np.minimum(stats["sqp_iter"] + 1, args.max_iter).sum())
@@ -551,7 +554,10 @@ def main():
         # exceed the wall time per step
         phases = {k: round(v / max(1, ncalls) / S * 1e3, 4) for k, v in tm.items()}
         phases.update({k: round(v[0] / max(1, ncalls) / S * 1e3, 4) for k, v in tmlp.items() if v[1]})
-        print(json.dumps({"phase_ms_per_group_step": phases, "groups": S, "solved_frac": solved,
+        fr = np.mean([x[2] for x in tsqp], axis=0) if nsqp else np.zeros(4)
+        print(json.dumps({"phase_ms_per_group_step": phases,
+                          "sqp_phase_frac": dict(zip(["set_qp", "solve_qp", "get_alpha", "step"], np.round(fr, 4).tolist())),
+                          "groups": S, "solved_frac": solved,
                           "sqp_iter_hist": np.bincount(stats["sqp_iter"], minlength=3).tolist(),
                           "ipm_iters_mean": float(stats["ipm_iters"].mean()),
                           "pcie_inclusive_solves_per_s": pcie}), file=sys.stderr)

@@ -207,6 +207,14 @@ int mpcc_timing_end(mpcc_engine* e, mpcc_timing* sum, int32_t* n_calls, int32_t*
 /* the collision-MLP launches of the last timing window (after mpcc_timing_end): total seconds and launch count of
  * k_mlp_self and of k_mlp_env, from HIP events around those launches alone on the engine stream */
 int mpcc_timing_mlp(mpcc_engine* e, double* self_s, int32_t* self_n, double* env_s, int32_t* env_n);
+/* the fused SQP kernel (k_sqp, with k_sqp_solo beside it) of the last timing window: the summed launch spans in
+ * seconds, the launch count, and the fractions of its waves' cycles in the phases of solveOCP's ComputeTime
+ * (osqp_interface.cpp:435-564): frac[0] set_qp (QP assembly and Hessian update of SQP iterations >= 1), frac[1]
+ * solve_qp (the QP solves and the correction), frac[2] get_alpha (line-search trials and the filter), frac[3] the
+ * step update.  mpcc_timing_end splits the k_sqp span into set_qp / solve_qp / get_alpha by these fractions (the
+ * step's share stays in total only, as in the reference).  n = 0 in the staged path (every phase has its own
+ * launches and events there). */
+int mpcc_timing_sqp(mpcc_engine* e, double* span_s, int32_t* n, double* frac4);
 /* the launches of one kernel of e's last timing window (kind: MPCC_TIMING_QP = the QP solve, k_sqp or k_ipm in
  * the staged path; MPCC_TIMING_MLP_SELF / _MLP_ENV = the collision networks) as [start, end] in ms after the
  * first event of `anchor`'s window (anchor = e, or another engine on the same device): several engines stepping

@@ -92,6 +92,22 @@ struct mpcc_engine {
     double last_mlp_self_s = 0, last_mlp_env_s = 0;                         // totals of the last timing window
     int last_mlp_self_n = 0, last_mlp_env_n = 0;
     int live_calls = 0;
+    // ComputeTime split of the fused SQP kernel (DevBuffers::phase_cyc): per-phase wave cycles on the device, the
+    // k_sqp spans of the last window and their split (mpcc_timing_sqp)
+    unsigned long long* d_phase = nullptr;
+    std::vector<std::pair<hipEvent_t, hipEvent_t>> lv_sqp;
+    double last_sqp_s = 0, last_frac[PH_N] = {0, 0, 0, 0};
+    int last_sqp_n = 0;
+    // phase fractions from the counters (reset afterwards on stream st); false if nothing was counted
+    bool phase_fracs(double (&f)[PH_N], hipStream_t st) {
+        unsigned long long h[PH_N];
+        HIPCHK(hipMemcpy(h, d_phase, sizeof h, hipMemcpyDeviceToHost));
+        HIPCHK(hipMemsetAsync(d_phase, 0, sizeof h, st));
+        double sum = 0;
+        for (int i = 0; i < PH_N; i++) sum += (double)h[i];
+        for (int i = 0; i < PH_N; i++) f[i] = sum > 0 ? (double)h[i] / sum : 0.0;
+        return sum > 0;
+    }
     hipEvent_t live_ev() {
         if (live_used == live_pool.size()) {
             hipEvent_t e;
@@ -108,6 +124,7 @@ struct mpcc_engine {
         if (d.isw != d.is) f(d.isw);
         f(d.lr); f(d.lrc); f(d.glam); f(d.gprev); f(d.aty); f(d.sp); f(d.lrq);
         f(d.dbg_trace);
+        f(d_phase);
         f(bchk);
         f(s_x0); f(s_u0); f(s_obs); f(s_u0out); f(s_hor); f(s_status); f(s_ok);
         f(nn_self.d); f(nn_env.d);
@@ -371,6 +388,15 @@ void quiesce(mpcc_engine* e) {
     }
 }
 
+// the fused kernel's span T over the ComputeTime fields by its waves' phase fractions: set_qp gets the in-kernel QP
+// assembly on top of k_setqp's launch, solve_qp the QP solves, get_alpha the line search; the step update's share
+// stays in total only (the reference times it in none of the four, osqp_interface.cpp:548-564)
+void split_sqp(mpcc_timing& t, double T, const double (&f)[PH_N]) {
+    t.set_qp += T * f[PH_SETQP];
+    t.solve_qp = T * f[PH_SOLVE];
+    t.get_alpha += T * f[PH_ALPHA];
+}
+
 constexpr int IPW_SQP = 4;  // instances per k_sqp wave (ipm.hip IPW)
 void run_batch(mpcc_engine* e, int B, hipStream_t st, mpcc_timing* timing, bool ocp = false) {
     DevConst c = e->make_const(B);
@@ -395,6 +421,9 @@ void run_batch(mpcc_engine* e, int B, hipStream_t st, mpcc_timing* timing, bool 
     };
     std::vector<std::pair<int, int>> set_qp, solve_qp, get_alpha;
     int t0 = -1, t_env0 = -1, t_env1 = -1, t_end = -1;
+    const bool fused = !e->staged_sqp || c.p.use_BFGS;
+    d.phase_cyc = (tm && fused) ? e->d_phase : nullptr;  // the fused kernels' ComputeTime split (PhaseClock)
+    bool sqp_timed = false;
     if (tm) t0 = mark();
     if (d.dbg_trace) HIPCHK(hipMemsetAsync(d.dbg_trace, 0, sizeof(double) * B * TRACE_IT * TRACE_W, st));
     launched = true;
@@ -423,7 +452,7 @@ void run_batch(mpcc_engine* e, int B, hipStream_t st, mpcc_timing* timing, bool 
     }
     if (tm) t_env1 = mark();
     const double* ucur = d.u0;
-    if (!e->staged_sqp || c.p.use_BFGS) {
+    if (fused) {
         // first QP assembly lane-per-stage, then the whole SQP loop per instance in one kernel (the damped-BFGS
         // option always on the fused 32-lane kernel)
         int a0 = -1, a1 = -1, b1 = -1;
@@ -470,6 +499,7 @@ void run_batch(mpcc_engine* e, int B, hipStream_t st, mpcc_timing* timing, bool 
             b1 = mark();
             set_qp.push_back({a0, a1});
             solve_qp.push_back({a1, b1});
+            sqp_timed = true;
         }
     } else {
     e->last_wide = DOF != 7;  // the staged loop's k_ipm: 16 lanes for the Panda (a wide debug QP before must not stick)
@@ -516,6 +546,8 @@ void run_batch(mpcc_engine* e, int B, hipStream_t st, mpcc_timing* timing, bool 
         for (auto& pr : set_qp) e->lv_setqp.push_back({evs[pr.first], evs[pr.second]});
         for (auto& pr : solve_qp) e->lv_ipm.push_back({evs[pr.first], evs[pr.second]});
         for (auto& pr : get_alpha) e->lv_alpha.push_back({evs[pr.first], evs[pr.second]});
+        if (sqp_timed)
+            for (auto& pr : solve_qp) e->lv_sqp.push_back({evs[pr.first], evs[pr.second]});
         e->live_calls++;
     }
     if (timing) {
@@ -527,6 +559,8 @@ void run_batch(mpcc_engine* e, int B, hipStream_t st, mpcc_timing* timing, bool 
         for (auto& pr : solve_qp) timing->solve_qp += el(pr.first, pr.second);
         for (auto& pr : get_alpha) timing->get_alpha += el(pr.first, pr.second);
         timing->total = el(t0, t_end);
+        double f[PH_N];
+        if (sqp_timed && !e->live && e->phase_fracs(f, st)) split_sqp(*timing, timing->solve_qp, f);
     }
 }
 
@@ -632,6 +666,8 @@ int mpcc_create(const mpcc_config* cfg, const mpcc_params* params, const char* n
         d.sqi = dmalloc<int32_t>(B * SQI);
         d.sqd = dmalloc<double>(B * SQ);
         d.order = dmalloc<int32_t>((size_t)order_slots((int)B) + B);
+        e->d_phase = dmalloc<unsigned long long>(PH_N);
+        HIPCHK(hipMemset(e->d_phase, 0, PH_N * sizeof(unsigned long long)));
         HIPCHK(hipMemset(d.guess, 0, B * NS * NXU * sizeof(double)));
         HIPCHK(hipMemset(d.valid, 0, B * sizeof(int32_t)));
         HIPCHK(hipMemset(d.fails, 0, B * sizeof(int32_t)));
@@ -931,7 +967,13 @@ int mpcc_timing_begin(mpcc_engine* e) {
     e->live_used = 0;
     e->live_calls = 0;
     e->lv_env.clear(); e->lv_setqp.clear(); e->lv_ipm.clear(); e->lv_alpha.clear(); e->lv_total.clear();
-    e->lv_mlp_self.clear(); e->lv_mlp_env.clear();
+    e->lv_mlp_self.clear(); e->lv_mlp_env.clear(); e->lv_sqp.clear();
+    try {
+        HIPCHK(hipMemsetAsync(e->d_phase, 0, PH_N * sizeof(unsigned long long), e->stream));
+    } catch (const HipError& x) {
+        e->live = false;
+        return fail(MPCC_E_HIP, x.what());
+    }
     return MPCC_OK;
 }
 
@@ -959,6 +1001,12 @@ int mpcc_timing_end(mpcc_engine* e, mpcc_timing* sum, int32_t* n_calls, int32_t*
         e->last_mlp_env_s = acc(e->lv_mlp_env);
         e->last_mlp_self_n = (int)e->lv_mlp_self.size();
         e->last_mlp_env_n = (int)e->lv_mlp_env.size();
+        e->last_sqp_s = acc(e->lv_sqp);
+        e->last_sqp_n = (int)e->lv_sqp.size();
+        double f[PH_N] = {0, 0, 0, 0};
+        HIPCHK(hipDeviceSynchronize());  // the counters of launches on caller streams too
+        if (e->phase_fracs(f, e->stream) && e->last_sqp_n) split_sqp(t, e->last_sqp_s, f);
+        for (int i = 0; i < PH_N; i++) e->last_frac[i] = f[i];
         if (sum) *sum = t;
         if (n_calls) *n_calls = e->live_calls;
         if (n_ipm) *n_ipm = (int32_t)e->lv_ipm.size();
@@ -1420,6 +1468,15 @@ int mpcc_build_flags(void) {
     f |= MPCC_BUILD_PROF;
 #endif
     return f;
+}
+
+int mpcc_timing_sqp(mpcc_engine* e, double* span_s, int32_t* n, double* frac4) {
+    if (!e) return fail(MPCC_E_INVALID, "mpcc_timing_sqp: null engine");
+    if (span_s) *span_s = e->last_sqp_s;
+    if (n) *n = e->last_sqp_n;
+    if (frac4)
+        for (int i = 0; i < PH_N; i++) frac4[i] = e->last_frac[i];
+    return MPCC_OK;
 }
 
 int mpcc_timing_mlp(mpcc_engine* e, double* self_s, int32_t* self_n, double* env_s, int32_t* env_n) {

@@ -107,6 +107,9 @@ static_assert(QS_POLY + 2 * 15 <= QS_YLB + 16 * QLINES, "bound block of <= 2 pol
 #ifndef MPCC_WIDE_RING
 #define MPCC_WIDE_RING 1
 #endif
+#ifndef MPCC_WIDE_TAIL
+#define MPCC_WIDE_TAIL 1  // tail mode for the wide-poly variants (ipm_tail.h, round 5)
+#endif
 constexpr int LRING_W = 2, QLINES_W = 14;
 static_assert(QS_POLY + NPC * 15 <= QS_YLB + 16 * QLINES_W, "bound block of all poly rows in QLINES_W lines");
 __host__ __device__ constexpr bool use_ring(int npm) { return npm <= 2 || (MPCC_WIDE_RING && npm >= 9); }
@@ -418,6 +421,26 @@ __device__ __forceinline__ void sweep_ring(int N, bool backward, In (&b)[D], Loa
     }
 }
 
+// Workspace field indices of the NPM variant (ipm_group and tail mode).  The wide-poly variants (NPM >= 9) order
+// their fields so that each light sweep's LDS-ring image is the shortest run from field 0: the poly slot state and
+// c_p^T z right after the iterate, then K and kff (predictor forward), the predictor step and c_p^T dza (corrector
+// forward), the gradient and F^-1 (corrector backward); c_p^T dz and the corrector step are read by the
+// factorization only.  The narrow variants keep the enum order (their poly slot state is packed into WF_ZV).
+template <int NPM>
+struct WsF {
+    static constexpr bool WLAY = NPM >= 9;
+    static constexpr int SL = WF_SL, LL = WF_LL, SU = WF_SU, LU = WF_LU, ZX = WF_ZX, ZV = WF_ZV;
+    static constexpr int SP = WLAY ? 6 : WF_SP, LP = WLAY ? 7 : WF_LP, PZ = WLAY ? 8 : WF_PZ;
+    static constexpr int KR = WLAY ? 9 : WF_KR, GVK = KR + 8, AX = GVK + 1, AV = AX + 1;
+    static constexpr int PA = WLAY ? AV + 1 : WF_PA, GX = WLAY ? PA + 1 : WF_GX, FI = GX + 1;
+    static constexpr int PD = WLAY ? FI + 4 : WF_PD, DX = WF_DX, DV = WF_DV;
+    static_assert(WLAY || (GVK == WF_GVK && AX == WF_AX && AV == WF_AV && FI == WF_FI), "narrow layout = enum");
+    static_assert(!WLAY || (PD == WF_PD && PD + 1 == DX), "wide layout: a permutation of the enum's fields");
+    // poly slot state packed into the upper lanes of the v field (<= 4 poly rows); c_p^T z, dza, dz cached in the
+    // workspace (wide-poly variants)
+    static constexpr bool PACKP = NPM <= 4, PCACHE = NPM >= 9;
+};
+
 #include "ipm_tail.h"
 
 }  // namespace
@@ -426,19 +449,13 @@ __device__ __forceinline__ void sweep_ring(int N, bool backward, In (&b)[D], Loa
 // idle through it.  Writes the step (d.step), QP status and IPM iteration count (d.sqi).
 template <int NPM>
 __device__ __forceinline__ bool ipm_group(const DevConst& c, const DevBuffers& d, double* smem) {
-    // Workspace field indices of this variant.  The wide-poly variants (NPM >= 9) order their fields so that each
-    // light sweep's LDS-ring image is the shortest run from field 0: the poly slot state and c_p^T z right after
-    // the iterate, then K and kff (predictor forward), the predictor step and c_p^T dza (corrector forward), the
-    // gradient and F^-1 (corrector backward); c_p^T dz and the corrector step are read by the factorization only.
-    // The narrow variants keep the enum order (their poly slot state is packed into WF_ZV).
-    constexpr bool WLAY = NPM >= 9;
-    constexpr int F_SL = WF_SL, F_LL = WF_LL, F_SU = WF_SU, F_LU = WF_LU, F_ZX = WF_ZX, F_ZV = WF_ZV;
-    constexpr int F_SP = WLAY ? 6 : WF_SP, F_LP = WLAY ? 7 : WF_LP, F_PZ = WLAY ? 8 : WF_PZ;
-    constexpr int F_KR = WLAY ? 9 : WF_KR, F_GVK = F_KR + 8, F_AX = F_GVK + 1, F_AV = F_AX + 1;
-    constexpr int F_PA = WLAY ? F_AV + 1 : WF_PA, F_GX = WLAY ? F_PA + 1 : WF_GX, F_FI = F_GX + 1;
-    constexpr int F_PD = WLAY ? F_FI + 4 : WF_PD, F_DX = WF_DX, F_DV = WF_DV;
-    static_assert(WLAY || (F_GVK == WF_GVK && F_AX == WF_AX && F_AV == WF_AV && F_FI == WF_FI), "narrow layout = enum");
-    static_assert(!WLAY || (F_PD == WF_PD && F_PD + 1 == F_DX), "wide layout: a permutation of the enum's fields");
+    // Workspace field indices of this variant (WsF)
+    using L = WsF<NPM>;
+    constexpr int F_SL = L::SL, F_LL = L::LL, F_SU = L::SU, F_LU = L::LU, F_ZX = L::ZX, F_ZV = L::ZV;
+    constexpr int F_SP = L::SP, F_LP = L::LP, F_PZ = L::PZ;
+    constexpr int F_KR = L::KR, F_GVK = L::GVK, F_AX = L::AX, F_AV = L::AV;
+    constexpr int F_PA = L::PA, F_GX = L::GX, F_FI = L::FI;
+    constexpr int F_PD = L::PD, F_DX = L::DX, F_DV = L::DV;
     constexpr int NPE = NPM > 0 ? NPM : 1;
     using In = StageIn<NPE>;
     const int lane = threadIdx.x;
@@ -542,12 +559,12 @@ __device__ __forceinline__ bool ipm_group(const DevConst& c, const DevBuffers& d
 
     // Poly slot state packed into the upper lanes of the v field (<= 4 poly rows): every sweep then loads
     // 6 workspace lines of slot and iterate state per stage instead of 8.
-    constexpr bool PACKP = NPM <= 4;
+    constexpr bool PACKP = L::PACKP;
     // Wide-poly variants: c_p^T z, c_p^T dza and c_p^T dz (11 reductions over the row's 16 lanes each) are formed
     // once per iteration where z, dza, dz are made, kept in the workspace (F_PZ, F_PA, F_PD) and read by the
     // other sweeps, which recomputed them from the same stored vectors (the same values: 3 evaluations per stage
     // and iteration instead of 11)
-    constexpr bool PCACHE = NPM >= 9;
+    constexpr bool PCACHE = L::PCACHE;
     // The same for 1 or 2 poly rows at no extra traffic: c_p^T z rides in the free lanes 10 + p of the packed F_ZV,
     // c_p^T dza and c_p^T dz in lanes 8 + p of F_AV and F_DV (whose v occupies lanes 0..7; readers mask them)
     constexpr bool PCN = MPCC_PCN && NPM >= 1 && NPM <= 2;
@@ -857,7 +874,9 @@ __device__ __forceinline__ bool ipm_group(const DevConst& c, const DevBuffers& d
     const double lam_scale = (attempt == 0) ? IPM_L0 : 0.0;
     const int max_it = (attempt == 0) ? IPM_MAX_IT_SCALED : IPM_MAX_IT;
     if (attempt == 1) {
-        run = entered && !conv;  // restart only the solves that did not converge from the scaled start
+        // restart only the solves that hit the cap or broke down from the scaled start; a P3 divergence is final
+        // (the oracle's solve_struct_ipm)
+        run = entered && !conv && !diverged;
         if (__ballot(run) == 0) break;
         if (run) diverged = false;
     }
@@ -903,13 +922,14 @@ __device__ __forceinline__ bool ipm_group(const DevConst& c, const DevBuffers& d
     if (run) alpha = 0.0;
     while (true) {
         if (__ballot(run) == 0) break;
-        if constexpr (NPM <= 2) {
+        if constexpr (NPM <= 2 || (MPCC_WIDE_TAIL && NPM >= 9)) {
             // Tail mode (ipm_tail.h): the wave's last running instance takes all four groups for the rest of its
             // solve.  Its iteration state goes to LDS and the solve continues in ipm_tail_solve after this function
             // returns (a call from here would change this function's register allocation); the wave's other
             // instances are done with this QP, and none of them waits for the restart of attempt 1.
             const unsigned long long lead = __ballot(run && t == 0);
-            if (c.tail && __popcll(lead) == 1 && __ballot(t == 0 && !run && entered && !conv && attempt == 0) == 0) {
+            if (c.tail && __popcll(lead) == 1 &&
+                __ballot(t == 0 && !run && entered && !conv && !diverged && attempt == 0) == 0) {
                 tail_gs = (__ffsll((long long)lead) - 1) >> 4;
                 tail_req = true;
                 if (lane == tail_gs * 16) {
@@ -1659,7 +1679,7 @@ __device__ __forceinline__ void solo_post(double* smem, double cmd) {
 template <int NPM, bool SB = false>
 __device__ __forceinline__ void sqp_qp_solve(const DevConst& c, const DevBuffers& d, double* smem) {
     if (sqp_ipm_phase<NPM>(c, d, smem)) {
-        if constexpr (NPM <= 2) {
+        if constexpr (NPM <= 2 || (MPCC_WIDE_TAIL && NPM >= 9)) {
             if constexpr (SB) {
                 solo_post(smem, 1.0);
                 ipm_tail_solve<NPM, SB_GB>(c, d, smem);
@@ -1719,6 +1739,7 @@ __device__ __forceinline__ void sqp_waves(const DevConst& c, const DevBuffers& d
 #else
 #define SPMARK(i) do { } while (0)
 #endif
+    PhaseClock ph(d.phase_cyc);  // the ComputeTime split (mpcc_timing): set_qp / solve_qp / get_alpha / step
     for (int it = 0; it < c.p.max_iter; it++) {
         bool act = valid && si[SQ_ACTIVE] != 0;
         if (__ballot(act) == 0) break;
@@ -1726,11 +1747,13 @@ __device__ __forceinline__ void sqp_waves(const DevConst& c, const DevBuffers& d
         sp_it++;
 #endif
         SPMARK(4);
+        ph.mark(PH_STEP);
         if (it > 0) {
             if (pb < c.Bn && psi[SQ_ACTIVE] != 0) sqp_setqp_phase(c, d, pb, pt, pst, pucur);
             bar();
         }
         SPMARK(0);
+        ph.mark(PH_SETQP);
         sqp_qp_solve<NPM, SB>(c, d, smem);
         bar();
         SPMARK(1);
@@ -1740,6 +1763,7 @@ __device__ __forceinline__ void sqp_waves(const DevConst& c, const DevBuffers& d
             sqp_qp_solve<NPM, SB>(c, d, smem);  // a failed correction keeps the step (Q6)
             bar();
         }
+        ph.mark(PH_SOLVE);
         act = valid && si[SQ_ACTIVE] != 0;
         const bool pact = pb < c.Bn && psi[SQ_ACTIVE] != 0;
         if (pact) sqp_trial_phase(c, d, pb, pt, pst, pucur, 1.0, true);
@@ -1755,6 +1779,7 @@ __device__ __forceinline__ void sqp_waves(const DevConst& c, const DevBuffers& d
                 sqp_trial_phase(c, d, pb, pt, pst, pucur, alpha, false);
             }
         }
+        ph.mark(PH_ALPHA);
         double nrm = 0.0;
         if (act) {
             const double alpha = d.sqd[(size_t)b * SQ + SQ_ALPHA];
@@ -1764,6 +1789,8 @@ __device__ __forceinline__ void sqp_waves(const DevConst& c, const DevBuffers& d
         if (act && t == 0) finish_iteration(c, d, b, nrm);
         bar();
     }
+    ph.mark(PH_STEP);
+    ph.flush(threadIdx.x == 0);
     if constexpr (SB) solo_post(smem, 0.0);  // the helper leaves
 #ifdef MPCC_IPM_PROF
     SPMARK(4);

@@ -18,7 +18,10 @@
 // in stage order, so a tail-mode solve is bitwise the normal one (tests/test_tail_mode.py checks it on the GPU;
 // only a tie of the fraction-to-boundary candidates within product rounding could pick the other candidate).
 //
-// Narrow variants only (NPM <= 2: the poly slot state packed into WF_ZV, no cached poly products).
+// Narrow variants (NPM <= 2: the poly slot state packed into WF_ZV) and, since round 5, the wide-poly variants
+// (NPM >= 9: the workspace layout WsF, the poly slot state in its own fields, c_p^T z / dza / dz cached in the
+// workspace, the poly Gram blocks of F, Gm and Hb on the matrix cores in phase A: the group transposes of ipm_group
+// act on four stages of one instance here instead of four instances).
 
 #ifndef MPCC_TAIL_P1
 #define MPCC_TAIL_P1 1  // phase B's P update without the instance transposes (0: ipm_group's form)
@@ -48,6 +51,7 @@ constexpr int TL_LC = TL_LB + 4 * 16 * 2;       // C -> D: per slot row (L, U, P
 constexpr int TL_LM = TL_LC + 4 * 16 * 14;      // per-group combine scratch: 64 lanes x 4
 static_assert((TL_STATE + 16) * 8 <= LRING * LG(LF_CBWD) * 1024, "tail-mode LDS inside the narrow variants' ring");
 static_assert((TL_LM + 64 * 4) * 8 <= LRING * LG(LF_CBWD) * 1024, "tail-mode LDS inside the narrow variants' ring");
+static_assert((TL_STATE + 16) * 8 <= LRING_W * LG(WF_PD, QLINES_W) * 1024, "tail-mode LDS inside the wide variants' ring");
 // The same layout for GB 16-lane groups (GB / 4 waves of one workgroup: solo blocks); GB = 4 is the
 // layout above.  Phase B's P exchange uses the K area of the wave's first group.
 template <int GB>
@@ -71,8 +75,11 @@ static_assert(TailLayout<SB_GB>::SIZE <= SB_CMD && TL_STATE + 16 <= SB_CMD, "sol
 
 template <int NPM, int GB>
 __device__ __attribute__((noinline)) void ipm_tail(const DevConst& c, const DevBuffers& d, double* smem, int b, TailIO& io) {
-    static_assert(NPM <= 2, "tail mode: narrow variants");
+    static_assert(NPM <= 2 || NPM >= 9, "tail mode: narrow and wide-poly variants");
+    static_assert(!(MPCC_PCN && NPM >= 1 && NPM <= 2), "tail mode does not carry the MPCC_PCN lane cache");
     static_assert(GB % 4 == 0, "whole waves");
+    using L = WsF<NPM>;
+    constexpr bool PACKP = L::PACKP, PCACHE = L::PCACHE, GRAM_MFMA = MPCC_GRAM_MFMA && NPM >= 9;
     using namespace dpp;
     using TLy = TailLayout<GB>;
     constexpr int NWV = GB / 4;  // waves on the instance
@@ -135,7 +142,7 @@ __device__ __attribute__((noinline)) void ipm_tail(const DevConst& c, const DevB
     };
     const bool own = G == 0;  // the group that stores what all groups computed redundantly (phases B, D)
 
-    // ---- stage loaders (ipm_group's, PACKP form)
+    // ---- stage loaders (ipm_group's)
     auto load_common = [&](int k, In& o) {
         const gdouble* q = qs_stage(k);
         o.lb = q[rowY ? QS_YLB + t : QS_DLB + j9];
@@ -150,12 +157,18 @@ __device__ __attribute__((noinline)) void ipm_tail(const DevConst& c, const DevB
         }
         const double pu = q[QS_POLY + 15 * (t < NPE ? t : 0) + 14];
         o.pub = (t < NPM) ? pu : INF;
-        o.sL = *ws(k, WF_SL); o.lL = *ws(k, WF_LL); o.sU = *ws(k, WF_SU); o.lU = *ws(k, WF_LU);
-        o.zx = *ws(k, WF_ZX);
-        const double zraw = *ws(k, WF_ZV);
-        o.sP = from_up<8>(zraw);
-        o.lP = from_up<12>(zraw);
-        o.zv = (t < 8) ? zraw : 0.0;
+        o.sL = *ws(k, L::SL); o.lL = *ws(k, L::LL); o.sU = *ws(k, L::SU); o.lU = *ws(k, L::LU);
+        o.zx = *ws(k, L::ZX);
+        if constexpr (PCACHE) { o.pz = *ws(k, L::PZ); o.pca = *ws(k, L::PA); o.pcd = *ws(k, L::PD); }
+        const double zraw = *ws(k, L::ZV);
+        if constexpr (PACKP) {
+            o.sP = from_up<8>(zraw);
+            o.lP = from_up<12>(zraw);
+            o.zv = (t < 8) ? zraw : 0.0;
+        } else {
+            o.sP = *ws(k, L::SP); o.lP = *ws(k, L::LP);
+            o.zv = zraw;
+        }
     };
     auto load_factor = [&](int k, In& o, bool upd) {
         load_common(k, o);
@@ -169,37 +182,44 @@ __device__ __attribute__((noinline)) void ipm_tail(const DevConst& c, const DevB
         o.m[9] = (t < 9) ? qv : 0.0;
         o.m[10] = (t < 8 && k < N) ? rv : 0.0;
         o.m[11] = (t < 8 && k < N) ? rr : 0.0;
-        const double x0 = *ws(k, WF_DX), x1 = *ws(k, WF_DV), x2 = *ws(k, WF_AX), x3 = *ws(k, WF_AV);
+        const double x0 = *ws(k, L::DX), x1 = *ws(k, L::DV), x2 = *ws(k, L::AX), x3 = *ws(k, L::AV);
         o.x0 = upd ? x0 : 0.0; o.x1 = upd ? x1 : 0.0; o.x2 = upd ? x2 : 0.0; o.x3 = upd ? x3 : 0.0;
     };
     auto load_fwd = [&](int k, In& o, bool corr) {
         load_common(k, o);
 #pragma unroll
-        for (int m = 0; m < 8; m++) o.m[m] = *ws(k, WF_KR + m);
-        o.m[8] = from_up<8>(*ws(k, WF_GVK));
+        for (int m = 0; m < 8; m++) o.m[m] = *ws(k, L::KR + m);
+        o.m[8] = from_up<8>(*ws(k, L::GVK));
         if (corr) {
-            o.x0 = *ws(k, WF_AX);
-            o.x1 = *ws(k, WF_AV);
+            o.x0 = *ws(k, L::AX);
+            o.x1 = *ws(k, L::AV);
         } else {
             o.x0 = o.x1 = 0.0;
         }
     };
     auto load_bwd = [&](int k, In& o) {
         load_common(k, o);
-        o.x0 = *ws(k, WF_AX); o.x2 = *ws(k, WF_GX);
-        o.x1 = *ws(k, WF_AV);
-        const double gvk = *ws(k, WF_GVK);
+        o.x0 = *ws(k, L::AX); o.x2 = *ws(k, L::GX);
+        o.x1 = *ws(k, L::AV);
+        const double gvk = *ws(k, L::GVK);
         o.x3 = (t < 8) ? gvk : 0.0;
 #pragma unroll
-        for (int m = 0; m < 8; m++) o.m[m] = *ws(k, WF_KR + m);
+        for (int m = 0; m < 8; m++) o.m[m] = *ws(k, L::KR + m);
 #pragma unroll
-        for (int m = 0; m < 4; m++) o.m[8 + m] = *ws(k, WF_FI + m);
+        for (int m = 0; m < 4; m++) o.m[8 + m] = *ws(k, L::FI + m);
     };
-    auto store_slots = [&](int k, double sL, double lL, double sU, double lU, double sP, double lP, double zx, double zv) {
-        *ws(k, WF_SL) = sL; *ws(k, WF_LL) = lL; *ws(k, WF_SU) = sU; *ws(k, WF_LU) = lU;
-        *ws(k, WF_ZX) = zx;
-        const double s8 = from_down<8>(sP), l12 = from_down<12>(lP);
-        *ws(k, WF_ZV) = (t < 8) ? zv : ((t < 12) ? s8 : l12);
+    // DPP with the whole row active: called unconditionally, the store itself under the caller's condition
+    auto store_slots = [&](bool st, int k, double sL, double lL, double sU, double lU, double sP, double lP, double zx,
+                           double zv) {
+        if constexpr (PACKP) {
+            const double s8 = from_down<8>(sP), l12 = from_down<12>(lP);
+            zv = (t < 8) ? zv : ((t < 12) ? s8 : l12);
+        }
+        if (!st) return;
+        *ws(k, L::SL) = sL; *ws(k, L::LL) = lL; *ws(k, L::SU) = sU; *ws(k, L::LU) = lU;
+        if constexpr (!PACKP) { *ws(k, L::SP) = sP; *ws(k, L::LP) = lP; }
+        *ws(k, L::ZX) = zx;
+        *ws(k, L::ZV) = zv;
     };
 
     // ---- stage-local helpers (ipm_group's)
@@ -307,13 +327,14 @@ __device__ __attribute__((noinline)) void ipm_tail(const DevConst& c, const DevB
             const double yx = rowY ? y : 0.0;
             const double cz = row_cz(k, yx, 0.0);
             const double pcz = poly_cz(cur, k, yx, 0.0);
+            if constexpr (PCACHE) { if (own) *ws(k, L::PZ) = pcz; }
             const bool aL = row_active(k, cur.lb), aU = row_active(k, cur.ub), aP = poly_slot_active(cur, k);
             double sL = 1, lL = 0, sU = 1, lU = 0, sP = 1, lP = 0;
             if (aL) { sL = fmax(-(sgnL * cz - sgnL * cur.lb), 1.0); lL = 1.0; }
             if (aU) { sU = fmax(-(sgnU * cz - sgnU * cur.ub), 1.0); lU = 1.0; }
             if (aP) { sP = fmax(-(sgnU * pcz - sgnU * cur.pub), 1.0); lP = 1.0; }
             mcount += (aL ? 1.0 : 0.0) + (aU ? 1.0 : 0.0) + (aP ? 1.0 : 0.0);
-            if (own) store_slots(k, sL, lL, sU, lU, sP, lP, yx, 0.0);
+            store_slots(own, k, sL, lL, sU, lU, sP, lP, yx, 0.0);
             const double y8 = from_up<1>(y);
             const double yn = (t == 7) ? fma2(m77, y, m78, y8) + bk : fma(mt, y, bk);
             y = (t < 9) ? yn : 0.0;
@@ -348,17 +369,23 @@ __device__ __attribute__((noinline)) void ipm_tail(const DevConst& c, const DevB
                 if (pending) {
                     const double dx = cur.x0, dv = cur.x1, ax = cur.x2, av = cur.x3;
                     const double cz = row_cz(k, zx, zv), cd = row_cz(k, dx, dv), ca = row_cz(k, ax, av);
-                    const double pcz = poly_cz(cur, k, zx, zv), pcd = poly_cz(cur, k, dx, dv), pca = poly_cz(cur, k, ax, av);
+                    double pcz, pcd, pca;
+                    if constexpr (PCACHE) {
+                        pcz = cur.pz; pcd = cur.pcd; pca = cur.pca;
+                    } else {
+                        pcz = poly_cz(cur, k, zx, zv); pcd = poly_cz(cur, k, dx, dv); pca = poly_cz(cur, k, ax, av);
+                    }
                     double rpd;
                     if (aL) { const SlotStep st = slot_corr(sgnL, lb, cz, ca, cd, sL, lL, sigma_mu, &rpd); sL += alpha * st.ds; lL += alpha * st.dl; }
                     if (aU) { const SlotStep st = slot_corr(sgnU, ub, cz, ca, cd, sU, lU, sigma_mu, &rpd); sU += alpha * st.ds; lU += alpha * st.dl; }
                     if (aP) { const SlotStep st = slot_corr(sgnU, cur.pub, pcz, pca, pcd, sP, lP, sigma_mu, &rpd); sP += alpha * st.ds; lP += alpha * st.dl; }
                     zx += alpha * dx;
                     zv += alpha * dv;
-                    if (vA) store_slots(k, sL, lL, sU, lU, sP, lP, zx, zv);
+                    store_slots(vA, k, sL, lL, sU, lU, sP, lP, zx, zv);
                 }
                 const double cz = row_cz(k, zx, zv);
                 const double pcz = poly_cz(cur, k, zx, zv);
+                if constexpr (PCACHE) { if (vA) *ws(k, L::PZ) = pcz; }
                 double WL = 0, WU = 0, WP = 0, cL = 0, cU = 0, cP = 0;
                 if (aL) { const double rp = slot_rp(sgnL, cz, lb, sL); const double ri = rcp(sL); WL = lL * ri; cL = slot_coef(ri, lL, rp, sL * lL); }
                 if (aU) { const double rp = slot_rp(sgnU, cz, ub, sU); const double ri = rcp(sU); WU = lU * ri; cU = slot_coef(ri, lU, rp, sU * lU); }
@@ -386,7 +413,7 @@ __device__ __attribute__((noinline)) void ipm_tail(const DevConst& c, const DevB
                         g0v = s + rt;
                     }
                 }
-                if (vA) *ws(k, WF_GX) = g0x;
+                if (vA) *ws(k, L::GX) = g0x;
                 double gx, gv;
                 assemble_grad(cur, k, g0x, g0v, dvr, cP, gx, gv);
                 const double wdv = from_up<9>(wd);
@@ -396,17 +423,69 @@ __device__ __attribute__((noinline)) void ipm_tail(const DevConst& c, const DevB
                     hF[i] = (i == t) ? Rt + ((t < 7) ? wdv : 0.0) : 0.0;
                     hG[i] = 0.0;
                 }
-                double Wb[NPE];
+                double dq[7];  // Gram: D[8 + a][8 + t], the poly terms of Hb's q block
+                if constexpr (GRAM_MFMA) {
+                    // ipm_group's Gram MFMA (D = sum_p w_p r_p r_p^T, r_p = [bv_p, 0, a_p, 0]), the wave's four groups
+                    // on their four stages: the same operands per group, so bitwise the normal path's blocks
+                    constexpr int KS = (NPM + 3) / 4;
+                    double xs_[KS][4][1], as_[KS][4][1];
 #pragma unroll
-                for (int p = 0; p < NPM; p++) {
-                    const bool live = (double)p < cur.np && k < N;
-                    const double wp = bcn(WP, p);
-                    Wb[p] = live ? wp : 0.0;
+                    for (int q = 0; q < KS; q++)
+#pragma unroll
+                        for (int gg = 0; gg < 4; gg++) {
+                            const int pp = 4 * q + gg;
+                            double x = 0.0, w = 0.0;
+                            if (pp < NPM) {
+                                const double a8 = from_down<8>(cur.pa[pp]);  // lane 8 + i <- a_p[i]
+                                x = (t < 8) ? cur.pb[pp] : a8;
+                                const bool live = (double)pp < cur.np && k < N;
+                                const double wp = bcn(WP, pp);
+                                w = live ? wp : 0.0;
+                            }
+                            xs_[q][gg][0] = x;
+                            as_[q][gg][0] = w * x;
+                        }
+#pragma unroll
+                    for (int q = 0; q < KS; q++) {
+                        group_transpose(xs_[q]);
+                        group_transpose(as_[q]);
+                    }
+                    double dg[4][4];
+#pragma unroll
+                    for (int j = 0; j < 4; j++) {
+                        d4 acc = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+                        for (int q = 0; q < KS; q++) acc = __builtin_amdgcn_mfma_f64_16x16x4f64(as_[q][j][0], xs_[q][j][0], acc, 0, 0, 0);
+#pragma unroll
+                        for (int r = 0; r < 4; r++) dg[j][r] = acc[r];
+                    }
+                    group_transpose(dg);
+                    const bool q7 = t < 7;
 #pragma unroll
                     for (int i = 0; i < 7; i++) {
-                        const double bv = bcn(cur.pb[p], i);
-                        hF[i] += Wb[p] * (bv * cur.pb[p]);
-                        hG[i] += Wb[p] * (bv * cur.pa[p]);
+                        const double dF = dg[i & 3][i >> 2];
+                        const double dG = from_up<8>(dg[i & 3][i >> 2]);
+                        hF[i] += q7 ? dF : 0.0;
+                        hG[i] += q7 ? dG : 0.0;
+                    }
+#pragma unroll
+                    for (int a = 0; a < 7; a++) {
+                        const double dd = from_up<8>(dg[(8 + a) & 3][(8 + a) >> 2]);
+                        dq[a] = q7 ? dd : 0.0;
+                    }
+                } else {
+                    double Wb[NPE];
+#pragma unroll
+                    for (int p = 0; p < NPM; p++) {
+                        const bool live = (double)p < cur.np && k < N;
+                        const double wp = bcn(WP, p);
+                        Wb[p] = live ? wp : 0.0;
+#pragma unroll
+                        for (int i = 0; i < 7; i++) {
+                            const double bv = bcn(cur.pb[p], i);
+                            hF[i] += Wb[p] * (bv * cur.pb[p]);
+                            hG[i] += Wb[p] * (bv * cur.pa[p]);
+                        }
                     }
                 }
                 if (k == N) {
@@ -422,10 +501,10 @@ __device__ __attribute__((noinline)) void ipm_tail(const DevConst& c, const DevB
                     }
                     if (vA) {
 #pragma unroll
-                        for (int m = 0; m < 8; m++) *ws(k, WF_KR + m) = 0.0;
-                        *ws(k, WF_GVK) = (t < 8) ? g0v : 0.0;
+                        for (int m = 0; m < 8; m++) *ws(k, L::KR + m) = 0.0;
+                        *ws(k, L::GVK) = (t < 8) ? g0v : 0.0;
 #pragma unroll
-                        for (int m = 0; m < 4; m++) *ws(k, WF_FI + m) = 0.0;
+                        for (int m = 0; m < 4; m++) *ws(k, L::FI + m) = 0.0;
                     }
                 } else {
                     // Hb base of rows a < 9: the q block with its poly terms (poly_hq), Q rows 7, 8 + the diagonal weight
@@ -435,6 +514,10 @@ __device__ __attribute__((noinline)) void ipm_tail(const DevConst& c, const DevB
                         hq[a] = Qr[a];
                         if (a == t) hq[a] += wd;
                     }
+                    if constexpr (GRAM_MFMA) {
+#pragma unroll
+                        for (int a = 0; a < 7; a++) hq[a] += dq[a];
+                    } else {
 #pragma unroll
                     for (int p = 0; p < NPM; p++) {
                         const bool live = (double)p < cur.np && k < N;
@@ -445,6 +528,7 @@ __device__ __attribute__((noinline)) void ipm_tail(const DevConst& c, const DevB
                             const double pa_ = bcn(cur.pa[p], a);
                             hq[a] += wb * (pa_ * cur.pa[p]);
                         }
+                    }
                     }
 #pragma unroll
                     for (int a = 0; a < 9; a++) {
@@ -679,13 +763,13 @@ __device__ __attribute__((noinline)) void ipm_tail(const DevConst& c, const DevB
                 for (int q2 = 0; q2 < 4; q2++) {
                     const double2 w = row[q2];
                     if (vC) {
-                        *ws(kg, WF_KR + 2 * q2) = w.x;
-                        *ws(kg, WF_KR + 2 * q2 + 1) = w.y;
+                        *ws(kg, L::KR + 2 * q2) = w.x;
+                        *ws(kg, L::KR + 2 * q2 + 1) = w.y;
                     }
                 }
                 if (vC) {
 #pragma unroll
-                    for (int m = 0; m < 4; m++) *ws(kg, WF_FI + m) = (t < 8) ? fi[m] : fi[4 + m];
+                    for (int m = 0; m < 4; m++) *ws(kg, L::FI + m) = (t < 8) ? fi[m] : fi[4 + m];
                 }
             }
             bsync();
@@ -727,7 +811,7 @@ __device__ __attribute__((noinline)) void ipm_tail(const DevConst& c, const DevB
                     pnew = gxa + ktf;
                 }
                 const double kffd = from_down<8>(kff);
-                if (own) *ws(k, WF_GVK) = (t < 8) ? g0v : kffd;
+                if (own) *ws(k, L::GVK) = (t < 8) ? g0v : kffd;
 #ifdef MPCC_IPM_DBGF
                 if (own) { *ws(k, 37) = pv; *ws(k, 38) = fv; *ws(k, 42) = pnew; *ws(k, 43) = kff; }
 #endif
@@ -802,9 +886,10 @@ __device__ __attribute__((noinline)) void ipm_tail(const DevConst& c, const DevB
         };
         fwd_sweep(false, [&](int k, bool vA, const In& cur, double xt_k, double dvv, double (&rr)[14]) {
             const bool aL = row_active(k, cur.lb), aU = row_active(k, cur.ub), aP = poly_slot_active(cur, k);
-            if (vA) { *ws(k, WF_AX) = xt_k; *ws(k, WF_AV) = dvv; }
+            if (vA) { *ws(k, L::AX) = xt_k; *ws(k, L::AV) = dvv; }
             const double cz = row_cz(k, cur.zx, cur.zv), ca = row_cz(k, xt_k, dvv);
-            const double pcz = poly_cz(cur, k, cur.zx, cur.zv), pca = poly_cz(cur, k, xt_k, dvv);
+            const double pcz = PCACHE ? cur.pz : poly_cz(cur, k, cur.zx, cur.zv), pca = poly_cz(cur, k, xt_k, dvv);
+            if constexpr (PCACHE) { if (vA) *ws(k, L::PA) = pca; }
             MinRatio loc(1.0);  // this stage's candidates; merged in stage order in D (strict <: the sequential scan)
             auto rec = [&](bool a, double sgn, double bnd, double czz, double caa, double s, double l, int r) {
                 double ds = 0.0, dl = 0.0, sv = 0.0, lv = 0.0;
@@ -852,8 +937,8 @@ __device__ __attribute__((noinline)) void ipm_tail(const DevConst& c, const DevB
                     load_bwd(k, cur);
                     const bool aL = row_active(k, cur.lb), aU = row_active(k, cur.ub), aP = poly_slot_active(cur, k);
                     const double cz = row_cz(k, cur.zx, cur.zv), ca = row_cz(k, cur.x0, cur.x1);
-                    const double pcz = poly_cz(cur, k, cur.zx, cur.zv);
-                    const double pca = poly_cz(cur, k, cur.x0, cur.x1);
+                    const double pcz = PCACHE ? cur.pz : poly_cz(cur, k, cur.zx, cur.zv);
+                    const double pca = PCACHE ? cur.pca : poly_cz(cur, k, cur.x0, cur.x1);
                     auto coef = [&](bool a, double sgn, double bnd, double czz, double caa, double s, double l) -> double {
                         if (!a) return 0.0;
                         const double rp = slot_rp(sgn, czz, bnd, s);
@@ -898,7 +983,7 @@ __device__ __attribute__((noinline)) void ipm_tail(const DevConst& c, const DevB
                     for (int q = 0; q < 4; q++) part -= m[8 + q] * ((t < 8) ? fb[q] : fb[4 + q]);
                     const double kff = part + from_up<8>(part);
                     const double kffd = from_down<8>(kff);
-                    if (own && t >= 8) *ws(k, WF_GVK) = kffd;
+                    if (own && t >= 8) *ws(k, L::GVK) = kffd;
                     const double p7 = from_down<1>(pvc);
                     double gxa = gx;  // g_x~ + A~^T p
                     if (t < 9) gxa = fma(mt, pvc, gxa);
@@ -933,13 +1018,14 @@ __device__ __attribute__((noinline)) void ipm_tail(const DevConst& c, const DevB
         fwd_sweep(true, [&](int k, bool vA, const In& cur, double xt_k, double dvv, double (&rr)[14]) {
             const bool aL = row_active(k, cur.lb), aU = row_active(k, cur.ub), aP = poly_slot_active(cur, k);
             if (vA) {
-                *ws(k, WF_DX) = xt_k;
-                *ws(k, WF_DV) = dvv;
+                *ws(k, L::DX) = xt_k;
+                *ws(k, L::DV) = dvv;
                 dzm = fmax(dzm, fmax(fabs(xt_k), fabs(dvv)));
             }
             const double cz = row_cz(k, cur.zx, cur.zv), cd = row_cz(k, xt_k, dvv), ca = row_cz(k, cur.x0, cur.x1);
-            const double pcz = poly_cz(cur, k, cur.zx, cur.zv), pcd = poly_cz(cur, k, xt_k, dvv);
-            const double pca = poly_cz(cur, k, cur.x0, cur.x1);
+            const double pcz = PCACHE ? cur.pz : poly_cz(cur, k, cur.zx, cur.zv), pcd = poly_cz(cur, k, xt_k, dvv);
+            const double pca = PCACHE ? cur.pca : poly_cz(cur, k, cur.x0, cur.x1);
+            if constexpr (PCACHE) { if (vA) *ws(k, L::PD) = pcd; }
             MinRatio loc(1e30);
             auto rec = [&](bool a, double sgn, double bnd, double czz, double caa, double cdd, double s, double l, int r) {
                 double ds = 0.0, dl = 0.0, sv = 0.0, lv = 0.0;
@@ -1034,7 +1120,7 @@ __device__ __attribute__((noinline)) void ipm_tail_solve(const DevConst& c, cons
     if constexpr (NWV > 1) __syncthreads();  // every wave has the state before the layout reuses its LDS
     ipm_tail<NPM, GB>(c, d, smem, b, io);
     it_total += io.it;
-    if (!io.conv && attempt == 0 && IPM_ATTEMPTS > 1) {
+    if (!io.conv && !io.diverged && attempt == 0 && IPM_ATTEMPTS > 1) {  // a P3 divergence is final
         io.it = 0; io.max_it = IPM_MAX_IT; io.pending = 0; io.conv = 0; io.diverged = 0; io.restart = 1;
         io.mu0 = 0.0; io.dz_prev = 1e30; io.sigma_mu = 0.0; io.mu_cur = 1e30; io.rp_cur = 1e30; io.alpha = 0.0;
         io.mcount = 0.0;
@@ -1062,8 +1148,8 @@ __device__ __attribute__((noinline)) void ipm_tail_solve(const DevConst& c, cons
     const double alpha = io.alpha;
     for (int k = 0; k <= N; k++) {
         const gdouble* wk = W + (size_t)k * IS;
-        const double zx = wk[WF_ZX * 16] + alpha * wk[WF_DX * 16];
-        const double zv = wk[WF_ZV * 16] + alpha * wk[WF_DV * 16];  // lanes < 8
+        const double zx = wk[WsF<NPM>::ZX * 16] + alpha * wk[WsF<NPM>::DX * 16];
+        const double zv = wk[WsF<NPM>::ZV * 16] + alpha * wk[WsF<NPM>::DV * 16];  // lanes < 8
         if (t < 9) stp[k * 17 + t] = zx;
         if (t < 8) stp[k * 17 + 9 + t] = (k < N) ? zv : 0.0;
     }

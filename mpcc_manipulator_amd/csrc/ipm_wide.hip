@@ -770,7 +770,7 @@ __device__ __forceinline__ void ipm_group(const DevConst& c, const DevBuffers& d
         const double lam_scale = (attempt == 0) ? IPM_L0 : 0.0;
         const int max_it = (attempt == 0) ? IPM_MAX_IT_SCALED : IPM_MAX_IT;
         if (attempt == 1) {
-            run = entered && !conv;
+            run = entered && !conv && !diverged;  // a P3 divergence is final (solve_struct_ipm)
             if (__ballot(run) == 0) break;
             if (run) diverged = false;
         }
@@ -1723,9 +1723,11 @@ __global__ void __launch_bounds__(64) k_sqp(DevConst, DevBuffers, const double* 
         if (valid)
             for (int e = t; e < NS * NXU; e += GW) d.glam[(size_t)b * NS * NXU + e] = 0.0;
     }
+    PhaseClock ph(d.phase_cyc);  // the ComputeTime split (mpcc_timing): set_qp / solve_qp / get_alpha / step
     for (int it = 0; it < c.p.max_iter; it++) {
         bool act = valid && si[SQ_ACTIVE] != 0;
         if (__ballot(act) == 0) break;
+        ph.mark(PH_STEP);
         // damped BFGS past LRX terms: restart from this iteration's exact Hessian (bfgs_pre)
         const bool restart = LR && it > 0 && act && si[SQ_NLR] + 2 > LRX;
         if (it > 0) {
@@ -1736,6 +1738,7 @@ __global__ void __launch_bounds__(64) k_sqp(DevConst, DevBuffers, const double* 
             if (act && !bfgs_pre(c, d, b, t, it, restart) && t == 0) { si[SQ_STATUS] = MPCC_NAN_HESSIAN; si[SQ_ACTIVE] = 0; }
             __syncthreads();
         }
+        ph.mark(PH_SETQP);  // setQP and the Hessian update (osqp_interface.cpp:435-475)
         sqp_ipm_phase<NPM, LR>(c, d, smem);
         __syncthreads();
         if (c.p.do_SOC) {  // SecondOrderCorrection (osqp_interface.cpp:506-535)
@@ -1750,6 +1753,7 @@ __global__ void __launch_bounds__(64) k_sqp(DevConst, DevBuffers, const double* 
             if (act) bfgs_post_qp(c, d, b, t);
             __syncthreads();
         }
+        ph.mark(PH_SOLVE);
         if (act) sqp_trial_phase(c, d, b, t, ucur, 1.0, true);
         __syncthreads();
         if (act && t == 0) accept_instance(c, d, b);
@@ -1761,6 +1765,7 @@ __global__ void __launch_bounds__(64) k_sqp(DevConst, DevBuffers, const double* 
                 sqp_trial_phase(c, d, b, t, ucur, alpha, false);
             }
         }
+        ph.mark(PH_ALPHA);
         double nrm = 0.0;
         if (act) {
             const double alpha = d.sqd[(size_t)b * SQ + SQ_ALPHA];
@@ -1771,6 +1776,8 @@ __global__ void __launch_bounds__(64) k_sqp(DevConst, DevBuffers, const double* 
         if (act && t == 0) finish_iteration(c, d, b, nrm);
         __syncthreads();
     }
+    ph.mark(PH_STEP);
+    ph.flush(threadIdx.x == 0);
 }
 
 template <int NPM, bool LR>

@@ -49,12 +49,35 @@ struct DevBuffers {
     // more than LRM low-rank terms (max_iter > 1 + LRM / 2): per term and stage the Woodbury column Q_j = M u_j (x~
     // and v parts) and the kff of its backward solve, [lrs][(N+1)][3][32 lanes]; null unless lrs > LRM
     double* lrq;
-    // low-rank terms allocated per instance (the stride of lr / lrc / lrq): the terms max_iter can produce,
-    // min(LRX, 2 (max_iter - 1)), rounded up to a multiple of 4 (>= LRM); 0 without use_BFGS
-    int lrs;
     // k_sqp's instance of each 16-lane group slot ([4 * (ceil(Bn / 4) + NSOLO)], -1: none) followed by the per-instance
     // cold-start flags of this step ([Bn], written by k_prepare); k_order builds the slots (solo waves)
     int32_t* order;
+    // ComputeTime split of the fused SQP kernels (mpcc_timing; osqp_interface.cpp:435-564): per-phase wave cycles
+    // summed over a launch's waves, [PH_SETQP, PH_SOLVE, PH_ALPHA, PH_STEP]; null unless timing is on
+    unsigned long long* phase_cyc;
+    // low-rank terms allocated per instance (the stride of lr / lrc / lrq): the terms max_iter can produce,
+    // min(LRX, 2 (max_iter - 1)), rounded up to a multiple of 4 (>= LRM); 0 without use_BFGS
+    int lrs;
+};
+constexpr int PH_SETQP = 0, PH_SOLVE = 1, PH_ALPHA = 2, PH_STEP = 3, PH_N = 4;
+// per-wave phase clock of the fused SQP kernels: mark(i) books the cycles since the previous mark to phase i; one
+// atomic add per phase and wave at the end (lane 0); nothing when timing is off
+struct PhaseClock {
+    unsigned long long* const out;
+    long long t0 = 0, acc[PH_N] = {0, 0, 0, 0};
+    __device__ explicit PhaseClock(unsigned long long* o) : out(o) {
+        if (out) t0 = clock64();
+    }
+    __device__ __forceinline__ void mark(int i) {
+        if (!out) return;
+        const long long t = clock64();
+        acc[i] += t - t0;
+        t0 = t;
+    }
+    __device__ __forceinline__ void flush(bool lane0) {
+        if (!out || !lane0) return;
+        for (int i = 0; i < PH_N; i++) atomicAdd(&out[i], (unsigned long long)acc[i]);
+    }
 };
 // Cold-started controllers (a regenerated initial guess) are the ones that take a second SQP iteration; k_sqp
 // gives each of the first NSOLO of them a wave of its own (tail mode from its first IPM iteration), so that they do

@@ -185,6 +185,7 @@ def lib(dof=7):
         "mpcc_build_id": (C.c_char_p, []),
         "mpcc_build_flags": (C.c_int, []),
         "mpcc_timing_mlp": (C.c_int, [V, C.POINTER(D), IP, C.POINTER(D), IP]),
+        "mpcc_timing_sqp": (C.c_int, [V, C.POINTER(D), IP, DP]),
         "mpcc_timing_intervals": (C.c_int, [V, V, C.c_int, C.c_int, DP, DP, IP]),
     }
     for name, (res, args) in sig.items():
@@ -574,6 +575,15 @@ class Engine:
         self._check(self.L.mpcc_timing_mlp(self.h, C.byref(ss), C.byref(ns), C.byref(se), C.byref(ne)),
                     "mpcc_timing_mlp")
         return {"k_mlp_self": (ss.value, ns.value), "k_mlp_env": (se.value, ne.value)}
+
+    def timing_sqp(self):
+        """After timing_end: (summed launch seconds, launches, phase fractions [set_qp, solve_qp, get_alpha, step]) of
+        the fused SQP kernel; the fractions split its span over the ComputeTime fields (0 launches: staged path)."""
+        sp = C.c_double()
+        n = C.c_int32()
+        fr = np.zeros(4)
+        self._check(self.L.mpcc_timing_sqp(self.h, C.byref(sp), C.byref(n), _dp(fr)), "mpcc_timing_sqp")
+        return sp.value, n.value, fr
 
     TIMING_KINDS = {"qp": 0, "k_mlp_self": 1, "k_mlp_env": 2}
 

@@ -1641,6 +1641,11 @@ static bool bfgs_update(const StructQP& S0, LowRank& lr, const std::vector<doubl
 // Returns 0 on success (step filled in reference layout: [y_0..y_N | v_0..v_{N-1}]), else Status.
 static const bool g_ipm_debug = std::getenv("MPCC_ORACLE_IPM_DEBUG") != nullptr;  // per-iteration log (debug)
 
+// debug statistics of the last attempt on this thread (MPCC_ORACLE_IPM_STATS): max mu / mu_0 over iterations >= 1 and
+// the first iteration at which it exceeded each threshold (-1: never)
+static thread_local double g_ipm_rmax = 0;
+static thread_local int g_ipm_cross[4] = {-1, -1, -1, -1};
+static const double g_ipm_thr[4] = {1e2, 1e3, 1e4, 1e5};
 static int solve_struct_ipm_from(const StructQP& S, std::vector<double>& step, int* iters_out, double s_floor,
                                  double lam_scale, int max_it, const LowRank* lr = nullptr) {
     const int N = S.N;
@@ -1702,7 +1707,13 @@ static int solve_struct_ipm_from(const StructQP& S, std::vector<double>& step, i
         // stalls; OSQP reports such a QP PrimalInfeasible (osqp_interface.cpp:497-499).  Converged
         // solves never exceed ~1.1 mu_0, so 1e6 mu_0 cannot cut a solve that would converge.
         if (it == 0) mu0 = mu;
-        else if (mu > IPM_DIV * mu0) {
+        else {
+            const double r = mu / mu0;  // debug statistics (MPCC_ORACLE_IPM_STATS)
+            if (r > g_ipm_rmax) g_ipm_rmax = r;
+            for (int q = 0; q < 4; q++)
+                if (g_ipm_cross[q] < 0 && r > g_ipm_thr[q]) g_ipm_cross[q] = it;
+        }
+        if (it > 0 && mu > IPM_DIV * mu0) {
             diverged = true;
             break;
         }
@@ -1840,8 +1851,21 @@ constexpr double IPM_S0 = 0.02, IPM_L0 = 0.002;
 constexpr int IPM_MAX_IT_SCALED = 30;
 static int solve_struct_ipm(const StructQP& S, std::vector<double>& step, int* iters_out, const LowRank* lr = nullptr) {
     int it1 = 0, it2 = 0;
+    static const bool stats = std::getenv("MPCC_ORACLE_IPM_STATS") != nullptr;  // debug: one line per QP solve
+    auto reset = [] { g_ipm_rmax = 0; for (int q = 0; q < 4; q++) g_ipm_cross[q] = -1; };
+    reset();
     int rc = solve_struct_ipm_from(S, step, &it1, IPM_S0, IPM_L0, IPM_MAX_IT_SCALED, lr);
-    if (rc != 0) rc = solve_struct_ipm_from(S, step, &it2, 1.0, 0.0, IPM_MAX_IT, lr);
+    const int rc1 = rc;
+    const double r1 = g_ipm_rmax;
+    int c1[4];
+    for (int q = 0; q < 4; q++) c1[q] = g_ipm_cross[q];
+    reset();
+    // the restart from the unit start point follows a scaled attempt that hit its cap or broke down
+    // (QP_MaxIterReached); a P3 divergence (QP_PrimalInfeasible) is final
+    if (rc == QP_MaxIterReached) rc = solve_struct_ipm_from(S, step, &it2, 1.0, 0.0, IPM_MAX_IT, lr);
+    if (stats)
+        std::fprintf(stderr, "ipmstat %d %d %d %d %.4g %d %d %d %d %.4g %d %d %d %d\n", it1, rc1, it2, rc, r1, c1[0], c1[1],
+                     c1[2], c1[3], g_ipm_rmax, g_ipm_cross[0], g_ipm_cross[1], g_ipm_cross[2], g_ipm_cross[3]);
     if (iters_out) *iters_out = it1 + it2;
     return rc;
 }

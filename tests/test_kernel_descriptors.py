@@ -13,10 +13,10 @@ import pytest
 
 LLVM = "/opt/rocm/lib/llvm/bin"
 # sizeof(DevConst) at this revision: the kernel-argument segment of k_ipm<9> (DevConst + DevBuffers, then the 256
-# bytes of HIP's hidden arguments) minus DevBuffers (29 pointers and the low-rank stride, 240 bytes).  Any private
+# bytes of HIP's hidden arguments) minus DevBuffers (30 pointers and the low-rank stride, 248 bytes).  Any private
 # segment this large could hold a copy.
 DEVCONST_BYTES = 3288
-DEVBUFFERS_BYTES = 240
+DEVBUFFERS_BYTES = 248
 PANDA_NARROW_MAX = 1740   # 1.7 KB: k_sqp / k_ipm of ipm.hip (16-lane interior point, tail mode included)
 WIDE_MAX = 2400           # 2.3 KB: the 32-lane kernels of ipm_wide.hip (mobile build, damped BFGS incl. the extended low-rank path)
 

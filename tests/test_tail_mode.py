@@ -50,6 +50,9 @@ def _assert_bitwise(a, b):
         assert np.array_equal(sa[k], sb[k]), k
 
 
+OBS = (0.48, 0.218, 0.521, 5.0)  # main_w_sim.py:42-45's obstacle (bench.py --config 1-all-rows)
+
+
 @pytest.mark.gpu
 @pytest.mark.parametrize("mask,B,qnoise,soc,staged", [
     (2, 4096, 0.005, 0, False),   # configs[1], the bench pool and noise
@@ -58,6 +61,9 @@ def _assert_bitwise(a, b):
     (2, 512, 0.005, 0, True),     # staged path (k_ipm)
     (0, 512, 0.005, 0, False),    # no polytopic row
     (3, 512, 0.005, 0, False),    # self collision + singularity: two polytopic rows
+    (7, 2048, 0.005, 0, False),   # the reference's default rows (11 poly rows, wide-poly variant), obstacle
+    (7, 512, 0.02, 0, False),     # wide-poly with filter rejections and restarts
+    (7, 256, 0.005, 1, True),     # wide-poly, staged path with the correction
 ])
 def test_tail_mode_bitwise(built_lib, monkeypatch, mask, B, qnoise, soc, staged):
     import mpcc_manipulator_amd as m
@@ -69,7 +75,7 @@ def test_tail_mode_bitwise(built_lib, monkeypatch, mask, B, qnoise, soc, staged)
     eng.close()
     track = m.track_from_points(X, Y, Z, q, ee)
     rng = np.random.default_rng(SEED + 41)
-    batch = batch_from_pool(_bench_pool(), B, rng, qnoise=qnoise)
+    batch = batch_from_pool(_bench_pool(), B, rng, qnoise=qnoise, obs=np.tile(OBS, (B, 1)) if mask == 7 else None)
     on = _solve(monkeypatch, True, params, mask, track, batch, staged)
     off = _solve(monkeypatch, False, params, mask, track, batch, staged)
     assert off[4] == 0
@@ -78,16 +84,19 @@ def test_tail_mode_bitwise(built_lib, monkeypatch, mask, B, qnoise, soc, staged)
 
 
 @pytest.mark.gpu
-def test_tail_mode_against_oracle(built_lib, oracle_lib, monkeypatch):
-    """The instances that finished in tail mode (the cold-started ones of the bench pool, two QPs) against the
-    oracle: status exact, inputs <= 1e-6 (north star), x0 update <= 1e-9."""
+@pytest.mark.parametrize("mask,B", [(2, 2048), (7, 1024)])
+def test_tail_mode_against_oracle(built_lib, oracle_lib, monkeypatch, mask, B):
+    """The instances that finished in tail mode (the cold-started ones of the bench pool, two QPs; with the default
+    rows the slowest QP of each wave) against the oracle: status exact, inputs <= 1e-6 (north star), x0 update
+    <= 1e-9."""
     import mpcc_manipulator_amd as m
-    o, P, track = make_oracle(N=20, max_iter=2, mask=2, nthreads=16)
+    o, P, track = make_oracle(N=20, max_iter=2, mask=mask, nthreads=16)
     params = m.load_params(N=20, overrides={"sqp": {"max_iter": 2}})
     pool = _bench_pool()
     rng = np.random.default_rng(SEED + 43)
-    x0, u0, obs, guess, valid, fails = batch_from_pool(pool, 2048, rng, qnoise=0.005)
-    xg, outg, (gg, vg, fg), st, n_tail = _solve(monkeypatch, True, params, 2, track, (x0, u0, obs, guess, valid, fails))
+    x0, u0, obs, guess, valid, fails = batch_from_pool(pool, B, rng, qnoise=0.005,
+                                                      obs=np.tile(OBS, (B, 1)) if mask == 7 else None)
+    xg, outg, (gg, vg, fg), st, n_tail = _solve(monkeypatch, True, params, mask, track, (x0, u0, obs, guess, valid, fails))
     assert n_tail > 0
     xo, go, vo, fo = x0.copy(), guess.copy(), valid.copy(), fails.copy()
     outo = o.run_mpc(xo, u0, obs, go, vo, fo)
