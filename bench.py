@@ -280,6 +280,9 @@ def main():
     ap.add_argument("--cpu-sample", type=int, default=1024)
     ap.add_argument("--cpu-seconds", type=float, default=15.0, help="CPU-baseline budget (bounded sample)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-all-cores", action="store_true",
+                    help="also time the oracle on every CPU of the affinity mask (cpu_baseline.all_cores, kind "
+                         "'measured'); default: the estimate from the job's CPU share")
     ap.add_argument("--traffic", default=None, help="PMC traffic summary (default profiles/pmc_traffic_<kernel>.json)")
     ap.add_argument("--dump-u0", default=None, help="rank 0 writes the last step's gathered u0 [world*B, 8] (.npy)")
     ap.add_argument("--sub-batches", type=int, default=2,
@@ -535,12 +538,24 @@ def main():
             args.cpu_threads = threads
             v, n, passes, dt, lat = cpu_baseline(pd, track, x0, u0, obs, guess, valid, fails, threads,
                                                  args.cpu_sample, args.cpu_seconds, dof=dof)
-            # the machine's other cores: the GPU box gives one GPU's job a CPU share (OMP_NUM_THREADS; gpurun:
-            # 16 of nproc), so the all-core figure is the measured per-thread rate times nproc, stated as an estimate
+            # the machine's other cores: the GPU box gives one GPU's job a CPU share (OMP_NUM_THREADS = 16 there,
+            # set by the harness, which asks jobs to keep their pools within it), so by default the all-core figure is
+            # the measured per-thread rate times nproc, stated as an estimate, with the measured 1 -> `threads`
+            # scaling efficiency beside it.  --cpu-all-cores measures it instead (a second oracle leg on every CPU of
+            # the affinity mask), for a machine the run owns.
+            rate1 = 1e3 / lat["mean_ms"]
             allc = {"value": v / threads * ci["nproc"], "cores": ci["nproc"], "kind": "estimate",
+                    "efficiency_vs_1thread": v / (threads * rate1),
                     "basis": f"measured {threads}-thread rate x {ci['nproc']}/{threads} (linear; instances are "
-                             f"independent, one per thread); single-thread rate from the latency run: "
-                             f"{1e3 / lat['mean_ms']:.1f} solves/s"}
+                             f"independent, one per thread; measured {threads}-thread efficiency against the "
+                             f"single-thread latency run ({rate1:.1f} solves/s): {v / (threads * rate1):.2f})"}
+            if args.cpu_all_cores and ci["usable"] > threads:
+                va, na, pa, dta, _ = cpu_baseline(pd, track, x0, u0, obs, guess, valid, fails, ci["usable"],
+                                                  args.cpu_sample, args.cpu_seconds, latency_n=1, dof=dof,
+                                                  latency_budget_s=0.0)
+                allc = {"value": va, "cores": ci["usable"], "kind": "measured",
+                        "sample": f"{pa} passes over the first {na} instances ({pa * na} solves, {dta:.1f} s), "
+                                  f"OpenMP {ci['usable']} threads"}
             cpu = {"value": v, "unit": "solves/s", "cores": threads, "kind": "port", "host": ci,
                    "all_cores": allc, "latency_1thread": lat,
                    "sample": f"{passes} passes over the first {n} instances of the same workload "

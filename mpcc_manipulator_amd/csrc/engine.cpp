@@ -470,7 +470,7 @@ void run_batch(mpcc_engine* e, int B, hipStream_t st, mpcc_timing* timing, bool 
             launch_order(cs, d, st);
             // solo blocks where the packed launch is one round of waves (at most one per SIMD): beyond that the
             // cold starts' time is spread over several rounds (B = 65,536: 2.078M with, 2.092M without, r04ah)
-            if (e->solo_mode == 2 && DOF == 7 && npm <= 2 && (c.Bn + IPW_SQP - 1) / IPW_SQP <= e->simds) {
+            if (e->solo_mode == 2 && DOF == 7 && (npm <= 2 || npm >= 9) && (c.Bn + IPW_SQP - 1) / IPW_SQP <= e->simds) {
                 // solo blocks: k_sqp_solo on the side stream beside k_sqp (which leaves the solo waves to it), joined
                 // before anything after k_sqp
                 // The kernel on the forked stream starts ≈30 µs after the one that follows k_order in its own stream

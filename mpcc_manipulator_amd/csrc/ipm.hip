@@ -107,6 +107,9 @@ static_assert(QS_POLY + 2 * 15 <= QS_YLB + 16 * QLINES, "bound block of <= 2 pol
 #ifndef MPCC_WIDE_RING
 #define MPCC_WIDE_RING 1
 #endif
+#ifndef MPCC_SLOT_SELECT
+#define MPCC_SLOT_SELECT 1  // the slot algebra of every lane without divergent branches (selects; A/B switch)
+#endif
 #ifndef MPCC_WIDE_TAIL
 #define MPCC_WIDE_TAIL 1  // tail mode for the wide-poly variants (ipm_tail.h, round 5)
 #endif
@@ -985,9 +988,21 @@ __device__ __forceinline__ bool ipm_group(const DevConst& c, const DevBuffers& d
                         pcz = poly_cz(cur, k, zx, zv); pcd = poly_cz(cur, k, dx, dv); pca = poly_cz(cur, k, ax, av);
                     }
                     double rpd;
+                    if constexpr (MPCC_SLOT_SELECT) {  // every slot computed, inactive ones kept by selects (no branches)
+                        auto upd = [&](bool a, double sgn, double bnd, double czz, double caa, double cdd, double& sv, double& lv) {
+                            const SlotStep st = slot_corr(sgn, bnd, czz, caa, cdd, sv, lv, sigma_mu, &rpd);
+                            const double sn = sv + alpha * st.ds, ln = lv + alpha * st.dl;
+                            sv = a ? sn : sv;
+                            lv = a ? ln : lv;
+                        };
+                        upd(aL, sgnL, lb, cz, ca, cd, sL, lL);
+                        upd(aU, sgnU, ub, cz, ca, cd, sU, lU);
+                        upd(aP, sgnU, cur.pub, pcz, pca, pcd, sP, lP);
+                    } else {
                     if (aL) { const SlotStep st = slot_corr(sgnL, lb, cz, ca, cd, sL, lL, sigma_mu, &rpd); sL += alpha * st.ds; lL += alpha * st.dl; }
                     if (aU) { const SlotStep st = slot_corr(sgnU, ub, cz, ca, cd, sU, lU, sigma_mu, &rpd); sU += alpha * st.ds; lU += alpha * st.dl; }
                     if (aP) { const SlotStep st = slot_corr(sgnU, cur.pub, pcz, pca, pcd, sP, lP, sigma_mu, &rpd); sP += alpha * st.ds; lP += alpha * st.dl; }
+                    }
                     zx += alpha * dx;
                     zv += alpha * dv;
                     if constexpr (!PCN) {
@@ -1005,9 +1020,22 @@ __device__ __forceinline__ bool ipm_group(const DevConst& c, const DevBuffers& d
                     if (run && pending) store_slots(k, sL, lL, sU, lU, sP, lP, zx, zv, pcz);
                 }
                 double WL = 0, WU = 0, WP = 0, cL = 0, cU = 0, cP = 0;
+                if constexpr (MPCC_SLOT_SELECT) {
+                    auto wc = [&](bool a, double sgn, double czz, double bnd, double sv, double lv, double& W, double& cf) {
+                        const double rp = slot_rp(sgn, czz, bnd, sv);
+                        const double ri = rcp(sv);
+                        const double w = lv * ri, cc = slot_coef(ri, lv, rp, sv * lv);
+                        W = a ? w : 0.0;
+                        cf = a ? cc : 0.0;
+                    };
+                    wc(aL, sgnL, cz, lb, sL, lL, WL, cL);
+                    wc(aU, sgnU, cz, ub, sU, lU, WU, cU);
+                    wc(aP, sgnU, pcz, cur.pub, sP, lP, WP, cP);
+                } else {
                 if (aL) { const double rp = slot_rp(sgnL, cz, lb, sL); const double ri = rcp(sL); WL = lL * ri; cL = slot_coef(ri, lL, rp, sL * lL); }
                 if (aU) { const double rp = slot_rp(sgnU, cz, ub, sU); const double ri = rcp(sU); WU = lU * ri; cU = slot_coef(ri, lU, rp, sU * lU); }
                 if (aP) { const double rp = slot_rp(sgnU, pcz, cur.pub, sP); const double ri = rcp(sP); WP = lP * ri; cP = slot_coef(ri, lP, rp, sP * lP); }
+                }
                 const double wd = WL + WU;                 // diagonal weight of row t
                 const double dvr = sgnL * cL + sgnU * cU;  // signed coefficient of row t
                 // ---- objective gradient g0 = H z + h (f_xu = 0; oracle order: sum over z, then + h)
@@ -1389,9 +1417,15 @@ __device__ __forceinline__ bool ipm_group(const DevConst& c, const DevBuffers& d
                     *ws(k, F_AV) = dvv;
                 }
                 auto rec = [&](bool a, double sgn, double bnd, double czz, double caa, double s, double l) {
-                    if (!a) return;
+                    if (!MPCC_SLOT_SELECT && !a) return;
                     const double rp = slot_rp(sgn, czz, bnd, s);
-                    const SlotStep st = slot_recover(rcp(s), l, rp, sgn * caa, s * l);
+                    SlotStep st = slot_recover(rcp(s), l, rp, sgn * caa, s * l);
+                    if constexpr (MPCC_SLOT_SELECT) {  // an inactive slot adds exact zeros (as tail mode's D phase)
+                        st.ds = a ? st.ds : 0.0;
+                        st.dl = a ? st.dl : 0.0;
+                        s = a ? s : 0.0;
+                        l = a ? l : 0.0;
+                    }
                     step_bound(amr, s, l, st);
                     mu_acc(S0, S1, S2, s, l, st.ds, st.dl);
                 };
@@ -1421,12 +1455,13 @@ __device__ __forceinline__ bool ipm_group(const DevConst& c, const DevBuffers& d
                 const double pcz = PCV ? cur.pz : poly_cz(cur, k, cur.zx, cur.zv);
                 const double pca = PCV ? cur.pca : poly_cz(cur, k, cur.x0, cur.x1);
                 auto coef = [&](bool a, double sgn, double bnd, double czz, double caa, double s, double l) -> double {
-                    if (!a) return 0.0;
+                    if (!MPCC_SLOT_SELECT && !a) return 0.0;
                     const double rp = slot_rp(sgn, czz, bnd, s);
                     const double ri = rcp(s);
                     const SlotStep pa = slot_recover(ri, l, rp, sgn * caa, s * l);
                     const double rc = fma(s, l, pa.ds * pa.dl) - smu;
-                    return slot_coef(ri, l, rp, rc);
+                    const double cf = slot_coef(ri, l, rp, rc);
+                    return a ? cf : 0.0;
                 };
                 const double cL = coef(aL, sgnL, cur.lb, cz, ca, cur.sL, cur.lL);
                 const double cU = coef(aU, sgnU, cur.ub, cz, ca, cur.sU, cur.lU);
@@ -1499,9 +1534,16 @@ __device__ __forceinline__ bool ipm_group(const DevConst& c, const DevBuffers& d
                     *ws(k, F_DV) = dvv;
                 }
                 auto rec = [&](bool a, double sgn, double bnd, double czz, double caa, double cdd, double s, double l) {
-                    if (!a) return;
+                    if (!MPCC_SLOT_SELECT && !a) return;
                     double rp;
-                    const SlotStep st = slot_corr(sgn, bnd, czz, caa, cdd, s, l, smu, &rp);
+                    SlotStep st = slot_corr(sgn, bnd, czz, caa, cdd, s, l, smu, &rp);
+                    if constexpr (MPCC_SLOT_SELECT) {
+                        st.ds = a ? st.ds : 0.0;
+                        st.dl = a ? st.dl : 0.0;
+                        s = a ? s : 0.0;
+                        l = a ? l : 0.0;
+                        rp = a ? rp : 0.0;
+                    }
                     step_bound(amc, s, l, st);
                     mu_acc(T0, T1, T2, s, l, st.ds, st.dl);
                     rpm = fmax(rpm, fabs(rp));
@@ -1667,13 +1709,14 @@ template <int NPM>
 __device__ __attribute__((noinline)) void solo_helper(const DevConst& c, const DevBuffers& d, double* smem) {
     while (true) {
         __syncthreads();
-        const double cmd = smem[SB_CMD];
+        const double cmd = smem[sb_cmd<NPM>()];
         if (cmd == 0.0) break;
         ipm_tail_solve<NPM, SB_GB>(c, d, smem);
     }
 }
+template <int NPM>
 __device__ __forceinline__ void solo_post(double* smem, double cmd) {
-    if (threadIdx.x == 0) smem[SB_CMD] = cmd;
+    if (threadIdx.x == 0) smem[sb_cmd<NPM>()] = cmd;
     __syncthreads();
 }
 template <int NPM, bool SB = false>
@@ -1681,7 +1724,7 @@ __device__ __forceinline__ void sqp_qp_solve(const DevConst& c, const DevBuffers
     if (sqp_ipm_phase<NPM>(c, d, smem)) {
         if constexpr (NPM <= 2 || (MPCC_WIDE_TAIL && NPM >= 9)) {
             if constexpr (SB) {
-                solo_post(smem, 1.0);
+                solo_post<NPM>(smem, 1.0);
                 ipm_tail_solve<NPM, SB_GB>(c, d, smem);
             } else {
                 ipm_tail_solve<NPM>(c, d, smem);
@@ -1791,7 +1834,7 @@ __device__ __forceinline__ void sqp_waves(const DevConst& c, const DevBuffers& d
     }
     ph.mark(PH_STEP);
     ph.flush(threadIdx.x == 0);
-    if constexpr (SB) solo_post(smem, 0.0);  // the helper leaves
+    if constexpr (SB) solo_post<NPM>(smem, 0.0);  // the helper leaves
 #ifdef MPCC_IPM_PROF
     SPMARK(4);
     if (threadIdx.x == 0 && blockIdx.x < PROF_WAVES) g_wave_t[PROF_WAVES + blockIdx.x] = __builtin_amdgcn_s_memrealtime();
@@ -1874,7 +1917,12 @@ bool launch_sqp_solo(const DevConst& c, const DevBuffers& d, const double* u_cur
         case 0: launch_sqp_solo_t<0>(c, d, u_cur, s); return true;
         case 1: launch_sqp_solo_t<1>(c, d, u_cur, s); return true;
         case 2: launch_sqp_solo_t<2>(c, d, u_cur, s); return true;
-        default: return false;  // tail mode (and so solo blocks): narrow variants only
+#if MPCC_WIDE_TAIL
+        case 9: launch_sqp_solo_t<9>(c, d, u_cur, s); return true;
+        case 10: launch_sqp_solo_t<10>(c, d, u_cur, s); return true;
+        case 11: launch_sqp_solo_t<11>(c, d, u_cur, s); return true;
+#endif
+        default: return false;  // tail mode (and so solo blocks) exists for these variants only
     }
 }
 void launch_sqp(const DevConst& c, const DevBuffers& d, const double* u_cur, int npmax, hipStream_t s) {

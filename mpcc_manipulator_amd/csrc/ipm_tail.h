@@ -69,9 +69,11 @@ static_assert(TailLayout<4>::END == TL_END && TailLayout<4>::LM == TL_LM && Tail
 #define MPCC_SB_WAVES 2
 #endif
 constexpr int SB_WAVES = MPCC_SB_WAVES, SB_GB = 4 * SB_WAVES;
-constexpr int WAVE_LDS = LRING * LG(LF_CBWD) * 1024 / 8;  // doubles of LDS per k_sqp wave (narrow variants)
-constexpr int SB_CMD = SB_WAVES * WAVE_LDS - 1;
-static_assert(TailLayout<SB_GB>::SIZE <= SB_CMD && TL_STATE + 16 <= SB_CMD, "solo-block LDS");
+// doubles of LDS per k_sqp wave of the NPM variant (ipm_wave_lds: the light sweeps' ring) and the command word's index
+template <int NPM>
+__host__ __device__ constexpr int sb_cmd() { return SB_WAVES * ipm_wave_lds(NPM) - 1; }
+static_assert(TailLayout<SB_GB>::SIZE <= sb_cmd<0>() && TL_STATE + 16 <= sb_cmd<0>(), "solo-block LDS (narrow)");
+static_assert(TailLayout<SB_GB>::SIZE <= sb_cmd<11>() && TL_STATE + 16 <= sb_cmd<11>(), "solo-block LDS (wide-poly)");
 
 template <int NPM, int GB>
 __device__ __attribute__((noinline)) void ipm_tail(const DevConst& c, const DevBuffers& d, double* smem, int b, TailIO& io) {

@@ -108,7 +108,7 @@ def test_tail_mode_against_oracle(built_lib, oracle_lib, monkeypatch, mask, B):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("mask,B,cold_every", [(2, 4096, 64), (3, 512, 8), (2, 512, 1)])
+@pytest.mark.parametrize("mask,B,cold_every", [(2, 4096, 64), (3, 512, 8), (2, 512, 1), (7, 1024, 16)])
 def test_solo_waves_bitwise(built_lib, monkeypatch, mask, B, cold_every):
     """Solo waves and solo blocks (csrc/kernels.hip k_order): k_sqp gives the first 64
     cold-started controllers a wave each (MPCC_SOLO=1) or, in k_sqp_solo, a block of two waves whose second joins the
@@ -123,7 +123,8 @@ def test_solo_waves_bitwise(built_lib, monkeypatch, mask, B, cold_every):
     eng.close()
     track = m.track_from_points(X, Y, Z, q, ee)
     rng = np.random.default_rng(SEED + 43)
-    x0, u0, obs, guess, valid, fails = batch_from_pool(_bench_pool(), B, rng, qnoise=0.005)
+    x0, u0, obs, guess, valid, fails = batch_from_pool(_bench_pool(), B, rng, qnoise=0.005,
+                                                      obs=np.tile(OBS, (B, 1)) if mask == 7 else None)
     valid[::cold_every] = 0
     nsl = 4 * ((B + 3) // 4 + 64)  # kernels.h order_slots: the map, then k_prepare's cold flags
     res, orders = {}, {}
