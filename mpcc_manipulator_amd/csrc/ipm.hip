@@ -108,7 +108,7 @@ static_assert(QS_POLY + 2 * 15 <= QS_YLB + 16 * QLINES, "bound block of <= 2 pol
 #define MPCC_WIDE_RING 1
 #endif
 #ifndef MPCC_SLOT_SELECT
-#define MPCC_SLOT_SELECT 1  // the slot algebra of every lane without divergent branches (selects; A/B switch)
+#define MPCC_SLOT_SELECT 0  // 1: the slot algebra without divergent branches (selects): 0.4% slower at configs[1] (r05g A/B)
 #endif
 #ifndef MPCC_WIDE_TAIL
 #define MPCC_WIDE_TAIL 1  // tail mode for the wide-poly variants (ipm_tail.h, round 5)

@@ -16,6 +16,8 @@
 //    27% -> 58% of the FP64 roof; k_mlp_self 5.9 -> 4.8 ms.
 //  * v_mfma_f64_16x16x4f64 accumulates as an ascending fma chain over k (bitwise,
 //    tools/probes/mfma_f64_probe.hip); the oracle's MLP uses the same chain.
+#include <type_traits>
+
 #include "dev_model.h"
 #include "dev_dpp.h"
 #include "kernels.h"
@@ -103,23 +105,23 @@ __device__ __forceinline__ void glds16_to(const void* src, unsigned lds_dst) {
     asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
                  : "=&s"(keep) : "v"(src), "s"(lds_dst) : "memory");
 }
-template <int KT, int RT>
+template <int KT, int RT, int NW = 4>
 __device__ __forceinline__ void mfma_layer_ring(const double* __restrict__ Wp, const d4 (&in)[KT], d4 (&out)[RT],
                                                 int lane, double* __restrict__ ring /* RING_SLOTS x RT*256 */) {
     constexpr int KS = 4 * KT;
     constexpr int CH = RT * 256;          // doubles per k-tile
-    constexpr int PT = CH / 2 / 256;      // 16-byte copies per thread per k-tile
-    static_assert(CH % 512 == 0, "mfma_layer_ring: whole 16-byte copies per thread");
+    constexpr int PT = CH / 2 / (64 * NW);  // 16-byte copies per thread per k-tile
+    static_assert(CH % (128 * NW) == 0, "mfma_layer_ring: whole 16-byte copies per thread");
     const int tid = threadIdx.x, w = tid >> 6;
     const unsigned base = (unsigned)(uintptr_t)(__attribute__((address_space(3))) char*)(char*)ring;
-    auto issue = [&](int kt) {  // k-tile kt into slot kt % RING_SLOTS; copy j of wave w: 1 KB at 4 KB j + 1 KB w
+    auto issue = [&](int kt) {  // k-tile kt into slot kt % RING_SLOTS; copy j of wave w: 1 KB at NW KB j + 1 KB w
         const unsigned slot = base + (unsigned)((kt % RING_SLOTS) * CH * 8);
 #pragma unroll
         for (int j = 0; j < PT; j++) {
-            const int e = tid + 256 * j;  // 16-byte element of the tile: double 2e = [t][r][lane]
+            const int e = tid + 64 * NW * j;  // 16-byte element of the tile: double 2e = [t][r][lane]
             const int t = e >> 7;
             glds16_to(Wp + ((size_t)t * KS + 4 * kt) * 64 + 2 * (e & 127),
-                      __builtin_amdgcn_readfirstlane(slot + 4096u * j + 1024u * w));
+                      __builtin_amdgcn_readfirstlane(slot + 1024u * (NW * j + w)));
         }
     };
 #pragma unroll
@@ -153,23 +155,26 @@ __device__ __forceinline__ void mfma_layer_ring(const double* __restrict__ Wp, c
 #ifndef MPCC_MLP_PF
 #define MPCC_MLP_PF 1
 #endif
-template <int KT, int RT>
+// RS ring slots: the barrier of tile kt sits in its last k-step, after which no wave reads tile kt's slot again, so the
+// copy of tile kt + 2 may go into it: two slots suffice (RS = 2; three keep one more tile of slack)
+template <int KT, int RT, int NW = 4, int RS = RING_SLOTS>
 __device__ __forceinline__ void mfma_layer_ring_pf(const double* __restrict__ Wp, const d4 (&in)[KT], d4 (&out)[RT],
-                                                   int lane, double* __restrict__ ring /* RING_SLOTS x RT*256 */) {
+                                                   int lane, double* __restrict__ ring /* RS x RT*256 */) {
     constexpr int KS = 4 * KT;
     constexpr int CH = RT * 256;
-    constexpr int PT = CH / 2 / 256;
-    static_assert(CH % 512 == 0, "mfma_layer_ring_pf: whole 16-byte copies per thread");
+    constexpr int PT = CH / 2 / (64 * NW);
+    static_assert(CH % (128 * NW) == 0, "mfma_layer_ring_pf: whole 16-byte copies per thread");
+    static_assert(RS >= 2, "two ring slots at least");
     const int tid = threadIdx.x, w = tid >> 6;
     const unsigned base = (unsigned)(uintptr_t)(__attribute__((address_space(3))) char*)(char*)ring;
     auto issue = [&](int kt) {
-        const unsigned slot = base + (unsigned)((kt % RING_SLOTS) * CH * 8);
+        const unsigned slot = base + (unsigned)((kt % RS) * CH * 8);
 #pragma unroll
         for (int j = 0; j < PT; j++) {
-            const int e = tid + 256 * j;
+            const int e = tid + 64 * NW * j;
             const int t = e >> 7;
             glds16_to(Wp + ((size_t)t * KS + 4 * kt) * 64 + 2 * (e & 127),
-                      __builtin_amdgcn_readfirstlane(slot + 4096u * j + 1024u * w));
+                      __builtin_amdgcn_readfirstlane(slot + 1024u * (NW * j + w)));
         }
     };
 #pragma unroll
@@ -187,7 +192,7 @@ __device__ __forceinline__ void mfma_layer_ring_pf(const double* __restrict__ Wp
     for (int t = 0; t < RT; t++) fr[t] = ring[(t * 4) * 64 + lane];
 #pragma unroll
     for (int kt = 0; kt < KT; kt++) {
-        const double* L = ring + (kt % RING_SLOTS) * CH;
+        const double* L = ring + (kt % RS) * CH;
 #pragma unroll
         for (int r = 0; r < 4; r++) {
             if (r == 3 && kt + 1 < KT) {
@@ -196,7 +201,7 @@ __device__ __forceinline__ void mfma_layer_ring_pf(const double* __restrict__ Wp
                 if (kt + 2 < KT) issue(kt + 2);
             }
             const bool nxt = r < 3 || kt + 1 < KT;
-            const double* Ln = (r < 3) ? L : ring + ((kt + 1) % RING_SLOTS) * CH;
+            const double* Ln = (r < 3) ? L : ring + ((kt + 1) % RS) * CH;
             const int rn = (r < 3) ? r + 1 : 0;
 #pragma unroll
             for (int t = 0; t < RT; t++) {
@@ -443,12 +448,28 @@ __global__ void __launch_bounds__(256) k_mlp_self(DevConst c, DevBuffers d, NNDe
 // (CPS = 4, D0 = 7: 4 samples per tile), 12 columns per sample instead of one 16-column tile with 11 used
 // (MPCC_ENV_SPLIT = 0: that form, CPS = 16).  A column's MFMA chain does not depend on the other columns of its
 // tile, so every output is bitwise that of the one-tile form.
-template <int CPS, int D0 = 0>
+// Blocks of ENV_WAVES waves around one LDS weight ring of ENV_SLOTS k-tiles (32 KiB each).  Two waves and two slots
+// (72 KiB with the biases) fit on a CU beside two one-wave-per-SIMD k_sqp waves of the other controller group (40 KiB
+// of LDS each); a four-wave block with three slots (104 KiB, four free SIMDs) could only start on a CU without any,
+// so with two groups the env network mostly waited for the other group's QP launch to drain (round 5 trace,
+// DESIGN.md §3.3).  The waves of a block share each tile's copy; the MFMAs per output are the same in any case.
+// Long launches (configs[2]: 1.3M samples) run mostly without the other group's QP launch beside them, and the
+// four-wave form streams half the weight bytes per sample: 214k against 212k solves/s; the two-wave form wins where
+// the launch is short (the reference's default rows at configs[1]'s batch: 324k -> 367k, profiles/r05h_*).  Launches of
+// at most ENV_SMALL samples take the two-wave blocks (MPCC_ENV_WAVES = 2 or 4 forces one form).
+#ifndef MPCC_ENV_WAVES
+#define MPCC_ENV_WAVES 0
+#endif
+constexpr int ENV_SMALL = 262144;
+template <int NW>
+constexpr int env_slots() { return (MPCC_MLP_PF && NW < 4) ? 2 : RING_SLOTS; }
+template <int CPS, int D0 = 0, int NW = 4>
 __device__ __forceinline__ void mlp_env_body(const DevConst& c, const DevBuffers& d, const NNDesc& nd, const double* __restrict__ W,
                                              int M, const double* __restrict__ qin, const double* __restrict__ obsin,
                                              double* __restrict__ rec, int S, double* wl, double* bl) {
+    constexpr int ENV_SLOTS = env_slots<NW>();
     const int lane = threadIdx.x & 63;
-    const int wave = blockIdx.x * 4 + (threadIdx.x >> 6);
+    const int wave = blockIdx.x * NW + (threadIdx.x >> 6);
     const int m = (16 / CPS) * wave + (lane & 15) / CPS;
     double q[DOF], obs[3];
     sample_input(c, d, m, M, qin, obsin, q, obs);
@@ -464,21 +485,22 @@ __device__ __forceinline__ void mlp_env_body(const DevConst& c, const DevBuffers
         x[7] = obs[0]; x[8] = obs[1]; x[9] = obs[2];
     }
     // the biases in LDS (see k_mlp_self); the first ring barrier publishes them
-    for (int l = 0; l < 4; l++) bl[l * 256 + threadIdx.x] = W[nd.offb[l] + threadIdx.x];
+    for (int l = 0; l < 4; l++)
+        for (int i = threadIdx.x; i < 256; i += 64 * NW) bl[l * 256 + i] = W[nd.offb[l] + i];
     if (threadIdx.x < 9) bl[1024 + threadIdx.x] = W[nd.offb[4] + threadIdx.x];
     d4 a0[2], a[16], h[16], o[1];
     nerf_input<10, CPS, D0>(x, a0, lane);
 #if MPCC_MLP_PF
-    mfma_layer_ring_pf<2, 16>(W + nd.offW[0], a0, a, lane, wl);
+    mfma_layer_ring_pf<2, 16, NW, ENV_SLOTS>(W + nd.offW[0], a0, a, lane, wl);
 #else
-    mfma_layer_ring<2, 16>(W + nd.offW[0], a0, a, lane, wl);
+    mfma_layer_ring<2, 16, NW>(W + nd.offW[0], a0, a, lane, wl);
 #endif
     relu_gate<16, CPS>(a, bl, lane);
     for (int l = 1; l <= 3; l++) {  // three 256 x 256 hidden layers share one unrolled body
 #if MPCC_MLP_PF
-        mfma_layer_ring_pf<16, 16>(W + nd.offW[l], a, h, lane, wl);
+        mfma_layer_ring_pf<16, 16, NW, ENV_SLOTS>(W + nd.offW[l], a, h, lane, wl);
 #else
-        mfma_layer_ring<16, 16>(W + nd.offW[l], a, h, lane, wl);
+        mfma_layer_ring<16, 16, NW>(W + nd.offW[l], a, h, lane, wl);
 #endif
         relu_gate<16, CPS>(h, bl + 256 * l, lane);
 #pragma unroll
@@ -497,23 +519,25 @@ constexpr bool ENV_SPLIT = MPCC_ENV_SPLIT && NBASE > 0;      // the mobile build
 constexpr int ENV_CPS = (NBASE > 0 && !ENV_SPLIT) ? 16 : 8;  // columns per sample of k_mlp_env
 constexpr int ENV_SPW = 16 / ENV_CPS;                        // samples per wave
 
-__global__ void __launch_bounds__(256) k_mlp_env(DevConst c, DevBuffers d, NNDesc nd, const double* __restrict__ W, int M,
-                                                 const double* __restrict__ qin, const double* __restrict__ obsin,
-                                                 double* __restrict__ rec, int S) {
+template <int NW>
+__global__ void __launch_bounds__(64 * NW) k_mlp_env(DevConst c, DevBuffers d, NNDesc nd, const double* __restrict__ W, int M,
+                                                    const double* __restrict__ qin, const double* __restrict__ obsin,
+                                                    double* __restrict__ rec, int S) {
     // no early exit: the hidden layers synchronize the block (a wave past M computes on a clamped
     // sample and write_out drops its result)
-    __shared__ __attribute__((aligned(16))) double wl[RING_SLOTS * 16 * 256];
+    __shared__ __attribute__((aligned(16))) double wl[env_slots<NW>() * 16 * 256];
     __shared__ double bl[4 * 256 + 16];
-    mlp_env_body<ENV_CPS>(c, d, nd, W, M, qin, obsin, rec, S, wl, bl);
+    mlp_env_body<ENV_CPS, 0, NW>(c, d, nd, W, M, qin, obsin, rec, S, wl, bl);
 }
 #if MPCC_DOF != 7
 // the mobile build's obstacle pass (ENV_SPLIT)
-__global__ void __launch_bounds__(256) k_mlp_env_obs(DevConst c, DevBuffers d, NNDesc nd, const double* __restrict__ W, int M,
-                                                     const double* __restrict__ qin, const double* __restrict__ obsin,
-                                                     double* __restrict__ rec, int S) {
-    __shared__ __attribute__((aligned(16))) double wl[RING_SLOTS * 16 * 256];
+template <int NW>
+__global__ void __launch_bounds__(64 * NW) k_mlp_env_obs(DevConst c, DevBuffers d, NNDesc nd, const double* __restrict__ W,
+                                                        int M, const double* __restrict__ qin,
+                                                        const double* __restrict__ obsin, double* __restrict__ rec, int S) {
+    __shared__ __attribute__((aligned(16))) double wl[env_slots<NW>() * 16 * 256];
     __shared__ double bl[4 * 256 + 16];
-    mlp_env_body<4, 7>(c, d, nd, W, M, qin, obsin, rec, S, wl, bl);
+    mlp_env_body<4, 7, NW>(c, d, nd, W, M, qin, obsin, rec, S, wl, bl);
 }
 #endif
 
@@ -524,12 +548,19 @@ void launch_nn(const DevConst& c, const DevBuffers& d, const NNDesc& nd, const d
         hipLaunchKernelGGL(k_mlp_self, dim3((M + 8 * SELF_CT - 1) / (8 * SELF_CT)), dim3(256), 0, s, c, d, nd, W, M, q, obs,
                            rec, rec_stride);
     else {
-        hipLaunchKernelGGL(k_mlp_env, dim3((M + 4 * ENV_SPW - 1) / (4 * ENV_SPW)), dim3(256), 0, s, c, d, nd, W, M, q, obs,
-                           rec, rec_stride);
+        const bool two = MPCC_ENV_WAVES == 2 || (MPCC_ENV_WAVES == 0 && M <= ENV_SMALL);
+        auto go = [&](auto nwc) {
+            constexpr int NW = decltype(nwc)::value;
+            hipLaunchKernelGGL(k_mlp_env<NW>, dim3((M + NW * ENV_SPW - 1) / (NW * ENV_SPW)), dim3(64 * NW), 0, s, c, d, nd, W,
+                               M, q, obs, rec, rec_stride);
 #if MPCC_DOF != 7
-        if constexpr (ENV_SPLIT)  // 4 waves x 4 samples
-            hipLaunchKernelGGL(k_mlp_env_obs, dim3((M + 15) / 16), dim3(256), 0, s, c, d, nd, W, M, q, obs, rec, rec_stride);
+            if constexpr (ENV_SPLIT)  // NW waves x 4 samples
+                hipLaunchKernelGGL(k_mlp_env_obs<NW>, dim3((M + 4 * NW - 1) / (4 * NW)), dim3(64 * NW), 0, s, c, d, nd, W, M, q,
+                                   obs, rec, rec_stride);
 #endif
+        };
+        if (two) go(std::integral_constant<int, 2>{});
+        else go(std::integral_constant<int, 4>{});
     }
 }
 
