@@ -1854,10 +1854,12 @@ static int solve_struct_ipm(const StructQP& S, std::vector<double>& step, int* i
     static const bool stats = std::getenv("MPCC_ORACLE_IPM_STATS") != nullptr;  // debug: one line per QP solve
     auto reset = [] { g_ipm_rmax = 0; for (int q = 0; q < 4; q++) g_ipm_cross[q] = -1; };
     reset();
-    // debug: start-point experiments (MPCC_ORACLE_IPM_S0 / _L0 override the scaled start; never set in tests)
+    // debug: start-point experiments (MPCC_ORACLE_IPM_S0 / _L0 / _CAP override the scaled start and its iteration
+    // cap; never set in tests)
     static const double s0 = std::getenv("MPCC_ORACLE_IPM_S0") ? std::atof(std::getenv("MPCC_ORACLE_IPM_S0")) : IPM_S0;
     static const double l0 = std::getenv("MPCC_ORACLE_IPM_L0") ? std::atof(std::getenv("MPCC_ORACLE_IPM_L0")) : IPM_L0;
-    int rc = solve_struct_ipm_from(S, step, &it1, s0, l0, IPM_MAX_IT_SCALED, lr);
+    static const int cap = std::getenv("MPCC_ORACLE_IPM_CAP") ? std::atoi(std::getenv("MPCC_ORACLE_IPM_CAP")) : IPM_MAX_IT_SCALED;
+    int rc = solve_struct_ipm_from(S, step, &it1, s0, l0, cap, lr);
     const int rc1 = rc;
     const double r1 = g_ipm_rmax;
     int c1[4];
