@@ -377,7 +377,11 @@ __device__ __forceinline__ void sample_input(const DevConst& c, const DevBuffers
 #define MPCC_SELF_CT 2
 #endif
 constexpr int SELF_CT = MPCC_SELF_CT;
-__global__ void __launch_bounds__(256) k_mlp_self(DevConst c, DevBuffers d, NNDesc nd, const double* __restrict__ W, int M,
+#ifndef MPCC_SELF_RING
+#define MPCC_SELF_RING 1
+#endif
+constexpr int SELF_RS = 3, SELF_SLOT = 512 + 4 * 256;  // ring slots; doubles per slot (W1 row tile + W2 k-tile)
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) k_mlp_self(DevConst c, DevBuffers d, NNDesc nd, const double* __restrict__ W, int M,
                                                   const double* __restrict__ qin, const double* __restrict__ obsin,
                                                   double* __restrict__ rec, int S) {
     const int lane = threadIdx.x & 63;
@@ -408,8 +412,37 @@ __global__ void __launch_bounds__(256) k_mlp_self(DevConst c, DevBuffers d, NNDe
 #ifndef MPCC_SELF_UNROLL
 #define MPCC_SELF_UNROLL 1
 #endif
+#if MPCC_SELF_RING
+    // the weights of tile t (W1 row tile t: 8 k-steps x 64 lanes, 4 KiB; W2 k-steps 4t..4t+3 of its 4 row tiles, 8 KiB)
+    // staged by the block into a 3-slot LDS ring, two tiles ahead (global_load_lds, no registers): 3 copies of 16 bytes
+    // per thread per tile; the fragments are then LDS reads instead of one L2 round trip per MFMA group
+    __shared__ __attribute__((aligned(16))) double ring[SELF_RS * SELF_SLOT];
+    const int tid = threadIdx.x, w = tid >> 6;
+    const unsigned rbase = (unsigned)(uintptr_t)(__attribute__((address_space(3))) char*)(char*)ring;
+    auto issue = [&](int t) {
+        const unsigned slot = rbase + (unsigned)((t % SELF_RS) * SELF_SLOT * 8);
+#pragma unroll
+        for (int j = 0; j < 3; j++) {
+            const int e = tid + 256 * j;  // 16-byte chunk of the slot: [W1 tile t: 256][W2 u = 0..3: 128 each]
+            const double* src = (e < 256) ? W1 + (size_t)t * 512 + 2 * e
+                                          : W2 + ((size_t)((e - 256) >> 7) * 64 + 4 * t) * 64 + 2 * ((e - 256) & 127);
+            glds16_to(src, __builtin_amdgcn_readfirstlane(slot + 1024u * (4 * j + w)));
+        }
+    };
+    issue(0);
+    issue(1);
+#endif
 #pragma unroll MPCC_SELF_UNROLL
     for (int t = 0; t < 16; t++) {
+#if MPCC_SELF_RING
+        // this wave's copies of tile t have landed once at most those of tile t + 1 are outstanding; the barrier
+        // publishes tile t and retires the slot of tile t - 1, which the copy of tile t + 2 overwrites
+        if (t + 1 < 16) asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
+        else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        if (t + 2 < 16) issue(t + 2);
+        const double* L = ring + (t % SELF_RS) * SELF_SLOT;
+#endif
         d4 z[SELF_CT][1];
 #pragma unroll
         for (int ct = 0; ct < SELF_CT; ct++) z[ct][0] = d4{0.0, 0.0, 0.0, 0.0};
@@ -417,7 +450,11 @@ __global__ void __launch_bounds__(256) k_mlp_self(DevConst c, DevBuffers d, NNDe
         // both zero): skipped, an fma with two zero factors leaves the accumulator as it is
 #pragma unroll
         for (int s = 0; s < 6; s++) {
+#if MPCC_SELF_RING
+            const double w = L[s * 64 + lane];
+#else
             const double w = W1[((size_t)t * 8 + s) * 64 + lane];
+#endif
 #pragma unroll
             for (int ct = 0; ct < SELF_CT; ct++)
                 z[ct][0] = __builtin_amdgcn_mfma_f64_16x16x4f64(w, a0[ct][s >> 2][s & 3], z[ct][0], 0, 0, 0);
@@ -428,7 +465,11 @@ __global__ void __launch_bounds__(256) k_mlp_self(DevConst c, DevBuffers d, NNDe
         for (int r = 0; r < 4; r++)
 #pragma unroll
             for (int u = 0; u < 4; u++) {
+#if MPCC_SELF_RING
+                const double w = L[512 + u * 256 + r * 64 + lane];
+#else
                 const double w = W2[((size_t)u * 64 + 4 * t + r) * 64 + lane];
+#endif
 #pragma unroll
                 for (int ct = 0; ct < SELF_CT; ct++)
                     a2[ct][u] = __builtin_amdgcn_mfma_f64_16x16x4f64(w, z[ct][0][r], a2[ct][u], 0, 0, 0);
