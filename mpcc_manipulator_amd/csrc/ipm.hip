@@ -113,6 +113,11 @@ static_assert(QS_POLY + 2 * 15 <= QS_YLB + 16 * QLINES, "bound block of <= 2 pol
 #ifndef MPCC_WIDE_TAIL
 #define MPCC_WIDE_TAIL 1  // tail mode for the wide-poly variants (ipm_tail.h, round 5)
 #endif
+#ifndef MPCC_RING_KIB
+#define MPCC_RING_KIB 39  // LDS ring of the narrow light sweeps per wave; each sweep keeps RING_KIB / LG(run) slots
+#endif
+constexpr int RING_KIB = MPCC_RING_KIB;
+static_assert(RING_KIB >= LRING * LG(LF_CBWD) && RING_KIB <= 40, "3 slots of the longest run; 4 waves inside 160 KiB");
 constexpr int LRING_W = 2, QLINES_W = 14;
 static_assert(QS_POLY + NPC * 15 <= QS_YLB + 16 * QLINES_W, "bound block of all poly rows in QLINES_W lines");
 __host__ __device__ constexpr bool use_ring(int npm) { return npm <= 2 || (MPCC_WIDE_RING && npm >= 9); }
@@ -123,14 +128,14 @@ static_assert(LF_CBWD + 1 <= NWF, "the odd last line of a ring slot reads one fi
 // doubles of LDS per k_sqp wave
 __host__ __device__ constexpr int ipm_wave_lds(int npmax) {
     const int uk = IPW * GRP_LDS;
-    const int ring = (npmax <= 2)     ? LRING * LG(LF_CBWD) * 128
+    const int ring = (npmax <= 2)     ? RING_KIB * 128
                      : use_ring(npmax) ? LRING_W * LG(WF_PD, QLINES_W) * 128
                                        : 0;
     return ring > uk ? ring : uk;
 }
 size_t ipm_lds_bytes(int /*N*/, int npmax) {
     const size_t uk = (size_t)IPW * GRP_LDS * sizeof(double);
-    const size_t ring = (npmax <= 2)          ? (size_t)LRING * LG(LF_CBWD) * 1024
+    const size_t ring = (npmax <= 2)          ? (size_t)RING_KIB * 1024
                         : use_ring(npmax)       ? (size_t)LRING_W * LG(WF_PD, QLINES_W) * 1024  // longest wide run: 26 fields
                                                 : 0;
     return ring > uk ? ring : uk;
@@ -698,6 +703,11 @@ __device__ __forceinline__ bool ipm_group(const DevConst& c, const DevBuffers& d
         if constexpr (NPM <= 2) return nf;
         else return nf == LF_PRED ? F_GVK + 1 : (nf == LF_CFWD ? F_PA + 1 : F_FI + 4);
     };
+    // slots of a sweep's ring: as many as the wave's ring LDS holds (narrow), RD (wide)
+    auto ring_depth = [](auto nfc) {
+        if constexpr (NPM <= 2) return RING_KIB / LG(decltype(nfc)::value);
+        else return ring_d(NPM);
+    };
     auto glds_stage = [&](int k, int slot, auto nfc) {
         constexpr int G = LG(ring_nf(nfc), QL);
         // the image's last record line and workspace line stay inside the stage (static), the stage inside the
@@ -705,7 +715,7 @@ __device__ __forceinline__ bool ipm_group(const DevConst& c, const DevBuffers& d
         static_assert(QB + 16 * 2 * (G > QL / 2 ? QL / 2 : G) <= QS, "ring record lines inside the stage record");
         static_assert(16 * 2 * (G - QL / 2) <= IS, "ring workspace lines inside the stage workspace");
         k = MPCC_BCHK(c.bchk, k, NS, BC_RING);
-        slot = MPCC_BCHK(c.bchk, slot, RD, BC_RING);
+        slot = MPCC_BCHK(c.bchk, slot, ring_depth(nfc), BC_RING);
         const char* qk = (const char*)(QSb + (size_t)k * QS + QB) + (t & 7) * 16 + (t >> 3) * 128;
         const char* wk = (const char*)(WSb + (size_t)k * IS) + (t & 7) * 16 + (t >> 3) * 128;
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // reads of the slot's previous stage retired
@@ -776,6 +786,7 @@ __device__ __forceinline__ bool ipm_group(const DevConst& c, const DevBuffers& d
     // stores only make that wait stricter).  The extra loads are drained before the ring's LDS is reused.
     auto lds_sweep = [&](bool backward, auto nfc, auto read, auto body) {
         constexpr int G = LG(ring_nf(nfc), QL);
+        constexpr int RD = ring_depth(nfc);
         auto s = [&](int i) { return backward ? N - i : i; };
         auto cl = [&](int i) { return s(i <= N ? i : N); };
 #pragma unroll

@@ -34,15 +34,20 @@ def _descriptors(lib, tmp):
             continue
         notes = subprocess.run([os.path.join(LLVM, "llvm-readelf"), "--notes", os.path.join(work, f)], check=True,
                                capture_output=True, text=True).stdout
-        name = None
+        # one YAML map per kernel ("  - .agpr_count: ..."); keys are sorted, so .group_segment_fixed_size and
+        # .kernarg_segment_size come before .name: collect the map, then file it under its name
+        cur = {}
         for line in notes.splitlines():
-            m = re.match(r"\s+\.name:\s+(\S+)", line)
-            if m:
-                name = m.group(1)
-                out.setdefault(name, {})
-            m = re.match(r"\s+\.(private_segment_fixed_size|kernarg_segment_size):\s+(\d+)", line)
-            if m and name:
-                out[name][m.group(1)] = int(m.group(2))
+            if line.startswith("  - ."):  # a kernel's map (its .args entries are indented further)
+                cur = {}
+            m = re.match(r"(?:  - |    )\.(\w+):\s+(\S+)", line)
+            if not m:
+                continue
+            if m.group(1) == "name":
+                out[m.group(2)] = cur
+            elif m.group(1) in ("private_segment_fixed_size", "kernarg_segment_size", "group_segment_fixed_size",
+                                "vgpr_count"):
+                cur[m.group(1)] = int(m.group(2))
     return out
 
 
@@ -68,4 +73,10 @@ def test_no_private_devconst_copy(built_lib, tmp_path):
         if dof == 7:
             ka = [v["kernarg_segment_size"] for k, v in kern.items() if k.startswith("_ZN4mpcc5k_ipmILi9E")]
             assert ka and ka[0] - DEVBUFFERS_BYTES - 256 == DEVCONST_BYTES
+            # the self-collision MLP at two waves per SIMD; the two-wave env blocks two per CU
+            # beside the interior point's waves
+            selfk = [v for k, v in kern.items() if k.startswith("_ZN4mpcc10k_mlp_self")]
+            assert selfk and selfk[0]["vgpr_count"] <= 256
+            env2 = [v for k, v in kern.items() if k.startswith("_ZN4mpcc9k_mlp_envILi2E")]
+            assert env2 and env2[0]["group_segment_fixed_size"] <= 80 * 1024
     assert seen["narrow"] >= 12 and seen["wide"] >= 8
