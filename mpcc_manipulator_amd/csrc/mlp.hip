@@ -213,6 +213,89 @@ __device__ __forceinline__ void mfma_layer_ring_pf(const double* __restrict__ Wp
     __syncthreads();  // the ring is free for the next layer's first copies
 }
 
+// relu_gate on one 16-row output tile (bias_t = the layer's bias from row 16 t): the same operations per element
+template <int CPS>
+__device__ __forceinline__ void relu_tile(d4& a, const double* __restrict__ bias_t, int lane) {
+    const bool isv = (lane & (CPS - 1)) == 0;
+    const bool hi = CPS == 8 && (lane & 8) != 0;
+#pragma unroll
+    for (int r = 0; r < 4; r++) {
+        const double z = a[r] + bias_t[(lane >> 4) + 4 * r];
+        double zs;
+        if constexpr (CPS == 4) {
+            zs = dpp_d<0x00>(z);
+        } else {
+            const double z0 = bc<0>(z), z8 = bc<8>(z);
+            zs = hi ? z8 : z0;
+        }
+        const bool on = zs > 0.0;
+        a[r] = isv ? (z > 0.0 ? z : 0.0) : (on ? a[r] : 0.0);
+    }
+}
+
+// The layers of one network as ONE stream of weight k-tiles through the LDS ring (mfma_layer_ring_pf per layer
+// started every layer with an empty ring: the first tile's L2 latency, a barrier and the previous layer's ReLU
+// epilogue with the matrix core idle).  Stream tile g goes to slot g % RS; a layer's last two k-steps issue the
+// next layer's first two tiles and read its first fragments, and the ReLU of the layer's input tile kt + 1 (the
+// previous layer's output, pre-activation, when bias_in is set) is formed during the MFMAs of tile kt.  Entry:
+// stream tiles g0 and g0 + 1 issued, g0 visible to the block, fr = its k-step-0 fragments; exit (KTN > 0): the
+// same for the next layer (KTN k-tiles at Wn).  Same fragments, same ascending k order per row tile and the
+// same ReLU arithmetic: bitwise mfma_layer_ring_pf + relu_gate.  All threads of the block must call it.
+template <int KT, int RT, int NW, int RS, int KTN, int CPS>
+__device__ __forceinline__ void mfma_layer_chain(const double* __restrict__ Wp, const double* __restrict__ Wn, int g0,
+                                                 d4 (&in)[KT], const double* __restrict__ bias_in, d4 (&out)[RT],
+                                                 double (&fr)[RT], int lane, double* __restrict__ ring) {
+    constexpr int KS = 4 * KT, KSN = 4 * KTN;
+    constexpr int CH = RT * 256;
+    constexpr int PT = CH / 2 / (64 * NW);
+    static_assert(CH % (128 * NW) == 0, "mfma_layer_chain: whole 16-byte copies per thread");
+    static_assert(RS >= 2 && KT >= 2 && (KTN == 0 || KTN >= 2), "two slots; two tiles per layer");
+    const int tid = threadIdx.x, w = tid >> 6;
+    const unsigned base = (unsigned)(uintptr_t)(__attribute__((address_space(3))) char*)(char*)ring;
+    auto issue = [&](const double* Wsrc, int ks, int j, int g) {
+        const unsigned slot = base + (unsigned)((g % RS) * CH * 8);
+#pragma unroll
+        for (int q = 0; q < PT; q++) {
+            const int e = tid + 64 * NW * q;
+            const int t = e >> 7;
+            glds16_to(Wsrc + ((size_t)t * ks + 4 * j) * 64 + 2 * (e & 127),
+                      __builtin_amdgcn_readfirstlane(slot + 1024u * (NW * q + w)));
+        }
+    };
+#pragma unroll
+    for (int t = 0; t < RT; t++) out[t] = d4{0.0, 0.0, 0.0, 0.0};
+    if (bias_in) relu_tile<CPS>(in[0], bias_in, lane);
+#pragma unroll
+    for (int kt = 0; kt < KT; kt++) {
+        const double* L = ring + ((g0 + kt) % RS) * CH;
+#pragma unroll
+        for (int r = 0; r < 4; r++) {
+            const bool more = kt + 1 < KT || KTN > 0;  // a next tile in the stream
+            if (r == 3 && more) {
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's copies of stream tile g0 + kt + 1
+                __syncthreads();
+                if (kt + 2 < KT) issue(Wp, KS, kt + 2, g0 + kt + 2);
+                else if (KTN > 0) issue(Wn, KSN, kt + 2 - KT, g0 + kt + 2);
+            }
+            const bool nxt = r < 3 || more;
+            const double* Ln = (r < 3) ? L : ring + ((g0 + kt + 1) % RS) * CH;
+            const int rn = (r < 3) ? r + 1 : 0;
+#pragma unroll
+            for (int t = 0; t < RT; t++) {
+                out[t] = __builtin_amdgcn_mfma_f64_16x16x4f64(fr[t], in[kt][r], out[t], 0, 0, 0);
+                if (nxt) fr[t] = Ln[(t * 4 + rn) * 64 + lane];
+            }
+            if (r == 0 && bias_in && kt + 1 < KT) {
+                // keep the ReLU of tile kt + 1 (and its bias reads) in this k-step: hoisted to the layer's start, the
+                // bias operands of all tiles held 128 more registers and spilled
+                __builtin_amdgcn_sched_barrier(0);
+                relu_tile<CPS>(in[kt + 1], bias_in + 16 * (kt + 1), lane);
+            }
+        }
+    }
+    if (KTN == 0) __syncthreads();  // end of the stream: the ring is free
+}
+
 // hidden-layer epilogue: value columns h = relu(z + b); tangent columns dh = (z + b > 0) ? dz : 0.
 // CPS = columns per sample: 8 (value + 7 tangents, 2 samples per 16-column tile), 4 (value + 3 tangents, 4 samples
 // per tile: the mobile env network's obstacle directions) or 16 (value + up to 15 tangents, one sample per tile).
@@ -501,6 +584,14 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) k
 #ifndef MPCC_ENV_WAVES
 #define MPCC_ENV_WAVES 0
 #endif
+#ifndef MPCC_ENV_CHAIN
+// 1: the layers' weight k-tiles as one ring stream (mfma_layer_chain); bitwise, but slower: configs[2] 209.7k against
+// 212.5-212.9k, default rows 361k against 367k (profiles/r05o_ab_env_chain_REJECTED.log)
+#define MPCC_ENV_CHAIN 0
+#endif
+#ifndef MPCC_ENV_CHAIN_LAZY
+#define MPCC_ENV_CHAIN_LAZY 0  // 1: the ReLU of a layer's input tiles inside its k-steps (spills: 208k, 331k)
+#endif
 constexpr int ENV_SMALL = 262144;
 template <int NW>
 constexpr int env_slots() { return (MPCC_MLP_PF && NW < 4) ? 2 : RING_SLOTS; }
@@ -531,6 +622,53 @@ __device__ __forceinline__ void mlp_env_body(const DevConst& c, const DevBuffers
     if (threadIdx.x < 9) bl[1024 + threadIdx.x] = W[nd.offb[4] + threadIdx.x];
     d4 a0[2], a[16], h[16], o[1];
     nerf_input<10, CPS, D0>(x, a0, lane);
+#if MPCC_ENV_CHAIN
+    {
+        // prologue of the weight stream: the input layer's two k-tiles (stream tiles 0, 1); the barrier also
+        // publishes the biases
+        constexpr int CH = 16 * 256, PT = CH / 2 / (64 * NW);
+        const unsigned base = (unsigned)(uintptr_t)(__attribute__((address_space(3))) char*)(char*)wl;
+        const int tid = threadIdx.x, w = tid >> 6;
+        const double* W0 = W + nd.offW[0];
+#pragma unroll
+        for (int j = 0; j < 2; j++)
+#pragma unroll
+            for (int q = 0; q < PT; q++) {
+                const int e = tid + 64 * NW * q;
+                const int t = e >> 7;
+                glds16_to(W0 + ((size_t)t * 8 + 4 * j) * 64 + 2 * (e & 127),
+                          __builtin_amdgcn_readfirstlane(base + (unsigned)((j % ENV_SLOTS) * CH * 8) + 1024u * (NW * q + w)));
+            }
+        asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PT) : "memory");
+        __syncthreads();
+        double fr[16];
+#pragma unroll
+        for (int t = 0; t < 16; t++) fr[t] = wl[(t * 4) * 64 + lane];
+        mfma_layer_chain<2, 16, NW, ENV_SLOTS, 16, CPS>(W0, W + nd.offW[1], 0, a0, nullptr, a, fr, lane, wl);
+#if MPCC_ENV_CHAIN_LAZY
+        for (int l = 1; l <= 2; l++) {  // hidden layers 1 and 2 share one unrolled body; layer 3 ends the stream
+            mfma_layer_chain<16, 16, NW, ENV_SLOTS, 16, CPS>(W + nd.offW[l], W + nd.offW[l + 1], 2 + 16 * (l - 1), a,
+                                                             bl + 256 * (l - 1), h, fr, lane, wl);
+#pragma unroll
+            for (int t = 0; t < 16; t++) a[t] = h[t];
+        }
+        mfma_layer_chain<16, 16, NW, ENV_SLOTS, 0, CPS>(W + nd.offW[3], nullptr, 34, a, bl + 512, h, fr, lane, wl);
+#else
+        relu_gate<16, CPS>(a, bl, lane);
+        for (int l = 1; l <= 2; l++) {
+            mfma_layer_chain<16, 16, NW, ENV_SLOTS, 16, CPS>(W + nd.offW[l], W + nd.offW[l + 1], 2 + 16 * (l - 1), a,
+                                                             nullptr, h, fr, lane, wl);
+            relu_gate<16, CPS>(h, bl + 256 * l, lane);
+#pragma unroll
+            for (int t = 0; t < 16; t++) a[t] = h[t];
+        }
+        mfma_layer_chain<16, 16, NW, ENV_SLOTS, 0, CPS>(W + nd.offW[3], nullptr, 34, a, nullptr, h, fr, lane, wl);
+#endif
+        relu_gate<16, CPS>(h, bl + 768, lane);
+#pragma unroll
+        for (int t = 0; t < 16; t++) a[t] = h[t];
+    }
+#else
 #if MPCC_MLP_PF
     mfma_layer_ring_pf<2, 16, NW, ENV_SLOTS>(W + nd.offW[0], a0, a, lane, wl);
 #else
@@ -547,6 +685,7 @@ __device__ __forceinline__ void mlp_env_body(const DevConst& c, const DevBuffers
 #pragma unroll
         for (int t = 0; t < 16; t++) a[t] = h[t];
     }
+#endif
     mfma_layer<16, 1>(W + nd.offW[4], a, o, lane);
     if constexpr (CPS == 8) write_out<9>(o[0], bl + 1024, lane, m, M, rec, S, R_ENV, R_DENV);
     else if constexpr (CPS == 4) write_out_obs<9>(o[0], lane, m, M, rec, S, dO);
