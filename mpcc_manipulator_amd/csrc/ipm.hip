@@ -110,6 +110,9 @@ static_assert(QS_POLY + 2 * 15 <= QS_YLB + 16 * QLINES, "bound block of <= 2 pol
 #ifndef MPCC_SLOT_SELECT
 #define MPCC_SLOT_SELECT 0  // 1: the slot algebra without divergent branches (selects): 0.4% slower at configs[1] (r05g A/B)
 #endif
+#ifndef MPCC_BC_HALVES
+#define MPCC_BC_HALVES 1  // half-row broadcasts (dpp::bc_halves) for the K-row products of the light sweeps
+#endif
 #ifndef MPCC_WIDE_TAIL
 #define MPCC_WIDE_TAIL 1  // tail mode for the wide-poly variants (ipm_tail.h, round 5)
 #endif
@@ -179,6 +182,47 @@ __device__ __forceinline__ void glds16(const void* src, unsigned lds_dst) {
 }
 // one ring slot: instruction i copies 2 lines of each instance (i < QL2: the QP record's bound block at qk,
 // then the workspace fields at wk), immediate offsets from the two per-lane bases
+#ifndef MPCC_GLDS_ONE
+#define MPCC_GLDS_ONE 1
+#endif
+#if MPCC_GLDS_ONE
+// The whole slot in ONE statement: M0 saved once, then stepped between copies (copy i of a run writes LDS at
+// dst + 1024 i through M0 = dst + 1024 i - OFF_i, OFF_i = 256 x its index in the run: +768 per copy, +256 QL2 + 768
+// from the record's run to the workspace's).  A statement per copy (glds16) spent 6 instructions on each (M0 saved,
+// set from a fresh SGPR sum, nop, load, M0 restored); at one wave per SIMD every instruction is an issue slot of the
+// light sweeps.  s_add_u32 sets SCC (clobbered); the nop after each M0 write is the LDS-DMA M0 hazard.
+#define GL_ADD(n) "s_add_u32 m0, m0, " #n "\n\ts_nop 0\n\t"
+#define GL_Q(o) "global_load_lds_dwordx4 %1, off offset:" #o "\n\t"
+#define GL_W(o) "global_load_lds_dwordx4 %2, off offset:" #o "\n\t"
+#define GL_WN(o) GL_ADD(768) GL_W(o)
+#define GL_QN(o) GL_ADD(768) GL_Q(o)
+#define GL_W7 GL_WN(256) GL_WN(512) GL_WN(768) GL_WN(1024) GL_WN(1280) GL_WN(1536) GL_WN(1792)
+#define GL_W8 GL_W7 GL_WN(2048)
+#define GL_W9 GL_W8 GL_WN(2304)
+#define GL_W10 GL_W9 GL_WN(2560)
+#define GL_W11 GL_W10 GL_WN(2816)
+#define GL_W12 GL_W11 GL_WN(3072)
+#define GL_HEAD "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\t" GL_Q(0)
+#define GL_Q2 GL_HEAD GL_QN(256) GL_ADD(1280) GL_W(0)
+#define GL_Q7 GL_HEAD GL_QN(256) GL_QN(512) GL_QN(768) GL_QN(1024) GL_QN(1280) GL_QN(1536) GL_ADD(2560) GL_W(0)
+#define GL_TAIL "s_mov_b32 m0, %0"
+#define GL_STMT(text) asm volatile(text : "=&s"(keep) : "v"(qk), "v"(wk), "s"(dst) : "memory", "scc")
+template <int G, int QL2>
+__device__ __forceinline__ void glds_slot(const char* qk, const char* wk, unsigned dst) {
+    unsigned keep;
+    if constexpr (QL2 == 2 && G == 10) GL_STMT(GL_Q2 GL_W7 GL_TAIL);
+    else if constexpr (QL2 == 2 && G == 11) GL_STMT(GL_Q2 GL_W8 GL_TAIL);
+    else if constexpr (QL2 == 2 && G == 13) GL_STMT(GL_Q2 GL_W10 GL_TAIL);
+    else if constexpr (QL2 == 7 && G == 15) GL_STMT(GL_Q7 GL_W7 GL_TAIL);
+    else if constexpr (QL2 == 7 && G == 16) GL_STMT(GL_Q7 GL_W8 GL_TAIL);
+    else if constexpr (QL2 == 7 && G == 17) GL_STMT(GL_Q7 GL_W9 GL_TAIL);
+    else if constexpr (QL2 == 7 && G == 18) GL_STMT(GL_Q7 GL_W10 GL_TAIL);
+    else if constexpr (QL2 == 7 && G == 19) GL_STMT(GL_Q7 GL_W11 GL_TAIL);
+    else if constexpr (QL2 == 7 && G == 20) GL_STMT(GL_Q7 GL_W12 GL_TAIL);
+    else static_assert(G < 0, "glds_slot: no statement for this slot shape");
+}
+#undef GL_STMT
+#endif
 template <int I, int G, int QL2>
 struct GldsBatch {
     __device__ __forceinline__ static void run(const char* qk, const char* wk, unsigned dst) {
@@ -720,7 +764,11 @@ __device__ __forceinline__ bool ipm_group(const DevConst& c, const DevBuffers& d
         const char* wk = (const char*)(WSb + (size_t)k * IS) + (t & 7) * 16 + (t >> 3) * 128;
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // reads of the slot's previous stage retired
         const unsigned dst = lds_base + (unsigned)(slot * G) * 1024u;
+#if MPCC_GLDS_ONE
+        glds_slot<G, QL / 2>(qk, wk, dst);
+#else
         GldsBatch<0, G, QL / 2>::run(qk, wk, dst);
+#endif
     };
     auto lds_common = [&](const double* im, In& o) {
         o.lb = im[o_lb];
@@ -850,17 +898,27 @@ __device__ __forceinline__ bool ipm_group(const DevConst& c, const DevBuffers& d
     };
     // forward step: v = K x~ + kff (lanes 0..7) and x~' = A~ x~ + B~ v (all lanes)
     auto fwd_step = [&](const In& in, double xt, double& v, double& xn) {
+        double part = 0.0;
+#if MPCC_BC_HALVES
+        // lane t < 8 multiplies K[t][m] by x~_m, lane 8 + i K[i][8 + m] by x~_(8+m): one half-row broadcast per term
+        const double xb8 = bc<8>(xt);
+        double xh[8];
+        bc_halves<8, 8>(xt, xh);
+#pragma unroll
+        for (int m = 0; m < 8; m++) part += in.m[m] * xh[m];
+#else
         double xb[16];
 #pragma unroll
         for (int m = 0; m < 16; m++) xb[m] = bcn(xt, m);
-        double part = 0.0;
 #pragma unroll
         for (int m = 0; m < 8; m++) part += in.m[m] * ((t < 8) ? xb[m] : xb[8 + m]);
+        const double xb8 = xb[8];
+#endif
         v = part + from_up<8>(part) + in.m[8];
         const double v7 = from_down<1>(v);
         const double vj = from_down<9>(v);
         if (t < 7) xn = fma2(mt, xt, gt, v);
-        else if (t == 7) xn = fma(g77, v, fma2(m77, xt, m78, xb[8]));
+        else if (t == 7) xn = fma(g77, v, fma2(m77, xt, m78, xb8));
         else if (t == 8) xn = fma2(m88, xt, g87, v7);
         else xn = vj;
     };
@@ -1487,12 +1545,19 @@ __device__ __forceinline__ bool ipm_group(const DevConst& c, const DevBuffers& d
                 const double pu9 = from_up<9>(pv), pu1 = from_up<1>(pv);  // DPP in uniform control flow
                 const double fg = fma(gt, pv, gv);
                 const double fv = (t < 7) ? fg + pu9 : fma(g87, pu1, fg);
+                double part = 0.0;
+#if MPCC_BC_HALVES
+                double fh4[4];
+                bc_halves<4, 4>(fv, fh4);
+#pragma unroll
+                for (int m = 0; m < 4; m++) part -= cur.m[8 + m] * fh4[m];
+#else
                 double fb[8];
 #pragma unroll
                 for (int i = 0; i < 8; i++) fb[i] = bcn(fv, i);
-                double part = 0.0;
 #pragma unroll
                 for (int m = 0; m < 4; m++) part -= cur.m[8 + m] * ((t < 8) ? fb[m] : fb[4 + m]);
+#endif
                 const double kff = part + from_up<8>(part);
                 const double kffd = from_down<8>(kff);  // lane 8+i <- kff_i
                 if (t >= 8) *ws(k, F_GVK) = kffd;

@@ -264,17 +264,26 @@ __device__ __attribute__((noinline)) void ipm_tail(const DevConst& c, const DevB
     };
     // forward step of the rollout from the K row halves + kff (m[0..8])
     auto fwd_step = [&](const double* m, double xt, double& v, double& xn) {
+        double part = 0.0;
+#if MPCC_BC_HALVES
+        const double xb8 = bc<8>(xt);
+        double xh[8];
+        bc_halves<8, 8>(xt, xh);
+#pragma unroll
+        for (int q = 0; q < 8; q++) part += m[q] * xh[q];
+#else
         double xb[16];
 #pragma unroll
         for (int q = 0; q < 16; q++) xb[q] = bcn(xt, q);
-        double part = 0.0;
 #pragma unroll
         for (int q = 0; q < 8; q++) part += m[q] * ((t < 8) ? xb[q] : xb[8 + q]);
+        const double xb8 = xb[8];
+#endif
         v = part + from_up<8>(part) + m[8];
         const double v7 = from_down<1>(v);
         const double vj = from_down<9>(v);
         if (t < 7) xn = fma2(mt, xt, gt, v);
-        else if (t == 7) xn = fma(g77, v, fma2(m77, xt, m78, xb[8]));
+        else if (t == 7) xn = fma(g77, v, fma2(m77, xt, m78, xb8));
         else if (t == 8) xn = fma2(m88, xt, g87, v7);
         else xn = vj;
     };
@@ -977,12 +986,19 @@ __device__ __attribute__((noinline)) void ipm_tail(const DevConst& c, const DevB
                     const double pu9 = from_up<9>(pvc), pu1 = from_up<1>(pvc);
                     const double fg = fma(gt, pvc, gv);
                     const double fv = (t < 7) ? fg + pu9 : fma(g87, pu1, fg);
+                    double part = 0.0;
+#if MPCC_BC_HALVES
+                    double fh4[4];
+                    bc_halves<4, 4>(fv, fh4);
+#pragma unroll
+                    for (int q = 0; q < 4; q++) part -= m[8 + q] * fh4[q];
+#else
                     double fb[8];
 #pragma unroll
                     for (int i = 0; i < 8; i++) fb[i] = bcn(fv, i);
-                    double part = 0.0;
 #pragma unroll
                     for (int q = 0; q < 4; q++) part -= m[8 + q] * ((t < 8) ? fb[q] : fb[4 + q]);
+#endif
                     const double kff = part + from_up<8>(part);
                     const double kffd = from_down<8>(kff);
                     if (own && t >= 8) *ws(k, L::GVK) = kffd;
