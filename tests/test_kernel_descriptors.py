@@ -79,4 +79,8 @@ def test_no_private_devconst_copy(built_lib, tmp_path):
             assert selfk and selfk[0]["vgpr_count"] <= 256
             env2 = [v for k, v in kern.items() if k.startswith("_ZN4mpcc9k_mlp_envILi2E")]
             assert env2 and env2[0]["group_segment_fixed_size"] <= 80 * 1024
+            # k_records at four waves per SIMD: the record is stored before the Gram matrix of the manipulability
+            # (holding pos, R and J through it took 194 registers)
+            recs = [v for k, v in kern.items() if k.startswith("_ZN4mpcc9k_records")]
+            assert recs and recs[0]["vgpr_count"] <= 128
     assert seen["narrow"] >= 12 and seen["wide"] >= 8
