@@ -586,14 +586,25 @@ __device__ __forceinline__ bool ipm_group(const DevConst& c, const DevBuffers& d
     if (run) {
         for (int k = t; k < NS; k += 16) fl |= (int)QSb[(size_t)k * QS + QS_FLAG];
         if (t < 8) {
+            // the input-block diagonals are read 8 stages at a time before the recursion uses them: loaded inside
+            // the loop (behind its early exit) they were 20 dependent HBM round trips at the start of every QP
             double prev_d = 0;
-            for (int k = 0; k < N; k++) {
-                const double dk = QSb[(size_t)k * QS + QS_R + t];
-                const double off = (k >= 1 && t < DOF) ? Hct : 0.0;
-                const double l = (k >= 1) ? off / prev_d : 0.0;
-                const double dd = dk - l * l;
-                if (dd <= 0) { fl |= 2; break; }
-                prev_d = sqrt(dd);
+            bool bad = false;
+            for (int k0 = 0; k0 < N && !bad; k0 += 8) {
+                double dk8[8];
+#pragma unroll
+                for (int q = 0; q < 8; q++) dk8[q] = QSb[(size_t)min(k0 + q, N - 1) * QS + QS_R + t];
+#pragma unroll
+                for (int q = 0; q < 8; q++) {
+                    const int k = k0 + q;
+                    if (bad || k >= N) break;
+                    const double dk = dk8[q];
+                    const double off = (k >= 1 && t < DOF) ? Hct : 0.0;
+                    const double l = (k >= 1) ? off / prev_d : 0.0;
+                    const double dd = dk - l * l;
+                    if (dd <= 0) { fl |= 2; bad = true; break; }
+                    prev_d = sqrt(dd);
+                }
             }
         }
     }
