@@ -110,6 +110,9 @@ static_assert(QS_POLY + 2 * 15 <= QS_YLB + 16 * QLINES, "bound block of <= 2 pol
 #ifndef MPCC_SLOT_SELECT
 #define MPCC_SLOT_SELECT 0  // 1: the slot algebra without divergent branches (selects): 0.4% slower at configs[1] (r05g A/B)
 #endif
+#ifndef MPCC_ROLL_RING
+#define MPCC_ROLL_RING 1  // the start-point rollout through a register ring of record-only loads (sweep_ring)
+#endif
 #ifndef MPCC_BC_HALVES
 #define MPCC_BC_HALVES 1  // half-row broadcasts (dpp::bc_halves) for the K-row products of the light sweeps
 #endif
@@ -966,6 +969,32 @@ __device__ __forceinline__ bool ipm_group(const DevConst& c, const DevBuffers& d
     double mcount = 0.0;
     if (run) {
         double y = 0.0;  // lane a < 9: y_a of stage k
+#if MPCC_ROLL_RING
+        // the rollout reads only the QP record (bounds, poly rows, b_k in x0), RD_ROLL - 1 stages ahead in a
+        // register ring (sweep_ring): with one stage ahead and the workspace fields of load_common besides, each
+        // stage waited on its loads
+        auto load_roll = [&](int k, In& o) {
+            const gdouble* q = qs_stage(k);
+            o.lb = q[rowY ? QS_YLB + t : QS_DLB + j9];
+            o.ub = q[rowY ? QS_YUB + t : QS_DUB + j9];
+            o.np = q[QS_NPOLY];
+            const int tp = t < 7 ? t : 0;
+#pragma unroll
+            for (int p = 0; p < NPE; p++) {
+                const double a = q[QS_POLY + 15 * p + tp], bv = q[QS_POLY + 15 * p + 7 + tp];
+                o.pa[p] = (NPM > 0 && t < 7) ? a : 0.0;
+                o.pb[p] = (NPM > 0 && t < 7) ? bv : 0.0;
+            }
+            const double pu = q[QS_POLY + 15 * (t < NPE ? t : 0) + 14];
+            o.pub = (t < NPM) ? pu : INF;
+            const double braw = q[QS_B + (t < 9 ? t : 0)];
+            o.x0 = (k < N && t < 9) ? braw : 0.0;
+        };
+        constexpr int RD_ROLL = (NPM <= 2) ? 4 : 2;
+        In rb[RD_ROLL];
+        sweep_ring<RD_ROLL>(N, false, rb, load_roll, [&](int k, In& cur) {
+            const double bk = cur.x0;
+#else
         double bk = 0, bkn = 0;
         load_common(0, cur);
         bk = (N > 0 && t < 9) ? QSb[QS_B + t] : 0.0;
@@ -974,6 +1003,7 @@ __device__ __forceinline__ bool ipm_group(const DevConst& c, const DevBuffers& d
                 load_common(k + 1, nxt);
                 bkn = (k + 1 < N && t < 9) ? QSb[(size_t)(k + 1) * QS + QS_B + t] : 0.0;
             }
+#endif
             const double yx = rowY ? y : 0.0;
             const double cz = row_cz(k, yx, 0.0);
             const double pcz = poly_cz(cur, k, yx, 0.0);
@@ -989,9 +1019,13 @@ __device__ __forceinline__ bool ipm_group(const DevConst& c, const DevBuffers& d
             const double y8 = from_up<1>(y);  // lane 7 <- y_8
             const double yn = (t == 7) ? fma2(m77, y, m78, y8) + bk : fma(mt, y, bk);
             y = (t < 9) ? yn : 0.0;
+#if MPCC_ROLL_RING
+        });
+#else
             cur = nxt;
             bk = bkn;
         }
+#endif
     }
     mcount = g_sum(mcount);
     PMARK(0);
