@@ -384,6 +384,37 @@ __device__ __forceinline__ double apply_elem(const DevConst& c, const DevBuffers
     return fabs(st[e]);
 }
 
+// apply_elem over elements e0, e0 + stride, ... of instance b, APB at a time: every load of a batch is issued before
+// its stores (gfx9 counts stores in vmcnt, so a load after a store waited for it: one HBM round trip per element);
+// returns max |step_e| over them
+template <int APB>
+__device__ inline double apply_range(const DevConst& c, const DevBuffers& d, int b, int e0, int stride, double alpha) {
+    const int N = c.N, n = (N + 1) * NXU;
+    double* g = d.guess + (size_t)b * n;
+    const double* st = d.step + (size_t)b * n;
+    double nrm = 0.0;
+    for (int base = e0; base < n; base += APB * stride) {
+        double gv[APB], sv[APB];
+#pragma unroll
+        for (int j = 0; j < APB; j++) {
+            const int e = min(base + j * stride, n - 1);
+            gv[j] = g[e];
+            sv[j] = st[e];
+        }
+#pragma unroll
+        for (int j = 0; j < APB; j++) {
+            const int e = base + j * stride;
+            if (e >= n) break;
+            const int k = e / NXU, a = e - NXU * k;
+            if (k == N && a >= NX) continue;
+            const double T = (a < NX) ? c.p.Tx[a] : c.p.Tu[a - NX];
+            g[e] = gv[j] + alpha * (T * sv[j]);
+            nrm = fmax(nrm, fabs(sv[j]));
+        }
+    }
+    return nrm;
+}
+
 // termination test after the step (osqp_interface.cpp:553-574); nrm = max |step| (order-free)
 __device__ inline void finish_iteration(const DevConst& c, const DevBuffers& d, int b, double nrm) {
     int32_t* si = d.sqi + (size_t)b * SQI;

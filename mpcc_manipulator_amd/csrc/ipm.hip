@@ -1947,7 +1947,7 @@ __device__ __forceinline__ void sqp_waves(const DevConst& c, const DevBuffers& d
         double nrm = 0.0;
         if (act) {
             const double alpha = d.sqd[(size_t)b * SQ + SQ_ALPHA];
-            for (int e = t; e < NS * 17; e += 16) nrm = fmax(nrm, apply_elem(c, d, b, e, alpha));
+            nrm = apply_range<8>(c, d, b, t, 16, alpha);
         }
         nrm = g_max(nrm);  // DPP: whole row active
         if (act && t == 0) finish_iteration(c, d, b, nrm);

@@ -1780,7 +1780,7 @@ __global__ void __launch_bounds__(64) k_sqp(DevConst, DevBuffers, const double* 
         if (act) {
             const double alpha = d.sqd[(size_t)b * SQ + SQ_ALPHA];
             if constexpr (LR) bfgs_post_step(c, d, b, t, alpha);
-            for (int e = t; e < NS * NXU; e += GW) nrm = fmax(nrm, apply_elem(c, d, b, e, alpha));
+            nrm = apply_range<8>(c, d, b, t, GW, alpha);
         }
         nrm = g_max32(nrm);
         if (act && t == 0) finish_iteration(c, d, b, nrm);
