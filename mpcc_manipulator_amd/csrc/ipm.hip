@@ -1788,7 +1788,21 @@ extern "C" int mpcc_debug_ipm_prof(unsigned long long* out, int reset) {
 // Phases of k_sqp as separate (non-inlined) functions: each has its own register allocation, so the
 // QP assembly and trial code does not add live ranges to the register-resident interior point.
 // the per-stage phases of k_sqp: lane t of st lanes works on stages t, t + st, ... (st = 16, a solo wave: 64)
+// MPCC_TRIAL_INLINE (default 1): the line-search trial inlined into the wave loop.  As a call it saved and restored
+// 256 callee-saved registers through scratch around every trial (its first loads queued behind those stores):
+// get_alpha 5.5% -> 3.7% of k_sqp, configs[1] 1.650-1.653M -> 1.663-1.672M (profiles/r05ab_ab_trial_inline.log).
+// MPCC_SETQP_INLINE: the same for the second and later QP assemblies.
+#ifndef MPCC_TRIAL_INLINE
+#define MPCC_TRIAL_INLINE 1
+#endif
+#ifndef MPCC_SETQP_INLINE
+#define MPCC_SETQP_INLINE 0
+#endif
+#if MPCC_SETQP_INLINE
+__device__ __forceinline__ void sqp_setqp_phase(const DevConst& c, const DevBuffers& d, int b, int t, int st,
+#else
 __device__ __attribute__((noinline)) void sqp_setqp_phase(const DevConst& c, const DevBuffers& d, int b, int t, int st,
+#endif
                                                           const double* __restrict__ ucur) {
     const int N = c.N, NS = N + 1;
     const SplineView sp = spl_of(c.spl, b);
@@ -1796,7 +1810,11 @@ __device__ __attribute__((noinline)) void sqp_setqp_phase(const DevConst& c, con
     for (int k = t; k <= N; k += st)
         setqp_stage(c, sp, gb, RecView{d.rec + (size_t)b * NS + k, c.S}, k, ucur, d.qs + ((size_t)b * NS + k) * QS);
 }
+#if MPCC_TRIAL_INLINE
+__device__ __forceinline__ void sqp_trial_phase(const DevConst& c, const DevBuffers& d, int b, int t, int st,
+#else
 __device__ __attribute__((noinline)) void sqp_trial_phase(const DevConst& c, const DevBuffers& d, int b, int t, int st,
+#endif
                                                           const double* __restrict__ ucur, double alpha, bool keep) {
     const int N = c.N, NS = N + 1;
     for (int k = t; k <= N; k += st) {
