@@ -1560,7 +1560,14 @@ __device__ __attribute__((noinline)) void sqp_setqp_phase(const DevConst& c, con
         setqp_stage(c, sp, gb, RecView{d.rec + (size_t)b * NS + k, c.S}, k, ucur, d.qs + ((size_t)b * NS + k) * QS,
                     keep_hess);
 }
+#ifndef MPCC_TRIAL_INLINE
+#define MPCC_TRIAL_INLINE 1  // the trial inlined into the wave loop (ipm.hip: no callee-saved spills per call)
+#endif
+#if MPCC_TRIAL_INLINE
+__device__ __forceinline__ void sqp_trial_phase(const DevConst& c, const DevBuffers& d, int b, int t,
+#else
 __device__ __attribute__((noinline)) void sqp_trial_phase(const DevConst& c, const DevBuffers& d, int b, int t,
+#endif
                                                           const double* __restrict__ ucur, double alpha, bool keep) {
     const int N = c.N, NS = N + 1;
     for (int k = t; k <= N; k += GW) {
