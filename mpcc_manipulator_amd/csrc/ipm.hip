@@ -114,7 +114,7 @@ static_assert(QS_POLY + 2 * 15 <= QS_YLB + 16 * QLINES, "bound block of <= 2 pol
 #define MPCC_ROLL_RING 1  // the start-point rollout through a register ring of record-only loads (sweep_ring)
 #endif
 #ifndef MPCC_BC_HALVES
-#define MPCC_BC_HALVES 1  // half-row broadcasts (dpp::bc_halves) for the K-row products of the light sweeps
+#define MPCC_BC_HALVES 0  // 1: half-row broadcasts (dpp::bc_halves) for the K-row products; faults in the bounds-checked build (r05am), off
 #endif
 #ifndef MPCC_WIDE_TAIL
 #define MPCC_WIDE_TAIL 1  // tail mode for the wide-poly variants (ipm_tail.h, round 5)
