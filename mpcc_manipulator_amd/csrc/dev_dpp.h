@@ -2,8 +2,6 @@
 #pragma once
 #include <hip/hip_runtime.h>
 
-#include <utility>
-
 namespace mpcc {
 namespace dpp {
 
@@ -32,31 +30,6 @@ __device__ __forceinline__ double bcn(double v, int n) {
         case 4: return bc<4>(v);   case 5: return bc<5>(v);   case 6: return bc<6>(v);   case 7: return bc<7>(v);
         case 8: return bc<8>(v);   case 9: return bc<9>(v);   case 10: return bc<10>(v); case 11: return bc<11>(v);
         case 12: return bc<12>(v); case 13: return bc<13>(v); case 14: return bc<14>(v); default: return bc<15>(v);
-    }
-}
-// out[m]: lanes 0..7 of each row <- lane m of the row, lanes 8..15 <- lane B0 + m (m < NT): row_newbcast moves
-// restricted by the bank mask (banks 0-1 / 2-3 = lanes 0-7 / 8-15) in place of two full broadcasts and a lane
-// select per term.  All first halves are issued before the second halves, so no DPP reads a register the
-// previous instruction wrote (that pair needs wait states).  The first moves' disabled lanes keep an opaque
-// value (an empty asm: no initialising instruction); the second moves overwrite them.
-__device__ __forceinline__ long long opaque_v() {
-    long long u;
-    asm volatile("" : "=v"(u));
-    return u;
-}
-template <int B0, int... M>
-__device__ __forceinline__ void bc_halves_seq(long long s, long long (&x)[sizeof...(M)], std::integer_sequence<int, M...>) {
-    ((x[M] = __builtin_amdgcn_update_dpp(opaque_v(), s, 0x150 + M, 0xF, 0x3, true)), ...);
-    ((x[M] = __builtin_amdgcn_update_dpp(x[M], s, 0x150 + B0 + M, 0xF, 0xC, true)), ...);
-}
-template <int NT, int B0>
-__device__ __forceinline__ void bc_halves(double v, double (&out)[NT]) {
-    long long x[NT];
-    bc_halves_seq<B0>((long long)__double_as_longlong(v), x, std::make_integer_sequence<int, NT>{});
-#pragma unroll
-    for (int m = 0; m < NT; m++) {
-        asm volatile("" : "+v"(x[m]));
-        out[m] = __longlong_as_double(x[m]);
     }
 }
 __device__ __forceinline__ double g_sum(double v) {

@@ -170,20 +170,26 @@ struct mpcc_engine {
         const size_t B = (size_t)maxB, NE = ((size_t)N + 1) * NXU;
         if (!d.isw) d.isw = dmalloc<double>(B * (N + 1) * ISW);
         if (!bfgs) return;
-        if (!d.glam) {
-            d.glam = dmalloc<double>(B * NE);
-            d.gprev = dmalloc<double>(B * NE);
-            d.aty = dmalloc<double>(B * NE);
-            d.sp = dmalloc<double>(B * NE);
-        }
+        // every set is allocated whole before it replaces the engine's pointers: a failed hipMalloc (thrown out of
+        // mpcc_set_params, which restores the old params) leaves the previous, consistent buffers in place
+        auto fr = [](double*& p) { if (p) (void)hipFree(p); p = nullptr; };
+        auto alloc_all = [&](std::initializer_list<std::pair<double**, size_t>> want) {
+            std::vector<double*> got;
+            try {
+                for (const auto& w : want) got.push_back(w.second ? dmalloc<double>(w.second) : nullptr);
+            } catch (...) {
+                for (double* p : got) fr(p);
+                throw;
+            }
+            size_t i = 0;
+            for (const auto& w : want) { fr(*w.first); *w.first = got[i++]; }
+        };
+        if (!d.glam || !d.gprev || !d.aty || !d.sp)
+            alloc_all({{&d.glam, B * NE}, {&d.gprev, B * NE}, {&d.aty, B * NE}, {&d.sp, B * NE}});
         const int lrs = bfgs_terms(max_iter);
         if (lrs > d.lrs) {
-            auto f = [](double*& p) { if (p) (void)hipFree(p); p = nullptr; };
-            f(d.lr); f(d.lrc); f(d.lrq);
-            d.lrs = 0;
-            d.lr = dmalloc<double>(B * lrs * NE);
-            d.lrc = dmalloc<double>(B * lrs);
-            if (lrs > LRM) d.lrq = dmalloc<double>(B * lrs * (N + 1) * 3 * 32);
+            alloc_all({{&d.lr, B * lrs * NE}, {&d.lrc, B * lrs},
+                       {&d.lrq, lrs > LRM ? B * lrs * (N + 1) * 3 * 32 : 0}});
             d.lrs = lrs;
         }
     }
@@ -390,10 +396,11 @@ void quiesce(mpcc_engine* e) {
 
 // the fused kernel's span T over the ComputeTime fields by its waves' phase fractions: set_qp gets the in-kernel QP
 // assembly on top of k_setqp's launch, solve_qp the QP solves, get_alpha the line search; the step update's share
-// stays in total only (the reference times it in none of the four, osqp_interface.cpp:548-564)
+// stays in total only (the reference times it in none of the four, osqp_interface.cpp:548-564).  t.solve_qp holds T
+// plus any staged k_ipm spans of the same window (MPCC_STAGED_SQP calls mixed with fused ones): only T is split.
 void split_sqp(mpcc_timing& t, double T, const double (&f)[PH_N]) {
     t.set_qp += T * f[PH_SETQP];
-    t.solve_qp = T * f[PH_SOLVE];
+    t.solve_qp = (t.solve_qp - T) + T * f[PH_SOLVE];
     t.get_alpha += T * f[PH_ALPHA];
 }
 

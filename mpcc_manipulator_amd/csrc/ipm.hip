@@ -113,9 +113,6 @@ static_assert(QS_POLY + 2 * 15 <= QS_YLB + 16 * QLINES, "bound block of <= 2 pol
 #ifndef MPCC_ROLL_RING
 #define MPCC_ROLL_RING 1  // the start-point rollout through a register ring of record-only loads (sweep_ring)
 #endif
-#ifndef MPCC_BC_HALVES
-#define MPCC_BC_HALVES 0  // 1: half-row broadcasts (dpp::bc_halves) for the K-row products; faults in the bounds-checked build (r05am), off
-#endif
 #ifndef MPCC_WIDE_TAIL
 #define MPCC_WIDE_TAIL 1  // tail mode for the wide-poly variants (ipm_tail.h, round 5)
 #endif
@@ -913,21 +910,12 @@ __device__ __forceinline__ bool ipm_group(const DevConst& c, const DevBuffers& d
     // forward step: v = K x~ + kff (lanes 0..7) and x~' = A~ x~ + B~ v (all lanes)
     auto fwd_step = [&](const In& in, double xt, double& v, double& xn) {
         double part = 0.0;
-#if MPCC_BC_HALVES
-        // lane t < 8 multiplies K[t][m] by x~_m, lane 8 + i K[i][8 + m] by x~_(8+m): one half-row broadcast per term
-        const double xb8 = bc<8>(xt);
-        double xh[8];
-        bc_halves<8, 8>(xt, xh);
-#pragma unroll
-        for (int m = 0; m < 8; m++) part += in.m[m] * xh[m];
-#else
         double xb[16];
 #pragma unroll
         for (int m = 0; m < 16; m++) xb[m] = bcn(xt, m);
 #pragma unroll
         for (int m = 0; m < 8; m++) part += in.m[m] * ((t < 8) ? xb[m] : xb[8 + m]);
         const double xb8 = xb[8];
-#endif
         v = part + from_up<8>(part) + in.m[8];
         const double v7 = from_down<1>(v);
         const double vj = from_down<9>(v);
@@ -1591,18 +1579,11 @@ __device__ __forceinline__ bool ipm_group(const DevConst& c, const DevBuffers& d
                 const double fg = fma(gt, pv, gv);
                 const double fv = (t < 7) ? fg + pu9 : fma(g87, pu1, fg);
                 double part = 0.0;
-#if MPCC_BC_HALVES
-                double fh4[4];
-                bc_halves<4, 4>(fv, fh4);
-#pragma unroll
-                for (int m = 0; m < 4; m++) part -= cur.m[8 + m] * fh4[m];
-#else
                 double fb[8];
 #pragma unroll
                 for (int i = 0; i < 8; i++) fb[i] = bcn(fv, i);
 #pragma unroll
                 for (int m = 0; m < 4; m++) part -= cur.m[8 + m] * ((t < 8) ? fb[m] : fb[4 + m]);
-#endif
                 const double kff = part + from_up<8>(part);
                 const double kffd = from_down<8>(kff);  // lane 8+i <- kff_i
                 if (t >= 8) *ws(k, F_GVK) = kffd;

@@ -265,20 +265,12 @@ __device__ __attribute__((noinline)) void ipm_tail(const DevConst& c, const DevB
     // forward step of the rollout from the K row halves + kff (m[0..8])
     auto fwd_step = [&](const double* m, double xt, double& v, double& xn) {
         double part = 0.0;
-#if MPCC_BC_HALVES
-        const double xb8 = bc<8>(xt);
-        double xh[8];
-        bc_halves<8, 8>(xt, xh);
-#pragma unroll
-        for (int q = 0; q < 8; q++) part += m[q] * xh[q];
-#else
         double xb[16];
 #pragma unroll
         for (int q = 0; q < 16; q++) xb[q] = bcn(xt, q);
 #pragma unroll
         for (int q = 0; q < 8; q++) part += m[q] * ((t < 8) ? xb[q] : xb[8 + q]);
         const double xb8 = xb[8];
-#endif
         v = part + from_up<8>(part) + m[8];
         const double v7 = from_down<1>(v);
         const double vj = from_down<9>(v);
@@ -987,18 +979,11 @@ __device__ __attribute__((noinline)) void ipm_tail(const DevConst& c, const DevB
                     const double fg = fma(gt, pvc, gv);
                     const double fv = (t < 7) ? fg + pu9 : fma(g87, pu1, fg);
                     double part = 0.0;
-#if MPCC_BC_HALVES
-                    double fh4[4];
-                    bc_halves<4, 4>(fv, fh4);
-#pragma unroll
-                    for (int q = 0; q < 4; q++) part -= m[8 + q] * fh4[q];
-#else
                     double fb[8];
 #pragma unroll
                     for (int i = 0; i < 8; i++) fb[i] = bcn(fv, i);
 #pragma unroll
                     for (int q = 0; q < 4; q++) part -= m[8 + q] * ((t < 8) ? fb[q] : fb[4 + q]);
-#endif
                     const double kff = part + from_up<8>(part);
                     const double kffd = from_down<8>(kff);
                     if (own && t >= 8) *ws(k, L::GVK) = kffd;

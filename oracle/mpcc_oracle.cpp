@@ -1638,6 +1638,33 @@ static bool bfgs_update(const StructQP& S0, LowRank& lr, const std::vector<doubl
     return true;
 }
 
+// qp_mode 2: BFGSUpdate (osqp_interface.cpp:683-715) verbatim on one dense Hess_ that is updated in place at every
+// SQP iteration, with no cap on the number of updates (the engine and qp_modes 0/1 restart past BFGS_MAX_TERMS
+// low-rank terms: deviation 7).  Same operation order as the Eigen expression
+// Hess - Bs * Bs^T / sBs + r * r^T / sr.
+static void bfgs_update_dense(std::vector<double>& H, int nv, const std::vector<double>& s, const std::vector<double>& dg) {
+    std::vector<double> Bs(nv, 0.0), r(nv);
+    for (int a = 0; a < nv; a++) {
+        double t = 0;
+        for (int b = 0; b < nv; b++) t += H[(size_t)a * nv + b] * s[b];
+        Bs[a] = t;
+    }
+    const double sBs = vdot(s, Bs), sy = vdot(s, dg);
+    double sr;
+    if (sy < 0.2 * sBs) {
+        const double theta = 0.8 * sBs / (sBs - sy);
+        for (int i = 0; i < nv; i++) r[i] = theta * dg[i] + (1 - theta) * Bs[i];
+        sr = theta * sy + (1 - theta) * sBs;
+    } else {
+        r = dg;
+        sr = sy;
+    }
+    if (sr < std::numeric_limits<double>::epsilon()) return;
+    for (int a = 0; a < nv; a++)
+        for (int b = 0; b < nv; b++)
+            H[(size_t)a * nv + b] = H[(size_t)a * nv + b] - Bs[a] * Bs[b] / sBs + r[a] * r[b] / sr;
+}
+
 // Returns 0 on success (step filled in reference layout: [y_0..y_N | v_0..v_{N-1}]), else Status.
 static const bool g_ipm_debug = std::getenv("MPCC_ORACLE_IPM_DEBUG") != nullptr;  // per-iteration log (debug)
 
@@ -2099,15 +2126,29 @@ static int solve_ocp(const Oracle& o, double* guess, const double* recs, const d
         }
         grad_L_prev = gl;
     };
+    const bool verbatim = o.opt.qp_mode == 2;  // the reference's dense in-place BFGSUpdate, no restart
+    std::vector<double> Hd;                    // its Hess_ (qp_mode 2)
     for (it = 0; it < p.max_iter; it++) {
         // setQP + PD / NaN checks of the normalized Hessian (:445-473)
         bool nan = false, pd = true;
-        bfgs_restart = bfgs && it > 0 && lr.r() + 2 > BFGS_MAX_TERMS;
+        bfgs_restart = bfgs && !verbatim && it > 0 && lr.r() + 2 > BFGS_MAX_TERMS;
         if (bfgs_restart) { lr.u.clear(); lr.c.clear(); }
-        if (o.opt.qp_mode == 1) {
+        if (o.opt.qp_mode == 1 || verbatim) {
             DenseQP q;
             set_qp(o, guess, recs, ucur, true, q);
-            if (bfgs) {  // dense form of the same BFGS matrix: P0 + sum_j c_j u_j u_j^T
+            if (bfgs && verbatim) {  // :438-453: Hess_ of setQP at iteration 0, then BFGSUpdate(Hess_, step_prev_, dgrad_L)
+                if (it == 0) Hd = q.P;
+                qd = q.g;
+                std::vector<double> gl(nv);
+                for (int i = 0; i < nv; i++) gl[i] = qd[i] + g_lam[i];
+                if (it > 0) {
+                    std::vector<double> dg(nv);
+                    for (int i = 0; i < nv; i++) dg[i] = gl[i] - grad_L_prev[i];
+                    bfgs_update_dense(Hd, nv, step_prev, dg);
+                }
+                grad_L_prev = gl;
+                q.P = Hd;
+            } else if (bfgs) {  // dense form of the same BFGS matrix: P0 + sum_j c_j u_j u_j^T
                 if (it == 0 || bfgs_restart) { P0 = q.P; build_struct_qp(o, guess, recs, ucur, S0); }
                 qd = q.g;
                 bfgs_grad(it);

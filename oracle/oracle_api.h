@@ -58,7 +58,8 @@ typedef struct {
 } OracleParams;
 
 typedef struct {
-    int    qp_mode;        /* 0 = riccati (stage-structured IPM), 1 = dense reference layout IPM */
+    int    qp_mode;        /* 0 = riccati (stage-structured IPM), 1 = dense reference layout IPM, 2 = dense with the
+                              reference's in-place BFGSUpdate verbatim (no low-rank cap / restart: deviation 7) */
     int    nthreads;       /* OpenMP threads for batch calls */
 } OracleOptions;
 

@@ -359,6 +359,39 @@ def test_bfgs_restart_layouts_agree(oracle_lib):
     assert np.abs(outs[0]["horizon"] - outs[1]["horizon"]).max() <= 1e-8
 
 
+def test_bfgs_deviation7_measured(oracle_lib):
+    """Deviation 7 kept visible: the oracle's qp_mode 2 runs the reference's BFGSUpdate verbatim
+    (osqp_interface.cpp:453, 683-715: one dense Hess_ updated in place at every SQP iteration, no cap), qp_mode 1 the
+    engine's rule (the same damped update held as low-rank terms, restarted from the exact Hessian past LRX = 28
+    terms).  Below 15 SQP iterations the two are the same matrix: statuses, iteration counts and inputs agree to
+    rounding.  Past it the restart changes the iterates; the test measures by how much and prints it (at N = 20,
+    B = 32, mask 7: 10 status flips, max |du0| 1.35)."""
+    from helpers import batch_from_pool, oracle_pool
+    N, B, mask = 12, 16, 7
+    ov = {"sqp": {"max_iter": 40, "use_BFGS": 1, "eps_prim": 3e-3}}
+    ob = (0.48, 0.218, 0.521, 5.0)
+    o0, _, _ = make_oracle(N=N, max_iter=3, mask=mask, overrides={"sqp": {"max_iter": 3}}, nthreads=8)
+    pool = oracle_pool(o0, 60, obs=ob)
+    rng = np.random.default_rng(SEED + 767)
+    x0, u0, obs, g, v, f = batch_from_pool(pool, B, rng, obs=np.tile(ob, (B, 1)), qnoise=0.02)
+    v[::2] = 0
+    outs = []
+    for qp_mode in (1, 2):
+        o, _, _ = make_oracle(N=N, max_iter=40, mask=mask, qp_mode=qp_mode, overrides=ov, nthreads=8)
+        outs.append(o.run_mpc(x0.copy(), u0, obs, g.copy(), v.copy(), f.copy()))
+    rule, verb = outs
+    short = (rule["sqp_iters"] < 15) & (verb["sqp_iters"] < 15)
+    assert short.sum() >= 4 and (~short).sum() >= 4, (rule["sqp_iters"], verb["sqp_iters"])
+    assert np.array_equal(rule["status"][short], verb["status"][short])
+    assert np.array_equal(rule["sqp_iters"][short], verb["sqp_iters"][short])
+    assert np.abs(rule["horizon"][short] - verb["horizon"][short]).max() <= 1e-9
+    flips = int(np.sum(rule["status"] != verb["status"]))
+    iters = int(np.sum(rule["sqp_iters"] != verb["sqp_iters"]))
+    du0 = float(np.abs(rule["u0"] - verb["u0"]).max())
+    print(f"deviation 7 (N={N}, B={B}): status flips {flips}, SQP-iteration changes {iters}, max |du0| {du0:.3g}")
+    assert iters >= 1 and du0 > 1e-6  # the restart is a real deviation past 15 iterations, not rounding
+
+
 def test_params_resolution(oracle_lib):
     """Params/*.json with the reference's override semantics: T_x/T_u (normalization.json:3-20)."""
     P = rp.resolve(N=20)
