@@ -64,7 +64,6 @@ def test_mixed_window_keeps_staged_spans(built_lib, monkeypatch):
     monkeypatch.setenv("MPCC_STAGED_SQP", "1")
     B = 256
     params = m.load_params(N=20, overrides={"sqp": {"max_iter": 2}})
-    bfgs = m.load_params(N=20, overrides={"sqp": {"max_iter": 2, "use_BFGS": 1}})
     eng = m.Engine(params, max_batch=B, constraint_mask=2)
     eng.set_track(*_track(m, eng))
     rng = np.random.default_rng(SEED + 901)
@@ -81,6 +80,8 @@ def test_mixed_window_keeps_staged_spans(built_lib, monkeypatch):
     eng.set_warmstart(guess, valid, fails)
     eng.timing_begin()
     eng.solve(x0.copy(), u0, obs)
+    bfgs = eng.params  # the engine's params (constraint mask 2), with use_BFGS switched on
+    bfgs.use_BFGS = 1
     eng.set_params(bfgs)
     eng.set_warmstart(guess, valid, fails)
     eng.solve(x0.copy(), u0, obs)
