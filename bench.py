@@ -110,6 +110,15 @@ def union_length(starts, ends):
 HBM_PEAK_BPS = 8.0e12  # MI355X HBM3E peak (spec), MI355X_MICROARCH.md
 
 
+def qs_doubles(dof):
+    """Doubles of one stage's QP record (csrc/dev_common.h QS: NX = DOF + 2, NU = DOF + 1, 11 polytopic rows of
+    2 DOF + 1, padded to whole 128-byte lines): 336 for the Panda, 480 for the Husky+Panda."""
+    nx, nu, npc = dof + 2, dof + 1, 11
+    ylb = (nx * nx + nx + 2 * nu + nx + 15) // 16 * 16
+    obj = ylb + 2 * nx + 2 * dof + 1 + npc * (2 * dof + 1) + 1
+    return (obj + 1 + 15) // 16 * 16
+
+
 def mlp_flops_per_sample(which, dof=7):
     """value + the DOF forward-mode Jacobian columns of one collision-MLP sample.
     self: 21 -> 256 -> 64 -> 1; env: 30 -> 256 x 4 -> 9 (F_self 0.285, F_env 3.21 MFLOP for the Panda)."""
@@ -464,24 +473,34 @@ def main():
     flops = flops_step * ncalls / max(1, nipm)  # per launch, on average
     # time the kernel ran: the union of all groups' launch intervals (S = 1: the sum of launch durations)
     busy = union_length(np.concatenate([a for a, _ in ivs]), np.concatenate([b for _, b in ivs])) * 1e-3
-    achieved = flops_step * ncalls / busy / 1e12 if busy > 0 else flops / t_ipm / 1e12
+    # per launch (the contract's figure): the algorithmic flops one launch is credited with over its mean duration;
+    # the S groups' launches overlap, so the chip-wide figure over the union of their intervals is reported beside it
+    achieved = flops / t_ipm / 1e12 if t_ipm > 0 else 0.0
+    achieved_union = flops_step * ncalls / busy / 1e12 if busy > 0 else achieved
     pmc = find_pmc(kname, Bs, N, args.mask, dof, args.traffic)
     traffic = pmc.get("hbm_bytes_per_launch") if pmc else None
     pflops = pmc_fp64_flops(pmc.get("counters")) if pmc else None
+    # the stage records one launch must move at least: every instance's QP record and step, read / written once per
+    # QP solved (QS + NX + NU doubles per stage), against which the counted traffic is compared
+    rec_io = (qps / max(1, S)) * (N + 1) * (qs_doubles(dof) + dof + 2 + dof + 1) * 8.0
     # k_sqp is a latency-bound FP64 kernel: VALU + DPP for the stage recursions, the matrix cores for P = Hb - U^T U
     # (and the poly Gram blocks of the wide variants); its roof is the FP64 peak (78.6 TFLOP/s for vector and matrix
     # alike on MI355X), its work the SURVEY's condensed-dense F_qp per QP actually solved; the PMC-counted FP64 flops
-    # it executed (VALU and MFMA) and its HBM fraction (PMC traffic of all launches / the time they ran / 8 TB/s) are
-    # reported beside it
+    # it executed (VALU and MFMA) and its counter-measured HBM traffic (not algorithmic bytes: mostly the interior
+    # point's streamed workspace) are reported beside it
     roof = {"kernel": kname, "bound": "valu+mfma", "achieved": achieved, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
             "frac": achieved / FP64_PEAK_TFLOPS, "traffic": traffic,
-            "hbm_frac": (traffic * nipm / busy / HBM_PEAK_BPS) if traffic and busy > 0 else None,
+            "achieved_union": achieved_union, "frac_union": achieved_union / FP64_PEAK_TFLOPS,
+            "counter_hbm_frac": (traffic * nipm / busy / HBM_PEAK_BPS) if traffic and busy > 0 else None,
+            "record_io_bytes_per_launch": rec_io,
+            "traffic_over_record_io": (traffic / rec_io) if traffic and rec_io > 0 else None,
             "pmc_fp64_flops_per_launch": pflops,
-            "pmc_fp64_frac": (pflops * nipm / busy / 1e12 / FP64_PEAK_TFLOPS) if pflops and busy > 0 else None,
+            "pmc_fp64_frac": (pflops / t_ipm / 1e12 / FP64_PEAK_TFLOPS) if pflops and t_ipm > 0 else None,
             "pmc_source": pmc.get("file") if pmc else None,
             "avg_launch_ms": t_ipm * 1e3, "launches_timed": nipm, "concurrent_groups": S,
             "busy_ms_per_step": busy / max(1, ncalls) * 1e3, "algorithmic_flops_per_launch": flops,
-            "work": "F_qp (SURVEY 8(d), condensed-dense QP) x QPs solved, over the union of the launches' intervals",
+            "work": "F_qp (SURVEY 8(d), condensed-dense QP) x QPs solved; frac per launch (mean launch duration), "
+                    "frac_union over the union of the S groups' concurrent launches",
             "qp_solves_per_step": qps}
     t_env, n_env = tmlp["k_mlp_env"]
     busy_env = union_length(np.concatenate([a for a, _ in ivs_env]), np.concatenate([b for _, b in ivs_env])) * 1e-3
@@ -505,7 +524,7 @@ def main():
         ach = fl * n_env / busy_env / 1e12
         roof = {"kernel": "k_mlp_env", "bound": "mfma", "achieved": ach, "peak": FP64_PEAK_TFLOPS,
                 "unit": "TFLOP/s", "frac": ach / FP64_PEAK_TFLOPS, "traffic": tr,
-                "hbm_frac": (tr * n_env / busy_env / HBM_PEAK_BPS) if tr else None, "avg_launch_ms": t_l * 1e3,
+                "counter_hbm_frac": (tr * n_env / busy_env / HBM_PEAK_BPS) if tr else None, "avg_launch_ms": t_l * 1e3,
                 "launches_timed": n_env, "concurrent_groups": S, "busy_ms_per_step": busy_env / max(1, ncalls) * 1e3,
                 "algorithmic_flops_per_launch": fl,
                 "work": "F_env (SURVEY 8(d): value + DOF Jacobian columns) x B/S (N+1) samples per launch, over the "

@@ -51,3 +51,10 @@ def test_union_length_of_launch_intervals():
     assert bench.union_length([0.0, 1.0, 5.0], [2.0, 3.0, 6.0]) == 4.0       # [0,3] + [5,6]
     assert bench.union_length([5.0, 0.0], [6.0, 10.0]) == 10.0               # nested, unsorted
     assert bench.union_length([-1.0, 0.0], [0.5, 0.25]) == 1.5               # times before the anchor
+
+
+def test_record_io_size_matches_qp_record_layout():
+    """The roofline's record-I/O bytes use the QP record size of csrc/dev_common.h (QS, whole 128-byte lines): 336
+    doubles for the Panda (its static_assert), 480 for the Husky+Panda."""
+    import bench
+    assert bench.qs_doubles(7) == 336 and bench.qs_doubles(10) == 480
