@@ -111,6 +111,8 @@ struct DevConst {
     int ocp;                         // 1: SolverInterface::solveOCP only (mpcc_solve_ocp), no MPC bookkeeping
     int tail;                        // 1: k_sqp's interior point runs a wave's last active instance in tail mode
     int solo;                        // k_sqp launches: group slots map to instances through d.order: 1 solo waves, 2 solo blocks
+    int subset;                      // k_records / k_setqp: 0 every instance; 1 the solo-block instances only (d.order's
+                                     // slots 4 r); 2 every instance but those (early solo blocks, engine.cpp run_batch)
     uint32_t* bchk;                  // bounds-checked build: per-lane violation bits (null otherwise)
 };
 

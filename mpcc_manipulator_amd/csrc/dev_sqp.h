@@ -19,6 +19,9 @@ namespace mpcc {
 // keep_hess (damped BFGS, SQP iteration >= 1): the state Hessian block and its NaN / PD flags stay those of
 // SQP iteration 0 (setQP is called without the Hessian, osqp_interface.cpp:441-442); the input diagonal is
 // constant and is rewritten unchanged.
+#ifndef MPCC_SETQP_PRELOAD
+#define MPCC_SETQP_PRELOAD 1
+#endif
 __device__ inline void setqp_stage(const DevConst& c, const SplineView& sp, const double* __restrict__ gb, const RecView& rv, int k,
                                    const double* __restrict__ ucur, double* __restrict__ q, bool keep_hess = false) {
     const mpcc_params& p = c.p;
@@ -29,6 +32,49 @@ __device__ inline void setqp_stage(const DevConst& c, const SplineView& sp, cons
     const double* uk = gb + NXU * k + NX;
     double fx[NX], fu[NU], fxx[NX * NX], fuu[NU];
     double obj = stage_cost(c, sp, xk, uk, rv, k, true, fx, fu, fxx, fuu);
+    // Every guess value the record needs after the cost, loaded before the record's first store: gfx9 counts stores
+    // in vmcnt, so a load issued after a store waits for it too (the y-box, ddq and dynamics loops below loaded from
+    // the guess between their stores: ~90 of the kernel's 109 full vmcnt waits).  The values and every operation on
+    // them are the same.  Addresses past the horizon are clamped to a valid stage and the value is not used.
+#if MPCC_SETQP_PRELOAD
+    const int kn = k < N ? k + 1 : k, kp = k > 0 ? k - 1 : k;
+    double xkv[NX], ukv[NU], xnv[NX], unv[DOF], upv[DOF], ucv[DOF], uib[NX], lub[NX], uub[NX], tub[NX];
+#pragma unroll
+    for (int a = 0; a < NX; a++) { xkv[a] = xk[a]; xnv[a] = gb[NXU * kn + a]; }
+#pragma unroll
+    for (int j = 0; j < NU; j++) ukv[j] = uk[j];
+#pragma unroll
+    for (int j = 0; j < DOF; j++) { unv[j] = gb[NXU * kn + NX + j]; upv[j] = gb[NXU * kp + NX + j]; ucv[j] = ucur[j]; }
+#pragma unroll
+    for (int m = 0; m < NX; m++) {
+        const int idx = NX * k + m, i = idx / NU, j = idx % NU;
+        uib[m] = gb[NXU * (i < N ? i : 0) + NX + j];
+        lub[m] = p.lu[j];  // kernel-argument loads at a lane-dependent index: loads like the guess's
+        uub[m] = p.uu[j];
+        tub[m] = Tu[j];
+    }
+#define XK(a) xkv[a]
+#define UK(j) ukv[j]
+#define UN(j) unv[j]
+#define UP(j) upv[j]
+#define XN(a) xnv[a]
+#define UC(j) ucv[j]
+#define UI(m, i, j) uib[m]
+#define LU(m, j) lub[m]
+#define UU(m, j) uub[m]
+#define TU(m, j) tub[m]
+#else
+#define XK(a) xk[a]
+#define UK(j) uk[j]
+#define UN(j) gb[NXU * (k + 1) + NX + (j)]
+#define UP(j) gb[NXU * (k - 1) + NX + (j)]
+#define XN(a) gb[NXU * (k + 1) + (a)]
+#define UC(j) ucur[j]
+#define UI(m, i, j) gb[NXU * (i) + NX + (j)]
+#define LU(m, j) p.lu[j]
+#define UU(m, j) p.uu[j]
+#define TU(m, j) Tu[j]
+#endif
     int flag = keep_hess ? ((int)q[QS_FLAG] & 3) : 0;
     for (int a = 0; a < NX; a++) {
         q[QS_q + a] = Tx[a] * fx[a];
@@ -69,40 +115,38 @@ __device__ inline void setqp_stage(const DevConst& c, const SplineView& sp, cons
         }
         // ddq cost (osqp_interface.cpp:166-217)
         if (k != N - 1) {
-            const double* un = gb + NXU * (k + 1) + NX;
             double sq = 0;
-            for (int j = 0; j < DOF; j++) sq += (un[j] - uk[j]) * (un[j] - uk[j]);
+            for (int j = 0; j < DOF; j++) sq += (UN(j) - UK(j)) * (UN(j) - UK(j));
             objd = rddq * sq;
         }
         for (int j = 0; j < DOF; j++) {
             double gg;
-            if (k == 0) gg = 2. * rddq * (uk[j] - gb[NXU * (k + 1) + NX + j]);
-            else if (k == N - 1) gg = 2. * rddq * (uk[j] - gb[NXU * (k - 1) + NX + j]);
-            else gg = 2. * rddq * (2. * uk[j] - gb[NXU * (k + 1) + NX + j] - gb[NXU * (k - 1) + NX + j]);
+            if (k == 0) gg = 2. * rddq * (UK(j) - UN(j));
+            else if (k == N - 1) gg = 2. * rddq * (UK(j) - UP(j));
+            else gg = 2. * rddq * (2. * UK(j) - UN(j) - UP(j));
             q[QS_r + j] += Tu[j] * gg;
             double cii = (k == 0 || k == N - 1) ? 2. * rddq : 4. * rddq;
             q[QS_R + j] += Tu[j] * cii * Tu[j];
         }
         for (int j = 0; j < NU; j++) if (isnan(q[QS_R + j])) flag |= 1;
         // dynamics offset b_k = -c_{k+1} = -Tx^-1 (x_{k+1} - (A x_k + B u_k + g))   (:247)
-        const double* xn = gb + NXU * (k + 1);
         for (int a = 0; a < NX; a++) {
             double s1 = 0, s2 = 0;
-            for (int m = 0; m < NX; m++) s1 += c.A[a * NX + m] * xk[m];
-            for (int m = 0; m < NU; m++) s2 += c.B[a * NU + m] * uk[m];
+            for (int m = 0; m < NX; m++) s1 += c.A[a * NX + m] * XK(m);
+            for (int m = 0; m < NU; m++) s2 += c.B[a * NU + m] * UK(m);
             double pred = s1 + s2 + 0.0;
-            q[QS_B + a] = -((1.0 / Tx[a]) * (xn[a] - pred));
+            q[QS_B + a] = -((1.0 / Tx[a]) * (XN(a) - pred));
         }
         // ddq rows (setBounds :279-297): v_0[j] (k=0) or v_k[j]-v_{k-1}[j] within (l - c) / coef
         for (int j = 0; j < DOF; j++) {
             double coef = 1. / p.Ts * Tu[j];
             double cc, lo, hi;
             if (k == 0) {
-                cc = 1. / p.Ts * uk[j];
-                lo = p.lddq[j] + 1. / p.Ts * ucur[j];
-                hi = p.uddq[j] + 1. / p.Ts * ucur[j];
+                cc = 1. / p.Ts * UK(j);
+                lo = p.lddq[j] + 1. / p.Ts * UC(j);
+                hi = p.uddq[j] + 1. / p.Ts * UC(j);
             } else {
-                cc = 1. / p.Ts * (uk[j] - gb[NXU * (k - 1) + NX + j]);
+                cc = 1. / p.Ts * (UK(j) - UP(j));
                 lo = p.lddq[j];
                 hi = p.uddq[j];
             }
@@ -113,7 +157,11 @@ __device__ inline void setqp_stage(const DevConst& c, const SplineView& sp, cons
         int np = 0;
         for (int r = 0; r < NPC; r++) {
             double val, a[DOF], bv[DOF];
+#if MPCC_SETQP_PRELOAD
+            if (!poly_row(c, ukv, rv, r, &val, true, a, bv)) continue;
+#else
             if (!poly_row(c, uk, rv, r, &val, true, a, bv)) continue;
+#endif
             double* row = q + QS_POLY + POLY_W * np;
             for (int j = 0; j < DOF; j++) { row[j] = a[j]; row[DOF + j] = bv[j]; }
             row[2 * DOF] = 0.0 - val;
@@ -132,15 +180,15 @@ __device__ inline void setqp_stage(const DevConst& c, const SplineView& sp, cons
     for (int m = 0; m < NX; m++) {
         double lo = p.lx[m], hi = p.ux[m];
         bool lo_inf = lo <= -BIG, hi_inf = hi >= BIG;
-        if (m == XS) { lo = fmax(xk[XS] - p.s_trust_region, 0.); hi = fmin(xk[XS] + p.s_trust_region, L); lo_inf = hi_inf = false; }
-        double ylo = lo_inf ? -INF : (lo - xk[m]) / Tx[m];
-        double yhi = hi_inf ? INF : (hi - xk[m]) / Tx[m];
+        if (m == XS) { lo = fmax(XK(XS) - p.s_trust_region, 0.); hi = fmin(XK(XS) + p.s_trust_region, L); lo_inf = hi_inf = false; }
+        double ylo = lo_inf ? -INF : (lo - XK(m)) / Tx[m];
+        double yhi = hi_inf ? INF : (hi - XK(m)) / Tx[m];
         const int idx = NX * k + m;
         const int i = idx / NU, j = idx % NU;
         if (i < N) {
-            const double ui = gb[NXU * i + NX + j];
-            if (p.lu[j] > -BIG) ylo = fmax(ylo, (p.lu[j] - ui) / Tu[j]);
-            if (p.uu[j] < BIG) yhi = fmin(yhi, (p.uu[j] - ui) / Tu[j]);
+            const double ui = UI(m, i, j);
+            if (LU(m, j) > -BIG) ylo = fmax(ylo, (LU(m, j) - ui) / TU(m, j));
+            if (UU(m, j) < BIG) yhi = fmin(yhi, (UU(m, j) - ui) / TU(m, j));
         }
         q[QS_YLB + m] = ylo;
         q[QS_YUB + m] = yhi;
@@ -153,6 +201,16 @@ __device__ inline void setqp_stage(const DevConst& c, const SplineView& sp, cons
     }
     q[QS_FLAG] = (double)flag;
     q[QS_OBJ] = obj + objd;
+#undef XK
+#undef UK
+#undef UN
+#undef UP
+#undef XN
+#undef UC
+#undef UI
+#undef LU
+#undef UU
+#undef TU
 }
 
 // ------------------------------------------------------------------------------------------------

@@ -61,6 +61,7 @@ struct mpcc_engine {
     bool wide_sqp = false;  // MPCC_WIDE_SQP=1: the 32-lane fused kernel for the Panda build too (experiment)
     int tail_mode = 1;      // MPCC_TAIL=0: no tail mode in k_sqp (A/B switch; results are bitwise the same)
     int solo_mode = 2;      // MPCC_SOLO: 0 no solo waves for cold starts in k_sqp, 1 solo waves, 2 (default) solo blocks
+    int early_solo = 1;     // MPCC_EARLY_SOLO=0: the solo blocks start after every instance's QP records (run_batch)
                             // (narrow variants; A/B switch, bitwise the same)
     bool last_wide = DOF != 7;  // the last solve's interior point ran on the 32-lane workspace (d.isw)
     uint32_t* bchk = nullptr;  // bounds-checked build: per-lane violation bits (dev_common.h MPCC_BCHK)
@@ -436,7 +437,34 @@ void run_batch(mpcc_engine* e, int B, hipStream_t st, mpcc_timing* timing, bool 
     launched = true;
     launch_prepare(c, d, st);
     launched = true;
-    if (tm) t_env0 = mark();
+    // Early solo blocks (configurations without collision networks): the cold starts that get solo blocks are the
+    // launch's critical path (k_sqp_solo ~0.15 ms longer than the packed k_sqp at configs[1]).  Their records and
+    // first QP records are built first, by launches over those instances alone (k_order's map, DevConst::subset 1), and
+    // k_sqp_solo starts on the side stream while the other instances' records and QP records (subset 2) are built;
+    // the packed k_sqp follows them on the group's stream.  Every instance's arithmetic is unchanged.
+    const int npm_c = poly_rows_max(c.p.constraint_mask);
+    const bool early_solo = fused && !(c.p.use_BFGS || e->wide_sqp) && DOF == 7 && e->solo_mode == 2 && e->tail_mode &&
+                            e->early_solo && !c.ocp && !(c.p.constraint_mask & (MPCC_CON_SELFCOL | MPCC_CON_ENVCOL)) &&
+                            (npm_c <= 2 || npm_c >= 9) && (c.Bn + IPW_SQP - 1) / IPW_SQP <= e->simds;
+    DevConst cs = c;  // the fused k_sqp's launch constants (solo slots)
+    hipStream_t side = nullptr;
+    if (early_solo) {
+        cs.solo = 2;
+        launch_order(cs, d, st);
+        if (tm) t_env0 = mark();
+        DevConst c1 = c;
+        c1.subset = 1;
+        launch_stage_records(c1, d, st);
+        launch_setqp(c1, d, d.u0, st);
+        side = e->side_stream();
+        HIPCHK(hipEventRecord(e->solo_fork, st));
+        HIPCHK(hipStreamWaitEvent(side, e->solo_fork, 0));
+        if (!launch_sqp_solo(cs, d, d.u0, npm_c, side)) throw std::logic_error("early solo blocks without tail mode");
+        HIPCHK(hipEventRecord(e->solo_join, side));
+        c.subset = 2;  // the remaining launches of the records and the first QP records: every other instance
+    } else if (tm) {
+        t_env0 = mark();
+    }
     launch_stage_records(c, d, st);
     launched = true;
     int m0 = -1, m1 = -1, m2 = -1;
@@ -465,14 +493,18 @@ void run_batch(mpcc_engine* e, int B, hipStream_t st, mpcc_timing* timing, bool 
         int a0 = -1, a1 = -1, b1 = -1;
         if (tm) a0 = mark();
         launch_setqp(c, d, ucur, st);
+        c.subset = 0;
         launched = true;
         if (tm) a1 = mark();
         e->last_wide = DOF != 7 || c.p.use_BFGS || e->wide_sqp;
-        if (c.p.use_BFGS || e->wide_sqp) launch_sqp_wide(c, d, ucur, poly_rows_max(c.p.constraint_mask), c.p.use_BFGS ? 1 : 0, st);
+        if (early_solo) {
+            launch_sqp(cs, d, ucur, npm_c, st);
+            HIPCHK(hipStreamWaitEvent(st, e->solo_join, 0));
+        } else if (c.p.use_BFGS || e->wide_sqp) launch_sqp_wide(c, d, ucur, poly_rows_max(c.p.constraint_mask), c.p.use_BFGS ? 1 : 0, st);
         else if (DOF == 7 && e->solo_mode && e->tail_mode && !c.ocp) {  // cold starts alone in a wave / block (k_prepare flags
                                                                        // them; the 16-lane interior point's tail mode)
-            DevConst cs = c;
-            const int npm = poly_rows_max(c.p.constraint_mask);
+            cs = c;
+            const int npm = npm_c;
             cs.solo = 1;
             launch_order(cs, d, st);
             // solo blocks where the packed launch is one round of waves (at most one per SIMD): beyond that the
@@ -640,6 +672,8 @@ int mpcc_create(const mpcc_config* cfg, const mpcc_params* params, const char* n
         e->tail_mode = (tl && tl[0] == '0') ? 0 : 1;
         const char* so = std::getenv("MPCC_SOLO");
         e->solo_mode = (so && so[0] == '0') ? 0 : (so && so[0] == '1') ? 1 : 2;
+        const char* es = std::getenv("MPCC_EARLY_SOLO");
+        e->early_solo = (es && es[0] == '0') ? 0 : 1;
         e->params = *params;
         e->params.N = cfg->N;
         e->params.Ts = cfg->Ts;

@@ -197,12 +197,34 @@ __device__ inline void robot_record(const DevConst& c, const double* q, double o
 constexpr bool FD_SPLIT = 2 * DOF + 1 <= 16;
 constexpr int RPT = FD_SPLIT ? 16 : ((DOF + 1 <= 8) ? 8 : 16);
 static_assert(DOF + 1 <= RPT, "one thread per gradient term");
+// The instance of record group t0 of a launch over c.subset (early solo blocks, engine.cpp run_batch): 0 record t0,
+// 1 stage t0 mod (N+1) of solo block t0 / (N+1)'s instance (d.order slot 4 r; -1 when the block has none), 2 record t0
+// unless its instance is in a solo block (k_order marks those 2 in the cold flags).  Returns the record index or -1;
+// the whole group of a record returns together.
+__device__ __forceinline__ int subset_record(const DevConst& c, const DevBuffers& d, int t0) {
+    const int NS = c.N + 1;
+    if (c.subset == 1) {
+        const int r = t0 / NS;
+        const int b = r < NSOLO ? d.order[4 * r] : -1;
+        return b < 0 ? -1 : b * NS + (t0 - r * NS);
+    }
+    if (t0 >= c.S) return -1;
+    if (c.subset == 2 && d.order[order_slots(c.Bn) + t0 / NS] == 2) return -1;
+    return t0;
+}
+__host__ __device__ inline long subset_records(const DevConst& c) { return c.subset == 1 ? (long)NSOLO * (c.N + 1) : c.S; }
 __global__ void __launch_bounds__(64) k_records(DevConst c, DevBuffers d) {
     const long g_t = (long)blockIdx.x * blockDim.x + threadIdx.x;
     const int S = c.S;
     const int t0 = (int)(g_t / RPT), u = (int)(g_t % RPT);
-    const bool live = t0 < S;
-    const int t = live ? t0 : S - 1;  // every lane of a record group evaluates (the split form exchanges values)
+    bool live = t0 < S;
+    int tr = t0;
+    if (c.subset) {  // whole record groups of 16 (RPT) lanes leave together
+        tr = subset_record(c, d, t0);
+        if (tr < 0) return;
+        live = true;
+    }
+    const int t = live ? tr : S - 1;  // every lane of a record group evaluates (the split form exchanges values)
     const int N = c.N;
     const int b = t / (N + 1), k = t - b * (N + 1);
     const double* g = d.guess + ((size_t)b * (N + 1) + k) * NXU;
@@ -254,8 +276,13 @@ __global__ void __launch_bounds__(64) k_records(DevConst c, DevBuffers d) {
 // k_setqp: stage QP record (setqp_stage, dev_sqp.h), one lane per (instance, stage)
 // ------------------------------------------------------------------------------------------------
 __global__ void __launch_bounds__(64) k_setqp(DevConst c, DevBuffers d, const double* __restrict__ ucur_all) {
-    const int t = blockIdx.x * blockDim.x + threadIdx.x;
-    if (t >= c.S) return;
+    int t = blockIdx.x * blockDim.x + threadIdx.x;
+    if (c.subset) {
+        t = subset_record(c, d, t);
+        if (t < 0) return;
+    } else if (t >= c.S) {
+        return;
+    }
     const int N = c.N;
     const int b = t / (N + 1), k = t - b * (N + 1);
     if (!d.sqi[(size_t)b * SQI + SQ_ACTIVE]) return;
@@ -460,7 +487,7 @@ __global__ void k_debug_cost(DevConst c, int M, const double* __restrict__ x, co
 __global__ void __launch_bounds__(64) k_order(DevConst c, DevBuffers d) {
     const int Bn = c.Bn, NSL = order_slots(Bn);
     int32_t* slot = d.order;
-    const int32_t* cold = d.order + NSL;
+    int32_t* cold = d.order + NSL;
     const int lane = threadIdx.x;
     for (int i = lane; i < NSL; i += 64) slot[i] = -1;
     __syncthreads();  // the -1 stores land before any slot's instance
@@ -480,7 +507,10 @@ __global__ void __launch_bounds__(64) k_order(DevConst c, DevBuffers d) {
             const unsigned long long m = __ballot(cd);
             const int before = cb + __popcll(m & below);
             if (b < Bn) {
-                if (cd && before < NSOLO) slot[4 * before] = b;
+                if (cd && before < NSOLO) {
+                    slot[4 * before] = b;
+                    cold[b] = 2;  // in a solo block (k_records / k_setqp subsets)
+                }
                 else slot[4 * NSOLO + b - min(before, NSOLO)] = b;
             }
             cb += __popcll(m);
@@ -500,10 +530,10 @@ void launch_order(const DevConst& c, const DevBuffers& d, hipStream_t s) {
     hipLaunchKernelGGL(k_order, dim3(1), dim3(64), 0, s, c, d);
 }
 void launch_stage_records(const DevConst& c, const DevBuffers& d, hipStream_t s) {
-    hipLaunchKernelGGL(k_records, dim3(nblk((long)c.S * RPT, 64)), dim3(64), 0, s, c, d);
+    hipLaunchKernelGGL(k_records, dim3(nblk(subset_records(c) * RPT, 64)), dim3(64), 0, s, c, d);
 }
 void launch_setqp(const DevConst& c, const DevBuffers& d, const double* u_cur, hipStream_t s) {
-    hipLaunchKernelGGL(k_setqp, dim3(nblk(c.S, 64)), dim3(64), 0, s, c, d, u_cur);
+    hipLaunchKernelGGL(k_setqp, dim3(nblk(subset_records(c), 64)), dim3(64), 0, s, c, d, u_cur);
 }
 void launch_soc(const DevConst& c, const DevBuffers& d, const double* u_cur, hipStream_t s) {
     hipLaunchKernelGGL(k_soc, dim3(nblk(c.S, 64)), dim3(64), 0, s, c, d, u_cur);
