@@ -20,7 +20,7 @@ namespace mpcc {
 // SQP iteration 0 (setQP is called without the Hessian, osqp_interface.cpp:441-442); the input diagonal is
 // constant and is rewritten unchanged.
 #ifndef MPCC_SETQP_PRELOAD
-#define MPCC_SETQP_PRELOAD 1
+#define MPCC_SETQP_PRELOAD (DOF == 7)  // the mobile build's larger arrays cost its fused kernels scratch
 #endif
 __device__ inline void setqp_stage(const DevConst& c, const SplineView& sp, const double* __restrict__ gb, const RecView& rv, int k,
                                    const double* __restrict__ ucur, double* __restrict__ q, bool keep_hess = false) {

@@ -275,7 +275,11 @@ __global__ void __launch_bounds__(64) k_records(DevConst c, DevBuffers d) {
 // ------------------------------------------------------------------------------------------------
 // k_setqp: stage QP record (setqp_stage, dev_sqp.h), one lane per (instance, stage)
 // ------------------------------------------------------------------------------------------------
-__global__ void __launch_bounds__(64) k_setqp(DevConst c, DevBuffers d, const double* __restrict__ ucur_all) {
+__global__ void __launch_bounds__(64) k_setqp(DevConst, DevBuffers, const double* __restrict__ ucur_all) {
+    // the arguments read in place (kernels.h kernarg_const): setqp_stage indexes the params' bound arrays at a
+    // lane-dependent position, which on a by-value parameter made the compiler copy it into the private segment
+    const DevConst& c = kernarg_const();
+    const DevBuffers& d = kernarg_buffers();
     int t = blockIdx.x * blockDim.x + threadIdx.x;
     if (c.subset) {
         t = subset_record(c, d, t);
