@@ -438,10 +438,11 @@ void run_batch(mpcc_engine* e, int B, hipStream_t st, mpcc_timing* timing, bool 
     launch_prepare(c, d, st);
     launched = true;
     // Early solo blocks (configurations without collision networks): the cold starts that get solo blocks are the
-    // launch's critical path (k_sqp_solo ~0.15 ms longer than the packed k_sqp at configs[1]).  Their records and
-    // first QP records are built first, by launches over those instances alone (k_order's map, DevConst::subset 1), and
-    // k_sqp_solo starts on the side stream while the other instances' records and QP records (subset 2) are built;
-    // the packed k_sqp follows them on the group's stream.  Every instance's arithmetic is unchanged.
+    // launch's critical path (k_sqp_solo ~0.15 ms longer than the packed k_sqp at configs[1]).  After k_order and the
+    // records of the solo instances alone (DevConst::subset 1), k_sqp_solo starts on the side stream and builds their
+    // first QP records itself (ipm.hip solo_prep), while the other instances' records and QP records are built on the
+    // group's stream (subset 2: k_order marks the solo instances) and the packed k_sqp follows them.  Every
+    // instance's arithmetic is unchanged.
     const int npm_c = poly_rows_max(c.p.constraint_mask);
     const bool early_solo = fused && !(c.p.use_BFGS || e->wide_sqp) && DOF == 7 && e->solo_mode == 2 && e->tail_mode &&
                             e->early_solo && !c.ocp && !(c.p.constraint_mask & (MPCC_CON_SELFCOL | MPCC_CON_ENVCOL)) &&
@@ -452,14 +453,17 @@ void run_batch(mpcc_engine* e, int B, hipStream_t st, mpcc_timing* timing, bool 
         cs.solo = 2;
         launch_order(cs, d, st);
         if (tm) t_env0 = mark();
+        // the solo instances' records, then the solo blocks on the side stream (they build their first QP records
+        // themselves), beside the other instances' records and QP records on the group's stream
         DevConst c1 = c;
         c1.subset = 1;
         launch_stage_records(c1, d, st);
-        launch_setqp(c1, d, d.u0, st);
         side = e->side_stream();
         HIPCHK(hipEventRecord(e->solo_fork, st));
         HIPCHK(hipStreamWaitEvent(side, e->solo_fork, 0));
-        if (!launch_sqp_solo(cs, d, d.u0, npm_c, side)) throw std::logic_error("early solo blocks without tail mode");
+        DevConst cso = cs;
+        cso.subset = 1;  // k_sqp_solo builds its instances' first QP records (ipm.hip solo_prep)
+        if (!launch_sqp_solo(cso, d, d.u0, npm_c, side)) throw std::logic_error("early solo blocks without tail mode");
         HIPCHK(hipEventRecord(e->solo_join, side));
         c.subset = 2;  // the remaining launches of the records and the first QP records: every other instance
     } else if (tm) {

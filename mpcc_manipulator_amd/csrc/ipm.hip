@@ -25,12 +25,16 @@
 //    the corrector forward sweep (exact identities of the oracle's update, rounding aside).
 #include <type_traits>
 
+// QP assembly, records and line-search pieces of k_sqp: oracle operation order, no FP contraction, exactly as
+// kernels.hip (-ffp-contract=off) builds them; the shared headers' helpers (dev_common.h's 3x3 products of the
+// kinematics and the spline frames) are parsed under the same setting, so the in-kernel records and QP records are
+// bitwise k_records' and k_setqp's
+#pragma clang fp contract(off)
 #include "dev_common.h"
 #include "dev_dpp.h"
 #include "kernels.h"
-// QP assembly and line-search pieces of k_sqp: oracle operation order, no FP contraction
-#pragma clang fp contract(off)
 #include "dev_sqp.h"
+#include "dev_records.h"
 #pragma clang fp contract(fast)
 
 namespace mpcc {
@@ -1980,12 +1984,22 @@ __global__ void __launch_bounds__(64) k_sqp(DevConst, DevBuffers, const double* 
 // k_sqp_solo (c.solo 2, launched beside k_sqp on a second stream): block r holds solo wave r's cold-started instance
 // (k_order's slot 4 r); wave 0 runs its SQP, wave 1 joins its tail-mode QP solves (solo_helper).  A block without a
 // cold instance returns at once.
+// Early solo blocks (engine.cpp run_batch, c.subset 1): the block builds its instance's first QP records itself
+// before the SQP loop (k_setqp's setqp_stage, the same arithmetic: fp-contract off as in kernels.hip), on the two SIMDs
+// it holds, instead of in a launch that waits for SIMDs the other instances' launches occupy.  The records come from
+// k_records over the solo instances (subset 1) before this launch.  Both waves take part.
+__device__ __attribute__((noinline)) void solo_prep(const DevConst& c, const DevBuffers& d, int b,
+                                                    const double* __restrict__ ucur_all) {
+    sqp_setqp_phase(c, d, b, (int)threadIdx.x, (int)blockDim.x, ucur_all + NU * b);
+    __syncthreads();  // the QP records before the SQP loop
+}
 template <int NPM>
 __global__ void __launch_bounds__(64 * SB_WAVES) k_sqp_solo(DevConst, DevBuffers, const double* __restrict__ ucur_all) {
     extern __shared__ __attribute__((aligned(16))) double smem[];
     const DevConst& c = kernarg_const();
     const DevBuffers& d = kernarg_buffers();
     if (d.order[blockIdx.x * IPW] < 0) return;
+    if (c.subset == 1) solo_prep(c, d, d.order[blockIdx.x * IPW], ucur_all);
     if (threadIdx.x >= 64) {
         solo_helper<NPM>(c, d, smem);
         return;

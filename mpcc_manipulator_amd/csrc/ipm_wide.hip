@@ -16,11 +16,12 @@
 //  * per-stage slacks, multipliers, iterate, steps and gains stream through a [field][32 lanes] global
 //    workspace, one stage ahead.  The predictor backward solve is fused into the factorization sweep and the
 //    iterate update applied lazily by the next one, as in ipm.hip.
+// QP assembly and line-search pieces of k_sqp: oracle operation order, no FP contraction, the shared headers'
+// helpers included (bitwise kernels.hip's k_setqp / k_trial, as in ipm.hip)
+#pragma clang fp contract(off)
 #include "dev_common.h"
 #include "dev_dpp.h"
 #include "kernels.h"
-// QP assembly and line-search pieces of k_sqp: oracle operation order, no FP contraction
-#pragma clang fp contract(off)
 #include "dev_sqp.h"
 #pragma clang fp contract(fast)
 
