@@ -53,7 +53,7 @@ constexpr double IPM_S0 = 0.02, IPM_L0 = 0.002;  // scaled start point (oracle: 
 #ifdef MPCC_DBG_IPM_STOP  // debug builds (tools/tail_ws_diff.py): stop every QP after that many iterations, no restart
 constexpr int IPM_MAX_IT_SCALED = MPCC_DBG_IPM_STOP, IPM_ATTEMPTS = 1;
 #else
-constexpr int IPM_MAX_IT_SCALED = 30, IPM_ATTEMPTS = 2;
+constexpr int IPM_MAX_IT_SCALED = 24, IPM_ATTEMPTS = 2;  // the oracle's (round 6: 30 -> 24)
 #endif
 constexpr double IPM_TAU = 0.995;    // fraction-to-boundary floor: tau = max(IPM_TAU, 1 - sqrt(mu))
 typedef __attribute__((address_space(1))) double gdouble;  // global-memory double (global_* loads/stores)

@@ -35,7 +35,7 @@ constexpr double IPM_TOL_MU = 1e-13, IPM_TOL_P = 1e-11, IPM_TOL_STEP = 1e-11;
 constexpr double IPM_TOL_FB = 1e-9;  // P2
 constexpr double IPM_DIV = 1e6;      // P3
 constexpr double IPM_S0 = 0.02, IPM_L0 = 0.002;
-constexpr int IPM_MAX_IT_SCALED = 30;
+constexpr int IPM_MAX_IT_SCALED = 24;  // the oracle's (round 6: 30 -> 24)
 constexpr double IPM_TAU = 0.995;
 typedef __attribute__((address_space(1))) double gdouble;
 typedef double d4 __attribute__((ext_vector_type(4)));

@@ -1875,7 +1875,7 @@ static int solve_struct_ipm_from(const StructQP& S, std::vector<double>& step, i
 // exactly the solve without the scaled attempt, so the scaled start can only change which iterate a
 // converging QP ends on (~1e-12), never a failure into a different failure.
 constexpr double IPM_S0 = 0.02, IPM_L0 = 0.002;
-constexpr int IPM_MAX_IT_SCALED = 30;
+constexpr int IPM_MAX_IT_SCALED = 24;  // round 6: 30 -> 24
 static int solve_struct_ipm(const StructQP& S, std::vector<double>& step, int* iters_out, const LowRank* lr = nullptr) {
     int it1 = 0, it2 = 0;
     static const bool stats = std::getenv("MPCC_ORACLE_IPM_STATS") != nullptr;  // debug: one line per QP solve
