@@ -521,9 +521,11 @@ def main():
         fl = samples * mlp_flops_per_sample("k_mlp_env", dof)
         pm = find_pmc("k_mlp_env", Bs, N, args.mask, dof)
         tr = pm.get("hbm_bytes_per_launch") if pm else None
-        ach = fl * n_env / busy_env / 1e12
+        ach = fl / t_l / 1e12  # per launch, as for k_sqp; the union of the groups' launches beside it
+        ach_u = fl * n_env / busy_env / 1e12
         roof = {"kernel": "k_mlp_env", "bound": "mfma", "achieved": ach, "peak": FP64_PEAK_TFLOPS,
                 "unit": "TFLOP/s", "frac": ach / FP64_PEAK_TFLOPS, "traffic": tr,
+                "achieved_union": ach_u, "frac_union": ach_u / FP64_PEAK_TFLOPS,
                 "counter_hbm_frac": (tr * n_env / busy_env / HBM_PEAK_BPS) if tr else None, "avg_launch_ms": t_l * 1e3,
                 "launches_timed": n_env, "concurrent_groups": S, "busy_ms_per_step": busy_env / max(1, ncalls) * 1e3,
                 "algorithmic_flops_per_launch": fl,
