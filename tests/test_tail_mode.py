@@ -108,6 +108,36 @@ def test_tail_mode_against_oracle(built_lib, oracle_lib, monkeypatch, mask, B):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("mask,B,cold_every", [(2, 4096, 64), (0, 512, 8), (3, 512, 8), (2, 512, 1)])
+def test_early_solo_bitwise(built_lib, monkeypatch, mask, B, cold_every):
+    """Early solo blocks (engine.cpp run_batch): the solo instances' records by a k_records launch over
+    them alone, their first QP records inside k_sqp_solo, the other instances' records and QP records by launches
+    that skip them.  Every output equals the old launch order's (MPCC_EARLY_SOLO=0), cold_every 1: more cold starts
+    than solo blocks.  Reference: mpc.cpp:79-89, the cold-start path these controllers take."""
+    import mpcc_manipulator_amd as m
+    params = m.load_params(N=20, overrides={"sqp": {"max_iter": 2}})
+    eng = m.Engine(params, max_batch=1, constraint_mask=mask)
+    X, Y, Z, q = m.load_default_track()
+    ee = eng.robot_records(np.array([[0, 0, 0, -np.pi / 2, 0, np.pi / 2, np.pi / 4]]), np.array([[3.0, 3.0, 3.0, 0.0]]))[0, :3]
+    eng.close()
+    track = m.track_from_points(X, Y, Z, q, ee)
+    rng = np.random.default_rng(SEED + 44)
+    x0, u0, obs, guess, valid, fails = batch_from_pool(_bench_pool(), B, rng, qnoise=0.005)
+    valid[::cold_every] = 0
+    res = {}
+    for early in ("0", "1"):
+        monkeypatch.setenv("MPCC_EARLY_SOLO", early)
+        eng = m.Engine(params, max_batch=B, constraint_mask=mask)
+        eng.set_track(*track)
+        eng.set_warmstart(guess, valid, fails)
+        x = x0.copy()
+        out = eng.solve(x, u0, obs)
+        res[early] = (x, out, eng.get_warmstart(B), eng.solve_stats(B), 0)
+        eng.close()
+    _assert_bitwise(res["1"], res["0"])
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("mask,B,cold_every", [(2, 4096, 64), (3, 512, 8), (2, 512, 1), (7, 1024, 16)])
 def test_solo_waves_bitwise(built_lib, monkeypatch, mask, B, cold_every):
     """Solo waves and solo blocks (csrc/kernels.hip k_order): k_sqp gives the first 64
