@@ -31,7 +31,13 @@ namespace mpcc {
 // group there).
 
 constexpr int IPM_MAX_IT = 60;
-constexpr double IPM_TOL_MU = 1e-13, IPM_TOL_P = 1e-11, IPM_TOL_STEP = 1e-11;
+#ifndef MPCC_TOL_MU
+#define MPCC_TOL_MU 1e-12  // round 6: 1e-13 -> 1e-12, the oracle's (solve_struct_ipm_from)
+#endif
+#ifndef MPCC_TOL_STEP
+#define MPCC_TOL_STEP 3e-9  // round 6: 1e-11 -> 3e-9, the oracle's
+#endif
+constexpr double IPM_TOL_MU = MPCC_TOL_MU, IPM_TOL_P = 1e-11, IPM_TOL_STEP = MPCC_TOL_STEP;
 constexpr double IPM_TOL_FB = 1e-9;  // P2
 constexpr double IPM_DIV = 1e6;      // P3
 constexpr double IPM_S0 = 0.02, IPM_L0 = 0.002;
