@@ -90,6 +90,10 @@ static_assert(NWF * 16 <= IS, "IPM workspace must fit the per-stage IS allocatio
 // per-instance LDS block (doubles): U and K of the current stage, [i*16 + c]
 constexpr int L_U = 0, L_K = 128;
 constexpr int GRP_LDS = 256 + 16;  // 16 mod 32 doubles: the two instances of a half-wave start 32 banks apart
+#ifndef MPCC_P_LDS
+#define MPCC_P_LDS 0  // 1: the factorization's P update moves Hb, U and P through LDS instead of permlane butterflies
+#endif
+constexpr int P_LDS_BASE = 1152;  // doubles from the wave's LDS base: past the groups' U/K areas (IPW * GRP_LDS)
 
 // LDS ring of the light sweeps (NPM <= 2): LRING slots, each holding one stage of the 4 instances of the
 // wave: the 4-line bound block of the QP record, then the sweep's workspace fields.  One global_load_lds
@@ -146,6 +150,9 @@ __host__ __device__ constexpr int ipm_wave_lds(int npmax) {
                                        : 0;
     return ring > uk ? ring : uk;
 }
+static_assert(P_LDS_BASE >= IPW * GRP_LDS, "P exchange past the groups' U/K areas");
+static_assert(P_LDS_BASE + 64 * 28 <= ipm_wave_lds(0) && P_LDS_BASE + 64 * 28 <= ipm_wave_lds(11),
+              "P exchange inside the wave's LDS");
 size_t ipm_lds_bytes(int /*N*/, int npmax) {
     const size_t uk = (size_t)IPW * GRP_LDS * sizeof(double);
     const size_t ring = (npmax <= 2)          ? (size_t)RING_KIB * 1024
@@ -1454,6 +1461,60 @@ __device__ __forceinline__ bool ipm_group(const DevConst& c, const DevBuffers& d
                     // of every instance j, and the products go back the same way.  (U^T U issued from C = 0
                     // right after U is formed, to overlap the solves, held its 16 results through them: more
                     // spills, k_sqp 3.40 ms against 3.31 ms; profiles/r03m_*.)
+#if MPCC_P_LDS
+                    // The instance <-> MFMA layout moves through the wave's LDS (free during the factorization
+                    // sweep: the light sweeps' ring is drained) instead of permlane butterflies: lane (j, c) stores
+                    // its Hb column in the order p(a) = 4 (a & 3) + (a >> 2) and its U column as [u0 u4 u1 u5 ..];
+                    // lane (g, c) then reads Hb_j[g + 4r][c] (r = 0..3) and U_j[g][c], U_j[4 + g][c] of every
+                    // instance j as three 16-byte reads, and the products return the same way.  Same MFMAs on the
+                    // same operands: bitwise the butterfly form.
+                    {
+                        double* const PX = smem + P_LDS_BASE;            // [64 lanes][18]: Hb, then the products
+                        double* const PU = smem + P_LDS_BASE + 64 * 18;  // [64 lanes][10]: U
+                        double2* const h2 = reinterpret_cast<double2*>(PX + lane * 18);
+#pragma unroll
+                        for (int q = 0; q < 8; q++) {
+                            const int p0 = 2 * q, p1 = 2 * q + 1;
+                            h2[q] = make_double2(hb[(p0 & 3) * 4 + (p0 >> 2)], hb[(p1 & 3) * 4 + (p1 >> 2)]);
+                        }
+                        double2* const u2 = reinterpret_cast<double2*>(PU + lane * 10);
+#pragma unroll
+                        for (int q = 0; q < 4; q++) u2[q] = make_double2(u[q], u[4 + q]);
+                        lds_sync();
+                        d4 acc[4];
+                        double2 uu[4];
+#pragma unroll
+                        for (int j = 0; j < 4; j++) {
+                            const int src = j * 16 + t;
+                            const double2* hs = reinterpret_cast<const double2*>(PX + src * 18 + grp * 4);
+                            const double2 h01 = hs[0], h23 = hs[1];
+                            acc[j] = d4{h01.x, h01.y, h23.x, h23.y};
+                            uu[j] = reinterpret_cast<const double2*>(PU + src * 10)[grp];
+                        }
+                        lds_sync();
+#pragma unroll
+                        for (int j = 0; j < 4; j++) {
+                            acc[j] = __builtin_amdgcn_mfma_f64_16x16x4f64(-uu[j].x, uu[j].x, acc[j], 0, 0, 0);
+                            acc[j] = __builtin_amdgcn_mfma_f64_16x16x4f64(-uu[j].y, uu[j].y, acc[j], 0, 0, 0);
+                        }
+#pragma unroll
+                        for (int j = 0; j < 4; j++) {
+                            double2* const rs = reinterpret_cast<double2*>(PX + (j * 16 + t) * 18 + grp * 4);
+                            rs[0] = make_double2(acc[j][0], acc[j][1]);
+                            rs[1] = make_double2(acc[j][2], acc[j][3]);
+                        }
+                        lds_sync();
+                        double pp[16];
+#pragma unroll
+                        for (int q = 0; q < 8; q++) {
+                            const double2 v = h2[q];
+                            pp[2 * q] = v.x;
+                            pp[2 * q + 1] = v.y;
+                        }
+#pragma unroll
+                        for (int a = 0; a < 16; a++) Pc[a] = pp[(a & 3) * 4 + (a >> 2)];
+                    }
+#else
                     double x[4][4], ua[4][1], ub[4][1];
 #pragma unroll
                     for (int g = 0; g < 4; g++) {
@@ -1478,6 +1539,7 @@ __device__ __forceinline__ bool ipm_group(const DevConst& c, const DevBuffers& d
                     for (int g = 0; g < 4; g++)
 #pragma unroll
                         for (int r = 0; r < 4; r++) Pc[g + 4 * r] = x[g][r];
+#endif
                 }
                 if constexpr (!MPCC_KR_EARLY) {
                 lds_sync();
