@@ -460,15 +460,19 @@ __device__ __forceinline__ void sample_input(const DevConst& c, const DevBuffers
 #define MPCC_SELF_CT 2
 #endif
 constexpr int SELF_CT = MPCC_SELF_CT;
+#ifndef MPCC_SELF_WAVES
+#define MPCC_SELF_WAVES 4  // waves per k_mlp_self block: 2, 4, or 0 = two for launches of at most ENV_SMALL samples
+#endif
 #ifndef MPCC_SELF_RING
 #define MPCC_SELF_RING 1
 #endif
 constexpr int SELF_RS = 3, SELF_SLOT = 512 + 4 * 256;  // ring slots; doubles per slot (W1 row tile + W2 k-tile)
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) k_mlp_self(DevConst c, DevBuffers d, NNDesc nd, const double* __restrict__ W, int M,
+template <int NW>
+__global__ void __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(2))) k_mlp_self(DevConst c, DevBuffers d, NNDesc nd, const double* __restrict__ W, int M,
                                                   const double* __restrict__ qin, const double* __restrict__ obsin,
                                                   double* __restrict__ rec, int S) {
     const int lane = threadIdx.x & 63;
-    const int wave = blockIdx.x * 4 + (threadIdx.x >> 6);
+    const int wave = blockIdx.x * NW + (threadIdx.x >> 6);
     int m[SELF_CT];
     d4 a0[SELF_CT][2], a2[SELF_CT][4], o[SELF_CT][1];
 #pragma unroll
@@ -488,7 +492,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) k
     // the biases in LDS: the epilogues read 64 of them per lane in a lane-dependent order, which as global loads
     // the allocator could only issue one at a time (one register pair free, a full wait each)
     __shared__ double sb[256 + 64 + 16];
-    for (int i = threadIdx.x; i < 256; i += 256) sb[i] = W[nd.offb[0] + i];
+    for (int i = threadIdx.x; i < 256; i += 64 * NW) sb[i] = W[nd.offb[0] + i];
     if (threadIdx.x < 64) sb[256 + threadIdx.x] = W[nd.offb[1] + threadIdx.x];
     if (threadIdx.x < 1) sb[320] = W[nd.offb[2]];
     __syncthreads();
@@ -502,14 +506,16 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) k
     __shared__ __attribute__((aligned(16))) double ring[SELF_RS * SELF_SLOT];
     const int tid = threadIdx.x, w = tid >> 6;
     const unsigned rbase = (unsigned)(uintptr_t)(__attribute__((address_space(3))) char*)(char*)ring;
+    static_assert(12 % NW == 0, "whole 16-byte copies per thread");
+    constexpr int SPT = 12 / NW;  // 16-byte copies per thread and tile (768 per slot)
     auto issue = [&](int t) {
         const unsigned slot = rbase + (unsigned)((t % SELF_RS) * SELF_SLOT * 8);
 #pragma unroll
-        for (int j = 0; j < 3; j++) {
-            const int e = tid + 256 * j;  // 16-byte chunk of the slot: [W1 tile t: 256][W2 u = 0..3: 128 each]
+        for (int j = 0; j < SPT; j++) {
+            const int e = tid + 64 * NW * j;  // 16-byte chunk of the slot: [W1 tile t: 256][W2 u = 0..3: 128 each]
             const double* src = (e < 256) ? W1 + (size_t)t * 512 + 2 * e
                                           : W2 + ((size_t)((e - 256) >> 7) * 64 + 4 * t) * 64 + 2 * ((e - 256) & 127);
-            glds16_to(src, __builtin_amdgcn_readfirstlane(slot + 1024u * (4 * j + w)));
+            glds16_to(src, __builtin_amdgcn_readfirstlane(slot + 1024u * (NW * j + w)));
         }
     };
     issue(0);
@@ -520,7 +526,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) k
 #if MPCC_SELF_RING
         // this wave's copies of tile t have landed once at most those of tile t + 1 are outstanding; the barrier
         // publishes tile t and retires the slot of tile t - 1, which the copy of tile t + 2 overwrites
-        if (t + 1 < 16) asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
+        if (t + 1 < 16) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(SPT) : "memory");
         else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
         if (t + 2 < 16) issue(t + 2);
@@ -724,10 +730,16 @@ __global__ void __launch_bounds__(64 * NW) k_mlp_env_obs(DevConst c, DevBuffers 
 void launch_nn(const DevConst& c, const DevBuffers& d, const NNDesc& nd, const double* W, int which, int M,
                const double* q, const double* obs, double* rec, int rec_stride, hipStream_t s) {
     if (M <= 0) return;
-    if (which == 0)  // 4 waves x SELF_CT tiles x 2 samples
-        hipLaunchKernelGGL(k_mlp_self, dim3((M + 8 * SELF_CT - 1) / (8 * SELF_CT)), dim3(256), 0, s, c, d, nd, W, M, q, obs,
-                           rec, rec_stride);
-    else {
+    if (which == 0) {  // NW waves x SELF_CT tiles x 2 samples
+        const bool two = MPCC_SELF_WAVES == 2 || (MPCC_SELF_WAVES == 0 && M <= ENV_SMALL);
+        auto go = [&](auto nwc) {
+            constexpr int NW = decltype(nwc)::value;
+            hipLaunchKernelGGL(k_mlp_self<NW>, dim3((M + 2 * NW * SELF_CT - 1) / (2 * NW * SELF_CT)), dim3(64 * NW), 0, s, c,
+                               d, nd, W, M, q, obs, rec, rec_stride);
+        };
+        if (two) go(std::integral_constant<int, 2>{});
+        else go(std::integral_constant<int, 4>{});
+    } else {
         const bool two = MPCC_ENV_WAVES == 2 || (MPCC_ENV_WAVES == 0 && M <= ENV_SMALL);
         auto go = [&](auto nwc) {
             constexpr int NW = decltype(nwc)::value;
