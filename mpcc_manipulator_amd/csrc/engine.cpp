@@ -71,6 +71,8 @@ struct mpcc_engine {
     hipStream_t solo_stream = nullptr;  // k_sqp_solo (solo blocks), forked from and joined to `stream` per launch
     int simds = 1024;                   // SIMDs of the device (4 per CU)
     hipEvent_t solo_fork = nullptr, solo_join = nullptr;
+    hipEvent_t nn_fork = nullptr, nn_join = nullptr;  // the self network on the side stream beside the env network
+    int nn_par = 0;  // MPCC_NN_PAR=1: the self network on the side stream beside the env network (A/B; slower)
     SplineTables track;
     bool has_track = false;
     double* d_spl = nullptr;
@@ -135,6 +137,8 @@ struct mpcc_engine {
         if (solo_stream) (void)hipStreamDestroy(solo_stream);
         if (solo_fork) (void)hipEventDestroy(solo_fork);
         if (solo_join) (void)hipEventDestroy(solo_join);
+        if (nn_fork) (void)hipEventDestroy(nn_fork);
+        if (nn_join) (void)hipEventDestroy(nn_join);
     }
 
     void set_model() {
@@ -472,6 +476,35 @@ void run_batch(mpcc_engine* e, int B, hipStream_t st, mpcc_timing* timing, bool 
     launch_stage_records(c, d, st);
     launched = true;
     int m0 = -1, m1 = -1, m2 = -1;
+    const bool nn_both = (c.p.constraint_mask & MPCC_CON_SELFCOL) && (c.p.constraint_mask & MPCC_CON_ENVCOL);
+    if (nn_both && e->nn_par && !early_solo) {
+        // The two collision networks (SelfCollisionModel / EnvCollisionModel, RobotData's update order) read the same
+        // stage records and write disjoint record fields: the self network runs on the side stream beside the env
+        // network, joined before the QP records.  Same kernels, same outputs.
+        hipStream_t sd = e->side_stream();
+        HIPCHK(hipEventRecord(e->nn_fork, st));
+        HIPCHK(hipStreamWaitEvent(sd, e->nn_fork, 0));
+        hipEvent_t s0 = nullptr, s1 = nullptr;
+        if (e->live) {
+            s0 = e->live_ev();
+            HIPCHK(hipEventRecord(s0, sd));
+        }
+        launch_nn(c, d, e->nn_self.desc, e->nn_self.d, 0, c.S, nullptr, nullptr, d.rec, c.S, sd);
+        if (e->live) {
+            s1 = e->live_ev();
+            HIPCHK(hipEventRecord(s1, sd));
+        }
+        HIPCHK(hipEventRecord(e->nn_join, sd));
+        if (e->live) m1 = mark();
+        launch_nn(c, d, e->nn_env.desc, e->nn_env.d, 1, c.S, nullptr, nullptr, d.rec, c.S, st);
+        launched = true;
+        if (e->live) {
+            m2 = mark();
+            e->lv_mlp_self.push_back({s0, s1});
+            e->lv_mlp_env.push_back({evs[m1], evs[m2]});
+        }
+        HIPCHK(hipStreamWaitEvent(st, e->nn_join, 0));
+    } else {
     if (e->live) m0 = mark();
     if (c.p.constraint_mask & MPCC_CON_SELFCOL)
     {
@@ -488,6 +521,7 @@ void run_batch(mpcc_engine* e, int B, hipStream_t st, mpcc_timing* timing, bool 
         m2 = mark();
         if (c.p.constraint_mask & MPCC_CON_SELFCOL) e->lv_mlp_self.push_back({evs[m0], evs[m1]});
         if (c.p.constraint_mask & MPCC_CON_ENVCOL) e->lv_mlp_env.push_back({evs[m1], evs[m2]});
+    }
     }
     if (tm) t_env1 = mark();
     const double* ucur = d.u0;
@@ -678,6 +712,8 @@ int mpcc_create(const mpcc_config* cfg, const mpcc_params* params, const char* n
         e->solo_mode = (so && so[0] == '0') ? 0 : (so && so[0] == '1') ? 1 : 2;
         const char* es = std::getenv("MPCC_EARLY_SOLO");
         e->early_solo = (es && es[0] == '0') ? 0 : 1;
+        const char* np = std::getenv("MPCC_NN_PAR");
+        e->nn_par = (np && np[0] == '1') ? 1 : 0;
         e->params = *params;
         e->params.N = cfg->N;
         e->params.Ts = cfg->Ts;
@@ -698,6 +734,8 @@ int mpcc_create(const mpcc_config* cfg, const mpcc_params* params, const char* n
         }
         HIPCHK(hipEventCreateWithFlags(&e->solo_fork, hipEventDisableTiming));
         HIPCHK(hipEventCreateWithFlags(&e->solo_join, hipEventDisableTiming));
+        HIPCHK(hipEventCreateWithFlags(&e->nn_fork, hipEventDisableTiming));
+        HIPCHK(hipEventCreateWithFlags(&e->nn_join, hipEventDisableTiming));
         const size_t B = (size_t)e->maxB, NS = (size_t)e->N + 1;
         DevBuffers& d = e->d;
         d.guess = dmalloc<double>(B * NS * NXU);
@@ -1178,7 +1216,7 @@ int mpcc_closed_loop(mpcc_engine* e, int B, int steps, double* x0, double* u0, c
         };
         if (use_graph && steps > 0) {
             HIPCHK(hipStreamSynchronize(st));
-            if (DOF == 7) (void)e->side_stream();  // created outside the capture (the solo blocks fork onto it)
+            (void)e->side_stream();  // created outside the capture (the solo blocks and the self network fork onto it)
             HIPCHK(hipStreamBeginCapture(st, hipStreamCaptureModeThreadLocal));
             step();
             HIPCHK(hipStreamEndCapture(st, &graph));

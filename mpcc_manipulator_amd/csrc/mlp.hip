@@ -751,7 +751,8 @@ void launch_nn(const DevConst& c, const DevBuffers& d, const NNDesc& nd, const d
                                    obs, rec, rec_stride);
 #endif
         };
-        if (two) go(std::integral_constant<int, 2>{});
+        if (MPCC_ENV_WAVES == 1) go(std::integral_constant<int, 1>{});  // A/B only: 243k against 377k at the default rows
+        else if (two) go(std::integral_constant<int, 2>{});
         else go(std::integral_constant<int, 4>{});
     }
 }
