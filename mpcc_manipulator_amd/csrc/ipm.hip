@@ -1940,6 +1940,18 @@ __global__ void __launch_bounds__(64) k_ipm(DevConst, DevBuffers) {
     sqp_qp_solve<NPM>(kernarg_const(), kernarg_buffers(), smem);
 }
 
+#ifdef MPCC_SOLO_TS  // timeline of the solo blocks (tools/solo_ts.py): s_memrealtime (100 MHz) per block at entry, after the
+                     // first QP records, and after the QP records / QP solve / step of SQP iterations 0 and 1
+__device__ unsigned long long g_solo_ts[64 * 8];
+#define SOLO_TS(i) do { if (threadIdx.x == 0 && blockIdx.x < 64) g_solo_ts[blockIdx.x * 8 + (i)] = __builtin_amdgcn_s_memrealtime(); } while (0)
+}  // namespace mpcc
+extern "C" int mpcc_debug_solo_ts(unsigned long long* out) {
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(mpcc::g_solo_ts), sizeof(unsigned long long) * 64 * 8) == hipSuccess ? 0 : -1;
+}
+namespace mpcc {
+#else
+#define SOLO_TS(i) do { } while (0)
+#endif
 // the SQP loop of one wave (k_sqp: each wave; k_sqp_solo: wave 0 of a solo block, SB)
 template <int NPM, bool SB>
 __device__ __forceinline__ void sqp_waves(const DevConst& c, const DevBuffers& d, const double* __restrict__ ucur_all,
@@ -1989,8 +2001,10 @@ __device__ __forceinline__ void sqp_waves(const DevConst& c, const DevBuffers& d
         }
         SPMARK(0);
         ph.mark(PH_SETQP);
+        if constexpr (SB) if (it < 2) SOLO_TS(2 + 3 * it);
         sqp_qp_solve<NPM, SB>(c, d, smem);
         bar();
+        if constexpr (SB) if (it < 2) SOLO_TS(3 + 3 * it);
         SPMARK(1);
         if (c.p.do_SOC) {  // SecondOrderCorrection (osqp_interface.cpp:506-535): same P, q, A, shifted bounds
             if (pb < c.Bn && psi[SQ_ACTIVE] != 0) sqp_soc_phase(c, d, pb, pt, pst, pucur);
@@ -2023,6 +2037,7 @@ __device__ __forceinline__ void sqp_waves(const DevConst& c, const DevBuffers& d
         nrm = g_max(nrm);  // DPP: whole row active
         if (act && t == 0) finish_iteration(c, d, b, nrm);
         bar();
+        if constexpr (SB) if (it < 2) SOLO_TS(4 + 3 * it);
     }
     ph.mark(PH_STEP);
     ph.flush(threadIdx.x == 0);
@@ -2067,7 +2082,9 @@ __global__ void __launch_bounds__(64 * SB_WAVES) k_sqp_solo(DevConst, DevBuffers
     const DevConst& c = kernarg_const();
     const DevBuffers& d = kernarg_buffers();
     if (d.order[blockIdx.x * IPW] < 0) return;
+    SOLO_TS(0);
     if (c.subset == 1) solo_prep(c, d, d.order[blockIdx.x * IPW], ucur_all);
+    SOLO_TS(1);
     if (threadIdx.x >= 64) {
         solo_helper<NPM>(c, d, smem);
         return;
