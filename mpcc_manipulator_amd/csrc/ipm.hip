@@ -1947,14 +1947,18 @@ __global__ void __launch_bounds__(64) k_ipm(DevConst, DevBuffers) {
 // QP records of every stage from that copy: the values are the same, so the QP records are bitwise setqp_stage's from
 // d.rec.  The solo instance's records were written by another launch, possibly through another XCD's L2, and each
 // lane's stage assembly otherwise waits on its record loads one dependent round trip at a time.
-__device__ __forceinline__ void setqp_staged(const DevConst& c, const DevBuffers& d, int b, int t, int st,
-                                             const double* __restrict__ ucur, double* smem, bool block) {
-    const int N = c.N, NS = N + 1;
+__device__ __forceinline__ void stage_records(const DevConst& c, const DevBuffers& d, int b, int t, int st, double* smem) {
+    const int NS = c.N + 1;
     const double* src = d.rec + (size_t)b * NS;
     for (int i = t; i < REC * NS; i += st) {
         const int f = i / NS, k = i - f * NS;
         smem[i] = src[(size_t)f * c.S + k];
     }
+}
+__device__ __forceinline__ void setqp_staged(const DevConst& c, const DevBuffers& d, int b, int t, int st,
+                                             const double* __restrict__ ucur, double* smem, bool block) {
+    const int N = c.N, NS = N + 1;
+    stage_records(c, d, b, t, st, smem);
     if (block) __syncthreads();
     else wave_sync();
     const SplineView sp = spl_of(c.spl, b);
@@ -2049,6 +2053,21 @@ __device__ __forceinline__ void sqp_waves(const DevConst& c, const DevBuffers& d
         ph.mark(PH_SOLVE);
         act = valid && si[SQ_ACTIVE] != 0;
         const bool pact = pb < c.Bn && psi[SQ_ACTIVE] != 0;
+#if MPCC_SOLO_RSTAGE
+        if (SB && one && REC * (c.N + 1) < sb_cmd<NPM>() - 1) {
+            if (pact) {  // the trial from an LDS copy of the instance's records (setqp_staged)
+                stage_records(c, d, pb, pt, pst, smem);
+                wave_sync();
+                const int NS = c.N + 1;
+                for (int k = pt; k < NS; k += pst) {
+                    double out[4];
+                    trial_stage(c, d, pb, k, 1.0, pucur, out, smem);
+                    double* tr = d.trial + ((size_t)pb * NS + k) * 4;
+                    for (int i = 0; i < 4; i++) tr[i] = out[i];
+                }
+            }
+        } else
+#endif
         if (pact) sqp_trial_phase(c, d, pb, pt, pst, pucur, 1.0, true);
         bar();
         SPMARK(2);
