@@ -311,7 +311,7 @@ __device__ inline void soc_stage(const DevConst& c, const SplineView& sp, const 
 // ddq block k, polytopic block k.  out = {obj, ddq objective, sum (l - c)^+, sum (c - u)^+}.
 // ------------------------------------------------------------------------------------------------
 __device__ inline void trial_stage(const DevConst& c, const DevBuffers& d, int b, int k, double alpha,
-                                   const double* __restrict__ ucur, double* out, const double* lrec = nullptr) {
+                                   const double* __restrict__ ucur, double* out) {
     const int N = c.N;
     const mpcc_params& p = c.p;
     const SplineView sp = spl_of(c.spl, b);
@@ -324,8 +324,7 @@ __device__ inline void trial_stage(const DevConst& c, const DevBuffers& d, int b
     double x[NX], u[NU];
     for (int a = 0; a < NX; a++) x[a] = tx(k, a);
     for (int a = 0; a < NU; a++) u[a] = tu(k, a);
-    // lrec: a copy of instance b's records as [REC][N + 1] (the solo blocks' LDS copy), the same values
-    const RecView rv = lrec ? RecView{lrec + k, N + 1} : RecView{d.rec + (size_t)b * (N + 1) + k, c.S};
+    RecView rv{d.rec + (size_t)b * (N + 1) + k, c.S};
     double fdum[NX], udum[NU], hdum[NX * NX], rdum[NU];
     double obj = stage_cost(c, sp, x, u, rv, k, false, fdum, udum, hdum, rdum);
     double objd = 0;

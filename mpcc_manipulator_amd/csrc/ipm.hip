@@ -1940,42 +1940,13 @@ __global__ void __launch_bounds__(64) k_ipm(DevConst, DevBuffers) {
     sqp_qp_solve<NPM>(kernarg_const(), kernarg_buffers(), smem);
 }
 
-#ifndef MPCC_SOLO_RSTAGE
-#define MPCC_SOLO_RSTAGE 0  // 1: a solo block's QP assemblies read its instance's stage records from LDS (staged in one pass)
-#endif
-// The stage records of instance b as [REC][NS] at smem (every load of the pass independent: one memory latency), and the
-// QP records of every stage from that copy: the values are the same, so the QP records are bitwise setqp_stage's from
-// d.rec.  The solo instance's records were written by another launch, possibly through another XCD's L2, and each
-// lane's stage assembly otherwise waits on its record loads one dependent round trip at a time.
-__device__ __forceinline__ void stage_records(const DevConst& c, const DevBuffers& d, int b, int t, int st, double* smem) {
-    const int NS = c.N + 1;
-    const double* src = d.rec + (size_t)b * NS;
-    for (int i = t; i < REC * NS; i += st) {
-        const int f = i / NS, k = i - f * NS;
-        smem[i] = src[(size_t)f * c.S + k];
-    }
-}
-__device__ __forceinline__ void setqp_staged(const DevConst& c, const DevBuffers& d, int b, int t, int st,
-                                             const double* __restrict__ ucur, double* smem, bool block) {
-    const int N = c.N, NS = N + 1;
-    stage_records(c, d, b, t, st, smem);
-    if (block) __syncthreads();
-    else wave_sync();
-    const SplineView sp = spl_of(c.spl, b);
-    const double* gb = d.guess + (size_t)b * NS * 17;
-    for (int k = t; k <= N; k += st)
-        setqp_stage(c, sp, gb, RecView{smem + k, NS}, k, ucur, d.qs + ((size_t)b * NS + k) * QS);
-}
 #ifdef MPCC_SOLO_TS  // timeline of the solo blocks (tools/solo_ts.py): s_memrealtime (100 MHz) per block at entry, after the
                      // first QP records, and after the QP records / QP solve / step of SQP iterations 0 and 1
 __device__ unsigned long long g_solo_ts[64 * 8];
-__device__ double g_solo_sink[128];
-__device__ unsigned long long g_solo_tc[64];  // MPCC_SOLO_TS_COST: end of the stage-cost-only pass
 #define SOLO_TS(i) do { if (threadIdx.x == 0 && blockIdx.x < 64) g_solo_ts[blockIdx.x * 8 + (i)] = __builtin_amdgcn_s_memrealtime(); } while (0)
 }  // namespace mpcc
-extern "C" int mpcc_debug_solo_ts(unsigned long long* out) {  // [64][8] timestamps, then [64] cost-pass ends
-    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(mpcc::g_solo_ts), sizeof(unsigned long long) * 64 * 8) != hipSuccess) return -1;
-    return hipMemcpyFromSymbol(out + 64 * 8, HIP_SYMBOL(mpcc::g_solo_tc), sizeof(unsigned long long) * 64) == hipSuccess ? 0 : -1;
+extern "C" int mpcc_debug_solo_ts(unsigned long long* out) {
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(mpcc::g_solo_ts), sizeof(unsigned long long) * 64 * 8) == hipSuccess ? 0 : -1;
 }
 namespace mpcc {
 #else
@@ -2025,15 +1996,6 @@ __device__ __forceinline__ void sqp_waves(const DevConst& c, const DevBuffers& d
         SPMARK(4);
         ph.mark(PH_STEP);
         if (it > 0) {
-#if MPCC_SOLO_RSTAGE
-            if constexpr (SB) {
-                if (REC * (c.N + 1) < sb_cmd<NPM>() - 1 && one) {
-                    if (pb < c.Bn && psi[SQ_ACTIVE] != 0) setqp_staged(c, d, pb, pt, pst, pucur, smem, false);
-                } else if (pb < c.Bn && psi[SQ_ACTIVE] != 0) {
-                    sqp_setqp_phase(c, d, pb, pt, pst, pucur);
-                }
-            } else
-#endif
             if (pb < c.Bn && psi[SQ_ACTIVE] != 0) sqp_setqp_phase(c, d, pb, pt, pst, pucur);
             bar();
         }
@@ -2053,21 +2015,6 @@ __device__ __forceinline__ void sqp_waves(const DevConst& c, const DevBuffers& d
         ph.mark(PH_SOLVE);
         act = valid && si[SQ_ACTIVE] != 0;
         const bool pact = pb < c.Bn && psi[SQ_ACTIVE] != 0;
-#if MPCC_SOLO_RSTAGE
-        if (SB && one && REC * (c.N + 1) < sb_cmd<NPM>() - 1) {
-            if (pact) {  // the trial from an LDS copy of the instance's records (setqp_staged)
-                stage_records(c, d, pb, pt, pst, smem);
-                wave_sync();
-                const int NS = c.N + 1;
-                for (int k = pt; k < NS; k += pst) {
-                    double out[4];
-                    trial_stage(c, d, pb, k, 1.0, pucur, out, smem);
-                    double* tr = d.trial + ((size_t)pb * NS + k) * 4;
-                    for (int i = 0; i < 4; i++) tr[i] = out[i];
-                }
-            }
-        } else
-#endif
         if (pact) sqp_trial_phase(c, d, pb, pt, pst, pucur, 1.0, true);
         bar();
         SPMARK(2);
@@ -2125,34 +2072,7 @@ __global__ void __launch_bounds__(64) k_sqp(DevConst, DevBuffers, const double* 
 // it holds, instead of in a launch that waits for SIMDs the other instances' launches occupy.  The records come from
 // k_records over the solo instances (subset 1) before this launch.  Both waves take part.
 __device__ __attribute__((noinline)) void solo_prep(const DevConst& c, const DevBuffers& d, int b,
-                                                    const double* __restrict__ ucur_all, double* smem, int lds_doubles) {
-#if MPCC_SOLO_RSTAGE
-    if (REC * (c.N + 1) < lds_doubles) {
-        setqp_staged(c, d, b, (int)threadIdx.x, (int)blockDim.x, ucur_all + NU * b, smem, true);
-        __syncthreads();  // the QP records before the SQP loop; the LDS copy is free again
-        return;
-    }
-#endif
-    (void)smem;
-    (void)lds_doubles;
-#ifdef MPCC_SOLO_TS_COST  // measurement only: the stage costs alone, timed before the QP records (tools/solo_ts.py)
-    {
-        const int N = c.N, NS = N + 1;
-        const SplineView sp = spl_of(c.spl, b);
-        const double* gb = d.guess + (size_t)b * NS * 17;
-        for (int k = threadIdx.x; k <= N; k += blockDim.x) {
-            double fx[NX], fu[NU], fxx[NX * NX], fuu[NU];
-            const double o = stage_cost(c, sp, gb + NXU * k, gb + NXU * k + NX, RecView{d.rec + (size_t)b * NS + k, c.S}, k,
-                                        true, fx, fu, fxx, fuu);
-            double acc = o;
-            for (int i = 0; i < NX; i++) acc += fx[i] + fxx[i * NX + i];
-            for (int i = 0; i < NU; i++) acc += fu[i] + fuu[i];
-            g_solo_sink[threadIdx.x] = acc;
-        }
-        __syncthreads();
-        if (threadIdx.x == 0 && blockIdx.x < 64) g_solo_tc[blockIdx.x] = __builtin_amdgcn_s_memrealtime();
-    }
-#endif
+                                                    const double* __restrict__ ucur_all) {
     sqp_setqp_phase(c, d, b, (int)threadIdx.x, (int)blockDim.x, ucur_all + NU * b);
     __syncthreads();  // the QP records before the SQP loop
 }
@@ -2163,7 +2083,7 @@ __global__ void __launch_bounds__(64 * SB_WAVES) k_sqp_solo(DevConst, DevBuffers
     const DevBuffers& d = kernarg_buffers();
     if (d.order[blockIdx.x * IPW] < 0) return;
     SOLO_TS(0);
-    if (c.subset == 1) solo_prep(c, d, d.order[blockIdx.x * IPW], ucur_all, smem, sb_cmd<NPM>() - 1);
+    if (c.subset == 1) solo_prep(c, d, d.order[blockIdx.x * IPW], ucur_all);
     SOLO_TS(1);
     if (threadIdx.x >= 64) {
         solo_helper<NPM>(c, d, smem);

@@ -38,14 +38,12 @@ def main():
     x0[:, :7] += rng.normal(0, 0.005, (4096 if B <= 4096 else B, 7))[:B]
     a = (x0, pool["u0"][idx], np.tile([3., 3., 3., 0.], (B, 1)))
     ws = (pool["guess"][idx], pool["valid"][idx].astype(np.int32), pool["fails"][idx].astype(np.int32))
-    buf = (C.c_ulonglong * (64 * 9))()
+    buf = (C.c_ulonglong * (64 * 8))()
     for _ in range(4):
         eng.set_warmstart(*ws)
         eng.solve(*[v.copy() for v in a])
     assert f(buf) == 0
-    raw = np.frombuffer(buf, dtype=np.uint64).astype(np.int64)
-    ts = raw[:64 * 8].reshape(64, 8)
-    tc = raw[64 * 8:]
+    ts = np.frombuffer(buf, dtype=np.uint64).reshape(64, 8).astype(np.int64)
     names = ["prep_done", "qp_records_0", "qp_0", "step_0", "qp_records_1", "qp_1", "step_1"]
     out = []
     for r in range(64):
@@ -53,8 +51,6 @@ def main():
             continue
         row = {n: round((ts[r, i + 1] - ts[r, 0]) / 100.0, 1) if ts[r, i + 1] >= ts[r, 0] else None
                for i, n in enumerate(names)}
-        if tc[r] >= ts[r, 0]:  # -DMPCC_SOLO_TS_COST builds: the stage-cost-only pass before the first QP records
-            row["cost_pass_done"] = round((tc[r] - ts[r, 0]) / 100.0, 1)
         out.append({"block": r, "us_from_entry": row})
     print(json.dumps({"batch": B, "solo_blocks": out}))
     eng.close()
